@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""bench.py — SpMM throughput on MI355X (BASELINE.json metric), one JSON line on rank 0.
+
+Workload (config.workload): ogbn-products-shaped synthetic power-law CSR (2,449,029 x 2,449,029,
+123,718,280 nnz) x dense N=128 fp32 — the config BASELINE.json's north-star target is quoted on
+(configs[2]); it fits one GPU.  A "step" is one SpMM over that matrix with inputs resident in HBM:
+  N=1   oneflow_spmm.spmm(...) (op layer -> C-ABI -> plan/main/reduce HIP kernels)
+  N>1   row split over N ranks: RCCL all-gather of the Split(0) dense shards + local SpMM
+        (strong scaling: the same matrix is divided across ranks).
+value = 2*nnz*N FLOPs per step (whole job) / max-over-ranks step time, in GFLOP/s.
+
+Extra objects: `roofline` (dominant kernel spmm_main, HIP events on its stream, algorithmic
+gather-model bytes) and `cpu_baseline` (the oracle's C restatement on the host
+cores, rank 0 at N=1 only, bounded sample).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config products] [--no-cpu-baseline]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "of-spmm_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+METRIC = "SpMM effective GFLOP/s + achieved HBM GB/s vs roofline, 1/2/4/8 MI355X"
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def alg_bytes(rows: int, nnz: int, n: int, s_v: int, s_i: int = 4) -> int:
+    """Gather model: row_ptr once, col/val once, one B row per nonzero, C once."""
+    return s_i * (rows + 1) + (s_i + s_v) * nnz + s_v * nnz * n + s_v * rows * n
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="products")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
+    ap.add_argument("--variant", type=int, default=0, help="force a kernel variant (VEC*100+LPR)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    import oneflow_spmm as fs
+    from oneflow_spmm import ops, synth
+    from oneflow_spmm.distributed import RowSplitSpmm
+
+    cfg = synth.CONFIGS[args.config]
+    m, k, nnz, n, dt = cfg["m"], cfg["k"], cfg["nnz"], cfg["n"], cfg["dtype"]
+    s_v = torch.empty(0, dtype=dt).element_size()
+    threads = args.cpu_threads
+
+    # ---- inputs (this rank's rows only), resident in HBM before timing -------------------------
+    t0 = time.time()
+    rp_full = synth.row_ptr(m, k, nnz)
+    lo, hi = fs._C.balanced_range(m, world, rank)
+    rows = hi - lo
+    cols = synth.columns(m, k, rp_full, lo, hi, threads=threads)
+    j0, j1 = int(rp_full[lo]), int(rp_full[hi])
+    nnz_local = j1 - j0
+    vals = synth.values(j0, j1, dt)
+    local_rp = torch.from_numpy((rp_full[lo:hi + 1] - rp_full[lo]).astype(np.int32))
+    d_rp = local_rp.to(device)
+    d_ci = torch.from_numpy(cols).to(device)
+    d_v = vals.to(device)
+    out = torch.empty((rows, n), dtype=dt, device=device)
+    log(f"[bench] inputs for rank {rank}: rows {rows} nnz {nnz_local} built in {time.time() - t0:.1f}s")
+
+    events = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    opts = ops.make_options(variant=args.variant) if args.variant else None
+    if world == 1:
+        d_b = synth.dense(0, k, n, dt, device=device)
+        if opts is None:
+            def step():
+                fs.spmm(d_rp, d_ci, d_v, m, k, d_b, out=out)
+        else:
+            kern = ops.SpmmCsrKernel(m, k, n, nnz, torch.int32, dt, device, opts)
+
+            def step():
+                kern(d_rp, d_ci, d_v, d_b, out)
+    else:
+        rs = RowSplitSpmm(m, k, n, nnz_local, dt, torch.int32, device)
+        d_ci = rs.remap_columns(d_ci)
+        klo, khi = rs.k_range
+        rs.shard_view().copy_(synth.dense(klo, khi, n, dt, device=device))
+
+        def step():
+            rs(d_rp, d_ci, d_v, out=out)
+
+    # ---- warmup + timed region -----------------------------------------------------------------
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t_start = time.perf_counter()
+    ev_start.record()
+    for _ in range(args.steps):
+        step()
+    ev_end.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed * 1e3 / args.steps
+    flops = 2.0 * nnz * n
+    value = flops * args.steps / elapsed / 1e9
+
+    # ---- dominant-kernel timing: events on the launch stream around the SpMM launches ---------
+    # N=1: the op call (plan + main + reduce; main dominates).  N>1: the local SpMM after the
+    # gather.  Measured over a separate short run so the timed region above has no extra events.
+    torch.cuda.synchronize()
+    spmm_ms, gather_ms = [], []
+    for _ in range(max(args.steps, 5)):
+        if world == 1:
+            events[1].record()
+            step()
+            events[2].record()
+        else:
+            rs(d_rp, d_ci, d_v, out=out, events=events)
+        torch.cuda.synchronize()
+        spmm_ms.append(events[1].elapsed_time(events[2]))
+        if world > 1:
+            gather_ms.append(events[0].elapsed_time(events[1]))
+    kern_ms = float(np.mean(spmm_ms))
+    bytes_launch = alg_bytes(rows, nnz_local, n, s_v)
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GFLOP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": {torch.float32: "f32", torch.bfloat16: "bf16", torch.float16: "f16",
+                  torch.float64: "f64"}[dt],
+        "data": "synthetic (deterministic Chung-Lu power-law CSR, gamma 2.5; dataset-shaped)",
+        "config": {"workload": f"{args.config}: CSR {m}x{k}, {nnz} nnz x dense N={n}",
+                   "m": m, "k": k, "nnz": nnz, "n": n, "index": "int32",
+                   "parallelism": "single GPU" if world == 1 else
+                   f"row-split x{world} + RCCL all-gather of B (padded shards)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "spmm_main_kernel (+plan/reduce, timed together)",
+                     "alg_bytes_per_launch": bytes_launch, "kernel_ms": round(kern_ms, 4)},
+    }
+    if world > 1:
+        result["extra"] = {"allgather_ms_rank0": round(float(np.mean(gather_ms)), 4),
+                           "spmm_ms_rank0": round(kern_ms, 4),
+                           "rows_rank0": rows, "nnz_rank0": nnz_local}
+
+    # ---- CPU baseline: oracle restatement on the host cores (rank 0, N=1 only) ---------------
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        from oracle import oracle
+        rp_np = rp_full
+        ci_np = cols.astype(np.int64)
+        v_np = vals.numpy() if dt != torch.bfloat16 else vals.view(torch.int16).numpy().view(np.uint16)
+        b_np = synth.dense(0, k, n, dt)
+        b_np = b_np.numpy() if dt != torch.bfloat16 else b_np.view(torch.int16).numpy().view(np.uint16)
+        dname = result["dtype"]
+        oracle.spmm(rp_np, ci_np, v_np, b_np, dtype=dname, nthreads=threads, row_end=min(m, 100000))
+        reps, t_cpu = 0, 0.0
+        while t_cpu < 10.0 and reps < 5:
+            t1 = time.perf_counter()
+            oracle.spmm(rp_np, ci_np, v_np, b_np, dtype=dname, nthreads=threads)
+            t_cpu += time.perf_counter() - t1
+            reps += 1
+        cpu_gflops = flops * reps / t_cpu / 1e9
+        result["cpu_baseline"] = {"value": round(cpu_gflops, 3), "unit": "GFLOP/s", "cores": threads,
+                                  "kind": "port",
+                                  "sample": f"full workload x{reps} runs ({t_cpu:.1f} s), oracle/spmm_oracle.c "
+                                            f"OpenMP {threads} threads, same inputs and schedule"}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        rs.close()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,231 @@
+/*
+ * ofx_spmm.h — the C-ABI drop-in boundary of the MI355X-native `spmm_csr` operator.
+ *
+ * Every entry point is `extern "C"`, takes plain pointers/sizes, returns an `int` status
+ * (OFX_OK == 0) and, on failure, leaves a human-readable message in the calling thread's
+ * `ofx_last_error()` buffer.  No torch / OneFlow types cross this boundary.
+ *
+ * What each group replaces in the reference (yuang-chen/of-spmm == OneFlow v0.8.1-dev; paths
+ * relative to the reference root).  The reference has NO SpMM, so the op-level
+ * entries replace the *composition* the reference would run today plus the OneFlow surfaces a
+ * new user op plugs into:
+ *
+ *  - ofx_spmm_csr / ofx_spmm_csr_workspace_size
+ *      the device kernel behind `REGISTER_USER_KERNEL("spmm_csr")` for the HIP device.
+ *      Semantics restate gather -> multiply -> unsorted_segment_sum:
+ *      oneflow/user/kernels/gather_kernel_util.cpp:72-92 (row copy of B[idx]),
+ *      oneflow/user/kernels/unsorted_segment_sum_kernel_util.cpp:29-45 (std::plus, index order).
+ *      Workspace size mirrors `SetInferTmpSizeFn` (oneflow/core/framework/user_op_kernel_registry.h:90)
+ *      and the "tmp_buffer" arg (oneflow/user/kernels/unsorted_segment_sum_kernel.cpp:162).
+ *      Launch is async on the given stream, allocates nothing, never synchronises
+ *      (kernel contract of oneflow/core/framework/op_kernel.h:287-318).
+ *  - ofx_spmm_csr_cpu
+ *      the DeviceType::kCPU kernel (row-parallel, idiom of oneflow/core/ep/cpu/cpu_stream.h:104-145).
+ *  - ofx_balanced_range / ofx_csr_row_slice
+ *      BalancedSplitter::At (oneflow/core/common/balanced_splitter.cpp:20-40) as used by
+ *      GetTensorSliceView4ParallelId (oneflow/core/job/nd_sbp_util.cpp:98-104) and the
+ *      OpKernelCache row-range pattern (oneflow/user/kernels/unsorted_segment_sum_kernel.cpp:46-78).
+ *  - ofx_device_* / ofx_stream_* / ofx_event_* / ofx_memcpy_async / ofx_memset_async / ofx_malloc
+ *      the ep device layer reduced to a thin C-ABI: ep::Device (oneflow/core/ep/include/device.h:33-62),
+ *      ep::Stream (stream.h:30-49), ep::Event (event.h:26-34), primitive::Memcpy (memcpy.h:33-39),
+ *      primitive::Memset (memset.h:26-32); CUDA impl oneflow/core/ep/cuda/cuda_stream.cpp:90-142.
+ *  - ofx_comm_* / ofx_allgather
+ *      ccl::AllGather (oneflow/user/kernels/collective_communication/include/all_gather.h:24-38),
+ *      CudaAllGather::Launch -> ncclAllGather (.../cuda/cuda_all_gather.cpp:25-47), and the comm
+ *      bootstrap of EagerNcclCommMgr (oneflow/core/job/eager_nccl_comm_manager.cpp:57-131).
+ *  - ofx_functional_spmm_csr
+ *      the functional entry `functional::SpmmCsr` (template oneflow/core/functional/impl/nn_functor.cpp:3861-3884)
+ *      -> op inference (oneflow/user/ops/spmm_op.cpp, our C++ mirror) -> kernel registry
+ *      (REGISTER_USER_KERNEL, oneflow/core/framework/user_op_registry_manager.h:81-84) -> Compute.
+ *
+ * Data-type codes are OneFlow's `DataType` numbering (oneflow/core/common/data_type.proto:4-26).
+ */
+#ifndef OFX_SPMM_H_
+#define OFX_SPMM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------------------------- */
+#define OFX_OK 0
+#define OFX_EINVAL 1       /* shape / dtype / argument mismatch (CHECK_*_OR_RETURN analogue) */
+#define OFX_EDEVICE 2      /* HIP runtime error (launch, memcpy, ...)                          */
+#define OFX_ENOMEM 3       /* allocation failed                                                */
+#define OFX_EUNSUPPORTED 4 /* dtype / layout combination not registered (OpKernelNotFound)     */
+#define OFX_ECOMM 5        /* RCCL error                                                       */
+#define OFX_EWORKSPACE 6   /* workspace smaller than ofx_spmm_csr_workspace_size()             */
+
+/* ---- OneFlow DataType codes (oneflow/core/common/data_type.proto:4-26) ------------------- */
+#define OFX_DT_FLOAT 2
+#define OFX_DT_DOUBLE 3
+#define OFX_DT_INT32 5
+#define OFX_DT_INT64 6
+#define OFX_DT_FLOAT16 9
+#define OFX_DT_BFLOAT16 11
+
+/* Message describing the last failure on the calling thread ("" if none). */
+const char* ofx_last_error(void);
+/* Library version string, e.g. "ofx-spmm 0.1.0 gfx950". */
+const char* ofx_version(void);
+
+/* ---- SpMM schedule options --------------------------------------------------------------
+ * Accumulation-order contract (identical in the CPU kernel, the HIP kernel and the oracle):
+ *   acc = 0; for j in row (ascending): acc = acc + (val[j] * B[col[j], :])     (mul, then add;
+ *   no FMA contraction; fp32 accumulator for f32/f16/bf16, f64 for f64; one rounding to T at the end)
+ * Rows longer than `split_threshold` nonzeros are cut into consecutive chunks of `chunk`
+ * nonzeros; each chunk is summed as above from 0, and the chunk partials are then added
+ * in chunk order into acc = 0.  split_threshold <= 0 selects the default
+ * ofx_spmm_default_split(n); split_threshold == INT64_MAX (or `ordered` != 0) never splits,
+ * which is exactly the reference composition's order.                                      */
+typedef struct ofx_spmm_options {
+  int64_t split_threshold; /* 0 = default                                                    */
+  int64_t chunk;           /* 0 = same as split_threshold                                    */
+  int32_t ordered;         /* != 0: never split (reference order, slower on hub rows)       */
+  int32_t variant;         /* 0 = auto; >0 forces a kernel variant (tuning / tests)          */
+} ofx_spmm_options;
+
+/* The default split threshold for dense width n (a fixed function of n; part of the numeric
+ * contract).  Written out in DESIGN.md §3 and restated by oracle/oracle.py.                */
+int64_t ofx_spmm_default_split(int64_t n);
+
+/* Bytes of device workspace `ofx_spmm_csr` needs for this problem (upper bound, depends
+ * only on shapes and options).  May be 0.                                                  */
+int ofx_spmm_csr_workspace_size(int idx_dtype, int val_dtype, int64_t m, int64_t k, int64_t n,
+                                int64_t nnz, const ofx_spmm_options* opts, size_t* bytes);
+
+/* C[r - row_begin, :] = sum_j values[j] * B[col_idx[j], :]  for r in [row_begin, row_end),
+ *   j in [row_ptr[r], row_ptr[r+1]).
+ *   row_ptr: idx_dtype[m+1]   col_idx: idx_dtype[nnz]   values: val_dtype[nnz]
+ *   b: val_dtype, k rows of stride ldb (>= n)          c: val_dtype, rows of stride ldc (>= n)
+ * All pointers are device pointers; `stream` is a hipStream_t (NULL = default stream).
+ * Asynchronous; no allocation; no host synchronisation.  0 <= row_begin <= row_end <= m.   */
+int ofx_spmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k, int64_t n,
+                 int64_t nnz, const void* row_ptr, const void* col_idx, const void* values,
+                 const void* b, int64_t ldb, void* c, int64_t ldc, int64_t row_begin,
+                 int64_t row_end, void* workspace, size_t workspace_bytes,
+                 const ofx_spmm_options* opts);
+
+/* Device-side structural check of a CSR (row_ptr monotone, row_ptr[0]==0, row_ptr[m]==nnz,
+ * 0 <= col < k).  Writes a 32-bit error code to *flag_dev (0 = ok, 1 = bad row_ptr,
+ * 2 = column out of range) asynchronously on `stream`.                                     */
+int ofx_csr_validate(void* stream, int idx_dtype, int64_t m, int64_t k, int64_t nnz,
+                     const void* row_ptr, const void* col_idx, void* flag_dev);
+
+/* CPU kernel (DeviceType::kCPU).  Same arguments and the same bits as ofx_spmm_csr, host
+ * pointers, synchronous; num_threads <= 0 uses OMP_NUM_THREADS / all cores.              */
+int ofx_spmm_csr_cpu(int num_threads, int idx_dtype, int val_dtype, int64_t m, int64_t k,
+                     int64_t n, int64_t nnz, const void* row_ptr, const void* col_idx,
+                     const void* values, const void* b, int64_t ldb, void* c, int64_t ldc,
+                     int64_t row_begin, int64_t row_end, const ofx_spmm_options* opts);
+
+/* ---- row partition (BalancedSplitter) ---------------------------------------------------- */
+int ofx_balanced_range(int64_t total, int64_t parts, int64_t idx, int64_t* begin, int64_t* end);
+/* Rebase a row slice of a CSR: out_row_ptr[i] = row_ptr[row_begin + i] - row_ptr[row_begin],
+ * i in [0, row_end-row_begin]; returns nnz offset/count.  Device version (async).          */
+int ofx_csr_row_slice(void* stream, int idx_dtype, const void* row_ptr, int64_t row_begin,
+                      int64_t row_end, void* out_row_ptr);
+int ofx_csr_row_slice_host(int idx_dtype, const void* row_ptr, int64_t row_begin,
+                           int64_t row_end, void* out_row_ptr, int64_t* nnz_begin,
+                           int64_t* nnz_end);
+
+/* ---- thin device layer (ep::Device / ep::Stream / ep::Event / primitives) --------------- */
+int ofx_device_count(int* count);
+int ofx_set_device(int device);
+int ofx_get_device(int* device);
+int ofx_device_synchronize(void);
+int ofx_malloc(void** ptr, size_t bytes);       /* 512-B aligned (ep::kMaxAlignmentRequirement) */
+int ofx_free(void* ptr);
+int ofx_host_malloc(void** ptr, size_t bytes);  /* pinned */
+int ofx_host_free(void* ptr);
+int ofx_stream_create(void** stream);
+int ofx_stream_destroy(void* stream);
+int ofx_stream_sync(void* stream);
+#define OFX_MEMCPY_H2D 1
+#define OFX_MEMCPY_D2H 2
+#define OFX_MEMCPY_D2D 3
+#define OFX_MEMCPY_DEFAULT 4
+int ofx_memcpy_async(void* stream, void* dst, const void* src, size_t bytes, int kind);
+int ofx_memset_async(void* stream, void* dst, int value, size_t bytes);
+int ofx_event_create(void** event, int timing);
+int ofx_event_destroy(void* event);
+int ofx_event_record(void* event, void* stream);
+int ofx_event_sync(void* event);
+int ofx_event_elapsed_ms(void* start, void* end, float* ms);
+int ofx_stream_wait_event(void* stream, void* event);
+
+/* ---- RCCL all-gather (ccl::AllGather) ---------------------------------------------------- */
+#define OFX_UNIQUE_ID_BYTES 128
+int ofx_comm_get_unique_id(void* uid_out /* OFX_UNIQUE_ID_BYTES */);
+int ofx_comm_init_rank(void** comm, int nranks, const void* uid, int rank);
+int ofx_comm_destroy(void* comm);
+/* out[r*count .. (r+1)*count) = in of rank r; count in elements of dtype. */
+int ofx_allgather(void* stream, const void* in, void* out, size_t count, int dtype, void* comm);
+
+/* ---- synthetic power-law CSR (deterministic, counter-based) ---------------- */
+/* row_ptr_out: int64[m+1].  Degrees of a Chung–Lu power law (exponent gamma), rows permuted. */
+int ofx_synth_row_ptr(int64_t m, int64_t k, int64_t nnz, double gamma, uint64_t seed,
+                      int64_t* row_ptr_out);
+/* Columns for rows [row_begin,row_end) written at col_out[row_ptr[r]-row_ptr[row_begin] ...],
+ * sorted ascending and unique per row.  idx_dtype int32/int64.  Host, OpenMP.              */
+int ofx_synth_columns(int64_t m, int64_t k, double gamma, uint64_t seed, const int64_t* row_ptr,
+                      int64_t row_begin, int64_t row_end, int idx_dtype, void* col_out,
+                      int num_threads);
+/* values[j - j_begin] for global nonzero ids j in [j_begin, j_end): U[-1,1) or exact-mode. */
+int ofx_synth_values_host(int val_dtype, int64_t j_begin, int64_t j_end, uint64_t seed, int exact,
+                          void* out);
+/* Dense rows [r_begin, r_end) of a k x n matrix with leading dim ld, on the device. */
+int ofx_synth_dense(void* stream, int val_dtype, int64_t r_begin, int64_t r_end, int64_t n,
+                    int64_t ld, uint64_t seed, int exact, void* out);
+int ofx_synth_dense_host(int val_dtype, int64_t r_begin, int64_t r_end, int64_t n, int64_t ld,
+                         uint64_t seed, int exact, void* out);
+
+/* ---- functional entry (Python binding -> C++ op/kernel registry -> device kernel) ------- */
+/* A tensor as the functional layer sees it: dtype code, device (-1 = CPU, >=0 HIP ordinal),
+ * rank-1/2 shape, row stride (elements) for rank-2, data pointer.                          */
+typedef struct ofx_tensor_desc {
+  int32_t dtype;
+  int32_t device;
+  int32_t ndim;
+  int32_t reserved;
+  int64_t shape[2];
+  int64_t stride[2];
+  void* data;
+} ofx_tensor_desc;
+/* Shape/dtype inference of op "spmm_csr" (oneflow/user/ops/spmm_op.cpp mirror). Fills
+ * out->dtype/ndim/shape; returns OFX_EINVAL with the op's error message on mismatch.      */
+int ofx_functional_spmm_csr_infer(const ofx_tensor_desc* row_ptr, const ofx_tensor_desc* col_idx,
+                                  const ofx_tensor_desc* values, int64_t a_num_rows,
+                                  int64_t a_num_cols, const ofx_tensor_desc* b,
+                                  ofx_tensor_desc* out);
+/* Runs the registered kernel for (op "spmm_csr", out->device's device type, dtype) on
+ * `stream` with a caller-provided tmp buffer (size: ofx_functional_spmm_csr_tmp_size).     */
+int ofx_functional_spmm_csr_tmp_size(const ofx_tensor_desc* row_ptr,
+                                     const ofx_tensor_desc* col_idx,
+                                     const ofx_tensor_desc* values, int64_t a_num_rows,
+                                     int64_t a_num_cols, const ofx_tensor_desc* b,
+                                     size_t* bytes);
+int ofx_functional_spmm_csr(void* stream, const ofx_tensor_desc* row_ptr,
+                            const ofx_tensor_desc* col_idx, const ofx_tensor_desc* values,
+                            int64_t a_num_rows, int64_t a_num_cols, const ofx_tensor_desc* b,
+                            ofx_tensor_desc* out, void* tmp, size_t tmp_bytes);
+/* Global (multi-rank) form: the kernel's OpKernelCache derives this rank's row range from
+ * (parallel_id, parallel_num) when out is split on axis 0 (out_split_axis 0; -1 = broadcast,
+ * 1 = column split); `out` is then the physical (local) slice.  num_threads: CPU kernel only. */
+int ofx_functional_spmm_csr_ex(void* stream, const ofx_tensor_desc* row_ptr,
+                               const ofx_tensor_desc* col_idx, const ofx_tensor_desc* values,
+                               int64_t a_num_rows, int64_t a_num_cols, const ofx_tensor_desc* b,
+                               ofx_tensor_desc* out, void* tmp, size_t tmp_bytes,
+                               int64_t parallel_id, int64_t parallel_num, int out_split_axis,
+                               int num_threads);
+/* The op's registered SBP signatures and no-grad inputs, as text (tests / introspection). */
+int ofx_op_spmm_csr_sbp_signatures(char* buf, size_t len);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OFX_SPMM_H_ */

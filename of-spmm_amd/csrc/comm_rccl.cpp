@@ -1,0 +1,74 @@
+// comm_rccl.cpp — RCCL all-gather of the dense matrix for the row-split operator.
+//
+// Replaces ccl::AllGather (oneflow/user/kernels/collective_communication/include/all_gather.h:24-38)
+// and its CUDA implementation CudaAllGather::Launch -> ncclAllGather
+// (oneflow/user/kernels/collective_communication/cuda/cuda_all_gather.cpp:25-47), plus the comm
+// bootstrap of EagerNcclCommMgr::CreateNcclComm (oneflow/core/job/eager_nccl_comm_manager.cpp:57-80):
+// rank 0 creates the unique id; the caller moves its 128 bytes to the other ranks (the reference
+// uses its gRPC ctrl KV; we use the torch.distributed store) and every rank calls init.
+// dtype map as oneflow/core/device/nccl_util.h:37-60.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+
+#include "ofx_internal.h"
+
+#define OFX_NCCL_CHECK(expr)                                                                   \
+  do {                                                                                         \
+    ncclResult_t ofx_r_ = (expr);                                                              \
+    if (ofx_r_ != ncclSuccess)                                                                 \
+      return ::ofx::fail(OFX_ECOMM, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(ofx_r_), \
+                         __FILE__, __LINE__);                                                  \
+  } while (0)
+
+static_assert(sizeof(ncclUniqueId) <= OFX_UNIQUE_ID_BYTES, "unique id does not fit");
+
+namespace {
+bool nccl_dtype(int dt, ncclDataType_t* out) {
+  switch (dt) {
+    case OFX_DT_FLOAT: *out = ncclFloat32; return true;
+    case OFX_DT_DOUBLE: *out = ncclFloat64; return true;
+    case OFX_DT_INT32: *out = ncclInt32; return true;
+    case OFX_DT_INT64: *out = ncclInt64; return true;
+    case OFX_DT_FLOAT16: *out = ncclFloat16; return true;
+    case OFX_DT_BFLOAT16: *out = ncclBfloat16; return true;
+    default: return false;
+  }
+}
+}  // namespace
+
+extern "C" int ofx_comm_get_unique_id(void* uid_out) {
+  OFX_REQUIRE(uid_out, OFX_EINVAL, "comm_get_unique_id: NULL");
+  ncclUniqueId id;
+  OFX_NCCL_CHECK(ncclGetUniqueId(&id));
+  std::memset(uid_out, 0, OFX_UNIQUE_ID_BYTES);
+  std::memcpy(uid_out, &id, sizeof(id));
+  return OFX_OK;
+}
+
+extern "C" int ofx_comm_init_rank(void** comm, int nranks, const void* uid, int rank) {
+  OFX_REQUIRE(comm && uid && nranks > 0 && rank >= 0 && rank < nranks, OFX_EINVAL,
+              "comm_init_rank: bad arguments (nranks=%d rank=%d)", nranks, rank);
+  ncclUniqueId id;
+  std::memcpy(&id, uid, sizeof(id));
+  ncclComm_t c;
+  OFX_NCCL_CHECK(ncclCommInitRank(&c, nranks, id, rank));
+  *comm = c;
+  return OFX_OK;
+}
+
+extern "C" int ofx_comm_destroy(void* comm) {
+  if (comm) OFX_NCCL_CHECK(ncclCommDestroy(static_cast<ncclComm_t>(comm)));
+  return OFX_OK;
+}
+
+extern "C" int ofx_allgather(void* stream, const void* in, void* out, size_t count, int dtype,
+                             void* comm) {
+  ncclDataType_t t;
+  OFX_REQUIRE(nccl_dtype(dtype, &t), OFX_EUNSUPPORTED, "allgather: unsupported dtype %d", dtype);
+  OFX_REQUIRE(comm && (count == 0 || (in && out)), OFX_EINVAL, "allgather: NULL argument");
+  OFX_NCCL_CHECK(ncclAllGather(in, out, count, t, static_cast<ncclComm_t>(comm),
+                               static_cast<hipStream_t>(stream)));
+  return OFX_OK;
+}

@@ -1,0 +1,116 @@
+// device_shim.cpp — the ep device layer reduced to a thin C-ABI over the HIP runtime.
+//
+// Replaces, for this op only: ep::Device (oneflow/core/ep/include/device.h:33-62; 512-B
+// alignment requirement device.h:29), ep::Stream / CudaStream (stream.h:30-49,
+// oneflow/core/ep/cuda/cuda_stream.cpp:90-142), ep::Event (event.h:26-34),
+// primitive::Memcpy (memcpy.h:33-39) and primitive::Memset (memset.h:26-32).
+// There is no device-manager registry: one process drives one GPU.
+#include <hip/hip_runtime.h>
+
+#include "ofx_internal.h"
+
+extern "C" int ofx_device_count(int* count) {
+  OFX_REQUIRE(count, OFX_EINVAL, "device_count: NULL");
+  OFX_HIP_CHECK(hipGetDeviceCount(count));
+  return OFX_OK;
+}
+extern "C" int ofx_set_device(int device) {
+  OFX_HIP_CHECK(hipSetDevice(device));
+  return OFX_OK;
+}
+extern "C" int ofx_get_device(int* device) {
+  OFX_REQUIRE(device, OFX_EINVAL, "get_device: NULL");
+  OFX_HIP_CHECK(hipGetDevice(device));
+  return OFX_OK;
+}
+extern "C" int ofx_device_synchronize(void) {
+  OFX_HIP_CHECK(hipDeviceSynchronize());
+  return OFX_OK;
+}
+extern "C" int ofx_malloc(void** ptr, size_t bytes) {
+  OFX_REQUIRE(ptr, OFX_EINVAL, "malloc: NULL");
+  *ptr = nullptr;
+  if (bytes == 0) return OFX_OK;
+  hipError_t e = hipMalloc(ptr, (bytes + 511) / 512 * 512);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return ofx::fail(OFX_ENOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+  }
+  return OFX_OK;
+}
+extern "C" int ofx_free(void* ptr) {
+  if (ptr) OFX_HIP_CHECK(hipFree(ptr));
+  return OFX_OK;
+}
+extern "C" int ofx_host_malloc(void** ptr, size_t bytes) {
+  OFX_REQUIRE(ptr, OFX_EINVAL, "host_malloc: NULL");
+  OFX_HIP_CHECK(hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault));
+  return OFX_OK;
+}
+extern "C" int ofx_host_free(void* ptr) {
+  if (ptr) OFX_HIP_CHECK(hipHostFree(ptr));
+  return OFX_OK;
+}
+extern "C" int ofx_stream_create(void** stream) {
+  OFX_REQUIRE(stream, OFX_EINVAL, "stream_create: NULL");
+  hipStream_t s;
+  OFX_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  *stream = s;
+  return OFX_OK;
+}
+extern "C" int ofx_stream_destroy(void* stream) {
+  if (stream) OFX_HIP_CHECK(hipStreamDestroy(static_cast<hipStream_t>(stream)));
+  return OFX_OK;
+}
+extern "C" int ofx_stream_sync(void* stream) {
+  OFX_HIP_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+  return OFX_OK;
+}
+extern "C" int ofx_memcpy_async(void* stream, void* dst, const void* src, size_t bytes, int kind) {
+  if (bytes == 0) return OFX_OK;
+  hipMemcpyKind k;
+  switch (kind) {
+    case OFX_MEMCPY_H2D: k = hipMemcpyHostToDevice; break;
+    case OFX_MEMCPY_D2H: k = hipMemcpyDeviceToHost; break;
+    case OFX_MEMCPY_D2D: k = hipMemcpyDeviceToDevice; break;
+    case OFX_MEMCPY_DEFAULT: k = hipMemcpyDefault; break;
+    default: return ofx::fail(OFX_EINVAL, "memcpy_async: bad kind %d", kind);
+  }
+  OFX_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, k, static_cast<hipStream_t>(stream)));
+  return OFX_OK;
+}
+extern "C" int ofx_memset_async(void* stream, void* dst, int value, size_t bytes) {
+  if (bytes == 0) return OFX_OK;
+  OFX_HIP_CHECK(hipMemsetAsync(dst, value, bytes, static_cast<hipStream_t>(stream)));
+  return OFX_OK;
+}
+extern "C" int ofx_event_create(void** event, int timing) {
+  OFX_REQUIRE(event, OFX_EINVAL, "event_create: NULL");
+  hipEvent_t e;
+  OFX_HIP_CHECK(hipEventCreateWithFlags(&e, timing ? hipEventDefault : hipEventDisableTiming));
+  *event = e;
+  return OFX_OK;
+}
+extern "C" int ofx_event_destroy(void* event) {
+  if (event) OFX_HIP_CHECK(hipEventDestroy(static_cast<hipEvent_t>(event)));
+  return OFX_OK;
+}
+extern "C" int ofx_event_record(void* event, void* stream) {
+  OFX_HIP_CHECK(hipEventRecord(static_cast<hipEvent_t>(event), static_cast<hipStream_t>(stream)));
+  return OFX_OK;
+}
+extern "C" int ofx_event_sync(void* event) {
+  OFX_HIP_CHECK(hipEventSynchronize(static_cast<hipEvent_t>(event)));
+  return OFX_OK;
+}
+extern "C" int ofx_event_elapsed_ms(void* start, void* end, float* ms) {
+  OFX_REQUIRE(ms, OFX_EINVAL, "event_elapsed_ms: NULL");
+  OFX_HIP_CHECK(hipEventElapsedTime(ms, static_cast<hipEvent_t>(start),
+                                    static_cast<hipEvent_t>(end)));
+  return OFX_OK;
+}
+extern "C" int ofx_stream_wait_event(void* stream, void* event) {
+  OFX_HIP_CHECK(hipStreamWaitEvent(static_cast<hipStream_t>(stream),
+                                   static_cast<hipEvent_t>(event), 0));
+  return OFX_OK;
+}

@@ -1,0 +1,150 @@
+// spmm_common.h — numeric contract shared by the HIP kernels (spmm_csr.hip) and the CPU kernel
+// (spmm_cpu.cpp): storage types, conversions, schedule (split) resolution, counter-based RNG.
+//
+// The accumulation contract restates the reference composition gather -> multiply ->
+// unsorted_segment_sum (oneflow/user/kernels/gather_kernel_util.cpp:72-92,
+// oneflow/user/kernels/unsorted_segment_sum_kernel_util.cpp:29-45: `out` zero-filled, then
+// `to = to + from` per index in ascending order, i.e. one multiply rounding then one add
+// rounding per nonzero; half/bf16 accumulate in fp32 as in
+// oneflow/user/kernels/unsorted_segment_sum_kernel.cpp:146-205).
+#ifndef OFX_SPMM_COMMON_H_
+#define OFX_SPMM_COMMON_H_
+
+#include <stdint.h>
+#include <string.h>
+
+#include "ofx_spmm.h"
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define OFX_HD __host__ __device__ __forceinline__
+#else
+#define OFX_HD static inline
+#endif
+
+namespace ofx {
+
+// 16-bit storage types (bit containers; arithmetic always happens in fp32).
+struct bf16 {
+  uint16_t x;
+};
+struct f16 {
+  uint16_t x;
+};
+
+OFX_HD float bits_to_f32(uint32_t u) { return __builtin_bit_cast(float, u); }
+OFX_HD uint32_t f32_to_bits(float f) { return __builtin_bit_cast(uint32_t, f); }
+
+OFX_HD float bf16_to_f32(uint16_t h) { return bits_to_f32(uint32_t(h) << 16); }
+// Round-to-nearest-even; NaN stays NaN (quiet bit forced).
+OFX_HD uint16_t f32_to_bf16(float f) {
+  const uint32_t u = f32_to_bits(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return uint16_t((u >> 16) | 0x40u);
+  return uint16_t((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+OFX_HD float f16_to_f32(uint16_t h) { return float(__builtin_bit_cast(_Float16, h)); }
+OFX_HD uint16_t f32_to_f16(float f) { return __builtin_bit_cast(uint16_t, _Float16(f)); }
+
+// Accumulator type and load/store conversions per storage type.
+template <typename T>
+struct Num;
+template <>
+struct Num<float> {
+  using acc = float;
+  OFX_HD static float load(float v) { return v; }
+  OFX_HD static float store(float a) { return a; }
+};
+template <>
+struct Num<double> {
+  using acc = double;
+  OFX_HD static double load(double v) { return v; }
+  OFX_HD static double store(double a) { return a; }
+};
+template <>
+struct Num<bf16> {
+  using acc = float;
+  OFX_HD static float load(bf16 v) { return bf16_to_f32(v.x); }
+  OFX_HD static bf16 store(float a) { return bf16{f32_to_bf16(a)}; }
+};
+template <>
+struct Num<f16> {
+  using acc = float;
+  OFX_HD static float load(f16 v) { return f16_to_f32(v.x); }
+  OFX_HD static f16 store(float a) { return f16{f32_to_f16(a)}; }
+};
+
+OFX_HD int dtype_size(int dt) {
+  switch (dt) {
+    case OFX_DT_FLOAT: return 4;
+    case OFX_DT_DOUBLE: return 8;
+    case OFX_DT_INT32: return 4;
+    case OFX_DT_INT64: return 8;
+    case OFX_DT_FLOAT16: return 2;
+    case OFX_DT_BFLOAT16: return 2;
+    default: return 0;
+  }
+}
+OFX_HD bool is_index_dtype(int dt) { return dt == OFX_DT_INT32 || dt == OFX_DT_INT64; }
+OFX_HD bool is_value_dtype(int dt) {
+  return dt == OFX_DT_FLOAT || dt == OFX_DT_DOUBLE || dt == OFX_DT_FLOAT16 ||
+         dt == OFX_DT_BFLOAT16;
+}
+
+// ---- schedule ---------------------------------------------------------------------------
+// Default split threshold: rows with more than T nonzeros are cut into chunks of T, where
+// T = clamp(65536 / n, 128, 8192) rounded down to a power of two (T*n ~ 64K multiply-adds
+// per chunk).  This is a fixed function of n and part of the numeric contract.
+OFX_HD int64_t default_split(int64_t n) {
+  int64_t t = n > 0 ? (int64_t)65536 / n : 8192;
+  if (t < 128) t = 128;
+  if (t > 8192) t = 8192;
+  int64_t p = 128;
+  while (p * 2 <= t) p *= 2;
+  return p;
+}
+
+struct Schedule {
+  int64_t split;  // rows with len > split are chunked; INT64_MAX = never
+  int64_t chunk;  // chunk length (the last chunk of a row takes the remainder: [chunk, 2*chunk))
+  int32_t variant;
+};
+
+static inline Schedule resolve_schedule(int64_t n, const ofx_spmm_options* o) {
+  Schedule s;
+  s.variant = o ? o->variant : 0;
+  if (o && o->ordered) {
+    s.split = INT64_MAX;
+    s.chunk = INT64_MAX;
+    return s;
+  }
+  s.split = (o && o->split_threshold > 0) ? o->split_threshold : default_split(n);
+  s.chunk = (o && o->chunk > 0) ? o->chunk : s.split;
+  if (s.chunk > s.split) s.chunk = s.split;  // every split row then has >= 1 full chunk
+  return s;
+}
+
+// Number of chunks of a split row of length len (> split): floor(len / chunk) — the last
+// chunk absorbs the remainder, so chunk k covers [k*chunk, (k+1)*chunk) for k < nc-1 and
+// [(nc-1)*chunk, len) for the last one.
+OFX_HD int64_t num_chunks(int64_t len, int64_t chunk) { return len / chunk; }
+
+// ---- counter-based RNG (synthetic inputs; identical on host and device) -----------------
+OFX_HD uint64_t splitmix64(uint64_t x) {
+  x += 0x9e3779b97f4a7c15ull;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+OFX_HD uint64_t hash2(uint64_t seed, uint64_t i) { return splitmix64(splitmix64(seed) ^ i); }
+// U[-1, 1) with 24 random bits: exactly representable in fp32.
+OFX_HD float u_pm1(uint64_t h) { return float((int64_t)(h >> 40) - (1 << 23)) * (1.0f / (1 << 23)); }
+// exact-mode draws: values in {-2,-1,1,2}, dense in integers [-8, 8].
+OFX_HD float exact_val(uint64_t h) {
+  const float t[4] = {-2.f, -1.f, 1.f, 2.f};
+  return t[(h >> 33) & 3];
+}
+OFX_HD float exact_dense(uint64_t h) { return float((int)((h >> 33) % 17) - 8); }
+
+}  // namespace ofx
+
+#endif  // OFX_SPMM_COMMON_H_

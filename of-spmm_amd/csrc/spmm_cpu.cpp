@@ -1,0 +1,156 @@
+// spmm_cpu.cpp — the DeviceType::kCPU kernel of op "spmm_csr" (SURVEY.md §8 row a2).
+//
+// Row-parallel over OpenMP in the idiom of CpuStream::ParallelFor
+// (oneflow/core/ep/cpu/cpu_stream.h:104-145): rows are independent, each row is reduced by
+// one thread in the contract order of spmm_common.h (gather -> multiply -> segment-sum,
+// oneflow/user/kernels/gather_kernel_util.cpp:72-92 + unsorted_segment_sum_kernel_util.cpp:29-45),
+// including the same hub-row chunking as the HIP kernel, so CPU and GPU produce identical bits.
+// Thread count: OMP_NUM_THREADS like oneflow/core/job/env_global_objects_scope.cpp:90-99.
+#pragma clang fp contract(off)
+
+#include <omp.h>
+
+#include <climits>
+#include <vector>
+
+#include "ofx_internal.h"
+#include "spmm_common.h"
+
+namespace ofx {
+namespace {
+
+template <typename T, typename I>
+void row_sum(const I* col, const T* val, const T* B, int64_t ldb, int64_t n, int64_t j0,
+             int64_t j1, typename Num<T>::acc* acc) {
+#pragma clang fp contract(off)
+  using A = typename Num<T>::acc;
+  for (int64_t c = 0; c < n; ++c) acc[c] = A(0);
+  for (int64_t j = j0; j < j1; ++j) {
+    const A v = Num<T>::load(val[j]);
+    const T* brow = B + (int64_t)col[j] * ldb;
+    for (int64_t c = 0; c < n; ++c) acc[c] = acc[c] + v * Num<T>::load(brow[c]);
+  }
+}
+
+template <typename T, typename I>
+int cpu_spmm(int nthreads, int64_t n, const I* rp, const I* col, const T* val, const T* B,
+             int64_t ldb, T* C, int64_t ldc, int64_t row_begin, int64_t row_end,
+             const Schedule& s) {
+#pragma clang fp contract(off)
+  using A = typename Num<T>::acc;
+  const int64_t rows = row_end - row_begin;
+#pragma omp parallel num_threads(nthreads)
+  {
+    std::vector<A> acc(n), part(n);
+#pragma omp for schedule(dynamic, 64)
+    for (int64_t g = 0; g < rows; ++g) {
+      const int64_t r = row_begin + g;
+      const int64_t j0 = (int64_t)rp[r], j1 = (int64_t)rp[r + 1];
+      const int64_t len = j1 - j0;
+      if (len <= s.split) {
+        row_sum<T, I>(col, val, B, ldb, n, j0, j1, acc.data());
+      } else {
+        const int64_t nc = num_chunks(len, s.chunk);
+        for (int64_t c = 0; c < n; ++c) acc[c] = A(0);
+        for (int64_t k = 0; k < nc; ++k) {
+          const int64_t a = j0 + k * s.chunk;
+          const int64_t b = (k == nc - 1) ? j1 : a + s.chunk;
+          row_sum<T, I>(col, val, B, ldb, n, a, b, part.data());
+          for (int64_t c = 0; c < n; ++c) acc[c] = acc[c] + part[c];
+        }
+      }
+      T* out = C + g * ldc;
+      for (int64_t c = 0; c < n; ++c) out[c] = Num<T>::store(acc[c]);
+    }
+  }
+  return OFX_OK;
+}
+
+template <typename I>
+int cpu_dispatch(int nthreads, int val_dtype, int64_t n, const void* rp, const void* col,
+                 const void* val, const void* b, int64_t ldb, void* c, int64_t ldc,
+                 int64_t row_begin, int64_t row_end, const Schedule& s) {
+  const I* r = static_cast<const I*>(rp);
+  const I* ci = static_cast<const I*>(col);
+  switch (val_dtype) {
+    case OFX_DT_FLOAT:
+      return cpu_spmm<float, I>(nthreads, n, r, ci, (const float*)val, (const float*)b, ldb,
+                                (float*)c, ldc, row_begin, row_end, s);
+    case OFX_DT_DOUBLE:
+      return cpu_spmm<double, I>(nthreads, n, r, ci, (const double*)val, (const double*)b, ldb,
+                                 (double*)c, ldc, row_begin, row_end, s);
+    case OFX_DT_BFLOAT16:
+      return cpu_spmm<bf16, I>(nthreads, n, r, ci, (const bf16*)val, (const bf16*)b, ldb,
+                               (bf16*)c, ldc, row_begin, row_end, s);
+    case OFX_DT_FLOAT16:
+      return cpu_spmm<f16, I>(nthreads, n, r, ci, (const f16*)val, (const f16*)b, ldb, (f16*)c,
+                              ldc, row_begin, row_end, s);
+    default: return fail(OFX_EUNSUPPORTED, "spmm_csr_cpu: unsupported value dtype %d", val_dtype);
+  }
+}
+
+}  // namespace
+}  // namespace ofx
+
+using namespace ofx;
+
+extern "C" int ofx_spmm_csr_cpu(int num_threads, int idx_dtype, int val_dtype, int64_t m,
+                                int64_t k, int64_t n, int64_t nnz, const void* row_ptr,
+                                const void* col_idx, const void* values, const void* b,
+                                int64_t ldb, void* c, int64_t ldc, int64_t row_begin,
+                                int64_t row_end, const ofx_spmm_options* opts) {
+  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED,
+              "spmm_csr_cpu: index dtype %d is not int32/int64", idx_dtype);
+  OFX_REQUIRE(is_value_dtype(val_dtype), OFX_EUNSUPPORTED,
+              "spmm_csr_cpu: unsupported value dtype %d", val_dtype);
+  OFX_REQUIRE(m >= 0 && k >= 0 && n >= 0 && nnz >= 0, OFX_EINVAL, "spmm_csr_cpu: negative size");
+  OFX_REQUIRE(0 <= row_begin && row_begin <= row_end && row_end <= m, OFX_EINVAL,
+              "spmm_csr_cpu: row range [%lld, %lld) outside [0, %lld)", (long long)row_begin,
+              (long long)row_end, (long long)m);
+  OFX_REQUIRE(ldb >= n && ldc >= n, OFX_EINVAL, "spmm_csr_cpu: ldb/ldc < n");
+  if (row_end == row_begin || n == 0) return OFX_OK;
+  OFX_REQUIRE(row_ptr && c && (nnz == 0 || (col_idx && values && b)), OFX_EINVAL,
+              "spmm_csr_cpu: NULL pointer");
+  const int nt = num_threads > 0 ? num_threads : omp_get_max_threads();
+  const Schedule s = resolve_schedule(n, opts);
+  if (idx_dtype == OFX_DT_INT32)
+    return cpu_dispatch<int32_t>(nt, val_dtype, n, row_ptr, col_idx, values, b, ldb, c, ldc,
+                                 row_begin, row_end, s);
+  return cpu_dispatch<int64_t>(nt, val_dtype, n, row_ptr, col_idx, values, b, ldb, c, ldc,
+                               row_begin, row_end, s);
+}
+
+// ---- BalancedSplitter (oneflow/core/common/balanced_splitter.cpp:20-40) -------------------
+extern "C" int ofx_balanced_range(int64_t total, int64_t parts, int64_t idx, int64_t* begin,
+                                  int64_t* end) {
+  OFX_REQUIRE(total >= 0 && parts > 0 && idx >= 0 && idx < parts && begin && end, OFX_EINVAL,
+              "balanced_range: bad arguments (total=%lld parts=%lld idx=%lld)", (long long)total,
+              (long long)parts, (long long)idx);
+  const int64_t base = total / parts, extra = total % parts;
+  // The first `extra` parts hold base+1 elements.
+  const int64_t lo = idx < extra ? idx * (base + 1) : extra * (base + 1) + (idx - extra) * base;
+  *begin = lo;
+  *end = lo + base + (idx < extra ? 1 : 0);
+  return OFX_OK;
+}
+
+extern "C" int ofx_csr_row_slice_host(int idx_dtype, const void* row_ptr, int64_t row_begin,
+                                      int64_t row_end, void* out_row_ptr, int64_t* nnz_begin,
+                                      int64_t* nnz_end) {
+  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "csr_row_slice_host: bad dtype");
+  OFX_REQUIRE(row_ptr && 0 <= row_begin && row_begin <= row_end, OFX_EINVAL,
+              "csr_row_slice_host: bad arguments");
+  auto run = [&](auto* rp, auto* out) {
+    const int64_t base = (int64_t)rp[row_begin];
+    if (out)
+      for (int64_t i = 0; i <= row_end - row_begin; ++i)
+        out[i] = (std::remove_pointer_t<decltype(out)>)((int64_t)rp[row_begin + i] - base);
+    if (nnz_begin) *nnz_begin = base;
+    if (nnz_end) *nnz_end = (int64_t)rp[row_end];
+  };
+  if (idx_dtype == OFX_DT_INT32)
+    run(static_cast<const int32_t*>(row_ptr), static_cast<int32_t*>(out_row_ptr));
+  else
+    run(static_cast<const int64_t*>(row_ptr), static_cast<int64_t*>(out_row_ptr));
+  return OFX_OK;
+}

@@ -1,0 +1,578 @@
+// spmm_csr.hip — CSR x dense SpMM for CDNA4 (gfx950), the hot path behind op "spmm_csr".
+//
+// Reference semantics (OneFlow has no SpMM): the composition
+//   gather rows B[col[j]]      oneflow/user/kernels/gather_kernel_util.cpp:72-92
+//   multiply by val[j]
+//   unsorted_segment_sum       oneflow/user/kernels/unsorted_segment_sum_kernel_util.cpp:29-45
+// without materialising the nnz x N intermediate and without the CUDA path's atomics
+// (unsorted_segment_sum_kernel_util.cu:67), which are non-deterministic.  Width dispatch and
+// 64-bit addressing follow the intent of gather_kernel_util.cu:29-107.
+//
+// Layout on the device: row_ptr I[m+1], col_idx I[nnz], values T[nnz],
+// B T[k][ldb] row-major, C T[rows][ldc] row-major.
+//
+// Kernels:
+//   spmm_plan    one thread per row: appends split ("hub") rows and their chunks to lists in
+//                the workspace (slot order is arbitrary; results do not depend on it).
+//   spmm_main    the dominant launch.  Lane-groups of LPR lanes; each lane owns VEC consecutive
+//                columns (16-B loads of B rows); col/val are loaded cooperatively (LPR < 64:
+//                coalesced, broadcast by ds_bpermute) or as wave-uniform scalar loads (LPR == 64);
+//                kUnroll B-row loads are in flight per lane before the in-order multiply-adds.
+//                Blocks [0, chunk_blocks) grid-stride over hub-row chunks -> fp32/fp64 partial
+//                rows in the workspace; the remaining blocks take one ordinary row per group.
+//   spmm_reduce  per hub row: sums its chunk partials in chunk order -> C row.
+// Every output element is produced by exactly one lane in a fixed order: results are
+// bitwise deterministic and equal to the CPU kernel / oracle with the same schedule.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+
+#include "ofx_internal.h"
+#include "spmm_common.h"
+
+namespace ofx {
+namespace {
+
+constexpr int kBlock = 256;        // 4 waves
+constexpr int kWavesPerBlock = kBlock / 64;
+constexpr int kUnroll = 8;         // B-row loads in flight per lane
+constexpr int64_t kMaxChunkBlocks = 1024;  // blocks that grid-stride over hub-row chunks
+constexpr int64_t kMaxReduceBlocks = 2048;
+
+template <typename T, int VEC>
+struct alignas(sizeof(T) * VEC) Pack {
+  T v[VEC];
+};
+
+template <typename A, int VEC>
+struct alignas(sizeof(A) * VEC > 16 ? 16 : sizeof(A) * VEC) AccPack {
+  A v[VEC];
+};
+
+__device__ __forceinline__ int32_t shfl(int32_t v, int src) { return __shfl(v, src); }
+__device__ __forceinline__ int64_t shfl(int64_t v, int src) {
+  return (int64_t)__shfl((long long)v, src);
+}
+__device__ __forceinline__ float shfl(float v, int src) { return __shfl(v, src); }
+__device__ __forceinline__ double shfl(double v, int src) { return __shfl(v, src); }
+
+__device__ __forceinline__ int64_t uniform64(int64_t v) {
+  const uint64_t u = (uint64_t)v;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// acc[e] += val[j] * B[col[j], cc + e] for j in [j0, j1), in ascending j, mul then add.
+// Bc = B + cc.  All lanes of a group call this with the same j0/j1.
+template <typename T, typename I, int VEC, int LPR>
+__device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* __restrict__ val,
+                                           const T* __restrict__ Bc, int64_t ldb, int64_t j0,
+                                           int64_t j1, int gl, int gbase, bool active,
+                                           typename Num<T>::acc (&acc)[VEC]) {
+#pragma clang fp contract(off)
+  using A = typename Num<T>::acc;
+  using P = Pack<T, VEC>;
+  if constexpr (LPR == 64) {
+    // j0/j1 are wave-uniform: col/val come through the scalar cache.
+    for (int64_t j = j0; j < j1; j += kUnroll) {
+      const int cnt = (int)((j1 - j) < kUnroll ? (j1 - j) : kUnroll);
+      P bv[kUnroll];
+      A vv[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        if (u < cnt) {
+          const int64_t cu = (int64_t)col[j + u];
+          vv[u] = Num<T>::load(val[j + u]);
+          if (active) bv[u] = *reinterpret_cast<const P*>(Bc + cu * ldb);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        if (u < cnt && active) {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + vv[u] * Num<T>::load(bv[u].v[e]);
+        }
+      }
+    }
+  } else {
+    for (int64_t jb = j0; jb < j1; jb += LPR) {
+      const int cnt = (int)((j1 - jb) < LPR ? (j1 - jb) : LPR);
+      I myc = 0;
+      A myv = 0;
+      if (gl < cnt) {
+        myc = col[jb + gl];
+        myv = Num<T>::load(val[jb + gl]);
+      }
+      for (int k = 0; k < cnt; k += kUnroll) {
+        P bv[kUnroll];
+        A vv[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+          const int src = gbase + ((k + u) & (LPR - 1));
+          const int64_t cu = (int64_t)shfl(myc, src);
+          vv[u] = shfl(myv, src);
+          if (k + u < cnt && active) bv[u] = *reinterpret_cast<const P*>(Bc + cu * ldb);
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+          if (k + u < cnt && active) {
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + vv[u] * Num<T>::load(bv[u].v[e]);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <typename T, int VEC>
+__device__ __forceinline__ void store_row(T* __restrict__ p, const typename Num<T>::acc (&acc)[VEC]) {
+  Pack<T, VEC> o;
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) o.v[e] = Num<T>::store(acc[e]);
+  *reinterpret_cast<Pack<T, VEC>*>(p) = o;
+}
+
+template <typename A, int VEC>
+__device__ __forceinline__ void store_partial(A* __restrict__ p, const A (&acc)[VEC]) {
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) p[e] = acc[e];
+}
+
+// ---- hub-row planning ----------------------------------------------------------------------
+// counters[0] = chunk items appended, counters[1] = hub rows appended.
+// hubs[3i..3i+2] = {local row, first item slot, number of chunks}; items[2s..2s+1] = {local row, chunk}.
+template <typename I>
+__global__ void __launch_bounds__(kBlock)
+    spmm_plan_kernel(const I* __restrict__ rp, int64_t row_begin, int64_t nrows, int64_t split,
+                     int64_t chunk, unsigned long long* counters, int64_t* hubs, int64_t* items) {
+  const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (g >= nrows) return;
+  const int64_t len = (int64_t)rp[row_begin + g + 1] - (int64_t)rp[row_begin + g];
+  if (len <= split) return;
+  const int64_t nc = num_chunks(len, chunk);
+  const int64_t slot = (int64_t)atomicAdd(&counters[0], (unsigned long long)nc);
+  const int64_t hi = (int64_t)atomicAdd(&counters[1], 1ull);
+  hubs[3 * hi + 0] = g;
+  hubs[3 * hi + 1] = slot;
+  hubs[3 * hi + 2] = nc;
+  for (int64_t c = 0; c < nc; ++c) {
+    items[2 * (slot + c) + 0] = g;
+    items[2 * (slot + c) + 1] = c;
+  }
+}
+
+// ---- main kernel: hub-row chunks (first `chunk_blocks` blocks) + ordinary rows ---------------
+template <typename T, typename I, int VEC, int LPR>
+__global__ void __launch_bounds__(kBlock)
+    spmm_main_kernel(const I* __restrict__ rp, const I* __restrict__ col,
+                     const T* __restrict__ val, const T* __restrict__ B, int64_t ldb,
+                     T* __restrict__ C, int64_t ldc, int64_t row_begin, int64_t nrows, int64_t n,
+                     int64_t split, int64_t chunk, int64_t chunk_blocks,
+                     const unsigned long long* __restrict__ counters,
+                     const int64_t* __restrict__ items, typename Num<T>::acc* __restrict__ part) {
+  using A = typename Num<T>::acc;
+  constexpr int GPW = 64 / LPR;
+  constexpr int GPB = kWavesPerBlock * GPW;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int gl = lane & (LPR - 1);
+  const int gbase = lane & ~(LPR - 1);
+  const int gsub = LPR == 64 ? 0 : lane / LPR;
+  if ((int64_t)blockIdx.x < chunk_blocks) {
+    // Hub-row chunks: grid-stride over the planned items -> fp32/fp64 partial rows.
+    const int64_t nitems = (int64_t)counters[0];
+    const int64_t stride = chunk_blocks * GPB;
+    for (int64_t s = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * GPW + gsub; s < nitems;
+         s += stride) {
+      int64_t lr = items[2 * s + 0];
+      int64_t c = items[2 * s + 1];
+      if constexpr (LPR == 64) {
+        lr = uniform64(lr);
+        c = uniform64(c);
+      }
+      const int64_t rs = (int64_t)rp[row_begin + lr];
+      const int64_t re = (int64_t)rp[row_begin + lr + 1];
+      const int64_t nc = num_chunks(re - rs, chunk);
+      const int64_t j0 = rs + c * chunk;
+      const int64_t j1 = (c == nc - 1) ? re : j0 + chunk;
+      for (int64_t c0 = 0; c0 < n; c0 += (int64_t)LPR * VEC) {
+        const int64_t cc = c0 + (int64_t)gl * VEC;
+        const bool active = cc < n;
+        A acc[VEC];
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[e] = A(0);
+        accumulate<T, I, VEC, LPR>(col, val, B + cc, ldb, j0, j1, gl, gbase, active, acc);
+        if (active) store_partial<A, VEC>(part + s * n + cc, acc);
+      }
+    }
+    return;
+  }
+  // Ordinary rows: one lane-group per row.
+  const int64_t g = (((int64_t)blockIdx.x - chunk_blocks) * kWavesPerBlock + wave) * GPW + gsub;
+  if (g >= nrows) return;
+  const int64_t r = row_begin + g;
+  int64_t j0 = (int64_t)rp[r];
+  int64_t j1 = (int64_t)rp[r + 1];
+  if constexpr (LPR == 64) {
+    j0 = uniform64(j0);
+    j1 = uniform64(j1);
+  }
+  if (j1 - j0 > split) return;  // hub row: chunk blocks + spmm_reduce own it
+  for (int64_t c0 = 0; c0 < n; c0 += (int64_t)LPR * VEC) {
+    const int64_t cc = c0 + (int64_t)gl * VEC;
+    const bool active = cc < n;
+    A acc[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc[e] = A(0);
+    accumulate<T, I, VEC, LPR>(col, val, B + cc, ldb, j0, j1, gl, gbase, active, acc);
+    if (active) store_row<T, VEC>(C + g * ldc + cc, acc);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock)
+    spmm_reduce_kernel(const unsigned long long* __restrict__ counters,
+                       const int64_t* __restrict__ hubs,
+                       const typename Num<T>::acc* __restrict__ part, T* __restrict__ C,
+                       int64_t ldc, int64_t n) {
+#pragma clang fp contract(off)
+  using A = typename Num<T>::acc;
+  const int64_t nhubs = (int64_t)counters[1];
+  for (int64_t h = blockIdx.x; h < nhubs; h += gridDim.x) {
+    const int64_t lr = hubs[3 * h + 0];
+    const int64_t slot = hubs[3 * h + 1];
+    const int64_t nc = hubs[3 * h + 2];
+    for (int64_t c = threadIdx.x; c < n; c += kBlock) {
+      A acc = A(0);
+      for (int64_t k = 0; k < nc; ++k) acc = acc + part[(slot + k) * n + c];
+      C[lr * ldc + c] = Num<T>::store(acc);
+    }
+  }
+}
+
+// ---- validation / slicing / synthetic dense ------------------------------------------------
+template <typename I>
+__global__ void csr_validate_kernel(const I* __restrict__ rp, const I* __restrict__ col,
+                                    int64_t m, int64_t k, int64_t nnz, unsigned int* flag) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t i = t0; i <= m; i += stride) {
+    const int64_t v = (int64_t)rp[i];
+    bool bad = (i == 0 && v != 0) || (i == m && v != nnz) || v < 0 || v > nnz;
+    if (!bad && i < m) bad = (int64_t)rp[i + 1] < v;
+    if (bad) atomicMax(flag, 1u);
+  }
+  for (int64_t j = t0; j < nnz; j += stride) {
+    const int64_t c = (int64_t)col[j];
+    if (c < 0 || c >= k) atomicMax(flag, 2u);
+  }
+}
+
+template <typename I>
+__global__ void csr_row_slice_kernel(const I* __restrict__ rp, int64_t row_begin, int64_t rows,
+                                     I* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i <= rows) out[i] = (I)((int64_t)rp[row_begin + i] - (int64_t)rp[row_begin]);
+}
+
+template <typename T>
+__global__ void synth_dense_kernel(int64_t r_begin, int64_t rows, int64_t n, int64_t ld,
+                                   uint64_t seed, int exact, T* __restrict__ out) {
+  const int64_t total = rows * n;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int64_t rr = i / n, cc = i - rr * n;
+    const uint64_t h = hash2(seed, (uint64_t)((r_begin + rr) * n + cc));
+    const float f = exact ? exact_dense(h) : u_pm1(h);
+    out[rr * ld + cc] = Num<T>::store((typename Num<T>::acc)f);
+  }
+}
+
+// ---- host-side dispatch ---------------------------------------------------------------------
+struct Launch {
+  hipStream_t stream;
+  const void *rp, *col, *val, *b;
+  void* c;
+  int64_t ldb, ldc, row_begin, nrows, n, nnz;
+  Schedule sched;
+  void* ws;
+  size_t ws_bytes;
+};
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct WsLayout {
+  size_t counters, hubs, items, part, total;
+  int64_t max_hubs, max_items;
+};
+
+WsLayout ws_layout(int64_t nnz, int64_t n, size_t acc_bytes, const Schedule& s) {
+  WsLayout w{};
+  if (s.split == INT64_MAX || nnz <= s.split) return w;  // no row can be split
+  w.max_hubs = nnz / (s.split + 1) + 1;
+  w.max_items = nnz / s.chunk + 1;
+  size_t off = 0;
+  w.counters = off;
+  off = align_up(off + 2 * sizeof(unsigned long long), 256);
+  w.hubs = off;
+  off = align_up(off + (size_t)w.max_hubs * 3 * sizeof(int64_t), 256);
+  w.items = off;
+  off = align_up(off + (size_t)w.max_items * 2 * sizeof(int64_t), 256);
+  w.part = off;
+  off = align_up(off + (size_t)w.max_items * (size_t)n * acc_bytes, 256);
+  w.total = off;
+  return w;
+}
+
+int pick_vec(int elem_bytes, const Launch& L, int forced_vec) {
+  const int maxvec = 16 / elem_bytes;
+  for (int v = maxvec; v >= 1; v /= 2) {
+    if (forced_vec && v != forced_vec) continue;
+    const size_t vb = (size_t)v * elem_bytes;
+    if (L.n % v == 0 && L.ldb % v == 0 && L.ldc % v == 0 &&
+        ((uintptr_t)L.b % vb) == 0 && ((uintptr_t)L.c % vb) == 0)
+      return v;
+  }
+  return 0;
+}
+
+int pick_lpr(int64_t n, int vec) {
+  const int64_t lanes = (n + vec - 1) / vec;
+  int l = 4;
+  while (l < 64 && l < lanes) l *= 2;
+  return l;
+}
+
+template <typename T, typename I, int VEC, int LPR>
+int launch_cfg(const Launch& L) {
+  using A = typename Num<T>::acc;
+  constexpr int GPW = 64 / LPR;
+  constexpr int64_t GPB = (int64_t)kWavesPerBlock * GPW;  // lane-groups per block
+  const I* rp = static_cast<const I*>(L.rp);
+  const I* col = static_cast<const I*>(L.col);
+  const T* val = static_cast<const T*>(L.val);
+  const T* B = static_cast<const T*>(L.b);
+  T* C = static_cast<T*>(L.c);
+  const WsLayout w = ws_layout(L.nnz, L.n, sizeof(A), L.sched);
+  const bool hubs = w.total > 0;
+  unsigned long long* counters = nullptr;
+  int64_t *hub = nullptr, *items = nullptr;
+  A* part = nullptr;
+  int64_t chunk_blocks = 0;
+  if (hubs) {
+    OFX_REQUIRE(L.ws != nullptr && L.ws_bytes >= w.total, OFX_EWORKSPACE,
+                "spmm_csr: workspace of %zu bytes is smaller than the %zu bytes required",
+                L.ws_bytes, w.total);
+    char* ws = static_cast<char*>(L.ws);
+    counters = reinterpret_cast<unsigned long long*>(ws + w.counters);
+    hub = reinterpret_cast<int64_t*>(ws + w.hubs);
+    items = reinterpret_cast<int64_t*>(ws + w.items);
+    part = reinterpret_cast<A*>(ws + w.part);
+    OFX_HIP_CHECK(hipMemsetAsync(counters, 0, 2 * sizeof(unsigned long long), L.stream));
+    const int64_t pgrid = (L.nrows + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL((spmm_plan_kernel<I>), dim3((unsigned)pgrid), dim3(kBlock), 0, L.stream, rp,
+                       L.row_begin, L.nrows, L.sched.split, L.sched.chunk, counters, hub, items);
+    OFX_HIP_CHECK(hipGetLastError());
+    chunk_blocks = (w.max_items + GPB - 1) / GPB;
+    if (chunk_blocks > kMaxChunkBlocks) chunk_blocks = kMaxChunkBlocks;
+  }
+  const int64_t grid = chunk_blocks + (L.nrows + GPB - 1) / GPB;
+  OFX_REQUIRE(grid < (int64_t)UINT32_MAX, OFX_EINVAL, "spmm_csr: too many rows (%lld)",
+              (long long)L.nrows);
+  hipLaunchKernelGGL((spmm_main_kernel<T, I, VEC, LPR>), dim3((unsigned)grid), dim3(kBlock), 0,
+                     L.stream, rp, col, val, B, L.ldb, C, L.ldc, L.row_begin, L.nrows, L.n,
+                     hubs ? L.sched.split : INT64_MAX, hubs ? L.sched.chunk : INT64_MAX,
+                     chunk_blocks, counters, items, part);
+  OFX_HIP_CHECK(hipGetLastError());
+  if (hubs) {
+    const int64_t rgrid = w.max_hubs < kMaxReduceBlocks ? w.max_hubs : kMaxReduceBlocks;
+    hipLaunchKernelGGL((spmm_reduce_kernel<T>), dim3((unsigned)rgrid), dim3(kBlock), 0, L.stream,
+                       counters, hub, part, C, L.ldc, L.n);
+    OFX_HIP_CHECK(hipGetLastError());
+  }
+  return OFX_OK;
+}
+
+template <typename T, typename I, int VEC>
+int launch_vec(const Launch& L, int lpr) {
+  switch (lpr) {
+    case 4: return launch_cfg<T, I, VEC, 4>(L);
+    case 8: return launch_cfg<T, I, VEC, 8>(L);
+    case 16: return launch_cfg<T, I, VEC, 16>(L);
+    case 32: return launch_cfg<T, I, VEC, 32>(L);
+    case 64: return launch_cfg<T, I, VEC, 64>(L);
+    default: return fail(OFX_EINVAL, "spmm_csr: unsupported lanes-per-row %d", lpr);
+  }
+}
+
+template <typename T, typename I>
+int launch_typed(const Launch& L) {
+  // variant = VEC * 100 + LPR forces a configuration (tuning / tests); 0 = auto.
+  const int forced_vec = L.sched.variant > 0 ? L.sched.variant / 100 : 0;
+  const int forced_lpr = L.sched.variant > 0 ? L.sched.variant % 100 : 0;
+  const int vec = pick_vec((int)sizeof(T), L, forced_vec);
+  OFX_REQUIRE(vec > 0, OFX_EINVAL,
+              "spmm_csr: variant %d not applicable (n=%lld ldb=%lld ldc=%lld or pointer alignment)",
+              L.sched.variant, (long long)L.n, (long long)L.ldb, (long long)L.ldc);
+  const int lpr = forced_lpr ? forced_lpr : pick_lpr(L.n, vec);
+  switch (vec) {
+    case 1: return launch_vec<T, I, 1>(L, lpr);
+    case 2: return launch_vec<T, I, 2>(L, lpr);
+    case 4:
+      if constexpr (sizeof(T) <= 4) return launch_vec<T, I, 4>(L, lpr);
+      break;
+    case 8:
+      if constexpr (sizeof(T) == 2) return launch_vec<T, I, 8>(L, lpr);
+      break;
+  }
+  return fail(OFX_EINVAL, "spmm_csr: unsupported vector width %d", vec);
+}
+
+template <typename I>
+int launch_idx(int val_dtype, const Launch& L) {
+  switch (val_dtype) {
+    case OFX_DT_FLOAT: return launch_typed<float, I>(L);
+    case OFX_DT_DOUBLE: return launch_typed<double, I>(L);
+    case OFX_DT_BFLOAT16: return launch_typed<bf16, I>(L);
+    case OFX_DT_FLOAT16: return launch_typed<f16, I>(L);
+    default: return fail(OFX_EUNSUPPORTED, "spmm_csr: unsupported value dtype %d", val_dtype);
+  }
+}
+
+size_t acc_bytes_of(int val_dtype) { return val_dtype == OFX_DT_DOUBLE ? 8 : 4; }
+
+int check_common(int idx_dtype, int val_dtype, int64_t m, int64_t k, int64_t n, int64_t nnz) {
+  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED,
+              "spmm_csr: index dtype %d is not int32/int64", idx_dtype);
+  OFX_REQUIRE(is_value_dtype(val_dtype), OFX_EUNSUPPORTED,
+              "spmm_csr: value dtype %d is not float/double/float16/bfloat16", val_dtype);
+  OFX_REQUIRE(m >= 0 && k >= 0 && n >= 0 && nnz >= 0, OFX_EINVAL,
+              "spmm_csr: negative size (m=%lld k=%lld n=%lld nnz=%lld)", (long long)m,
+              (long long)k, (long long)n, (long long)nnz);
+  OFX_REQUIRE(idx_dtype == OFX_DT_INT64 || (nnz <= INT32_MAX && k <= INT32_MAX), OFX_EINVAL,
+              "spmm_csr: int32 indices cannot address nnz=%lld / k=%lld", (long long)nnz,
+              (long long)k);
+  return OFX_OK;
+}
+
+}  // namespace
+}  // namespace ofx
+
+using namespace ofx;
+
+extern "C" int64_t ofx_spmm_default_split(int64_t n) { return default_split(n); }
+
+extern "C" int ofx_spmm_csr_workspace_size(int idx_dtype, int val_dtype, int64_t m, int64_t k,
+                                           int64_t n, int64_t nnz, const ofx_spmm_options* opts,
+                                           size_t* bytes) {
+  OFX_REQUIRE(bytes != nullptr, OFX_EINVAL, "spmm_csr_workspace_size: bytes is NULL");
+  int rc = check_common(idx_dtype, val_dtype, m, k, n, nnz);
+  if (rc) return rc;
+  const Schedule s = resolve_schedule(n, opts);
+  *bytes = ws_layout(nnz, n, acc_bytes_of(val_dtype), s).total;
+  return OFX_OK;
+}
+
+extern "C" int ofx_spmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k,
+                            int64_t n, int64_t nnz, const void* row_ptr, const void* col_idx,
+                            const void* values, const void* b, int64_t ldb, void* c, int64_t ldc,
+                            int64_t row_begin, int64_t row_end, void* workspace,
+                            size_t workspace_bytes, const ofx_spmm_options* opts) {
+  int rc = check_common(idx_dtype, val_dtype, m, k, n, nnz);
+  if (rc) return rc;
+  OFX_REQUIRE(0 <= row_begin && row_begin <= row_end && row_end <= m, OFX_EINVAL,
+              "spmm_csr: row range [%lld, %lld) outside [0, %lld)", (long long)row_begin,
+              (long long)row_end, (long long)m);
+  OFX_REQUIRE(ldb >= n && ldc >= n, OFX_EINVAL, "spmm_csr: ldb=%lld / ldc=%lld < n=%lld",
+              (long long)ldb, (long long)ldc, (long long)n);
+  const int64_t nrows = row_end - row_begin;
+  if (nrows == 0 || n == 0) return OFX_OK;  // nothing to write
+  OFX_REQUIRE(row_ptr && c, OFX_EINVAL, "spmm_csr: NULL row_ptr or output");
+  OFX_REQUIRE(nnz == 0 || (col_idx && values && b), OFX_EINVAL,
+              "spmm_csr: NULL col_idx/values/b with nnz=%lld", (long long)nnz);
+  Launch L{static_cast<hipStream_t>(stream), row_ptr, col_idx, values, b, c, ldb, ldc,
+           row_begin, nrows, n, nnz, resolve_schedule(n, opts), workspace, workspace_bytes};
+  if (idx_dtype == OFX_DT_INT32) return launch_idx<int32_t>(val_dtype, L);
+  return launch_idx<int64_t>(val_dtype, L);
+}
+
+extern "C" int ofx_csr_validate(void* stream, int idx_dtype, int64_t m, int64_t k, int64_t nnz,
+                                const void* row_ptr, const void* col_idx, void* flag_dev) {
+  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "csr_validate: bad index dtype %d",
+              idx_dtype);
+  OFX_REQUIRE(row_ptr && flag_dev && (nnz == 0 || col_idx), OFX_EINVAL,
+              "csr_validate: NULL pointer");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  OFX_HIP_CHECK(hipMemsetAsync(flag_dev, 0, sizeof(unsigned int), s));
+  int64_t work = std::max<int64_t>(m + 1, nnz);
+  int64_t grid = std::min<int64_t>((work + 255) / 256, 4096);
+  if (grid < 1) grid = 1;
+  if (idx_dtype == OFX_DT_INT32)
+    hipLaunchKernelGGL(csr_validate_kernel<int32_t>, dim3((unsigned)grid), dim3(256), 0, s,
+                       static_cast<const int32_t*>(row_ptr), static_cast<const int32_t*>(col_idx),
+                       m, k, nnz, static_cast<unsigned int*>(flag_dev));
+  else
+    hipLaunchKernelGGL(csr_validate_kernel<int64_t>, dim3((unsigned)grid), dim3(256), 0, s,
+                       static_cast<const int64_t*>(row_ptr), static_cast<const int64_t*>(col_idx),
+                       m, k, nnz, static_cast<unsigned int*>(flag_dev));
+  OFX_HIP_CHECK(hipGetLastError());
+  return OFX_OK;
+}
+
+extern "C" int ofx_csr_row_slice(void* stream, int idx_dtype, const void* row_ptr,
+                                 int64_t row_begin, int64_t row_end, void* out_row_ptr) {
+  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "csr_row_slice: bad index dtype %d",
+              idx_dtype);
+  OFX_REQUIRE(0 <= row_begin && row_begin <= row_end, OFX_EINVAL,
+              "csr_row_slice: bad row range [%lld, %lld)", (long long)row_begin,
+              (long long)row_end);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t rows = row_end - row_begin;
+  const int64_t grid = (rows + 1 + 255) / 256;
+  if (idx_dtype == OFX_DT_INT32)
+    hipLaunchKernelGGL(csr_row_slice_kernel<int32_t>, dim3((unsigned)grid), dim3(256), 0, s,
+                       static_cast<const int32_t*>(row_ptr), row_begin, rows,
+                       static_cast<int32_t*>(out_row_ptr));
+  else
+    hipLaunchKernelGGL(csr_row_slice_kernel<int64_t>, dim3((unsigned)grid), dim3(256), 0, s,
+                       static_cast<const int64_t*>(row_ptr), row_begin, rows,
+                       static_cast<int64_t*>(out_row_ptr));
+  OFX_HIP_CHECK(hipGetLastError());
+  return OFX_OK;
+}
+
+extern "C" int ofx_synth_dense(void* stream, int val_dtype, int64_t r_begin, int64_t r_end,
+                               int64_t n, int64_t ld, uint64_t seed, int exact, void* out) {
+  OFX_REQUIRE(r_begin <= r_end && ld >= n && n >= 0, OFX_EINVAL, "synth_dense: bad shape");
+  const int64_t rows = r_end - r_begin;
+  if (rows == 0 || n == 0) return OFX_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t total = rows * n;
+  const int64_t grid = std::min<int64_t>((total + 255) / 256, 65536);
+  switch (val_dtype) {
+    case OFX_DT_FLOAT:
+      hipLaunchKernelGGL(synth_dense_kernel<float>, dim3((unsigned)grid), dim3(256), 0, s, r_begin,
+                         rows, n, ld, seed, exact, static_cast<float*>(out));
+      break;
+    case OFX_DT_DOUBLE:
+      hipLaunchKernelGGL(synth_dense_kernel<double>, dim3((unsigned)grid), dim3(256), 0, s,
+                         r_begin, rows, n, ld, seed, exact, static_cast<double*>(out));
+      break;
+    case OFX_DT_BFLOAT16:
+      hipLaunchKernelGGL(synth_dense_kernel<bf16>, dim3((unsigned)grid), dim3(256), 0, s, r_begin,
+                         rows, n, ld, seed, exact, static_cast<bf16*>(out));
+      break;
+    case OFX_DT_FLOAT16:
+      hipLaunchKernelGGL(synth_dense_kernel<f16>, dim3((unsigned)grid), dim3(256), 0, s, r_begin,
+                         rows, n, ld, seed, exact, static_cast<f16*>(out));
+      break;
+    default: return fail(OFX_EUNSUPPORTED, "synth_dense: unsupported dtype %d", val_dtype);
+  }
+  OFX_HIP_CHECK(hipGetLastError());
+  return OFX_OK;
+}

@@ -1,0 +1,22 @@
+// op_generated.cpp — the registration `oneflow_tblgen` would emit for op "spmm_csr"
+// (pattern tools/oneflow-tblgen/op_schema_source.inc:32-100): inputs, outputs, typed attrs with
+// their ODS defaults, and the static infer/SBP/dtype/input-modifier functions of SpmmCsrOp.
+#include "oneflow/core/framework/op_generated.h"
+
+namespace oneflow {
+
+REGISTER_USER_OP("spmm_csr")
+    .Input("a_csr_row_ptr")
+    .Input("a_csr_col_idx")
+    .Input("a_csr_values")
+    .Input("b")
+    .Output("out")
+    .Attr<int64_t>("a_num_rows", 0)
+    .Attr<int64_t>("a_num_cols", 0)
+    .SetLogicalTensorDescInferFn(SpmmCsrOp::InferLogicalTensorDesc)
+    .SetPhysicalTensorDescInferFn(SpmmCsrOp::InferPhysicalTensorDesc)
+    .SetGetSbpFn(SpmmCsrOp::GetSbp)
+    .SetDataTypeInferFn(SpmmCsrOp::InferDataType)
+    .SetInputArgModifyFn(SpmmCsrOp::ModifyInputArg);
+
+}  // namespace oneflow

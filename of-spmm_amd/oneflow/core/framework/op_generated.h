@@ -1,0 +1,22 @@
+// op_generated.h — the declaration `oneflow_tblgen` would emit for the ODS entry of
+// op "spmm_csr" (oneflow/ir/spmm_csr.td; generator tools/oneflow-tblgen/op_schema_header.inc:34-99).
+#ifndef OFX_ONEFLOW_SHIM_OP_GENERATED_H_
+#define OFX_ONEFLOW_SHIM_OP_GENERATED_H_
+
+#include "oneflow/core/framework/framework.h"
+
+namespace oneflow {
+
+class SpmmCsrOp {
+ public:
+  static Maybe<void> InferLogicalTensorDesc(user_op::InferContext* ctx);
+  static Maybe<void> InferPhysicalTensorDesc(user_op::InferContext* ctx);
+  static Maybe<void> GetSbp(user_op::SbpContext* ctx);
+  static Maybe<void> InferDataType(user_op::InferContext* ctx);
+  static Maybe<void> ModifyInputArg(const user_op::GetInputArgModifier& GetInputArgModifierFn,
+                                    const user_op::UserOpConfWrapper& conf);
+};
+
+}  // namespace oneflow
+
+#endif  // OFX_ONEFLOW_SHIM_OP_GENERATED_H_

@@ -1,0 +1,237 @@
+/*
+ * spmm_functor.cpp — functional::SpmmCsr and its C-ABI entry (the Python binding calls this).
+ *
+ * Mirrors the functional layer of the reference: YAML signature
+ *   "Tensor (Tensor a_csr_row_ptr, Tensor a_csr_col_idx, Tensor a_csr_values, Int64 a_num_rows,
+ *            Int64 a_num_cols, Tensor b) => SpmmCsr"      (template functional_api.yaml:1062-1065)
+ * and the functor pattern of oneflow/core/functional/impl/nn_functor.cpp:3861-3884 (argument
+ * checks as RuntimeError, then OpInterpUtil::Dispatch).  "Dispatch" here is the eager-local
+ * interpreter reduced to what one op needs (oneflow/core/framework/op_interpreter/
+ * eager_local_op_interpreter.cpp:74-160): run the op's logical/dtype inference, choose the one
+ * matching kernel (StatefulOpKernel::ChooseOpKernel, oneflow/user/kernels/stateful_opkernel.cpp:873-910),
+ * init its cache (:912-935) and Compute on the device stream.  Output/tmp memory is owned by the
+ * caller, as the VM owns it in the reference (oneflow/core/vm/op_call_instruction_policy.cpp:28-36).
+ */
+#include <mutex>
+
+#include "oneflow/core/framework/framework.h"
+#include "ofx_internal.h"
+#include "ofx_spmm.h"
+
+namespace oneflow {
+namespace {
+
+using DescMap = std::map<std::pair<std::string, int32_t>, user_op::TensorDesc>;
+
+Shape ShapeOf(const ofx_tensor_desc* d) {
+  std::vector<int64_t> dims;
+  for (int i = 0; i < d->ndim; ++i) dims.push_back(d->shape[i]);
+  return Shape(dims);
+}
+
+int ToStatus(const Maybe<void>& m) {
+  if (m.IsOk()) return OFX_OK;
+  return ofx::fail(OFX_EINVAL, "%s: %s", m.kind().c_str(), m.message().c_str());
+}
+
+Maybe<void> CheckArgs(const ofx_tensor_desc* row_ptr, const ofx_tensor_desc* col_idx,
+                      const ofx_tensor_desc* values, const ofx_tensor_desc* b) {
+  CHECK_OR_RETURN(row_ptr && col_idx && values && b)
+      << Error::RuntimeError() << "spmm_csr: NULL tensor argument";
+  CHECK_OR_RETURN(row_ptr->ndim >= 1 && row_ptr->ndim <= 2 && col_idx->ndim >= 1 &&
+                  col_idx->ndim <= 2 && values->ndim >= 1 && values->ndim <= 2 && b->ndim >= 1 &&
+                  b->ndim <= 2)
+      << Error::RuntimeError() << "spmm_csr: tensors must be 1-D or 2-D";
+  CHECK_OR_RETURN(row_ptr->device == col_idx->device && row_ptr->device == values->device &&
+                  row_ptr->device == b->device)
+      << Error::RuntimeError() << "spmm_csr: expected all tensors on the same device, got "
+      << row_ptr->device << ", " << col_idx->device << ", " << values->device << ", "
+      << b->device;
+  return Maybe<void>::Ok();
+}
+
+Maybe<void> Infer(const ofx_tensor_desc* row_ptr, const ofx_tensor_desc* col_idx,
+                  const ofx_tensor_desc* values, int64_t m, int64_t k, const ofx_tensor_desc* b,
+                  user_op::TensorDesc* out) {
+  JUST(CheckArgs(row_ptr, col_idx, values, b));
+  const user_op::OpRegistryResult* op = user_op::UserOpRegistryMgr::Get().GetOpRegistryResult("spmm_csr");
+  CHECK_OR_RETURN(op != nullptr) << Error::RuntimeError() << "op spmm_csr is not registered";
+  DescMap in;
+  in[{"a_csr_row_ptr", 0}] = user_op::TensorDesc(ShapeOf(row_ptr), (DataType)row_ptr->dtype);
+  in[{"a_csr_col_idx", 0}] = user_op::TensorDesc(ShapeOf(col_idx), (DataType)col_idx->dtype);
+  in[{"a_csr_values", 0}] = user_op::TensorDesc(ShapeOf(values), (DataType)values->dtype);
+  in[{"b", 0}] = user_op::TensorDesc(ShapeOf(b), (DataType)b->dtype);
+  user_op::InferContext ctx(in, {{"a_num_rows", m}, {"a_num_cols", k}});
+  JUST(op->logical_infer(&ctx));
+  JUST(op->dtype_infer(&ctx));
+  *out = ctx.OutputTensorDesc("out", 0);
+  return Maybe<void>::Ok();
+}
+
+struct KernelEntry {
+  const user_op::OpKernelRegistryResult* reg;
+  std::unique_ptr<user_op::OpKernel> kernel;
+};
+
+// Kernel objects are shared and const, cached per registration (stateful_opkernel.cpp:887-908).
+const user_op::OpKernel* GetKernel(const user_op::OpKernelRegistryResult* reg) {
+  static std::mutex mu;
+  static std::map<const void*, std::unique_ptr<user_op::OpKernel>> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  auto& slot = cache[reg];
+  if (!slot) slot.reset(reg->create_fn());
+  return slot.get();
+}
+
+Maybe<void> Choose(const ofx_tensor_desc* row_ptr, const ofx_tensor_desc* b, int device,
+                   const user_op::OpKernelRegistryResult** reg) {
+  user_op::KernelRegContext rc;
+  rc.device_type = device < 0 ? DeviceType::kCPU : DeviceType::kHIP;
+  rc.dtypes[{"out", 0}] = (DataType)b->dtype;
+  rc.dtypes[{"a_csr_row_ptr", 0}] = (DataType)row_ptr->dtype;
+  return user_op::UserOpRegistryMgr::Get().GetOpKernelRegistryResult("spmm_csr", rc, reg);
+}
+
+}  // namespace
+}  // namespace oneflow
+
+using namespace oneflow;
+
+extern "C" int ofx_functional_spmm_csr_infer(const ofx_tensor_desc* row_ptr,
+                                             const ofx_tensor_desc* col_idx,
+                                             const ofx_tensor_desc* values, int64_t a_num_rows,
+                                             int64_t a_num_cols, const ofx_tensor_desc* b,
+                                             ofx_tensor_desc* out) {
+  user_op::TensorDesc od;
+  int rc = ToStatus(Infer(row_ptr, col_idx, values, a_num_rows, a_num_cols, b, &od));
+  if (rc) return rc;
+  if (out) {
+    out->dtype = od.data_type();
+    out->ndim = (int32_t)od.shape().NumAxes();
+    for (int i = 0; i < out->ndim; ++i) out->shape[i] = od.shape().At(i);
+    out->device = b->device;
+  }
+  return OFX_OK;
+}
+
+extern "C" int ofx_functional_spmm_csr_tmp_size(const ofx_tensor_desc* row_ptr,
+                                                const ofx_tensor_desc* col_idx,
+                                                const ofx_tensor_desc* values, int64_t a_num_rows,
+                                                int64_t a_num_cols, const ofx_tensor_desc* b,
+                                                size_t* bytes) {
+  OFX_REQUIRE(bytes, OFX_EINVAL, "spmm_csr_tmp_size: bytes is NULL");
+  user_op::TensorDesc od;
+  int rc = ToStatus(Infer(row_ptr, col_idx, values, a_num_rows, a_num_cols, b, &od));
+  if (rc) return rc;
+  const user_op::OpKernelRegistryResult* reg = nullptr;
+  rc = ToStatus(Choose(row_ptr, b, b->device, &reg));
+  if (rc) return rc;
+  user_op::InferSizeContext sc;
+  sc.descs[{"a_csr_row_ptr", 0}] = user_op::TensorDesc(ShapeOf(row_ptr), (DataType)row_ptr->dtype);
+  sc.descs[{"a_csr_col_idx", 0}] = user_op::TensorDesc(ShapeOf(col_idx), (DataType)col_idx->dtype);
+  sc.descs[{"b", 0}] = user_op::TensorDesc(ShapeOf(b), (DataType)b->dtype);
+  sc.attrs = {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols}};
+  *bytes = reg->infer_tmp_size ? reg->infer_tmp_size(&sc) : 0;
+  return OFX_OK;
+}
+
+extern "C" int ofx_functional_spmm_csr_ex(void* stream, const ofx_tensor_desc* row_ptr,
+                                          const ofx_tensor_desc* col_idx,
+                                          const ofx_tensor_desc* values, int64_t a_num_rows,
+                                          int64_t a_num_cols, const ofx_tensor_desc* b,
+                                          ofx_tensor_desc* out, void* tmp, size_t tmp_bytes,
+                                          int64_t parallel_id, int64_t parallel_num,
+                                          int out_split_axis, int num_threads) {
+  OFX_REQUIRE(out, OFX_EINVAL, "spmm_csr: out is NULL");
+  OFX_REQUIRE(parallel_num >= 1 && parallel_id >= 0 && parallel_id < parallel_num, OFX_EINVAL,
+              "spmm_csr: bad parallel context %lld/%lld", (long long)parallel_id,
+              (long long)parallel_num);
+  user_op::TensorDesc od;
+  int rc = ToStatus(Infer(row_ptr, col_idx, values, a_num_rows, a_num_cols, b, &od));
+  if (rc) return rc;
+  // The physical out of a row split holds only this rank's rows (S(0) slice of the logical out).
+  int64_t phys_rows = od.shape().At(0);
+  int64_t lo = 0, hi = phys_rows;
+  if (parallel_num > 1 && out_split_axis == 0) {
+    ofx_balanced_range(phys_rows, parallel_num, parallel_id, &lo, &hi);
+    phys_rows = hi - lo;
+  }
+  OFX_REQUIRE(out->ndim == 2 && out->shape[0] == phys_rows && out->shape[1] == od.shape().At(1) &&
+                  out->dtype == (int32_t)od.data_type() && out->device == b->device,
+              OFX_EINVAL,
+              "spmm_csr: out must be a (%lld, %lld) tensor of dtype %d on device %d",
+              (long long)phys_rows, (long long)od.shape().At(1), (int)od.data_type(), b->device);
+  const user_op::OpKernelRegistryResult* reg = nullptr;
+  rc = ToStatus(Choose(row_ptr, b, b->device, &reg));
+  if (rc) return rc;
+  const user_op::OpKernel* kernel = GetKernel(reg);
+
+  user_op::Tensor t_rp(ShapeOf(row_ptr), (DataType)row_ptr->dtype, row_ptr->data);
+  user_op::Tensor t_ci(ShapeOf(col_idx), (DataType)col_idx->dtype, col_idx->data);
+  user_op::Tensor t_v(ShapeOf(values), (DataType)values->dtype, values->data);
+  user_op::Tensor t_b(ShapeOf(b), (DataType)b->dtype, b->data, b->ndim == 2 ? b->stride[0] : -1);
+  user_op::Tensor t_o(ShapeOf(out), (DataType)out->dtype, out->data, out->stride[0]);
+  user_op::Tensor t_tmp(Shape({(int64_t)tmp_bytes}), kChar, tmp);
+  std::map<std::pair<std::string, int32_t>, user_op::Tensor*> tensors = {
+      {{"a_csr_row_ptr", 0}, &t_rp}, {{"a_csr_col_idx", 0}, &t_ci}, {{"a_csr_values", 0}, &t_v},
+      {{"b", 0}, &t_b},              {{"out", 0}, &t_o}};
+  if (tmp) tensors[{"tmp_buffer", 0}] = &t_tmp;
+  const DeviceType dev = b->device < 0 ? DeviceType::kCPU : DeviceType::kHIP;
+  ep::CpuStream cpu_stream(num_threads);
+  ep::HipStream hip_stream(stream, b->device);
+  ep::Stream* s = dev == DeviceType::kCPU ? static_cast<ep::Stream*>(&cpu_stream)
+                                          : static_cast<ep::Stream*>(&hip_stream);
+  const user_op::AttrMap attrs = {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols}};
+  user_op::KernelCacheContext cache_ctx(
+      ParallelContext(parallel_id, parallel_num),
+      {{"out", out_split_axis == 0 ? "S(0)" : (out_split_axis == 1 ? "S(1)" : "B")}},
+      {{"out", od}}, dev);
+  user_op::KernelComputeContext ctx(s, tensors, attrs, dev);
+  try {
+    std::shared_ptr<user_op::OpKernelCache> cache = kernel->InitOpKernelCache(&cache_ctx);
+    if (phys_rows == 0 || od.shape().At(1) == 0) {
+      if (!kernel->AlwaysComputeWhenAllOutputsEmpty()) return OFX_OK;
+    }
+    kernel->Compute(&ctx, nullptr, cache.get());
+  } catch (const KernelCheckError& e) {
+    return ofx::fail(OFX_EINVAL, "%s", e.msg.c_str());
+  }
+  return OFX_OK;
+}
+
+extern "C" int ofx_functional_spmm_csr(void* stream, const ofx_tensor_desc* row_ptr,
+                                       const ofx_tensor_desc* col_idx,
+                                       const ofx_tensor_desc* values, int64_t a_num_rows,
+                                       int64_t a_num_cols, const ofx_tensor_desc* b,
+                                       ofx_tensor_desc* out, void* tmp, size_t tmp_bytes) {
+  return ofx_functional_spmm_csr_ex(stream, row_ptr, col_idx, values, a_num_rows, a_num_cols, b,
+                                    out, tmp, tmp_bytes, 0, 1, -1, 0);
+}
+
+// SBP signatures of the op, for the tests: "arg:sbp,arg:sbp;..." into buf.
+extern "C" int ofx_op_spmm_csr_sbp_signatures(char* buf, size_t len) {
+  const user_op::OpRegistryResult* op = user_op::UserOpRegistryMgr::Get().GetOpRegistryResult("spmm_csr");
+  OFX_REQUIRE(op && buf && len > 0, OFX_EINVAL, "spmm_csr not registered or NULL buffer");
+  user_op::SbpContext ctx;
+  int rc = ToStatus(op->get_sbp(&ctx));
+  if (rc) return rc;
+  std::string s;
+  for (const auto& sig : ctx.signatures()) {
+    if (!s.empty()) s += ";";
+    for (size_t i = 0; i < sig.size(); ++i) s += (i ? "," : "") + sig[i].first + ":" + sig[i].second;
+  }
+  // input-arg modifiers: which inputs have requires_grad disabled
+  std::map<std::string, user_op::InputArgModifier> mods;
+  user_op::GetInputArgModifier get = [&](const std::string& n, int32_t) { return &mods[n]; };
+  rc = ToStatus(op->input_modify(get, user_op::UserOpConfWrapper()));
+  if (rc) return rc;
+  s += "|no_grad:";
+  bool first = true;
+  for (const auto& kv : mods)
+    if (!kv.second.requires_grad) {
+      s += (first ? "" : ",") + kv.first;
+      first = false;
+    }
+  snprintf(buf, len, "%s", s.c_str());
+  return OFX_OK;
+}

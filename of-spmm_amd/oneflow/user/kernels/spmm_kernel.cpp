@@ -1,0 +1,142 @@
+/*
+ * spmm_kernel.cpp — kernels of op "spmm_csr" for DeviceType::kCPU and DeviceType::kHIP.
+ *
+ * Pattern of a OneFlow user kernel with a row-range cache, following
+ * oneflow/user/kernels/unsorted_segment_sum_kernel.cpp:46-78 (OpKernelCache holding
+ * [lower, upper) from the out SBP, BalancedSplitter via GetTensorSliceView4ParallelId,
+ * oneflow/core/job/nd_sbp_util.cpp:98-104) and :146-205 (tmp buffer via SetInferTmpSizeFn).
+ * The device work is the C-ABI: ofx_spmm_csr (HIP, async on the op's stream) and
+ * ofx_spmm_csr_cpu (host).  Kernel errors are fatal CHECKs as in
+ * oneflow/user/kernels/matrix_vector_product_kernel.cpp:98-109.
+ */
+#include "oneflow/core/framework/framework.h"
+#include "ofx_spmm.h"
+
+namespace oneflow {
+
+namespace {
+
+class SpmmCsrOpKernelCache final : public user_op::OpKernelCache {
+ public:
+  SpmmCsrOpKernelCache(int64_t lower, int64_t upper) : lower_(lower), upper_(upper) {}
+  ~SpmmCsrOpKernelCache() override = default;
+  int64_t lower() const { return lower_; }
+  int64_t upper() const { return upper_; }
+
+ private:
+  const int64_t lower_;
+  const int64_t upper_;
+};
+
+std::shared_ptr<user_op::OpKernelCache> CreateSpmmCsrOpKernelCache(user_op::KernelCacheContext* ctx) {
+  if (ctx->parallel_ctx().parallel_num() > 1 && ctx->Sbp4ArgName("out") == "S(0)") {
+    const user_op::TensorDesc* out_logical = ctx->LogicalTensorDesc4ArgNameAndIndex("out", 0);
+    const BalancedSplitter bs(out_logical->shape().At(0), ctx->parallel_ctx().parallel_num());
+    const auto range = bs.At(ctx->parallel_ctx().parallel_id());
+    return std::make_shared<SpmmCsrOpKernelCache>(range.first, range.second);
+  }
+  return nullptr;
+}
+
+int DtCode(DataType dt) { return static_cast<int>(dt); }
+
+template <DeviceType device_type>
+class SpmmCsrKernel final : public user_op::OpKernel, public user_op::CudaGraphSupport {
+ public:
+  SpmmCsrKernel() = default;
+  ~SpmmCsrKernel() override = default;
+
+  std::shared_ptr<user_op::OpKernelCache> InitOpKernelCache(
+      user_op::KernelCacheContext* ctx) const override {
+    return CreateSpmmCsrOpKernelCache(ctx);
+  }
+
+  bool AlwaysComputeWhenAllOutputsEmpty() const override { return false; }
+
+ private:
+  using user_op::OpKernel::Compute;
+  void Compute(user_op::KernelComputeContext* ctx, user_op::OpKernelState*,
+               const user_op::OpKernelCache* cache) const override {
+    const user_op::Tensor* row_ptr = ctx->Tensor4ArgNameAndIndex("a_csr_row_ptr", 0);
+    const user_op::Tensor* col_idx = ctx->Tensor4ArgNameAndIndex("a_csr_col_idx", 0);
+    const user_op::Tensor* values = ctx->Tensor4ArgNameAndIndex("a_csr_values", 0);
+    const user_op::Tensor* b = ctx->Tensor4ArgNameAndIndex("b", 0);
+    user_op::Tensor* out = ctx->Tensor4ArgNameAndIndex("out", 0);
+    const int64_t m = ctx->Attr<int64_t>("a_num_rows");
+    const int64_t k = ctx->Attr<int64_t>("a_num_cols");
+    OFX_KERNEL_CHECK(b->shape_view().NumAxes() == 2, "b Numdims should be equal to 2. ");
+    OFX_KERNEL_CHECK(out->shape_view().NumAxes() == 2, "out Numdims should be equal to 2. ");
+    OFX_KERNEL_CHECK(out->data_type() == b->data_type(), "out datatype should be equal to b. ");
+    const int64_t n = out->shape_view().At(1);
+    const int64_t nnz = col_idx->shape_view().elem_cnt();
+    int64_t row_begin = 0;
+    int64_t row_end = m;
+    if (cache != nullptr) {
+      const auto* range = dynamic_cast<const SpmmCsrOpKernelCache*>(cache);
+      OFX_KERNEL_CHECK(range != nullptr, "unexpected kernel cache type");
+      row_begin = range->lower();
+      row_end = range->upper();
+    }
+    OFX_KERNEL_CHECK(out->shape_view().At(0) == row_end - row_begin,
+                     "out rows " << out->shape_view().At(0) << " != row range "
+                                 << row_end - row_begin);
+    const int idx_dt = DtCode(row_ptr->data_type());
+    const int val_dt = DtCode(values->data_type());
+    int rc;
+    if (device_type == DeviceType::kHIP) {
+      user_op::Tensor* tmp = ctx->Tensor4ArgNameAndIndex("tmp_buffer", 0);
+      void* ws = tmp ? tmp->mut_dptr() : nullptr;
+      const size_t ws_bytes = tmp ? (size_t)tmp->shape_view().elem_cnt() : 0;
+      void* stream = ctx->stream()->As<ep::HipStream>()->hip_stream();
+      rc = ofx_spmm_csr(stream, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(), col_idx->dptr(),
+                        values->dptr(), b->dptr(), b->row_stride(), out->mut_dptr(),
+                        out->row_stride(), row_begin, row_end, ws, ws_bytes, nullptr);
+    } else {
+      const int threads = ctx->stream()->As<ep::CpuStream>()->num_threads();
+      rc = ofx_spmm_csr_cpu(threads, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
+                            col_idx->dptr(), values->dptr(), b->dptr(), b->row_stride(),
+                            out->mut_dptr(), out->row_stride(), row_begin, row_end, nullptr);
+    }
+    OFX_KERNEL_CHECK(rc == OFX_OK, "spmm_csr kernel failed (" << rc << "): " << ofx_last_error());
+  }
+};
+
+size_t InferSpmmCsrTmpSize(user_op::InferSizeContext* ctx) {
+  const user_op::TensorDesc& row_ptr = ctx->InputTensorDesc("a_csr_row_ptr", 0);
+  const user_op::TensorDesc& col_idx = ctx->InputTensorDesc("a_csr_col_idx", 0);
+  const user_op::TensorDesc& b = ctx->InputTensorDesc("b", 0);
+  size_t bytes = 0;
+  const int rc = ofx_spmm_csr_workspace_size(
+      DtCode(row_ptr.data_type()), DtCode(b.data_type()), ctx->Attr<int64_t>("a_num_rows"),
+      ctx->Attr<int64_t>("a_num_cols"), b.shape().At(1), col_idx.shape().At(0), nullptr, &bytes);
+  return rc == OFX_OK ? bytes : 0;
+}
+
+}  // namespace
+
+#define REGISTER_SPMM_CSR_KERNEL(device, dtype, itype)                                         \
+  REGISTER_USER_KERNEL("spmm_csr")                                                            \
+      .SetCreateFn<SpmmCsrKernel<device>>()                                                   \
+      .SetIsMatchedHob((user_op::HobDeviceType() == device)                                   \
+                       && (user_op::HobDataType("out", 0) == dtype)                           \
+                       && (user_op::HobDataType("a_csr_row_ptr", 0) == itype))                \
+      .SetInferTmpSizeFn(device == DeviceType::kHIP                                           \
+                             ? std::function<size_t(user_op::InferSizeContext*)>(             \
+                                   InferSpmmCsrTmpSize)                                       \
+                             : std::function<size_t(user_op::InferSizeContext*)>(             \
+                                   [](user_op::InferSizeContext*) -> size_t { return 0; }));
+
+#define REGISTER_SPMM_CSR_KERNEL_ALL_INDEX(device, dtype) \
+  REGISTER_SPMM_CSR_KERNEL(device, dtype, kInt32)         \
+  REGISTER_SPMM_CSR_KERNEL(device, dtype, kInt64)
+
+#define REGISTER_SPMM_CSR_KERNEL_ALL(device)              \
+  REGISTER_SPMM_CSR_KERNEL_ALL_INDEX(device, kFloat)      \
+  REGISTER_SPMM_CSR_KERNEL_ALL_INDEX(device, kDouble)     \
+  REGISTER_SPMM_CSR_KERNEL_ALL_INDEX(device, kFloat16)    \
+  REGISTER_SPMM_CSR_KERNEL_ALL_INDEX(device, kBFloat16)
+
+REGISTER_SPMM_CSR_KERNEL_ALL(DeviceType::kCPU)
+REGISTER_SPMM_CSR_KERNEL_ALL(DeviceType::kHIP)
+
+}  // namespace oneflow

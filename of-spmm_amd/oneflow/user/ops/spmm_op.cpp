@@ -1,0 +1,118 @@
+/*
+ * spmm_op.cpp — op "spmm_csr": out[M, N] = A_csr[M, K] @ b[K, N].
+ *
+ * Written for OneFlow's user-op surface exactly as a new op in oneflow/user/ops would be
+ * (templates: oneflow/user/ops/matrix_vector_product_op.cpp:73-107 for infer/SBP structure,
+ * oneflow/user/ops/unsorted_segment_sum_op.cpp:21-80 for index-dtype checks and the
+ * requires_grad=false input modifier).  Errors are CHECK_*_OR_RETURN -> Maybe -> Python
+ * exception, as in the reference.
+ *
+ * SBP signatures:
+ *   A parts B, b B,    out S(0)   row split: each rank computes its BalancedSplitter row range
+ *                                 (the framework all-gathers b from S(0) -> B first).
+ *   A parts B, b S(1), out S(1)   column split of the dense operand, no communication.
+ */
+#include "oneflow/core/framework/framework.h"
+#include "oneflow/core/framework/op_generated.h"
+
+namespace oneflow {
+
+namespace {
+
+constexpr const char* kRowPtr = "a_csr_row_ptr";
+constexpr const char* kColIdx = "a_csr_col_idx";
+constexpr const char* kValues = "a_csr_values";
+
+Maybe<void> InferTensorDesc4SpmmCsr(user_op::InferContext* ctx) {
+  const user_op::TensorDesc& row_ptr = ctx->InputTensorDesc(kRowPtr, 0);
+  const user_op::TensorDesc& col_idx = ctx->InputTensorDesc(kColIdx, 0);
+  const user_op::TensorDesc& values = ctx->InputTensorDesc(kValues, 0);
+  const user_op::TensorDesc& b = ctx->InputTensorDesc("b", 0);
+  const int64_t m = ctx->Attr<int64_t>("a_num_rows");
+  const int64_t k = ctx->Attr<int64_t>("a_num_cols");
+  CHECK_GE_OR_RETURN(m, 0) << Error::RuntimeError() << "a_num_rows must be non-negative. ";
+  CHECK_GE_OR_RETURN(k, 0) << Error::RuntimeError() << "a_num_cols must be non-negative. ";
+  CHECK_EQ_OR_RETURN(row_ptr.shape().NumAxes(), 1)
+      << Error::RuntimeError() << "a_csr_row_ptr should be 1-D, got shape "
+      << row_ptr.shape().ToString();
+  CHECK_EQ_OR_RETURN(col_idx.shape().NumAxes(), 1)
+      << Error::RuntimeError() << "a_csr_col_idx should be 1-D, got shape "
+      << col_idx.shape().ToString();
+  CHECK_EQ_OR_RETURN(values.shape().NumAxes(), 1)
+      << Error::RuntimeError() << "a_csr_values should be 1-D, got shape "
+      << values.shape().ToString();
+  CHECK_EQ_OR_RETURN(b.shape().NumAxes(), 2)
+      << Error::RuntimeError() << "b should be 2-D, got shape " << b.shape().ToString();
+  CHECK_EQ_OR_RETURN(row_ptr.shape().At(0), m + 1)
+      << Error::RuntimeError() << "a_csr_row_ptr should have a_num_rows + 1 elements. ";
+  CHECK_EQ_OR_RETURN(col_idx.shape().At(0), values.shape().At(0))
+      << Error::RuntimeError() << "a_csr_col_idx and a_csr_values should have nnz elements each. ";
+  CHECK_EQ_OR_RETURN(b.shape().At(0), k)
+      << Error::RuntimeError() << "Dim K should be equal to b's dim0 (a_num_cols). ";
+  ctx->SetOutputShape("out", 0, Shape({m, b.shape().At(1)}));
+  return Maybe<void>::Ok();
+}
+
+Maybe<void> InferDataType4SpmmCsr(user_op::InferContext* ctx) {
+  const DataType index_dtype = ctx->InputDType(kRowPtr, 0);
+  CHECK_OR_RETURN(IsIndexDataType(index_dtype))
+      << Error::TypeError() << "a_csr_row_ptr should be int32 or int64, got "
+      << DataType_Name(index_dtype);
+  CHECK_EQ_OR_RETURN(ctx->InputDType(kColIdx, 0), index_dtype)
+      << Error::TypeError() << "a_csr_col_idx should have the dtype of a_csr_row_ptr. ";
+  const DataType dtype = ctx->InputDType("b", 0);
+  CHECK_EQ_OR_RETURN(ctx->InputDType(kValues, 0), dtype)
+      << Error::TypeError() << "a_csr_values datatype should be equal to b. ";
+  CHECK_OR_RETURN(dtype == kFloat || dtype == kDouble || dtype == kFloat16 || dtype == kBFloat16)
+      << Error::TypeError() << "spmm_csr supports float, double, float16, bfloat16; got "
+      << DataType_Name(dtype);
+  ctx->SetOutputDType("out", 0, dtype);
+  return Maybe<void>::Ok();
+}
+
+}  // namespace
+
+/* static */ Maybe<void> SpmmCsrOp::InferLogicalTensorDesc(user_op::InferContext* ctx) {
+  return InferTensorDesc4SpmmCsr(ctx);
+}
+
+/* static */ Maybe<void> SpmmCsrOp::InferPhysicalTensorDesc(user_op::InferContext* ctx) {
+  return InferLogicalTensorDesc(ctx);
+}
+
+/* static */ Maybe<void> SpmmCsrOp::GetSbp(user_op::SbpContext* ctx) {
+  // Row split: the CSR is broadcast, b is gathered to broadcast, out rows are split.
+  ctx->NewBuilder()
+      .Broadcast(user_op::OpArg(kRowPtr, 0))
+      .Broadcast(user_op::OpArg(kColIdx, 0))
+      .Broadcast(user_op::OpArg(kValues, 0))
+      .Broadcast(user_op::OpArg("b", 0))
+      .Split(user_op::OpArg("out", 0), 0)
+      .Build();
+  // Column split of the dense operand: no exchange at all.
+  ctx->NewBuilder()
+      .Broadcast(user_op::OpArg(kRowPtr, 0))
+      .Broadcast(user_op::OpArg(kColIdx, 0))
+      .Broadcast(user_op::OpArg(kValues, 0))
+      .Split(user_op::OpArg("b", 0), 1)
+      .Split(user_op::OpArg("out", 0), 1)
+      .Build();
+  return Maybe<void>::Ok();
+}
+
+/* static */ Maybe<void> SpmmCsrOp::InferDataType(user_op::InferContext* ctx) {
+  return InferDataType4SpmmCsr(ctx);
+}
+
+/* static */ Maybe<void> SpmmCsrOp::ModifyInputArg(
+    const user_op::GetInputArgModifier& GetInputArgModifierFn, const user_op::UserOpConfWrapper&) {
+  user_op::InputArgModifier* row_ptr_modifier = GetInputArgModifierFn(kRowPtr, 0);
+  CHECK_NOTNULL_OR_RETURN(row_ptr_modifier);
+  row_ptr_modifier->set_requires_grad(false);
+  user_op::InputArgModifier* col_idx_modifier = GetInputArgModifierFn(kColIdx, 0);
+  CHECK_NOTNULL_OR_RETURN(col_idx_modifier);
+  col_idx_modifier->set_requires_grad(false);
+  return Maybe<void>::Ok();
+}
+
+}  // namespace oneflow

@@ -1,0 +1,126 @@
+"""oneflow_spmm._C — the functional binding `spmm_csr`, mirroring `oneflow._C.spmm_csr`.
+
+Signature (functional YAML entry, pattern oneflow/core/functional/functional_api.yaml:1062-1065):
+    "Tensor (Tensor a_csr_row_ptr, Tensor a_csr_col_idx, Tensor a_csr_values,
+             Int64 a_num_rows, Int64 a_num_cols, Tensor b) => SpmmCsr"
+Tensors are torch tensors (PyTorch-ROCm supplies device memory and streams); the call goes
+through the C-ABI into the C++ op registry (oneflow/user/ops/spmm_op.cpp inference, kernel
+choice, Compute) and launches the HIP kernel on torch's current stream.  CPU tensors run the
+op's DeviceType::kCPU kernel (the reference registers CPU kernels the same way); GPU tensors run
+only the HIP kernel — there is no fallback between them.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import LIB, TensorDesc, check
+
+_TORCH_TO_DT = {
+    torch.float32: _lib.DT_FLOAT,
+    torch.float64: _lib.DT_DOUBLE,
+    torch.float16: _lib.DT_FLOAT16,
+    torch.bfloat16: _lib.DT_BFLOAT16,
+    torch.int32: _lib.DT_INT32,
+    torch.int64: _lib.DT_INT64,
+}
+_DT_TO_TORCH = {v: k for k, v in _TORCH_TO_DT.items()}
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    try:
+        return _TORCH_TO_DT[dt]
+    except KeyError:
+        raise TypeError(f"spmm_csr: unsupported dtype {dt}") from None
+
+
+def _device_index(t: torch.Tensor) -> int:
+    if t.device.type == "cpu":
+        return -1
+    if t.device.type != "cuda":  # PyTorch-ROCm names HIP devices "cuda"
+        raise RuntimeError(f"spmm_csr: unsupported device {t.device}")
+    return t.device.index if t.device.index is not None else torch.cuda.current_device()
+
+
+def _prep(t: torch.Tensor, name: str, matrix: bool = False) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"spmm_csr: {name} must be a tensor, got {type(t).__name__}")
+    if matrix and t.dim() == 2 and t.stride(1) == 1 and t.stride(0) >= t.shape[1]:
+        return t  # row-strided views are consumed in place (ldb)
+    return t.contiguous()
+
+
+def desc(t: torch.Tensor) -> TensorDesc:
+    d = TensorDesc()
+    d.dtype = dtype_code(t.dtype)
+    d.device = _device_index(t)
+    d.ndim = t.dim()
+    if d.ndim > 2:
+        raise RuntimeError(f"spmm_csr: tensors must be 1-D or 2-D, got {t.dim()}-D")
+    for i in range(t.dim()):
+        d.shape[i] = t.shape[i]
+        d.stride[i] = t.stride(i)
+    d.data = t.data_ptr() if t.numel() > 0 else None
+    return d
+
+
+def current_stream_handle(t: torch.Tensor):
+    if t.device.type == "cpu":
+        return None
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def spmm_csr(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor,
+             a_csr_values: torch.Tensor, a_num_rows: int, a_num_cols: int, b: torch.Tensor, *,
+             out: torch.Tensor | None = None, _parallel=None, num_threads: int = 0) -> torch.Tensor:
+    """out[M, N] = CSR(a_csr_row_ptr, a_csr_col_idx, a_csr_values; M x K) @ b[K, N].
+
+    `_parallel=(parallel_id, parallel_num, out_split_axis)` runs the global form: with
+    out_split_axis 0 this rank computes its BalancedSplitter row slice (the physical S(0) out).
+    """
+    rp = _prep(a_csr_row_ptr, "a_csr_row_ptr")
+    ci = _prep(a_csr_col_idx, "a_csr_col_idx")
+    vals = _prep(a_csr_values, "a_csr_values")
+    bb = _prep(b, "b", matrix=True)
+    d_rp, d_ci, d_v, d_b = desc(rp), desc(ci), desc(vals), desc(bb)
+    od = TensorDesc()
+    check(LIB.ofx_functional_spmm_csr_infer(ctypes.byref(d_rp), ctypes.byref(d_ci), ctypes.byref(d_v),
+                                            int(a_num_rows), int(a_num_cols), ctypes.byref(d_b),
+                                            ctypes.byref(od)), "spmm_csr")
+    pid, pnum, axis = _parallel if _parallel is not None else (0, 1, -1)
+    rows, n = od.shape[0], od.shape[1]
+    if pnum > 1 and axis == 0:
+        lo, hi = balanced_range(rows, pnum, pid)
+        rows = hi - lo
+    if out is None:
+        out = torch.empty((rows, n), dtype=_DT_TO_TORCH[od.dtype], device=bb.device)
+    d_o = desc(out)
+    tmp_bytes = ctypes.c_size_t(0)
+    check(LIB.ofx_functional_spmm_csr_tmp_size(ctypes.byref(d_rp), ctypes.byref(d_ci), ctypes.byref(d_v),
+                                               int(a_num_rows), int(a_num_cols), ctypes.byref(d_b),
+                                               ctypes.byref(tmp_bytes)), "spmm_csr")
+    tmp = None
+    if tmp_bytes.value:
+        tmp = torch.empty(tmp_bytes.value, dtype=torch.uint8, device=bb.device)
+    check(LIB.ofx_functional_spmm_csr_ex(current_stream_handle(bb), ctypes.byref(d_rp),
+                                         ctypes.byref(d_ci), ctypes.byref(d_v), int(a_num_rows),
+                                         int(a_num_cols), ctypes.byref(d_b), ctypes.byref(d_o),
+                                         tmp.data_ptr() if tmp is not None else None,
+                                         tmp_bytes.value, pid, pnum, axis, int(num_threads)),
+          "spmm_csr")
+    return out
+
+
+def balanced_range(total: int, parts: int, idx: int) -> tuple[int, int]:
+    lo, hi = ctypes.c_int64(), ctypes.c_int64()
+    check(LIB.ofx_balanced_range(total, parts, idx, ctypes.byref(lo), ctypes.byref(hi)),
+          "balanced_range")
+    return lo.value, hi.value
+
+
+def sbp_signatures() -> str:
+    buf = ctypes.create_string_buffer(4096)
+    check(LIB.ofx_op_spmm_csr_sbp_signatures(buf, len(buf)), "sbp")
+    return buf.value.decode()

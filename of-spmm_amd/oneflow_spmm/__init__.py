@@ -1,0 +1,16 @@
+"""oneflow_spmm — MI355X-native `spmm_csr` operator with OneFlow's user-op surface.
+
+    import oneflow_spmm as flow_spmm
+    out = flow_spmm.spmm(row_ptr, col_idx, values, num_rows, num_cols, b)   # oneflow.spmm
+    out = flow_spmm._C.spmm_csr(...)                                          # oneflow._C.spmm_csr
+
+Re-exports mirror python/oneflow/__init__.py:158-160 (`from oneflow._C import ... as mv`).
+"""
+from . import _C, _lib, ops, synth  # noqa: F401
+from ._C import spmm_csr
+from ._C import spmm_csr as spmm
+from ._lib import OfxError
+
+__version__ = _lib.LIB.ofx_version().decode()
+
+__all__ = ["spmm", "spmm_csr", "OfxError", "ops", "synth", "_C"]

@@ -1,0 +1,119 @@
+"""Loader of libofx_spmm.so (the C-ABI of include/ofx_spmm.h) with ctypes signatures.
+
+There is deliberately no fallback: if the native library is missing the import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libofx_spmm.so")
+
+# OneFlow DataType codes (oneflow/core/common/data_type.proto:4-26)
+DT_FLOAT, DT_DOUBLE, DT_INT32, DT_INT64, DT_FLOAT16, DT_BFLOAT16 = 2, 3, 5, 6, 9, 11
+
+OFX_OK, OFX_EINVAL, OFX_EDEVICE, OFX_ENOMEM, OFX_EUNSUPPORTED, OFX_ECOMM, OFX_EWORKSPACE = range(7)
+MEMCPY_H2D, MEMCPY_D2H, MEMCPY_D2D, MEMCPY_DEFAULT = 1, 2, 3, 4
+UNIQUE_ID_BYTES = 128
+
+
+class OfxError(RuntimeError):
+    """A failed C-ABI call; `code` is the ofx status."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+class Options(ctypes.Structure):
+    _fields_ = [("split_threshold", ctypes.c_int64), ("chunk", ctypes.c_int64),
+                ("ordered", ctypes.c_int32), ("variant", ctypes.c_int32)]
+
+
+class TensorDesc(ctypes.Structure):
+    _fields_ = [("dtype", ctypes.c_int32), ("device", ctypes.c_int32), ("ndim", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("shape", ctypes.c_int64 * 2),
+                ("stride", ctypes.c_int64 * 2), ("data", ctypes.c_void_p)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"oneflow_spmm: native library {LIB_PATH} is missing; build it with "
+            "`make -C of-spmm_amd` or `python -c 'import __graft_entry__ as g; g.build()'`. "
+            "There is no CPU/torch fallback for the HIP path.")
+    lib = ctypes.CDLL(LIB_PATH)
+    i32, i64, u64, p, sz = ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t
+    popt = ctypes.POINTER(Options)
+    pdesc = ctypes.POINTER(TensorDesc)
+    sigs = {
+        "ofx_last_error": ([], ctypes.c_char_p),
+        "ofx_version": ([], ctypes.c_char_p),
+        "ofx_spmm_default_split": ([i64], i64),
+        "ofx_spmm_csr_workspace_size": ([i32, i32, i64, i64, i64, i64, popt, ctypes.POINTER(sz)], i32),
+        "ofx_spmm_csr": ([p, i32, i32, i64, i64, i64, i64, p, p, p, p, i64, p, i64, i64, i64, p, sz,
+                          popt], i32),
+        "ofx_csr_validate": ([p, i32, i64, i64, i64, p, p, p], i32),
+        "ofx_spmm_csr_cpu": ([i32, i32, i32, i64, i64, i64, i64, p, p, p, p, i64, p, i64, i64, i64,
+                              popt], i32),
+        "ofx_balanced_range": ([i64, i64, i64, ctypes.POINTER(i64), ctypes.POINTER(i64)], i32),
+        "ofx_csr_row_slice": ([p, i32, p, i64, i64, p], i32),
+        "ofx_csr_row_slice_host": ([i32, p, i64, i64, p, ctypes.POINTER(i64), ctypes.POINTER(i64)], i32),
+        "ofx_device_count": ([ctypes.POINTER(i32)], i32),
+        "ofx_set_device": ([i32], i32),
+        "ofx_get_device": ([ctypes.POINTER(i32)], i32),
+        "ofx_device_synchronize": ([], i32),
+        "ofx_malloc": ([ctypes.POINTER(p), sz], i32),
+        "ofx_free": ([p], i32),
+        "ofx_host_malloc": ([ctypes.POINTER(p), sz], i32),
+        "ofx_host_free": ([p], i32),
+        "ofx_stream_create": ([ctypes.POINTER(p)], i32),
+        "ofx_stream_destroy": ([p], i32),
+        "ofx_stream_sync": ([p], i32),
+        "ofx_memcpy_async": ([p, p, p, sz, i32], i32),
+        "ofx_memset_async": ([p, p, i32, sz], i32),
+        "ofx_event_create": ([ctypes.POINTER(p), i32], i32),
+        "ofx_event_destroy": ([p], i32),
+        "ofx_event_record": ([p, p], i32),
+        "ofx_event_sync": ([p], i32),
+        "ofx_event_elapsed_ms": ([p, p, ctypes.POINTER(ctypes.c_float)], i32),
+        "ofx_stream_wait_event": ([p, p], i32),
+        "ofx_comm_get_unique_id": ([p], i32),
+        "ofx_comm_init_rank": ([ctypes.POINTER(p), i32, p, i32], i32),
+        "ofx_comm_destroy": ([p], i32),
+        "ofx_allgather": ([p, p, p, sz, i32, p], i32),
+        "ofx_synth_row_ptr": ([i64, i64, i64, ctypes.c_double, u64, p], i32),
+        "ofx_synth_columns": ([i64, i64, ctypes.c_double, u64, p, i64, i64, i32, p, i32], i32),
+        "ofx_synth_values_host": ([i32, i64, i64, u64, i32, p], i32),
+        "ofx_synth_dense": ([p, i32, i64, i64, i64, i64, u64, i32, p], i32),
+        "ofx_synth_dense_host": ([i32, i64, i64, i64, i64, u64, i32, p], i32),
+        "ofx_functional_spmm_csr_infer": ([pdesc, pdesc, pdesc, i64, i64, pdesc, pdesc], i32),
+        "ofx_functional_spmm_csr_tmp_size": ([pdesc, pdesc, pdesc, i64, i64, pdesc,
+                                              ctypes.POINTER(sz)], i32),
+        "ofx_functional_spmm_csr": ([p, pdesc, pdesc, pdesc, i64, i64, pdesc, pdesc, p, sz], i32),
+        "ofx_functional_spmm_csr_ex": ([p, pdesc, pdesc, pdesc, i64, i64, pdesc, pdesc, p, sz, i64,
+                                        i64, i32, i32], i32),
+        "ofx_op_spmm_csr_sbp_signatures": ([ctypes.c_char_p, sz], i32),
+    }
+    for name, (args, res) in sigs.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    return lib, tuple(sigs)
+
+
+LIB, EXPORTED = _load()
+
+
+def last_error() -> str:
+    return LIB.ofx_last_error().decode(errors="replace")
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc == OFX_OK:
+        return
+    msg = last_error()
+    if msg.startswith("TypeError"):
+        raise TypeError(msg)
+    raise OfxError(rc, f"{what}: {msg}" if what else msg)

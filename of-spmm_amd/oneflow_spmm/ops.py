@@ -1,0 +1,114 @@
+"""Direct C-ABI entry points (below the op layer): the device kernel with explicit schedule
+options and workspace, the CPU kernel, CSR validation and row slicing.  Used by the row-split
+wrapper, the benchmark and the parity tests; `oneflow_spmm.spmm` is the op-level API.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._C import current_stream_handle, dtype_code
+from ._lib import LIB, Options, check
+
+INT64_MAX = (1 << 63) - 1
+
+
+def make_options(split: int = 0, chunk: int = 0, ordered: bool = False, variant: int = 0) -> Options:
+    return Options(int(split), int(chunk), 1 if ordered else 0, int(variant))
+
+
+def default_split(n: int) -> int:
+    return int(LIB.ofx_spmm_default_split(int(n)))
+
+
+def workspace_size(idx_dtype: torch.dtype, val_dtype: torch.dtype, m: int, k: int, n: int, nnz: int,
+                   options: Options | None = None) -> int:
+    out = ctypes.c_size_t(0)
+    check(LIB.ofx_spmm_csr_workspace_size(dtype_code(idx_dtype), dtype_code(val_dtype), m, k, n, nnz,
+                                          ctypes.byref(options) if options else None,
+                                          ctypes.byref(out)), "workspace_size")
+    return out.value
+
+
+class SpmmCsrKernel:
+    """Holds the workspace for repeated launches of one problem shape (the OneFlow tmp buffer)."""
+
+    def __init__(self, m: int, k: int, n: int, nnz: int, idx_dtype: torch.dtype,
+                 val_dtype: torch.dtype, device, options: Options | None = None):
+        self.m, self.k, self.n, self.nnz = m, k, n, nnz
+        self.idx_dt, self.val_dt = dtype_code(idx_dtype), dtype_code(val_dtype)
+        self.options = options
+        ws = workspace_size(idx_dtype, val_dtype, m, k, n, nnz, options)
+        self.workspace = torch.empty(max(ws, 1), dtype=torch.uint8, device=device)
+        self.ws_bytes = ws
+
+    def __call__(self, row_ptr, col_idx, values, b, out, row_begin=0, row_end=None, stream=None):
+        row_end = self.m if row_end is None else row_end
+        s = stream if stream is not None else current_stream_handle(b)
+        check(LIB.ofx_spmm_csr(s, self.idx_dt, self.val_dt, self.m, self.k, self.n, self.nnz,
+                               row_ptr.data_ptr(), col_idx.data_ptr() if col_idx.numel() else None,
+                               values.data_ptr() if values.numel() else None,
+                               b.data_ptr() if b.numel() else None, b.stride(0), out.data_ptr(),
+                               out.stride(0), row_begin, row_end, self.workspace.data_ptr(),
+                               self.ws_bytes, ctypes.byref(self.options) if self.options else None),
+              "spmm_csr")
+        return out
+
+
+def spmm_csr_device(row_ptr, col_idx, values, b, m, k, *, out=None, row_begin=0, row_end=None,
+                    options: Options | None = None):
+    """One launch of the HIP kernel (C-ABI ofx_spmm_csr) on torch's current stream."""
+    if b.device.type != "cuda":
+        raise RuntimeError("spmm_csr_device: HIP kernel needs device tensors")
+    row_end = m if row_end is None else row_end
+    if out is None:
+        out = torch.empty((row_end - row_begin, b.shape[1]), dtype=b.dtype, device=b.device)
+    kern = SpmmCsrKernel(m, k, b.shape[1], col_idx.numel(), row_ptr.dtype, b.dtype, b.device, options)
+    return kern(row_ptr, col_idx, values, b, out, row_begin, row_end)
+
+
+def spmm_csr_cpu(row_ptr, col_idx, values, b, m, k, *, out=None, row_begin=0, row_end=None,
+                 options: Options | None = None, num_threads: int = 0):
+    """The DeviceType::kCPU kernel (C-ABI ofx_spmm_csr_cpu), host tensors."""
+    row_end = m if row_end is None else row_end
+    if out is None:
+        out = torch.empty((row_end - row_begin, b.shape[1]), dtype=b.dtype)
+    check(LIB.ofx_spmm_csr_cpu(int(num_threads), dtype_code(row_ptr.dtype), dtype_code(b.dtype), m, k,
+                               b.shape[1], col_idx.numel(), row_ptr.data_ptr(),
+                               col_idx.data_ptr() if col_idx.numel() else None,
+                               values.data_ptr() if values.numel() else None,
+                               b.data_ptr() if b.numel() else None, b.stride(0), out.data_ptr(),
+                               out.stride(0), row_begin, row_end,
+                               ctypes.byref(options) if options else None), "spmm_csr_cpu")
+    return out
+
+
+def validate_csr(row_ptr, col_idx, m, k) -> int:
+    """Device-side CSR check; returns 0 ok, 1 bad row_ptr, 2 column out of range (syncs)."""
+    flag = torch.zeros(1, dtype=torch.int32, device=row_ptr.device)
+    check(LIB.ofx_csr_validate(current_stream_handle(row_ptr), dtype_code(row_ptr.dtype), m, k,
+                               col_idx.numel(), row_ptr.data_ptr(),
+                               col_idx.data_ptr() if col_idx.numel() else None, flag.data_ptr()),
+          "csr_validate")
+    return int(flag.item())
+
+
+def csr_row_slice(row_ptr, row_begin: int, row_end: int):
+    """Rebased row_ptr of rows [row_begin, row_end) (+ the nnz range it covers)."""
+    out = torch.empty(row_end - row_begin + 1, dtype=row_ptr.dtype, device=row_ptr.device)
+    if row_ptr.device.type == "cpu":
+        lo, hi = ctypes.c_int64(), ctypes.c_int64()
+        check(LIB.ofx_csr_row_slice_host(dtype_code(row_ptr.dtype), row_ptr.data_ptr(), row_begin,
+                                         row_end, out.data_ptr(), ctypes.byref(lo), ctypes.byref(hi)),
+              "csr_row_slice")
+        return out, lo.value, hi.value
+    check(LIB.ofx_csr_row_slice(current_stream_handle(row_ptr), dtype_code(row_ptr.dtype),
+                                row_ptr.data_ptr(), row_begin, row_end, out.data_ptr()),
+          "csr_row_slice")
+    return out, None, None
+
+
+__all__ = ["make_options", "default_split", "workspace_size", "SpmmCsrKernel", "spmm_csr_device",
+           "spmm_csr_cpu", "validate_csr", "csr_row_slice", "INT64_MAX", "_lib"]

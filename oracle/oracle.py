@@ -1,0 +1,150 @@
+"""oracle.py — ctypes/numpy front end of the CPU SpMM restatement (spmm_oracle.c).
+
+TEST INFRASTRUCTURE ONLY.  Imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg as the *checker*; the product package (of-spmm_amd/oneflow_spmm) never imports
+it.  Parity status: unpinned against reference-held fixtures (the reference has no SpMM and no
+test pinning one); cross-validated against scipy.sparse and torch.sparse_csr
+(tests/golden/make_golden.py, tests/test_oracle.py).
+
+Semantics (see spmm_oracle.c header for the reference file:line anchors):
+  C[r, :] = sum_{j in row r, ascending} val[j] * B[col[j], :]   from +0, multiply then add.
+16-bit types are carried as numpy uint16 bit patterns (bf16) / float16 and computed in fp32,
+rounded once at the end (oneflow/user/kernels/unsorted_segment_sum_kernel.cpp:146-205).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+INT64_MAX = (1 << 63) - 1
+
+
+def build() -> str:
+    path = os.path.join(_HERE, "liboracle.so")
+    src = os.path.join(_HERE, "spmm_oracle.c")
+    if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return path
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        _LIB = ctypes.CDLL(build())
+        i64, p, c_int = ctypes.c_int64, ctypes.c_void_p, ctypes.c_int
+        _LIB.orc_spmm_f32.argtypes = [i64, i64, i64, p, p, p, p, i64, p, i64, i64, i64, i64, i64, c_int]
+        _LIB.orc_spmm_f64.argtypes = _LIB.orc_spmm_f32.argtypes
+        _LIB.orc_spmm_f32_ref64.argtypes = [i64, p, p, p, p, i64, p, p, i64, i64, c_int]
+        _LIB.orc_balanced_range.argtypes = [i64, i64, i64, ctypes.POINTER(i64), ctypes.POINTER(i64)]
+    return _LIB
+
+
+def default_split(n: int) -> int:
+    """Restates the operator's documented default hub-row threshold:
+    T = clamp(65536 // n, 128, 8192) rounded down to a power of two."""
+    t = 65536 // n if n > 0 else 8192
+    t = min(max(t, 128), 8192)
+    p = 128
+    while p * 2 <= t:
+        p *= 2
+    return p
+
+
+def balanced_range(total: int, parts: int, idx: int) -> tuple[int, int]:
+    lo, hi = ctypes.c_int64(), ctypes.c_int64()
+    lib().orc_balanced_range(total, parts, idx, ctypes.byref(lo), ctypes.byref(hi))
+    return lo.value, hi.value
+
+
+# ---- 16-bit helpers ------------------------------------------------------------------------
+def bf16_bits_to_f32(bits: np.ndarray) -> np.ndarray:
+    return (bits.astype(np.uint32) << 16).view(np.float32)
+
+
+def f32_to_bf16_bits(x: np.ndarray) -> np.ndarray:
+    """Round-to-nearest-even; NaN stays NaN."""
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    nan = (u & 0x7FFFFFFF) > 0x7F800000
+    r[nan] = ((u[nan] >> 16) | 0x40).astype(np.uint16)
+    return r
+
+
+def _schedule(n, split, chunk, ordered):
+    if ordered:
+        return INT64_MAX, INT64_MAX
+    s = split if split and split > 0 else default_split(n)
+    c = chunk if chunk and chunk > 0 else s
+    return s, min(c, s)
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def spmm(row_ptr, col_idx, values, b, *, dtype="f32", row_begin=0, row_end=None, split=0, chunk=0,
+         ordered=False, nthreads=None, k=None):
+    """Oracle SpMM.  dtype in {"f32","f64","bf16","f16"}; bf16 arrays are uint16 bit patterns.
+    Returns C rows [row_begin, row_end) in the storage dtype (bf16 -> uint16 bits)."""
+    m = len(row_ptr) - 1
+    row_end = m if row_end is None else row_end
+    n = b.shape[1]
+    k = b.shape[0] if k is None else k
+    rp = np.ascontiguousarray(row_ptr, dtype=np.int64)
+    ci = np.ascontiguousarray(col_idx, dtype=np.int64)
+    s, c = _schedule(n, split, chunk, ordered)
+    nt = nthreads or min(os.cpu_count() or 1, 16)
+    rows = row_end - row_begin
+    if dtype == "f64":
+        v = np.ascontiguousarray(values, dtype=np.float64)
+        bb = np.ascontiguousarray(b, dtype=np.float64)
+        out = np.zeros((rows, n), dtype=np.float64)
+        rc = lib().orc_spmm_f64(m, k, n, _p(rp), _p(ci), _p(v), _p(bb), n, _p(out), n,
+                                row_begin, row_end, s, c, nt)
+    else:
+        if dtype == "bf16":
+            v, bb = bf16_bits_to_f32(np.asarray(values)), bf16_bits_to_f32(np.asarray(b))
+        else:
+            v = np.asarray(values).astype(np.float32)
+            bb = np.asarray(b).astype(np.float32)
+        v, bb = np.ascontiguousarray(v), np.ascontiguousarray(bb)
+        out = np.zeros((rows, n), dtype=np.float32)
+        rc = lib().orc_spmm_f32(m, k, n, _p(rp), _p(ci), _p(v), _p(bb), n, _p(out), n,
+                                row_begin, row_end, s, c, nt)
+    if rc != 0:
+        raise ValueError("oracle: column index out of range")
+    if dtype == "bf16":
+        return f32_to_bf16_bits(out)
+    if dtype == "f16":
+        return out.astype(np.float16)
+    return out
+
+
+def ref64(row_ptr, col_idx, values_f32, b_f32, *, row_begin=0, row_end=None, nthreads=None):
+    """fp64 product C64 and |.|-sum bound of an fp32 (or upcast 16-bit) problem."""
+    m = len(row_ptr) - 1
+    row_end = m if row_end is None else row_end
+    n = b_f32.shape[1]
+    rp = np.ascontiguousarray(row_ptr, dtype=np.int64)
+    ci = np.ascontiguousarray(col_idx, dtype=np.int64)
+    v = np.ascontiguousarray(values_f32, dtype=np.float32)
+    bb = np.ascontiguousarray(b_f32, dtype=np.float32)
+    rows = row_end - row_begin
+    c64 = np.zeros((rows, n))
+    ab = np.zeros((rows, n))
+    lib().orc_spmm_f32_ref64(n, _p(rp), _p(ci), _p(v), _p(bb), n, _p(c64), _p(ab), row_begin,
+                             row_end, nthreads or min(os.cpu_count() or 1, 16))
+    return c64, ab
+
+
+def within_tolerance(c, c64, absum, rtol):
+    """|C - C64| <= rtol * absum + 1e-30 elementwise (SURVEY.md §8c acceptance)."""
+    err = np.abs(np.asarray(c, dtype=np.float64) - c64)
+    bound = rtol * absum + 1e-30
+    ok = err <= bound
+    return bool(ok.all()), float((err / (absum + 1e-30)).max(initial=0.0))

@@ -1,0 +1,156 @@
+/*
+ * spmm_oracle.c — CPU restatement of the reference's SpMM semantics.  TEST INFRASTRUCTURE ONLY:
+ * imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker;
+ * never linked into, or called by, the product (of-spmm_amd/).
+ *
+ * Parity status: the reference (OneFlow v0.8.1-dev) contains no SpMM and no test pinning one
+ *  -> "parity unpinned" against reference-held fixtures.  The restatement is
+ * anchored on the reference's own CPU building blocks and cross-checked against scipy.sparse and
+ * torch.sparse_csr in tests/golden/make_golden.py:
+ *
+ *   gather     oneflow/user/kernels/gather_kernel_util.cpp:72-92
+ *              out[i,:] = in[idx[i],:]   (CHECK_GE(idx, 0); rows outside the shard zero-filled)
+ *   multiply   elementwise val[i] * out[i,:]  (one fp rounding)
+ *   segsum     oneflow/user/kernels/unsorted_segment_sum_kernel_util.cpp:29-45
+ *              out zero-filled (Memset, unsorted_segment_sum_kernel.cpp:95-96), then for i in
+ *              ascending order: to = to + from  (std::transform with std::plus<T>)
+ *   split      BalancedSplitter::At, oneflow/core/common/balanced_splitter.cpp:20-40
+ *
+ * Composed over a CSR (segment id of nonzero j = its row): C[r,:] = sum_j val[j]*B[col[j],:],
+ * accumulated from +0 in ascending j with a multiply rounding and an add rounding per term.
+ * `split`/`chunk` reproduce the operator's documented hub-row schedule so the
+ * device result can be checked bit-for-bit; split = INT64_MAX is the pure reference order.
+ *
+ * Build: `make -C oracle` (gcc, OpenMP) -> oracle/liboracle.so.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#pragma GCC optimize("no-fast-math")
+
+/* balanced_splitter.cpp:20-40: first (total % parts) parts get one extra element. */
+void orc_balanced_range(int64_t total, int64_t parts, int64_t idx, int64_t* lo, int64_t* hi) {
+  const int64_t base = total / parts;
+  const int64_t rem = total % parts;
+  if (idx < rem) {
+    *lo = (base + 1) * idx;
+    *hi = *lo + base + 1;
+  } else {
+    *lo = (base + 1) * rem + base * (idx - rem);
+    *hi = *lo + base;
+  }
+}
+
+/* One segment [j0, j1) of row sums, f32 mul-then-add, from +0 (gather -> mul -> segsum). */
+static void seg_f32(const int64_t* col, const float* val, const float* b, int64_t ldb, int64_t n,
+                    int64_t j0, int64_t j1, float* acc) {
+  for (int64_t c = 0; c < n; ++c) acc[c] = 0.0f;
+  for (int64_t j = j0; j < j1; ++j) {
+    const float* from = b + col[j] * ldb; /* gather */
+    for (int64_t c = 0; c < n; ++c) {
+      const float prod = val[j] * from[c]; /* multiply (rounded; built -ffp-contract=off) */
+      acc[c] = acc[c] + prod;              /* segment-sum */
+    }
+  }
+}
+
+static void seg_f64(const int64_t* col, const double* val, const double* b, int64_t ldb,
+                    int64_t n, int64_t j0, int64_t j1, double* acc) {
+  for (int64_t c = 0; c < n; ++c) acc[c] = 0.0;
+  for (int64_t j = j0; j < j1; ++j) {
+    const double* from = b + col[j] * ldb;
+    for (int64_t c = 0; c < n; ++c) {
+      const double prod = val[j] * from[c];
+      acc[c] = acc[c] + prod;
+    }
+  }
+}
+
+/* C (rows [row_begin,row_end), written from C[0]) = A @ B in f32 with the given schedule.
+ * Returns 0, or -1 on an out-of-range column (the reference's CHECK_GE / bounds). */
+int orc_spmm_f32(int64_t m, int64_t k, int64_t n, const int64_t* rp, const int64_t* col,
+                 const float* val, const float* b, int64_t ldb, float* c, int64_t ldc,
+                 int64_t row_begin, int64_t row_end, int64_t split, int64_t chunk,
+                 int nthreads) {
+  int bad = 0;
+  (void)m;
+  for (int64_t j = rp[row_begin]; j < rp[row_end]; ++j)
+    if (col[j] < 0 || col[j] >= k) bad = 1;
+  if (bad) return -1;
+#pragma omp parallel num_threads(nthreads)
+  {
+    float* part = (float*)__builtin_alloca(sizeof(float) * (n > 0 ? n : 1));
+#pragma omp for schedule(dynamic, 64)
+    for (int64_t r = row_begin; r < row_end; ++r) {
+      float* out = c + (r - row_begin) * ldc;
+      const int64_t j0 = rp[r], j1 = rp[r + 1], len = j1 - j0;
+      if (len <= split) {
+        seg_f32(col, val, b, ldb, n, j0, j1, out);
+      } else {
+        const int64_t nc = len / chunk;
+        for (int64_t x = 0; x < n; ++x) out[x] = 0.0f;
+        for (int64_t q = 0; q < nc; ++q) {
+          const int64_t a = j0 + q * chunk;
+          const int64_t e = (q == nc - 1) ? j1 : a + chunk;
+          seg_f32(col, val, b, ldb, n, a, e, part);
+          for (int64_t x = 0; x < n; ++x) out[x] = out[x] + part[x];
+        }
+      }
+    }
+  }
+  return 0;
+}
+
+int orc_spmm_f64(int64_t m, int64_t k, int64_t n, const int64_t* rp, const int64_t* col,
+                 const double* val, const double* b, int64_t ldb, double* c, int64_t ldc,
+                 int64_t row_begin, int64_t row_end, int64_t split, int64_t chunk,
+                 int nthreads) {
+  int bad = 0;
+  (void)m;
+  for (int64_t j = rp[row_begin]; j < rp[row_end]; ++j)
+    if (col[j] < 0 || col[j] >= k) bad = 1;
+  if (bad) return -1;
+#pragma omp parallel num_threads(nthreads)
+  {
+    double* part = (double*)__builtin_alloca(sizeof(double) * (n > 0 ? n : 1));
+#pragma omp for schedule(dynamic, 64)
+    for (int64_t r = row_begin; r < row_end; ++r) {
+      double* out = c + (r - row_begin) * ldc;
+      const int64_t j0 = rp[r], j1 = rp[r + 1], len = j1 - j0;
+      if (len <= split) {
+        seg_f64(col, val, b, ldb, n, j0, j1, out);
+      } else {
+        const int64_t nc = len / chunk;
+        for (int64_t x = 0; x < n; ++x) out[x] = 0.0;
+        for (int64_t q = 0; q < nc; ++q) {
+          const int64_t a = j0 + q * chunk;
+          const int64_t e = (q == nc - 1) ? j1 : a + chunk;
+          seg_f64(col, val, b, ldb, n, a, e, part);
+          for (int64_t x = 0; x < n; ++x) out[x] = out[x] + part[x];
+        }
+      }
+    }
+  }
+  return 0;
+}
+
+/* fp64 reference of an f32 problem (C64) and the |.|-sum bound sum_j |val_j|*|B_col_j,c|,
+ * used by the tolerance check |C - C64| <= rtol * absum. */
+void orc_spmm_f32_ref64(int64_t n, const int64_t* rp, const int64_t* col, const float* val,
+                        const float* b, int64_t ldb, double* c64, double* absum,
+                        int64_t row_begin, int64_t row_end, int nthreads) {
+#pragma omp parallel for schedule(dynamic, 64) num_threads(nthreads)
+  for (int64_t r = row_begin; r < row_end; ++r) {
+    double* o = c64 + (r - row_begin) * n;
+    double* a = absum + (r - row_begin) * n;
+    for (int64_t x = 0; x < n; ++x) o[x] = a[x] = 0.0;
+    for (int64_t j = rp[r]; j < rp[r + 1]; ++j) {
+      const float* from = b + col[j] * ldb;
+      for (int64_t x = 0; x < n; ++x) {
+        o[x] += (double)val[j] * (double)from[x];
+        a[x] += fabs((double)val[j]) * fabs((double)from[x]);
+      }
+    }
+  }
+}
