@@ -40,16 +40,11 @@ constexpr int kBlock = 256;        // 4 waves
 constexpr int kWavesPerBlock = kBlock / 64;
 constexpr int kUnroll = 8;         // B-row loads in flight per lane
 constexpr int64_t kMaxChunkBlocks = 1024;  // blocks that grid-stride over hub-row chunks
-constexpr int64_t kMaxReduceBlocks = 2048;
+constexpr int64_t kMaxReduceBlocks = 16384;
 
 template <typename T, int VEC>
 struct alignas(sizeof(T) * VEC) Pack {
   T v[VEC];
-};
-
-template <typename A, int VEC>
-struct alignas(sizeof(A) * VEC > 16 ? 16 : sizeof(A) * VEC) AccPack {
-  A v[VEC];
 };
 
 __device__ __forceinline__ int32_t shfl(int32_t v, int src) { return __shfl(v, src); }
@@ -143,26 +138,129 @@ __device__ __forceinline__ void store_partial(A* __restrict__ p, const A (&acc)[
   for (int e = 0; e < VEC; ++e) p[e] = acc[e];
 }
 
-// ---- hub-row planning ----------------------------------------------------------------------
-// counters[0] = chunk items appended, counters[1] = hub rows appended.
-// hubs[3i..3i+2] = {local row, first item slot, number of chunks}; items[2s..2s+1] = {local row, chunk}.
+// ---- hub-row planning (three small launches, no contended atomics) --------------------------
+// Rows are taken kPlanRows per block.  plan_count: per-block (hubs, chunks) totals.  plan_scan:
+// one block turns them into exclusive offsets and writes the totals to counters[0] (= chunk
+// items) and counters[1] (= hub rows).  plan_write: each block re-derives its rows' flags, scans
+// them in LDS and writes hubs[3i..3i+2] = {local row, first item slot, chunks} and
+// items[2s..2s+1] = {local row, chunk} in ascending row order (deterministic layout).
+constexpr int kPlanRowsPerThread = 4;
+constexpr int64_t kPlanRows = (int64_t)kBlock * kPlanRowsPerThread;
+
+template <typename I>
+__device__ __forceinline__ void plan_row(const I* __restrict__ rp, int64_t row_begin, int64_t nrows,
+                                         int64_t g, int64_t split, int64_t chunk, int64_t& hub,
+                                         int64_t& nc) {
+  hub = 0;
+  nc = 0;
+  if (g < nrows) {
+    const int64_t len = (int64_t)rp[row_begin + g + 1] - (int64_t)rp[row_begin + g];
+    if (len > split) {
+      hub = 1;
+      nc = num_chunks(len, chunk);
+    }
+  }
+}
+
+// Block-wide exclusive scan of two int64 values (256 threads); returns the block totals.
+__device__ __forceinline__ void block_scan2(int64_t& a, int64_t& b, int64_t& tot_a, int64_t& tot_b) {
+  __shared__ int64_t sa[kBlock], sb[kBlock];
+  const int t = threadIdx.x;
+  sa[t] = a;
+  sb[t] = b;
+  __syncthreads();
+  for (int off = 1; off < kBlock; off <<= 1) {
+    const int64_t xa = t >= off ? sa[t - off] : 0;
+    const int64_t xb = t >= off ? sb[t - off] : 0;
+    __syncthreads();
+    sa[t] += xa;
+    sb[t] += xb;
+    __syncthreads();
+  }
+  tot_a = sa[kBlock - 1];
+  tot_b = sb[kBlock - 1];
+  a = sa[t] - a;  // exclusive
+  b = sb[t] - b;
+  __syncthreads();
+}
+
 template <typename I>
 __global__ void __launch_bounds__(kBlock)
-    spmm_plan_kernel(const I* __restrict__ rp, int64_t row_begin, int64_t nrows, int64_t split,
-                     int64_t chunk, unsigned long long* counters, int64_t* hubs, int64_t* items) {
-  const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (g >= nrows) return;
-  const int64_t len = (int64_t)rp[row_begin + g + 1] - (int64_t)rp[row_begin + g];
-  if (len <= split) return;
-  const int64_t nc = num_chunks(len, chunk);
-  const int64_t slot = (int64_t)atomicAdd(&counters[0], (unsigned long long)nc);
-  const int64_t hi = (int64_t)atomicAdd(&counters[1], 1ull);
-  hubs[3 * hi + 0] = g;
-  hubs[3 * hi + 1] = slot;
-  hubs[3 * hi + 2] = nc;
-  for (int64_t c = 0; c < nc; ++c) {
-    items[2 * (slot + c) + 0] = g;
-    items[2 * (slot + c) + 1] = c;
+    spmm_plan_count_kernel(const I* __restrict__ rp, int64_t row_begin, int64_t nrows,
+                           int64_t split, int64_t chunk, int64_t* __restrict__ block_tot) {
+  int64_t hubs = 0, chunks = 0;
+  const int64_t base = (int64_t)blockIdx.x * kPlanRows + (int64_t)threadIdx.x * kPlanRowsPerThread;
+#pragma unroll
+  for (int q = 0; q < kPlanRowsPerThread; ++q) {
+    int64_t h, nc;
+    plan_row(rp, row_begin, nrows, base + q, split, chunk, h, nc);
+    hubs += h;
+    chunks += nc;
+  }
+  int64_t th, tc;
+  block_scan2(hubs, chunks, th, tc);
+  if (threadIdx.x == 0) {
+    block_tot[2 * blockIdx.x + 0] = th;
+    block_tot[2 * blockIdx.x + 1] = tc;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock)
+    spmm_plan_scan_kernel(int64_t* __restrict__ block_tot, int64_t nblocks,
+                          unsigned long long* __restrict__ counters) {
+  int64_t carry_h = 0, carry_c = 0;
+  for (int64_t b0 = 0; b0 < nblocks; b0 += kBlock) {
+    const int64_t b = b0 + threadIdx.x;
+    int64_t h = b < nblocks ? block_tot[2 * b] : 0;
+    int64_t c = b < nblocks ? block_tot[2 * b + 1] : 0;
+    int64_t th, tc;
+    block_scan2(h, c, th, tc);
+    if (b < nblocks) {
+      block_tot[2 * b] = carry_h + h;
+      block_tot[2 * b + 1] = carry_c + c;
+    }
+    carry_h += th;
+    carry_c += tc;
+  }
+  if (threadIdx.x == 0) {
+    counters[0] = (unsigned long long)carry_c;
+    counters[1] = (unsigned long long)carry_h;
+  }
+}
+
+template <typename I>
+__global__ void __launch_bounds__(kBlock)
+    spmm_plan_write_kernel(const I* __restrict__ rp, int64_t row_begin, int64_t nrows,
+                           int64_t split, int64_t chunk, const int64_t* __restrict__ block_off,
+                           int64_t* __restrict__ hubs, int64_t* __restrict__ items) {
+  int64_t h[kPlanRowsPerThread], nc[kPlanRowsPerThread];
+  int64_t sum_h = 0, sum_c = 0;
+  const int64_t base = (int64_t)blockIdx.x * kPlanRows + (int64_t)threadIdx.x * kPlanRowsPerThread;
+#pragma unroll
+  for (int q = 0; q < kPlanRowsPerThread; ++q) {
+    plan_row(rp, row_begin, nrows, base + q, split, chunk, h[q], nc[q]);
+    sum_h += h[q];
+    sum_c += nc[q];
+  }
+  int64_t th, tc;
+  block_scan2(sum_h, sum_c, th, tc);
+  if (th == 0) return;  // block-uniform
+  int64_t hi = block_off[2 * blockIdx.x] + sum_h;
+  int64_t slot = block_off[2 * blockIdx.x + 1] + sum_c;
+#pragma unroll
+  for (int q = 0; q < kPlanRowsPerThread; ++q) {
+    if (h[q]) {
+      const int64_t g = base + q;
+      hubs[3 * hi + 0] = g;
+      hubs[3 * hi + 1] = slot;
+      hubs[3 * hi + 2] = nc[q];
+      for (int64_t c = 0; c < nc[q]; ++c) {
+        items[2 * (slot + c) + 0] = g;
+        items[2 * (slot + c) + 1] = c;
+      }
+      ++hi;
+      slot += nc[q];
+    }
   }
 }
 
@@ -242,14 +340,24 @@ __global__ void __launch_bounds__(kBlock)
                        int64_t ldc, int64_t n) {
 #pragma clang fp contract(off)
   using A = typename Num<T>::acc;
+  constexpr int kPre = 16;  // partial rows in flight per thread (the adds stay in chunk order)
   const int64_t nhubs = (int64_t)counters[1];
   for (int64_t h = blockIdx.x; h < nhubs; h += gridDim.x) {
     const int64_t lr = hubs[3 * h + 0];
     const int64_t slot = hubs[3 * h + 1];
     const int64_t nc = hubs[3 * h + 2];
     for (int64_t c = threadIdx.x; c < n; c += kBlock) {
+      const A* p = part + slot * n + c;
       A acc = A(0);
-      for (int64_t k = 0; k < nc; ++k) acc = acc + part[(slot + k) * n + c];
+      int64_t q = 0;
+      for (; q + kPre <= nc; q += kPre) {
+        A v[kPre];
+#pragma unroll
+        for (int u = 0; u < kPre; ++u) v[u] = p[(q + u) * n];
+#pragma unroll
+        for (int u = 0; u < kPre; ++u) acc = acc + v[u];
+      }
+      for (; q < nc; ++q) acc = acc + p[q * n];
       C[lr * ldc + c] = Num<T>::store(acc);
     }
   }
@@ -307,18 +415,21 @@ struct Launch {
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 struct WsLayout {
-  size_t counters, hubs, items, part, total;
-  int64_t max_hubs, max_items;
+  size_t counters, block_tot, hubs, items, part, total;
+  int64_t max_hubs, max_items, plan_blocks;
 };
 
-WsLayout ws_layout(int64_t nnz, int64_t n, size_t acc_bytes, const Schedule& s) {
+WsLayout ws_layout(int64_t nrows, int64_t nnz, int64_t n, size_t acc_bytes, const Schedule& s) {
   WsLayout w{};
   if (s.split == INT64_MAX || nnz <= s.split) return w;  // no row can be split
   w.max_hubs = nnz / (s.split + 1) + 1;
   w.max_items = nnz / s.chunk + 1;
+  w.plan_blocks = (nrows + kPlanRows - 1) / kPlanRows;
   size_t off = 0;
   w.counters = off;
   off = align_up(off + 2 * sizeof(unsigned long long), 256);
+  w.block_tot = off;
+  off = align_up(off + (size_t)w.plan_blocks * 2 * sizeof(int64_t), 256);
   w.hubs = off;
   off = align_up(off + (size_t)w.max_hubs * 3 * sizeof(int64_t), 256);
   w.items = off;
@@ -358,7 +469,7 @@ int launch_cfg(const Launch& L) {
   const T* val = static_cast<const T*>(L.val);
   const T* B = static_cast<const T*>(L.b);
   T* C = static_cast<T*>(L.c);
-  const WsLayout w = ws_layout(L.nnz, L.n, sizeof(A), L.sched);
+  const WsLayout w = ws_layout(L.nrows, L.nnz, L.n, sizeof(A), L.sched);
   const bool hubs = w.total > 0;
   unsigned long long* counters = nullptr;
   int64_t *hub = nullptr, *items = nullptr;
@@ -373,10 +484,16 @@ int launch_cfg(const Launch& L) {
     hub = reinterpret_cast<int64_t*>(ws + w.hubs);
     items = reinterpret_cast<int64_t*>(ws + w.items);
     part = reinterpret_cast<A*>(ws + w.part);
-    OFX_HIP_CHECK(hipMemsetAsync(counters, 0, 2 * sizeof(unsigned long long), L.stream));
-    const int64_t pgrid = (L.nrows + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL((spmm_plan_kernel<I>), dim3((unsigned)pgrid), dim3(kBlock), 0, L.stream, rp,
-                       L.row_begin, L.nrows, L.sched.split, L.sched.chunk, counters, hub, items);
+    auto* block_tot = reinterpret_cast<int64_t*>(ws + w.block_tot);
+    const unsigned pgrid = (unsigned)w.plan_blocks;
+    hipLaunchKernelGGL((spmm_plan_count_kernel<I>), dim3(pgrid), dim3(kBlock), 0, L.stream, rp,
+                       L.row_begin, L.nrows, L.sched.split, L.sched.chunk, block_tot);
+    OFX_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(spmm_plan_scan_kernel, dim3(1), dim3(kBlock), 0, L.stream, block_tot,
+                       w.plan_blocks, counters);
+    OFX_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL((spmm_plan_write_kernel<I>), dim3(pgrid), dim3(kBlock), 0, L.stream, rp,
+                       L.row_begin, L.nrows, L.sched.split, L.sched.chunk, block_tot, hub, items);
     OFX_HIP_CHECK(hipGetLastError());
     chunk_blocks = (w.max_items + GPB - 1) / GPB;
     if (chunk_blocks > kMaxChunkBlocks) chunk_blocks = kMaxChunkBlocks;
@@ -474,7 +591,7 @@ extern "C" int ofx_spmm_csr_workspace_size(int idx_dtype, int val_dtype, int64_t
   int rc = check_common(idx_dtype, val_dtype, m, k, n, nnz);
   if (rc) return rc;
   const Schedule s = resolve_schedule(n, opts);
-  *bytes = ws_layout(nnz, n, acc_bytes_of(val_dtype), s).total;
+  *bytes = ws_layout(m, nnz, n, acc_bytes_of(val_dtype), s).total;
   return OFX_OK;
 }
 
