@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <type_traits>
 
 #include "ofx_internal.h"
 #include "spmm_common.h"
@@ -37,14 +38,64 @@ namespace ofx {
 namespace {
 
 constexpr int kBlock = 256;        // 4 waves
-constexpr int kWavesPerBlock = kBlock / 64;
-constexpr int kUnroll = 8;         // B-row loads in flight per lane
 constexpr int64_t kMaxChunkBlocks = 1024;  // blocks that grid-stride over hub-row chunks
 constexpr int64_t kMaxReduceBlocks = 16384;
 
 template <typename T, int VEC>
 struct alignas(sizeof(T) * VEC) Pack {
   T v[VEC];
+};
+
+// Compile-time kernel configuration: VEC elements per lane, LPR lanes per row-group, U B-row
+// loads in flight per lane, WPB waves per block, NT = non-temporal hints on the once-touched
+// streams (col_idx, values, C) so they do not displace B rows from L2 / Infinity Cache.
+template <int VEC_, int LPR_, int U_ = 8, int WPB_ = 4, bool NT_ = false>
+struct Cfg {
+  static constexpr int VEC = VEC_, LPR = LPR_, U = U_, WPB = WPB_;
+  static constexpr bool NT = NT_;
+};
+
+template <typename X>
+struct RawOf {
+  using type = X;
+};
+template <>
+struct RawOf<bf16> {
+  using type = uint16_t;
+};
+template <>
+struct RawOf<f16> {
+  using type = uint16_t;
+};
+
+template <bool NT, typename X>
+__device__ __forceinline__ X ld_stream(const X* p) {
+  if constexpr (NT) {
+    using R = typename RawOf<X>::type;
+    const R r = __builtin_nontemporal_load(reinterpret_cast<const R*>(p));
+    return __builtin_bit_cast(X, r);
+  } else {
+    return *p;
+  }
+}
+
+template <int BYTES>
+struct RawVec;
+template <>
+struct RawVec<16> {
+  typedef uint32_t type __attribute__((ext_vector_type(4)));
+};
+template <>
+struct RawVec<8> {
+  typedef uint32_t type __attribute__((ext_vector_type(2)));
+};
+template <>
+struct RawVec<4> {
+  typedef uint32_t type;
+};
+template <>
+struct RawVec<2> {
+  typedef uint16_t type;
 };
 
 __device__ __forceinline__ int32_t shfl(int32_t v, int src) { return __shfl(v, src); }
@@ -63,12 +114,13 @@ __device__ __forceinline__ int64_t uniform64(int64_t v) {
 
 // acc[e] += val[j] * B[col[j], cc + e] for j in [j0, j1), in ascending j, mul then add.
 // Bc = B + cc.  All lanes of a group call this with the same j0/j1.
-template <typename T, typename I, int VEC, int LPR>
+template <typename T, typename I, typename K>
 __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* __restrict__ val,
                                            const T* __restrict__ Bc, int64_t ldb, int64_t j0,
                                            int64_t j1, int gl, int gbase, bool active,
-                                           typename Num<T>::acc (&acc)[VEC]) {
+                                           typename Num<T>::acc (&acc)[K::VEC]) {
 #pragma clang fp contract(off)
+  constexpr int VEC = K::VEC, LPR = K::LPR, kUnroll = K::U;
   using A = typename Num<T>::acc;
   using P = Pack<T, VEC>;
   if constexpr (LPR == 64) {
@@ -80,8 +132,8 @@ __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* _
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         if (u < cnt) {
-          const int64_t cu = (int64_t)col[j + u];
-          vv[u] = Num<T>::load(val[j + u]);
+          const int64_t cu = (int64_t)ld_stream<K::NT>(col + j + u);
+          vv[u] = Num<T>::load(ld_stream<K::NT>(val + j + u));
           if (active) bv[u] = *reinterpret_cast<const P*>(Bc + cu * ldb);
         }
       }
@@ -99,8 +151,8 @@ __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* _
       I myc = 0;
       A myv = 0;
       if (gl < cnt) {
-        myc = col[jb + gl];
-        myv = Num<T>::load(val[jb + gl]);
+        myc = ld_stream<K::NT>(col + jb + gl);
+        myv = Num<T>::load(ld_stream<K::NT>(val + jb + gl));
       }
       for (int k = 0; k < cnt; k += kUnroll) {
         P bv[kUnroll];
@@ -124,12 +176,17 @@ __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* _
   }
 }
 
-template <typename T, int VEC>
+template <typename T, int VEC, bool NT>
 __device__ __forceinline__ void store_row(T* __restrict__ p, const typename Num<T>::acc (&acc)[VEC]) {
   Pack<T, VEC> o;
 #pragma unroll
   for (int e = 0; e < VEC; ++e) o.v[e] = Num<T>::store(acc[e]);
-  *reinterpret_cast<Pack<T, VEC>*>(p) = o;
+  if constexpr (NT && (sizeof(o) == 16 || sizeof(o) == 8 || sizeof(o) == 4 || sizeof(o) == 2)) {
+    using R = typename RawVec<sizeof(o)>::type;
+    __builtin_nontemporal_store(__builtin_bit_cast(R, o), reinterpret_cast<R*>(p));
+  } else {
+    *reinterpret_cast<Pack<T, VEC>*>(p) = o;
+  }
 }
 
 template <typename A, int VEC>
@@ -265,8 +322,8 @@ __global__ void __launch_bounds__(kBlock)
 }
 
 // ---- main kernel: hub-row chunks (first `chunk_blocks` blocks) + ordinary rows ---------------
-template <typename T, typename I, int VEC, int LPR>
-__global__ void __launch_bounds__(kBlock)
+template <typename T, typename I, typename K>
+__global__ void __launch_bounds__(64 * K::WPB)
     spmm_main_kernel(const I* __restrict__ rp, const I* __restrict__ col,
                      const T* __restrict__ val, const T* __restrict__ B, int64_t ldb,
                      T* __restrict__ C, int64_t ldc, int64_t row_begin, int64_t nrows, int64_t n,
@@ -274,8 +331,9 @@ __global__ void __launch_bounds__(kBlock)
                      const unsigned long long* __restrict__ counters,
                      const int64_t* __restrict__ items, typename Num<T>::acc* __restrict__ part) {
   using A = typename Num<T>::acc;
+  constexpr int VEC = K::VEC, LPR = K::LPR, kWaves = K::WPB;
   constexpr int GPW = 64 / LPR;
-  constexpr int GPB = kWavesPerBlock * GPW;
+  constexpr int GPB = kWaves * GPW;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int gl = lane & (LPR - 1);
@@ -285,7 +343,7 @@ __global__ void __launch_bounds__(kBlock)
     // Hub-row chunks: grid-stride over the planned items -> fp32/fp64 partial rows.
     const int64_t nitems = (int64_t)counters[0];
     const int64_t stride = chunk_blocks * GPB;
-    for (int64_t s = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * GPW + gsub; s < nitems;
+    for (int64_t s = ((int64_t)blockIdx.x * kWaves + wave) * GPW + gsub; s < nitems;
          s += stride) {
       int64_t lr = items[2 * s + 0];
       int64_t c = items[2 * s + 1];
@@ -304,14 +362,14 @@ __global__ void __launch_bounds__(kBlock)
         A acc[VEC];
 #pragma unroll
         for (int e = 0; e < VEC; ++e) acc[e] = A(0);
-        accumulate<T, I, VEC, LPR>(col, val, B + cc, ldb, j0, j1, gl, gbase, active, acc);
+        accumulate<T, I, K>(col, val, B + cc, ldb, j0, j1, gl, gbase, active, acc);
         if (active) store_partial<A, VEC>(part + s * n + cc, acc);
       }
     }
     return;
   }
   // Ordinary rows: one lane-group per row.
-  const int64_t g = (((int64_t)blockIdx.x - chunk_blocks) * kWavesPerBlock + wave) * GPW + gsub;
+  const int64_t g = (((int64_t)blockIdx.x - chunk_blocks) * kWaves + wave) * GPW + gsub;
   if (g >= nrows) return;
   const int64_t r = row_begin + g;
   int64_t j0 = (int64_t)rp[r];
@@ -327,8 +385,8 @@ __global__ void __launch_bounds__(kBlock)
     A acc[VEC];
 #pragma unroll
     for (int e = 0; e < VEC; ++e) acc[e] = A(0);
-    accumulate<T, I, VEC, LPR>(col, val, B + cc, ldb, j0, j1, gl, gbase, active, acc);
-    if (active) store_row<T, VEC>(C + g * ldc + cc, acc);
+    accumulate<T, I, K>(col, val, B + cc, ldb, j0, j1, gl, gbase, active, acc);
+    if (active) store_row<T, VEC, K::NT>(C + g * ldc + cc, acc);
   }
 }
 
@@ -459,11 +517,11 @@ int pick_lpr(int64_t n, int vec) {
   return l;
 }
 
-template <typename T, typename I, int VEC, int LPR>
+template <typename T, typename I, typename K>
 int launch_cfg(const Launch& L) {
   using A = typename Num<T>::acc;
-  constexpr int GPW = 64 / LPR;
-  constexpr int64_t GPB = (int64_t)kWavesPerBlock * GPW;  // lane-groups per block
+  constexpr int GPW = 64 / K::LPR;
+  constexpr int64_t GPB = (int64_t)K::WPB * GPW;  // lane-groups per block
   const I* rp = static_cast<const I*>(L.rp);
   const I* col = static_cast<const I*>(L.col);
   const T* val = static_cast<const T*>(L.val);
@@ -501,7 +559,7 @@ int launch_cfg(const Launch& L) {
   const int64_t grid = chunk_blocks + (L.nrows + GPB - 1) / GPB;
   OFX_REQUIRE(grid < (int64_t)UINT32_MAX, OFX_EINVAL, "spmm_csr: too many rows (%lld)",
               (long long)L.nrows);
-  hipLaunchKernelGGL((spmm_main_kernel<T, I, VEC, LPR>), dim3((unsigned)grid), dim3(kBlock), 0,
+  hipLaunchKernelGGL((spmm_main_kernel<T, I, K>), dim3((unsigned)grid), dim3(64 * K::WPB), 0,
                      L.stream, rp, col, val, B, L.ldb, C, L.ldc, L.row_begin, L.nrows, L.n,
                      hubs ? L.sched.split : INT64_MAX, hubs ? L.sched.chunk : INT64_MAX,
                      chunk_blocks, counters, items, part);
@@ -518,17 +576,43 @@ int launch_cfg(const Launch& L) {
 template <typename T, typename I, int VEC>
 int launch_vec(const Launch& L, int lpr) {
   switch (lpr) {
-    case 4: return launch_cfg<T, I, VEC, 4>(L);
-    case 8: return launch_cfg<T, I, VEC, 8>(L);
-    case 16: return launch_cfg<T, I, VEC, 16>(L);
-    case 32: return launch_cfg<T, I, VEC, 32>(L);
-    case 64: return launch_cfg<T, I, VEC, 64>(L);
+    case 4: return launch_cfg<T, I, Cfg<VEC, 4>>(L);
+    case 8: return launch_cfg<T, I, Cfg<VEC, 8>>(L);
+    case 16: return launch_cfg<T, I, Cfg<VEC, 16>>(L);
+    case 32: return launch_cfg<T, I, Cfg<VEC, 32>>(L);
+    case 64: return launch_cfg<T, I, Cfg<VEC, 64>>(L);
     default: return fail(OFX_EINVAL, "spmm_csr: unsupported lanes-per-row %d", lpr);
   }
 }
 
+// Tuning table (variant = 10000 + id), float values / int32 indices only; every entry computes the
+// same bits (the accumulation order does not depend on the launch shape).
+template <typename T, typename I>
+int launch_tuned(const Launch& L, int id) {
+  if constexpr (std::is_same<T, float>::value && std::is_same<I, int32_t>::value) {
+    OFX_REQUIRE(L.n % 4 == 0 && L.ldb % 4 == 0 && L.ldc % 4 == 0 && ((uintptr_t)L.b % 16) == 0 &&
+                    ((uintptr_t)L.c % 16) == 0,
+                OFX_EINVAL, "spmm_csr: tuning variant %d needs 16-B aligned rows", L.sched.variant);
+    switch (id) {
+      case 1: return launch_cfg<T, I, Cfg<4, 32, 8, 4, false>>(L);
+      case 2: return launch_cfg<T, I, Cfg<4, 32, 8, 4, true>>(L);
+      case 3: return launch_cfg<T, I, Cfg<4, 32, 8, 1, false>>(L);
+      case 4: return launch_cfg<T, I, Cfg<4, 32, 16, 4, false>>(L);
+      case 5: return launch_cfg<T, I, Cfg<4, 32, 4, 4, false>>(L);
+      case 6: return launch_cfg<T, I, Cfg<4, 32, 8, 2, true>>(L);
+      case 7: return launch_cfg<T, I, Cfg<4, 32, 8, 8, false>>(L);
+      case 8: return launch_cfg<T, I, Cfg<4, 32, 16, 4, true>>(L);
+      case 9: return launch_cfg<T, I, Cfg<4, 16, 8, 4, false>>(L);
+      case 10: return launch_cfg<T, I, Cfg<4, 16, 8, 4, true>>(L);
+      default: break;
+    }
+  }
+  return fail(OFX_EINVAL, "spmm_csr: unknown tuning variant %d for this dtype", L.sched.variant);
+}
+
 template <typename T, typename I>
 int launch_typed(const Launch& L) {
+  if (L.sched.variant >= 10000) return launch_tuned<T, I>(L, L.sched.variant - 10000);
   // variant = VEC * 100 + LPR forces a configuration (tuning / tests); 0 = auto.
   const int forced_vec = L.sched.variant > 0 ? L.sched.variant / 100 : 0;
   const int forced_lpr = L.sched.variant > 0 ? L.sched.variant % 100 : 0;

@@ -256,3 +256,32 @@ def test_products_scale_sampled_rows(device):
     assert_bitwise(out_h[1_000_000:1_100_000], ref, "row block")
     # a checksum of checksums over all rows (size-independent): row sums vs oracle's
     assert torch.isfinite(out_h).all()
+
+
+def test_row_split_rccl_single_rank(device):
+    """The RCCL C-ABI path (unique id -> comm init -> in-place ncclAllGather -> local SpMM) with one
+    rank; multi-rank semantics are covered by tests/test_distributed_gloo.py."""
+    import socket
+
+    import torch.distributed as dist
+    from oneflow_spmm.distributed import RowSplitSpmm
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=device)
+    try:
+        rng = np.random.default_rng(17)
+        m, k, n = 777, 555, 64
+        rp, ci, v = random_csr(m, k, power_law_degrees(m, 20000, k, rng), rng)
+        b = random_dense(k, n, rng)
+        rs = RowSplitSpmm(m, k, n, ci.numel(), torch.float32, torch.int32, device)
+        assert rs.comm_kind == "rccl"
+        rs.shard_view().copy_(b.to(device))
+        out = rs(rp.to(device), rs.remap_columns(ci.to(device)), v.to(device))
+        torch.cuda.synchronize()
+        assert_bitwise(out, oracle_spmm(rp, ci, v, b), "rccl row split")
+        rs.close()
+    finally:
+        dist.destroy_process_group()

@@ -1,0 +1,89 @@
+"""CPU: pin the oracle against the golden fixtures (scipy f64 / torch.sparse f32 / exact cases /
+integer partition vectors).  Parity with the reference itself is unpinned (no SpMM there)."""
+import glob
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+CASES = sorted(glob.glob(os.path.join(GOLD, "*.npz")))
+
+
+def test_manifest_hashes():
+    man = json.load(open(os.path.join(GOLD, "MANIFEST.json")))
+    for name, digest in man["files"].items():
+        assert hashlib.sha256(open(os.path.join(GOLD, name), "rb").read()).hexdigest() == digest, name
+
+
+@pytest.mark.parametrize("path", CASES, ids=[os.path.basename(p) for p in CASES])
+def test_oracle_matches_fixture(path):
+    z = np.load(path)  # allow_pickle=False (default)
+    rp, c, v, b = z["row_ptr"], z["col_idx"], z["values"], z["b"]
+    e64, absum, e32 = z["expected_f64"], z["absum"], z["expected_t32"]
+    for ordered in (True, False):
+        got = oracle.spmm(rp, c, v, b, ordered=ordered, nthreads=4)
+        ok, worst = oracle.within_tolerance(got, e64, absum, 1e-5)
+        assert ok, f"{path} ordered={ordered}: worst rel {worst}"
+        ok, worst = oracle.within_tolerance(got, e32.astype(np.float64), absum, 2e-6 * 8)
+        assert ok, f"{path} vs torch.sparse: worst rel {worst}"
+        if "exact" in path:
+            np.testing.assert_array_equal(got, e64.astype(np.float32))
+            np.testing.assert_array_equal(got, e32)
+    c64, ab = oracle.ref64(rp, c, v, b)
+    np.testing.assert_allclose(c64, e64, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(ab, absum, rtol=1e-12, atol=1e-12)
+
+
+def test_oracle_reference_order_is_sequential():
+    """The ordered oracle is literally ((0 + p0) + p1) + ... with p = fl(val*b): check one row by hand."""
+    z = np.load(os.path.join(GOLD, "n3_f32.npz"))
+    rp, c, v, b = z["row_ptr"], z["col_idx"], z["values"], z["b"]
+    got = oracle.spmm(rp, c, v, b, ordered=True, nthreads=1)
+    for r in (1, 50):
+        acc = np.zeros(3, dtype=np.float32)
+        for j in range(rp[r], rp[r + 1]):
+            acc = (acc + (np.float32(v[j]) * b[c[j]]).astype(np.float32)).astype(np.float32)
+        np.testing.assert_array_equal(got[r], acc)
+
+
+def test_oracle_chunked_schedule_by_hand():
+    z = np.load(os.path.join(GOLD, "hub_n128_f32.npz"))
+    rp, c, v, b = z["row_ptr"], z["col_idx"], z["values"], z["b"]
+    split, chunk = 512, 512
+    got = oracle.spmm(rp, c, v, b, split=split, chunk=chunk, nthreads=2)
+    r = 3  # 2900 nonzeros -> 5 chunks, the last one 852 long
+    j0, j1 = rp[r], rp[r + 1]
+    nc = (j1 - j0) // chunk
+    acc = np.zeros(128, dtype=np.float32)
+    for q in range(nc):
+        a = j0 + q * chunk
+        e = j1 if q == nc - 1 else a + chunk
+        part = np.zeros(128, dtype=np.float32)
+        for j in range(a, e):
+            part = (part + (v[j] * b[c[j]]).astype(np.float32)).astype(np.float32)
+        acc = (acc + part).astype(np.float32)
+    np.testing.assert_array_equal(got[r], acc)
+
+
+def test_balanced_range_fixture():
+    part = json.load(open(os.path.join(GOLD, "partition.json")))
+    for key, ranges in part["balanced"].items():
+        total, g = map(int, key.split("/"))
+        for r, (lo, hi) in enumerate(ranges):
+            assert oracle.balanced_range(total, g, r) == (lo, hi)
+
+
+def test_bf16_rounding_helpers():
+    x = np.array([1.0, 1.00390625, 1.005859375, -3.3, 0.0, -0.0, np.inf, np.nan], dtype=np.float32)
+    bits = oracle.f32_to_bf16_bits(x)
+    back = oracle.bf16_bits_to_f32(bits)
+    assert back[0] == 1.0 and back[1] == 1.0  # tie to even
+    assert back[2] == np.float32(1.0078125)
+    assert np.isnan(back[-1]) and np.isinf(back[-2])
+    assert oracle.default_split(128) == 512 and oracle.default_split(1) == 8192
+    assert oracle.default_split(256) == 256 and oracle.default_split(1024) == 128
