@@ -86,6 +86,10 @@ typedef struct ofx_spmm_options {
   int64_t chunk;           /* 0 = same as split_threshold                                    */
   int32_t ordered;         /* != 0: never split (reference order, slower on hub rows)       */
   int32_t variant;         /* 0 = auto; >0 forces a kernel variant (tuning / tests)          */
+  int64_t heavy_threshold; /* device work order: non-split rows are binned by degree (bins  *
+                            * > t first, then the rest in index order;                       *
+                            * t = this; 0 = auto (5x mean degree); < 0 = index order.  No    *
+                            * numeric effect.                                                */
 } ofx_spmm_options;
 
 /* The default split threshold for dense width n (a fixed function of n; part of the numeric

@@ -106,12 +106,16 @@ OFX_HD int64_t default_split(int64_t n) {
 struct Schedule {
   int64_t split;  // rows with len > split are chunked; INT64_MAX = never
   int64_t chunk;  // chunk length (the last chunk of a row takes the remainder: [chunk, 2*chunk))
+  int64_t heavy;  // degree-bin threshold for the device work order (no numeric effect);
+                  // 0 = auto, INT64_MAX = off
   int32_t variant;
 };
 
 static inline Schedule resolve_schedule(int64_t n, const ofx_spmm_options* o) {
   Schedule s;
   s.variant = o ? o->variant : 0;
+  const int64_t h = o ? o->heavy_threshold : 0;
+  s.heavy = h > 0 ? h : (h < 0 ? INT64_MAX : 0);  // 0 = auto (device launch: 5x mean degree)
   if (o && o->ordered) {
     s.split = INT64_MAX;
     s.chunk = INT64_MAX;

@@ -28,7 +28,8 @@ class OfxError(RuntimeError):
 
 class Options(ctypes.Structure):
     _fields_ = [("split_threshold", ctypes.c_int64), ("chunk", ctypes.c_int64),
-                ("ordered", ctypes.c_int32), ("variant", ctypes.c_int32)]
+                ("ordered", ctypes.c_int32), ("variant", ctypes.c_int32),
+                ("heavy_threshold", ctypes.c_int64)]
 
 
 class TensorDesc(ctypes.Structure):

@@ -15,8 +15,10 @@ from ._lib import LIB, Options, check
 INT64_MAX = (1 << 63) - 1
 
 
-def make_options(split: int = 0, chunk: int = 0, ordered: bool = False, variant: int = 0) -> Options:
-    return Options(int(split), int(chunk), 1 if ordered else 0, int(variant))
+def make_options(split: int = 0, chunk: int = 0, ordered: bool = False, variant: int = 0,
+                 heavy: int = 0) -> Options:
+    """heavy: rows longer than this (not split) are scheduled first; 0 = default, <0 = off."""
+    return Options(int(split), int(chunk), 1 if ordered else 0, int(variant), int(heavy))
 
 
 def default_split(n: int) -> int:

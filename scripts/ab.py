@@ -3,7 +3,8 @@
 
     python scripts/ab.py [--config products] [--rounds 8] [--reps 5] [--variants 0,264,432,...]
 
-Variant codes: 0 = the op's auto choice; VEC*100+LPR forces (VEC, LPR); "ordered" = no hub split.
+Variant codes: 0 = the op's auto choice; VEC*100+LPR forces (VEC, LPR); "ordered" = no hub split;
+a suffix "h<thr>" sets the heavy-row threshold (h-1 = off), e.g. 10002h256.
 Prints per-variant median/min ms and gather-model GB/s; checks every variant is bit-identical to
 the auto variant on the first round.
 """
@@ -28,6 +29,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default="0,432,264,464,232")
     ap.add_argument("--split", type=int, default=0)
+    ap.add_argument("--heavy", type=int, default=0, help="0 default, <0 off")
     args = ap.parse_args()
     from oneflow_spmm import ops, synth
     from bench import alg_bytes
@@ -45,7 +47,8 @@ def main():
         if name == "ordered":
             opts = ops.make_options(ordered=True)
         else:
-            opts = ops.make_options(variant=int(name), split=args.split)
+            vv, _, h = name.partition("h")
+            opts = ops.make_options(variant=int(vv), split=args.split, heavy=int(h) if h else args.heavy)
         kernels[name] = ops.SpmmCsrKernel(m, k, n, nnz, torch.int32, dt, dev, opts)
         outs[name] = torch.empty((m, n), dtype=dt, device=dev)
     times = {name: [] for name in kernels}

@@ -1,6 +1,7 @@
 #!/bin/bash
-# Profiles bench.py on one MI355X: kernel-trace stats, then FETCH_SIZE and WRITE_SIZE in their own
-# passes (gfx950: FETCH_SIZE counts half the bytes of wide coalesced reads).
+# Profiles bench.py on one MI355X with rocprofv3: a kernel-trace/stats pass, then PMC passes, each
+# in its own run (counters never combined with other trace domains).  Raw outputs go to
+# gpurun_out/prof_<tag>/; scripts/rocprof_summary.py condenses them for profiles/.
 # usage: scripts/profile.sh <tag> [bench args...]
 set -u
 TAG=${1:-r01}; shift || true
@@ -9,8 +10,15 @@ export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace_bench.json 2> $OUT/trace.err || exit $?
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py $ARGS > $OUT/fetch_bench.json 2> $OUT/fetch.err || exit $?
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py $ARGS > $OUT/write_bench.json 2> $OUT/write.err || exit $?
-timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/hit -o run -- python3 bench.py $ARGS > $OUT/hit_bench.json 2> $OUT/hit.err || exit $?
+run() {  # name, rocprofv3 options...
+  local name=$1; shift
+  timeout -k 10 300 rocprofv3 "$@" --output-format csv -d $OUT/$name -o run -- python3 bench.py $ARGS \
+    > $OUT/${name}_bench.json 2> $OUT/${name}.err
+}
+run trace --kernel-trace --stats || exit $?
+run fetch --pmc FETCH_SIZE || exit $?
+run write --pmc WRITE_SIZE || exit $?
+run rdreq --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_BUBBLE_sum || exit $?
+run rd128 --pmc TCC_EA0_RDREQ_128B TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum || exit $?
+run hit --pmc TCC_HIT_sum TCC_MISS_sum || exit $?
 echo done

@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Condense a scripts/profile.sh output directory into profiles/<tag>_rocprof.md and .json:
+per-kernel average duration (kernel-trace stats) and per-dispatch PMC averages, plus the
+corrected beyond-L2 byte count per launch of the dominant kernel."""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    name = name.replace("void ", "").replace("ofx::(anonymous namespace)::", "")
+    return name.split("(")[0]
+
+
+def main(src, tag, dst="profiles"):
+    stats = []
+    for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
+        stats.append({"kernel": short(r["Name"]), "full_name": r["Name"], "calls": int(r["Calls"]),
+                      "avg_us": float(r["AverageNs"]) / 1e3, "min_us": float(r["MinNs"]) / 1e3,
+                      "max_us": float(r["MaxNs"]) / 1e3, "pct": float(r["Percentage"])})
+    pmc = defaultdict(lambda: defaultdict(list))
+    for sub in sorted(os.listdir(src)):
+        f = os.path.join(src, sub, "run_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        for r in csv.DictReader(open(f)):
+            pmc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    pmc_avg = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in pmc.items()}
+    main_k = max(stats, key=lambda s: s["pct"])["kernel"]
+    c = pmc_avg.get(main_k, {})
+    traffic = {}
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        # gfx950: FETCH_SIZE tallies 128-B requests of wide streaming reads at 64 B (x2 correction,
+        # MI355X_MICROARCH.md §HBM); WRITE_SIZE is exact for 16-B-per-lane stores.
+        traffic["fetch_size_bytes_raw"] = c["FETCH_SIZE"] * 1024
+        traffic["write_size_bytes"] = c["WRITE_SIZE"] * 1024
+        traffic["read_bytes_corrected_x2"] = 2 * c["FETCH_SIZE"] * 1024
+    if "TCC_EA0_RDREQ_128B" in c:
+        rd = 128 * c["TCC_EA0_RDREQ_128B"] + 64 * c.get("TCC_EA0_RDREQ_64B_sum", 0) + 32 * c.get("TCC_EA0_RDREQ_32B_sum", 0)
+        traffic["read_bytes_by_request_size"] = rd
+    if traffic:
+        rd = traffic.get("read_bytes_by_request_size", traffic.get("read_bytes_corrected_x2"))
+        traffic["beyond_l2_bytes_per_launch"] = rd + traffic.get("write_size_bytes", 0)
+    out = {"tag": tag, "dominant_kernel": main_k, "kernels": stats, "pmc_avg_per_dispatch": pmc_avg,
+           "traffic": traffic}
+    os.makedirs(dst, exist_ok=True)
+    json.dump(out, open(os.path.join(dst, f"{tag}_rocprof.json"), "w"), indent=1)
+    with open(os.path.join(dst, f"{tag}_rocprof.md"), "w") as f:
+        f.write(f"# rocprofv3 summary — {tag}\n\nSource: `scripts/profile.sh` raw CSVs ({src}).\n\n")
+        f.write("| kernel | calls | avg us | min us | max us | % |\n|---|---|---|---|---|---|\n")
+        for s in stats:
+            f.write(f"| {s['kernel']} | {s['calls']} | {s['avg_us']:.1f} | {s['min_us']:.1f} | {s['max_us']:.1f} | {s['pct']:.2f} |\n")
+        f.write("\n## PMC (average per dispatch)\n\n")
+        for k, d in pmc_avg.items():
+            f.write(f"- **{k}**: " + ", ".join(f"{n}={v:.4g}" for n, v in sorted(d.items())) + "\n")
+        f.write("\n## Traffic of the dominant kernel per launch\n\n")
+        for n, v in traffic.items():
+            f.write(f"- {n}: {v:.4g} bytes ({v / 1e9:.3f} GB)\n")
+    print(json.dumps(traffic))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

@@ -101,8 +101,8 @@ def test_direct_abi_argument_checks():
     sz = ctypes.c_size_t()
     assert L.ofx_spmm_csr_workspace_size(7, 2, 1, 1, 1, 1, None, ctypes.byref(sz)) == _lib.OFX_EUNSUPPORTED
     assert L.ofx_spmm_csr_workspace_size(5, 2, -1, 1, 1, 1, None, ctypes.byref(sz)) == _lib.OFX_EINVAL
-    assert L.ofx_spmm_csr_workspace_size(5, 2, 10, 10, 128, 100, None, ctypes.byref(sz)) == 0
-    assert sz.value == 0  # no row can exceed the split threshold
+    assert L.ofx_spmm_csr_workspace_size(5, 2, 10, 10, 128, 6, None, ctypes.byref(sz)) == 0
+    assert sz.value == 0  # every row is in the lightest degree bin: no plan, no workspace
     assert L.ofx_spmm_csr_workspace_size(5, 2, 10, 10, 128, 100000, None, ctypes.byref(sz)) == 0
     assert sz.value > 0
     rc = L.ofx_spmm_csr(None, 5, 2, 4, 4, 4, 0, None, None, None, None, 4, None, 4, 3, 2, None, 0, None)
