@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--variant", type=int, default=0, help="force a kernel variant (VEC*100+LPR)")
+    ap.add_argument("--force-rowsplit", action="store_true",
+                    help="run the N>1 code path (RCCL all-gather + local SpMM) even with one rank")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -63,8 +65,13 @@ def main():
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+    rowsplit = world > 1 or args.force_rowsplit
+    if rowsplit:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29571")
+            os.environ.setdefault("RANK", "0")
+        dist.init_process_group("nccl", device_id=device, world_size=world, rank=rank)
 
     import oneflow_spmm as fs
     from oneflow_spmm import ops, synth
@@ -93,7 +100,7 @@ def main():
 
     events = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     opts = ops.make_options(variant=args.variant) if args.variant else None
-    if world == 1:
+    if not rowsplit:
         d_b = synth.dense(0, k, n, dt, device=device)
         if opts is None:
             def step():
@@ -116,7 +123,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if rowsplit:
         dist.barrier()
     torch.cuda.synchronize()
     ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -126,11 +133,11 @@ def main():
         step()
     ev_end.record()
     torch.cuda.synchronize()
-    if world > 1:
+    if rowsplit:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
-    if world > 1:
+    if rowsplit:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -144,7 +151,7 @@ def main():
     torch.cuda.synchronize()
     spmm_ms, gather_ms = [], []
     for _ in range(max(args.steps, 5)):
-        if world == 1:
+        if not rowsplit:
             events[1].record()
             step()
             events[2].record()
@@ -152,11 +159,22 @@ def main():
             rs(d_rp, d_ci, d_v, out=out, events=events)
         torch.cuda.synchronize()
         spmm_ms.append(events[1].elapsed_time(events[2]))
-        if world > 1:
+        if rowsplit:
             gather_ms.append(events[0].elapsed_time(events[1]))
     kern_ms = float(np.mean(spmm_ms))
     bytes_launch = alg_bytes(rows, nnz_local, n, s_v)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+
+    # HBM-side traffic of the dominant kernel per launch from the committed rocprofv3 PMC summary
+    # of this same workload (scripts/profile.sh + scripts/rocprof_summary.py; beyond-L2 bytes =
+    # 128 B x TCC_EA0_RDREQ_128B (== 2 x FETCH_SIZE on gfx950) + WRITE_SIZE).
+    traffic, traffic_src = None, None
+    prof = os.path.join(ROOT, "profiles", f"{args.config}_rocprof.json")
+    if not rowsplit and os.path.exists(prof):
+        pj = json.load(open(prof))
+        t = pj.get("traffic", {}).get("beyond_l2_bytes_per_launch")
+        if t:
+            traffic, traffic_src = float(t), os.path.relpath(prof, ROOT)
 
     result = {
         "metric": METRIC,
@@ -174,14 +192,16 @@ def main():
         "data": "synthetic (deterministic Chung-Lu power-law CSR, gamma 2.5; dataset-shaped)",
         "config": {"workload": f"{args.config}: CSR {m}x{k}, {nnz} nnz x dense N={n}",
                    "m": m, "k": k, "nnz": nnz, "n": n, "index": "int32",
-                   "parallelism": "single GPU" if world == 1 else
+                   "parallelism": "single GPU" if not rowsplit else
                    f"row-split x{world} + RCCL all-gather of B (padded shards)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_unit": "bytes per launch (beyond L2: Infinity Cache + HBM)",
+                     "traffic_source": traffic_src,
                      "kernel": "spmm_main_kernel (+plan/reduce, timed together)",
                      "alg_bytes_per_launch": bytes_launch, "kernel_ms": round(kern_ms, 4)},
     }
-    if world > 1:
+    if rowsplit:
         result["extra"] = {"allgather_ms_rank0": round(float(np.mean(gather_ms)), 4),
                            "spmm_ms_rank0": round(kern_ms, 4),
                            "rows_rank0": rows, "nnz_rank0": nnz_local}
@@ -209,7 +229,7 @@ def main():
                                             f"OpenMP {threads} threads, same inputs and schedule"}
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if rowsplit:
         rs.close()
         dist.destroy_process_group()
 

@@ -285,3 +285,29 @@ def test_row_split_rccl_single_rank(device):
         rs.close()
     finally:
         dist.destroy_process_group()
+
+
+def test_hipgraph_capture_replay(device):
+    """The op launches are capture-safe (no allocation / sync inside): capture into a graph,
+    replay on new data, same bits as eager."""
+    rng = np.random.default_rng(33)
+    m, k, n = 20000, 20000, 128
+    deg = power_law_degrees(m, 400000, k, rng)
+    rp, ci, v = random_csr(m, k, deg, rng)
+    b = random_dense(k, n, rng).to(device)
+    rp, ci, v = rp.to(device), ci.to(device), v.to(device)
+    out = torch.empty((m, n), device=device)
+    kern = ops.SpmmCsrKernel(m, k, n, ci.numel(), torch.int32, torch.float32, device)
+    s = torch.cuda.Stream(device)
+    s.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(s):
+        kern(rp, ci, v, b, out)  # warm (outside capture)
+    torch.cuda.current_stream(device).wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        kern(rp, ci, v, b, out)
+    b.copy_(random_dense(k, n, np.random.default_rng(34)).to(device))
+    g.replay()
+    torch.cuda.synchronize()
+    ref = oracle_spmm(rp.cpu(), ci.cpu(), v.cpu(), b.cpu())
+    assert_bitwise(out, ref, "graph replay")
