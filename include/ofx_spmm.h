@@ -126,6 +126,39 @@ int ofx_spmm_csr_cpu(int num_threads, int idx_dtype, int val_dtype, int64_t m, i
                      const void* values, const void* b, int64_t ldb, void* c, int64_t ldc,
                      int64_t row_begin, int64_t row_end, const ofx_spmm_options* opts);
 
+/* ---- gradient building blocks ---------------------------------------
+ * For C = A @ B:  dB = A^T @ dC  (transpose once per graph, gather A's values through `perm`,
+ * then ofx_spmm_csr on A^T)  and  dvalues = SDDMM(dC, B) on A's sparsity pattern.
+ * Transpose: out_row_ptr I[k+1], out_col_idx I[nnz] (= row ids of A), out_perm I[nnz] (A^T's
+ * t-th nonzero is A's nonzero perm[t]); entries of each A^T row in ascending A-row order
+ * (stable), so dB follows the forward accumulation contract.  Device version needs a workspace
+ * (nnz <= 2^31-1).                                                                          */
+int ofx_csr_transpose_workspace_size(int idx_dtype, int64_t m, int64_t k, int64_t nnz,
+                                     size_t* bytes);
+int ofx_csr_transpose(void* stream, int idx_dtype, int64_t m, int64_t k, int64_t nnz,
+                      const void* row_ptr, const void* col_idx, void* out_row_ptr,
+                      void* out_col_idx, void* out_perm, void* workspace, size_t workspace_bytes);
+int ofx_csr_transpose_cpu(int idx_dtype, int64_t m, int64_t k, int64_t nnz, const void* row_ptr,
+                          const void* col_idx, void* out_row_ptr, void* out_col_idx,
+                          void* out_perm);
+/* dst[t] = src[perm[t]] for t < nnz (any 2/4/8-byte value dtype). */
+int ofx_gather_values(void* stream, int idx_dtype, int val_dtype, int64_t nnz, const void* perm,
+                      const void* src, void* dst);
+/* out[j] = sum_n a[r - row_begin, n] * b[col_idx[j], n] for the nonzeros j of rows
+ * r in [row_begin, row_end).  Order: products rounded, 8-element leaves summed sequentially from
+ * +0, leaves (zero-padded to a power of two) added pairwise; fp32 accumulation for 16-bit types.
+ * n <= 2048.  Asynchronous, workspace from ofx_sddmm_csr_workspace_size.                    */
+int ofx_sddmm_csr_workspace_size(int idx_dtype, int val_dtype, int64_t m, int64_t n, int64_t nnz,
+                                 size_t* bytes);
+int ofx_sddmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k, int64_t n,
+                  int64_t nnz, const void* row_ptr, const void* col_idx, const void* a,
+                  int64_t lda, const void* b, int64_t ldb, void* out, int64_t row_begin,
+                  int64_t row_end, void* workspace, size_t workspace_bytes);
+int ofx_sddmm_csr_cpu(int num_threads, int idx_dtype, int val_dtype, int64_t m, int64_t k,
+                      int64_t n, int64_t nnz, const void* row_ptr, const void* col_idx,
+                      const void* a, int64_t lda, const void* b, int64_t ldb, void* out,
+                      int64_t row_begin, int64_t row_end);
+
 /* ---- row partition (BalancedSplitter) ---------------------------------------------------- */
 int ofx_balanced_range(int64_t total, int64_t parts, int64_t idx, int64_t* begin, int64_t* end);
 /* Rebase a row slice of a CSR: out_row_ptr[i] = row_ptr[row_begin + i] - row_ptr[row_begin],

@@ -154,3 +154,107 @@ extern "C" int ofx_csr_row_slice_host(int idx_dtype, const void* row_ptr, int64_
     run(static_cast<const int64_t*>(row_ptr), static_cast<int64_t*>(out_row_ptr));
   return OFX_OK;
 }
+
+// ---- backward building blocks on the host (DeviceType::kCPU; same bits as the HIP kernels) ---
+namespace ofx {
+namespace {
+
+template <typename I>
+void cpu_transpose(int64_t m, int64_t k, int64_t nnz, const I* rp, const I* col, I* out_rp,
+                   I* out_col, I* out_perm) {
+  std::vector<int64_t> cnt(k + 1, 0);
+  for (int64_t j = 0; j < nnz; ++j) ++cnt[(int64_t)col[j] + 1];
+  for (int64_t c = 0; c < k; ++c) cnt[c + 1] += cnt[c];
+  for (int64_t c = 0; c <= k; ++c) out_rp[c] = (I)cnt[c];
+  for (int64_t r = 0; r < m; ++r)  // rows ascending -> stable within each column
+    for (int64_t j = (int64_t)rp[r]; j < (int64_t)rp[r + 1]; ++j) {
+      const int64_t pos = cnt[(int64_t)col[j]]++;
+      out_col[pos] = (I)r;
+      out_perm[pos] = (I)j;
+    }
+}
+
+template <typename T, typename I>
+void cpu_sddmm(int nthreads, int64_t n, const I* rp, const I* col, const T* a, int64_t lda,
+               const T* b, int64_t ldb, T* out, int64_t row_begin, int64_t row_end) {
+#pragma clang fp contract(off)
+  using A = typename Num<T>::acc;
+  const int64_t leaves = (n + 7) / 8;
+  int64_t padded = 1;
+  while (padded < leaves) padded *= 2;
+#pragma omp parallel num_threads(nthreads)
+  {
+    std::vector<A> leaf(padded);
+#pragma omp for schedule(dynamic, 64)
+    for (int64_t r = row_begin; r < row_end; ++r) {
+      const T* arow = a + (r - row_begin) * lda;
+      for (int64_t j = (int64_t)rp[r]; j < (int64_t)rp[r + 1]; ++j) {
+        const T* brow = b + (int64_t)col[j] * ldb;
+        for (int64_t l = 0; l < padded; ++l) {
+          A s = A(0);
+          for (int64_t e = 8 * l; e < 8 * l + 8 && e < n; ++e)
+            s = s + Num<T>::load(arow[e]) * Num<T>::load(brow[e]);
+          leaf[l] = s;
+        }
+        for (int64_t w = 1; w < padded; w *= 2)
+          for (int64_t l = 0; l < padded; l += 2 * w) leaf[l] = leaf[l] + leaf[l + w];
+        out[j] = Num<T>::store(leaf[0]);
+      }
+    }
+  }
+}
+
+}  // namespace
+}  // namespace ofx
+
+extern "C" int ofx_csr_transpose_cpu(int idx_dtype, int64_t m, int64_t k, int64_t nnz,
+                                     const void* row_ptr, const void* col_idx, void* out_row_ptr,
+                                     void* out_col_idx, void* out_perm) {
+  OFX_REQUIRE(m >= 0 && k >= 0 && nnz >= 0 && row_ptr && out_row_ptr &&
+                  (nnz == 0 || (col_idx && out_col_idx && out_perm)),
+              OFX_EINVAL, "csr_transpose_cpu: bad arguments");
+  if (idx_dtype == OFX_DT_INT32)
+    cpu_transpose<int32_t>(m, k, nnz, (const int32_t*)row_ptr, (const int32_t*)col_idx,
+                           (int32_t*)out_row_ptr, (int32_t*)out_col_idx, (int32_t*)out_perm);
+  else if (idx_dtype == OFX_DT_INT64)
+    cpu_transpose<int64_t>(m, k, nnz, (const int64_t*)row_ptr, (const int64_t*)col_idx,
+                           (int64_t*)out_row_ptr, (int64_t*)out_col_idx, (int64_t*)out_perm);
+  else
+    return fail(OFX_EUNSUPPORTED, "csr_transpose_cpu: bad index dtype %d", idx_dtype);
+  return OFX_OK;
+}
+
+extern "C" int ofx_sddmm_csr_cpu(int num_threads, int idx_dtype, int val_dtype, int64_t m,
+                                 int64_t k, int64_t n, int64_t nnz, const void* row_ptr,
+                                 const void* col_idx, const void* a, int64_t lda, const void* b,
+                                 int64_t ldb, void* out, int64_t row_begin, int64_t row_end) {
+  OFX_REQUIRE(is_index_dtype(idx_dtype) && is_value_dtype(val_dtype), OFX_EUNSUPPORTED,
+              "sddmm_csr_cpu: unsupported dtypes (%d, %d)", idx_dtype, val_dtype);
+  OFX_REQUIRE(m >= 0 && k >= 0 && n > 0 && nnz >= 0 && lda >= n && ldb >= n && 0 <= row_begin &&
+                  row_begin <= row_end && row_end <= m,
+              OFX_EINVAL, "sddmm_csr_cpu: bad sizes");
+  if (row_end == row_begin || nnz == 0) return OFX_OK;
+  const int nt = num_threads > 0 ? num_threads : omp_get_max_threads();
+  auto run = [&](auto* ip) {
+    using I = std::remove_const_t<std::remove_pointer_t<decltype(ip)>>;
+    const I* rp = (const I*)row_ptr;
+    const I* ci = (const I*)col_idx;
+    switch (val_dtype) {
+      case OFX_DT_FLOAT:
+        cpu_sddmm<float, I>(nt, n, rp, ci, (const float*)a, lda, (const float*)b, ldb, (float*)out, row_begin, row_end);
+        break;
+      case OFX_DT_DOUBLE:
+        cpu_sddmm<double, I>(nt, n, rp, ci, (const double*)a, lda, (const double*)b, ldb, (double*)out, row_begin, row_end);
+        break;
+      case OFX_DT_BFLOAT16:
+        cpu_sddmm<bf16, I>(nt, n, rp, ci, (const bf16*)a, lda, (const bf16*)b, ldb, (bf16*)out, row_begin, row_end);
+        break;
+      default:
+        cpu_sddmm<f16, I>(nt, n, rp, ci, (const f16*)a, lda, (const f16*)b, ldb, (f16*)out, row_begin, row_end);
+        break;
+    }
+  };
+  if (idx_dtype == OFX_DT_INT32) run((const int32_t*)nullptr);
+  else run((const int64_t*)nullptr);
+  return OFX_OK;
+}

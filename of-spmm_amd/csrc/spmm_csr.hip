@@ -33,9 +33,15 @@
 
 #include "ofx_internal.h"
 #include "spmm_common.h"
+#include "spmm_plan.h"
 
 namespace ofx {
 namespace {
+
+using plan::WorkList;
+using plan::WsLayout;
+using plan::launch_plan;
+using plan::ws_layout;
 
 constexpr int kBlock = 256;        // 4 waves
 constexpr int64_t kMaxReduceBlocks = 16384;
@@ -194,176 +200,6 @@ __device__ __forceinline__ void store_partial(A* __restrict__ p, const A (&acc)[
   for (int e = 0; e < VEC; ++e) p[e] = acc[e];
 }
 
-// ---- work planning (three small launches, no contended atomics) ----------------------------
-// Every row gets a class: hub (len > split: cut into chunks -> partials + spmm_reduce) or one of
-// kBins degree bins (kBins = 2: bin 0 = heavy, len > heavy; bin 1 = the rest; with more bins the
-// thresholds step by 4x).  The main kernel walks ONE work list: the hub chunks first, then the
-// non-hub rows bin by bin (a stable counting sort by degree), so the longest work starts first
-// and the grid ends on short rows.  Two bins measured best on MI355X: the light rows keep index
-// order (sequential row_ptr reads and C writes); more bins cost products-scale 1.2% in random
-// row_ptr/C traffic.  Rows are taken kPlanRows per block.
-//   plan_count  per-block totals of (hubs, hub chunks, rows per bin)
-//   plan_scan   one block: exclusive offsets across blocks; counters[0] = hub chunks,
-//               counters[1] = hubs, counters[2 + b] = start of bin b in `order`
-//   plan_write  hubs[3i..3i+2] = {local row, first chunk slot, chunks},
-//               items[2s..2s+1] = {local row, chunk} for s < counters[0],
-//               order[...] = local row, bins in order, ascending rows inside a bin.
-// The layout is a pure function of row_ptr (deterministic); the partial of chunk s is part[s].
-constexpr int kPlanRowsPerThread = 4;
-constexpr int64_t kPlanRows = (int64_t)kBlock * kPlanRowsPerThread;
-constexpr int kBins = 2;
-constexpr int kPlanVals = 2 + kBins;  // hubs, chunks, bins...
-
-template <typename I>
-__device__ __forceinline__ int plan_row(const I* __restrict__ rp, int64_t row_begin, int64_t nrows,
-                                        int64_t g, int64_t split, int64_t chunk, int64_t heavy,
-                                        int64_t& nc) {
-  nc = 0;
-  if (g >= nrows) return -2;  // no row
-  const int64_t len = (int64_t)rp[row_begin + g + 1] - (int64_t)rp[row_begin + g];
-  if (len > split) {
-    nc = num_chunks(len, chunk);
-    return -1;  // hub
-  }
-  if (heavy == INT64_MAX) return kBins - 1;  // binning off: one bin, identity order
-  int64_t t = heavy;
-  for (int b = 0; b < kBins - 1; ++b, t >>= 2)
-    if (len > t) return b;
-  return kBins - 1;
-}
-
-// Block-wide exclusive scan of kPlanVals int64 values (256 threads); returns the block totals.
-__device__ __forceinline__ void block_scan_vals(int64_t (&v)[kPlanVals], int64_t (&tot)[kPlanVals]) {
-  __shared__ int64_t sh[kPlanVals][kBlock];
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int i = 0; i < kPlanVals; ++i) sh[i][t] = v[i];
-  __syncthreads();
-  for (int off = 1; off < kBlock; off <<= 1) {
-    int64_t x[kPlanVals];
-#pragma unroll
-    for (int i = 0; i < kPlanVals; ++i) x[i] = t >= off ? sh[i][t - off] : 0;
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kPlanVals; ++i) sh[i][t] += x[i];
-    __syncthreads();
-  }
-#pragma unroll
-  for (int i = 0; i < kPlanVals; ++i) {
-    tot[i] = sh[i][kBlock - 1];
-    v[i] = sh[i][t] - v[i];  // exclusive
-  }
-  __syncthreads();
-}
-
-template <typename I>
-__device__ __forceinline__ void plan_thread(const I* __restrict__ rp, int64_t row_begin,
-                                            int64_t nrows, int64_t base, int64_t split,
-                                            int64_t chunk, int64_t heavy,
-                                            int (&cls)[kPlanRowsPerThread],
-                                            int64_t (&nc)[kPlanRowsPerThread],
-                                            int64_t (&v)[kPlanVals]) {
-#pragma unroll
-  for (int i = 0; i < kPlanVals; ++i) v[i] = 0;
-#pragma unroll
-  for (int q = 0; q < kPlanRowsPerThread; ++q) {
-    cls[q] = plan_row(rp, row_begin, nrows, base + q, split, chunk, heavy, nc[q]);
-    if (cls[q] == -1) {
-      v[0] += 1;
-      v[1] += nc[q];
-    } else if (cls[q] >= 0) {
-#pragma unroll
-      for (int b = 0; b < kBins; ++b) v[2 + b] += (cls[q] == b);
-    }
-  }
-}
-
-template <typename I>
-__global__ void __launch_bounds__(kBlock)
-    spmm_plan_count_kernel(const I* __restrict__ rp, int64_t row_begin, int64_t nrows,
-                           int64_t split, int64_t chunk, int64_t heavy,
-                           int64_t* __restrict__ block_tot) {
-  int cls[kPlanRowsPerThread];
-  int64_t nc[kPlanRowsPerThread], v[kPlanVals], tot[kPlanVals];
-  const int64_t base = (int64_t)blockIdx.x * kPlanRows + (int64_t)threadIdx.x * kPlanRowsPerThread;
-  plan_thread(rp, row_begin, nrows, base, split, chunk, heavy, cls, nc, v);
-  block_scan_vals(v, tot);
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int i = 0; i < kPlanVals; ++i) block_tot[kPlanVals * blockIdx.x + i] = tot[i];
-  }
-}
-
-__global__ void __launch_bounds__(kBlock)
-    spmm_plan_scan_kernel(int64_t* __restrict__ block_tot, int64_t nblocks,
-                          unsigned long long* __restrict__ counters) {
-  int64_t carry[kPlanVals];
-#pragma unroll
-  for (int i = 0; i < kPlanVals; ++i) carry[i] = 0;
-  for (int64_t b0 = 0; b0 < nblocks; b0 += kBlock) {
-    const int64_t b = b0 + threadIdx.x;
-    int64_t v[kPlanVals], tot[kPlanVals];
-#pragma unroll
-    for (int i = 0; i < kPlanVals; ++i) v[i] = b < nblocks ? block_tot[kPlanVals * b + i] : 0;
-    block_scan_vals(v, tot);
-    if (b < nblocks) {
-#pragma unroll
-      for (int i = 0; i < kPlanVals; ++i) block_tot[kPlanVals * b + i] = carry[i] + v[i];
-    }
-#pragma unroll
-    for (int i = 0; i < kPlanVals; ++i) carry[i] += tot[i];
-  }
-  if (threadIdx.x == 0) {
-    counters[0] = (unsigned long long)carry[1];
-    counters[1] = (unsigned long long)carry[0];
-    int64_t start = 0;
-    for (int b = 0; b < kBins; ++b) {
-      counters[2 + b] = (unsigned long long)start;
-      start += carry[2 + b];
-    }
-  }
-}
-
-template <typename I>
-__global__ void __launch_bounds__(kBlock)
-    spmm_plan_write_kernel(const I* __restrict__ rp, int64_t row_begin, int64_t nrows,
-                           int64_t split, int64_t chunk, int64_t heavy,
-                           const int64_t* __restrict__ block_off,
-                           const unsigned long long* __restrict__ counters,
-                           int64_t* __restrict__ hubs, int64_t* __restrict__ items,
-                           int64_t* __restrict__ order) {
-  int cls[kPlanRowsPerThread];
-  int64_t nc[kPlanRowsPerThread], v[kPlanVals], tot[kPlanVals];
-  const int64_t base = (int64_t)blockIdx.x * kPlanRows + (int64_t)threadIdx.x * kPlanRowsPerThread;
-  plan_thread(rp, row_begin, nrows, base, split, chunk, heavy, cls, nc, v);
-  block_scan_vals(v, tot);
-  const int64_t* off = block_off + kPlanVals * blockIdx.x;
-  int64_t hi = off[0] + v[0];
-  int64_t slot = off[1] + v[1];
-  int64_t pos[kBins];
-#pragma unroll
-  for (int b = 0; b < kBins; ++b) pos[b] = (int64_t)counters[2 + b] + off[2 + b] + v[2 + b];
-#pragma unroll
-  for (int q = 0; q < kPlanRowsPerThread; ++q) {
-    const int64_t g = base + q;
-    if (cls[q] == -1) {
-      hubs[3 * hi + 0] = g;
-      hubs[3 * hi + 1] = slot;
-      hubs[3 * hi + 2] = nc[q];
-      for (int64_t c = 0; c < nc[q]; ++c) {
-        items[2 * (slot + c) + 0] = g;
-        items[2 * (slot + c) + 1] = c;
-      }
-      ++hi;
-      slot += nc[q];
-    } else if (cls[q] >= 0) {
-#pragma unroll
-      for (int b = 0; b < kBins; ++b)
-        if (cls[q] == b) order[pos[b]++] = g;
-    }
-  }
-}
-
 // ---- main kernel: one work list = hub chunks, then rows in bin order ------------------------
 // Without a plan (`order` == nullptr) the list is simply the rows in index order.
 template <typename T, typename I, typename K>
@@ -506,42 +342,6 @@ struct Launch {
   size_t ws_bytes;
 };
 
-inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
-
-struct WsLayout {
-  size_t counters, block_tot, hubs, items, order, part, total;
-  int64_t max_hubs, max_chunks, plan_blocks;
-};
-
-// The plan (and so a workspace) is used when some row can be a hub or fall outside the lightest
-// bin; otherwise the work list is the identity and no workspace is needed.
-constexpr int64_t kMinBinRows = 16384;  // below this the grid is one wave of blocks: no tail
-
-WsLayout ws_layout(int64_t nrows, int64_t nnz, int64_t n, size_t acc_bytes, const Schedule& s) {
-  WsLayout w{};
-  const bool bin = s.heavy != INT64_MAX && nrows >= kMinBinRows;
-  const bool hub = s.split != INT64_MAX && nnz > s.split;
-  if (!bin && !hub) return w;  // identity work list: no plan, no workspace
-  w.max_hubs = s.split == INT64_MAX ? 0 : nnz / (s.split + 1) + 1;
-  w.max_chunks = s.split == INT64_MAX ? 0 : nnz / s.chunk + 1;
-  w.plan_blocks = (nrows + kPlanRows - 1) / kPlanRows;
-  size_t off = 0;
-  w.counters = off;
-  off = align_up(off + (2 + kBins) * sizeof(unsigned long long), 256);
-  w.block_tot = off;
-  off = align_up(off + (size_t)w.plan_blocks * kPlanVals * sizeof(int64_t), 256);
-  w.hubs = off;
-  off = align_up(off + (size_t)w.max_hubs * 3 * sizeof(int64_t), 256);
-  w.items = off;
-  off = align_up(off + (size_t)w.max_chunks * 2 * sizeof(int64_t), 256);
-  w.order = off;
-  off = align_up(off + (size_t)nrows * sizeof(int64_t), 256);
-  w.part = off;
-  off = align_up(off + (size_t)w.max_chunks * (size_t)n * acc_bytes, 256);
-  w.total = off;
-  return w;
-}
-
 int pick_vec(int elem_bytes, const Launch& L, int forced_vec) {
   const int maxvec = 16 / elem_bytes;
   for (int v = maxvec; v >= 1; v /= 2) {
@@ -573,39 +373,18 @@ int launch_cfg(const Launch& L) {
   T* C = static_cast<T*>(L.c);
   const WsLayout w = ws_layout(L.nrows, L.nnz, L.n, sizeof(A), L.sched);
   const bool plan = w.total > 0;
-  // Heavy-bin threshold: rows above ~5x the mean degree go first (measured: products and the
-  // 1M power-law config both peak at 4-6x the mean).  Order only, never numerics.
-  int64_t heavy = L.sched.heavy;
-  if (heavy == 0) {
-    const int64_t mean = L.nrows > 0 ? (L.nnz + L.nrows - 1) / L.nrows : 1;
-    heavy = 5 * mean < 16 ? 16 : 5 * mean;
-  }
-  unsigned long long* counters = nullptr;
-  int64_t *hub = nullptr, *items = nullptr, *order = nullptr;
-  A* part = nullptr;
+  WorkList wl{};
   if (plan) {
     OFX_REQUIRE(L.ws != nullptr && L.ws_bytes >= w.total, OFX_EWORKSPACE,
                 "spmm_csr: workspace of %zu bytes is smaller than the %zu bytes required",
                 L.ws_bytes, w.total);
-    char* ws = static_cast<char*>(L.ws);
-    counters = reinterpret_cast<unsigned long long*>(ws + w.counters);
-    hub = reinterpret_cast<int64_t*>(ws + w.hubs);
-    items = reinterpret_cast<int64_t*>(ws + w.items);
-    order = reinterpret_cast<int64_t*>(ws + w.order);
-    part = reinterpret_cast<A*>(ws + w.part);
-    auto* block_tot = reinterpret_cast<int64_t*>(ws + w.block_tot);
-    const unsigned pgrid = (unsigned)w.plan_blocks;
-    hipLaunchKernelGGL((spmm_plan_count_kernel<I>), dim3(pgrid), dim3(kBlock), 0, L.stream, rp,
-                       L.row_begin, L.nrows, L.sched.split, L.sched.chunk, heavy, block_tot);
-    OFX_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(spmm_plan_scan_kernel, dim3(1), dim3(kBlock), 0, L.stream, block_tot,
-                       w.plan_blocks, counters);
-    OFX_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL((spmm_plan_write_kernel<I>), dim3(pgrid), dim3(kBlock), 0, L.stream, rp,
-                       L.row_begin, L.nrows, L.sched.split, L.sched.chunk, heavy, block_tot,
-                       counters, hub, items, order);
-    OFX_HIP_CHECK(hipGetLastError());
+    const int rc = launch_plan<I>(L.stream, rp, L.row_begin, L.nrows, L.nnz, L.sched, w,
+                                  static_cast<char*>(L.ws), &wl);
+    if (rc) return rc;
   }
+  unsigned long long* counters = wl.counters;
+  int64_t *hub = wl.hubs, *items = wl.items, *order = wl.order;
+  A* part = reinterpret_cast<A*>(wl.part);
   // Work list length <= hub chunks + rows; surplus groups exit at once.
   const int64_t work = L.nrows + (plan ? w.max_chunks : 0);
   const int64_t grid = (work + GPB - 1) / GPB;

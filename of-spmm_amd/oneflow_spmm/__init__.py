@@ -3,14 +3,15 @@
     import oneflow_spmm as flow_spmm
     out = flow_spmm.spmm(row_ptr, col_idx, values, num_rows, num_cols, b)   # oneflow.spmm
     out = flow_spmm._C.spmm_csr(...)                                          # oneflow._C.spmm_csr
+`spmm` is differentiable in the values and in b (autograd.py: SDDMM and A^T @ dC).
 
 Re-exports mirror python/oneflow/__init__.py:158-160 (`from oneflow._C import ... as mv`).
 """
-from . import _C, _lib, ops, synth  # noqa: F401
+from . import _C, _lib, autograd, ops, synth  # noqa: F401
 from ._C import spmm_csr
-from ._C import spmm_csr as spmm
 from ._lib import OfxError
+from .autograd import csr_transpose, sddmm, spmm
 
 __version__ = _lib.LIB.ofx_version().decode()
 
-__all__ = ["spmm", "spmm_csr", "OfxError", "ops", "synth", "_C"]
+__all__ = ["spmm", "spmm_csr", "sddmm", "csr_transpose", "OfxError", "ops", "synth", "autograd", "_C"]

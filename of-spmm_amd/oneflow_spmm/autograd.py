@@ -1,0 +1,150 @@
+"""Gradients of `spmm_csr`: d(values) by SDDMM, d(b) by SpMM with A^T.
+
+Mirrors what a OneFlow gradient function for the op would do (pattern
+oneflow/core/autograd/gradient_funcs/matrix_vector_product.cpp:26-91: capture what the backward
+needs, then call the grad functors): for out = A @ b,
+    d(values)[j] = <d(out)[row(j), :], b[col(j), :]>      ofx_sddmm_csr
+    d(b)         = A^T @ d(out)                            ofx_csr_transpose (cached per graph)
+                                                           + ofx_gather_values + ofx_spmm_csr
+The index inputs never get gradients (spmm_op.cpp ModifyInputArg).  All device work runs in the
+HIP kernels; CPU tensors run the kCPU kernels.  Both give the same bits (contracts in
+include/ofx_spmm.h).
+"""
+from __future__ import annotations
+
+import ctypes
+from collections import OrderedDict
+
+import torch
+
+from . import ops
+from ._C import current_stream_handle, dtype_code, spmm_csr
+from ._lib import LIB, check
+
+
+# ---- building blocks ----------------------------------------------------------------------------
+def csr_transpose(row_ptr: torch.Tensor, col_idx: torch.Tensor, k: int):
+    """Structure of A^T: (row_ptr_T [k+1], col_idx_T [nnz] = rows of A, perm [nnz])."""
+    m = row_ptr.numel() - 1
+    nnz = col_idx.numel()
+    it = row_ptr.dtype
+    dev = row_ptr.device
+    rp_t = torch.empty(k + 1, dtype=it, device=dev)
+    ci_t = torch.empty(nnz, dtype=it, device=dev)
+    perm = torch.empty(nnz, dtype=it, device=dev)
+    idt = dtype_code(it)
+    ptr = lambda t: t.data_ptr() if t.numel() else None  # noqa: E731
+    if dev.type == "cpu":
+        check(LIB.ofx_csr_transpose_cpu(idt, m, k, nnz, row_ptr.data_ptr(), ptr(col_idx),
+                                        rp_t.data_ptr(), ptr(ci_t), ptr(perm)), "csr_transpose")
+        return rp_t, ci_t, perm
+    ws_bytes = ctypes.c_size_t(0)
+    check(LIB.ofx_csr_transpose_workspace_size(idt, m, k, nnz, ctypes.byref(ws_bytes)), "csr_transpose")
+    ws = torch.empty(max(ws_bytes.value, 1), dtype=torch.uint8, device=dev)
+    check(LIB.ofx_csr_transpose(current_stream_handle(row_ptr), idt, m, k, nnz, row_ptr.data_ptr(),
+                                ptr(col_idx), rp_t.data_ptr(), ptr(ci_t), ptr(perm),
+                                ws.data_ptr(), ws_bytes.value), "csr_transpose")
+    return rp_t, ci_t, perm
+
+
+def gather_values(perm: torch.Tensor, values: torch.Tensor) -> torch.Tensor:
+    """values[perm] (device kernel on GPU)."""
+    if values.device.type == "cpu":
+        return values[perm.long()]
+    out = torch.empty_like(values)
+    check(LIB.ofx_gather_values(current_stream_handle(values), dtype_code(perm.dtype),
+                                dtype_code(values.dtype), values.numel(),
+                                perm.data_ptr() if perm.numel() else None,
+                                values.data_ptr() if values.numel() else None,
+                                out.data_ptr() if out.numel() else None), "gather_values")
+    return out
+
+
+def sddmm(row_ptr: torch.Tensor, col_idx: torch.Tensor, a: torch.Tensor, b: torch.Tensor, *,
+          row_begin: int = 0, row_end: int | None = None, num_threads: int = 0) -> torch.Tensor:
+    """out[j] = <a[row(j) - row_begin, :], b[col_idx[j], :]> for the nonzeros of rows
+    [row_begin, row_end) (other entries of `out` stay 0)."""
+    m = row_ptr.numel() - 1
+    row_end = m if row_end is None else row_end
+    n = b.shape[1]
+    k = b.shape[0]
+    nnz = col_idx.numel()
+    a = a if (a.dim() == 2 and a.stride(1) == 1) else a.contiguous()
+    b = b if (b.dim() == 2 and b.stride(1) == 1) else b.contiguous()
+    out = torch.zeros(nnz, dtype=b.dtype, device=b.device)
+    if nnz == 0 or row_end == row_begin or n == 0:
+        return out
+    idt, vdt = dtype_code(row_ptr.dtype), dtype_code(b.dtype)
+    if b.device.type == "cpu":
+        check(LIB.ofx_sddmm_csr_cpu(int(num_threads), idt, vdt, m, k, n, nnz, row_ptr.data_ptr(),
+                                    col_idx.data_ptr(), a.data_ptr(), a.stride(0), b.data_ptr(),
+                                    b.stride(0), out.data_ptr(), row_begin, row_end), "sddmm_csr")
+        return out
+    ws_bytes = ctypes.c_size_t(0)
+    check(LIB.ofx_sddmm_csr_workspace_size(idt, vdt, m, n, nnz, ctypes.byref(ws_bytes)), "sddmm_csr")
+    ws = torch.empty(max(ws_bytes.value, 1), dtype=torch.uint8, device=b.device)
+    check(LIB.ofx_sddmm_csr(current_stream_handle(b), idt, vdt, m, k, n, nnz, row_ptr.data_ptr(),
+                            col_idx.data_ptr(), a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
+                            out.data_ptr(), row_begin, row_end, ws.data_ptr(), ws_bytes.value),
+          "sddmm_csr")
+    return out
+
+
+# ---- transpose cache (the sparsity pattern of a GNN graph is static across layers/steps) -------
+class _TransposeCache:
+    def __init__(self, capacity: int = 4):
+        self.capacity = capacity
+        self.entries: OrderedDict = OrderedDict()
+
+    def get(self, row_ptr, col_idx, k):
+        key = (row_ptr.data_ptr(), col_idx.data_ptr(), row_ptr._version, col_idx._version,
+               row_ptr.numel(), col_idx.numel(), k, str(row_ptr.device))
+        hit = self.entries.get(key)
+        if hit is not None:
+            self.entries.move_to_end(key)
+            return hit[2]
+        t = csr_transpose(row_ptr, col_idx, k)
+        # keep the source tensors alive so their storage (and so the key) cannot be reused
+        self.entries[key] = (row_ptr, col_idx, t)
+        while len(self.entries) > self.capacity:
+            self.entries.popitem(last=False)
+        return t
+
+
+TRANSPOSE_CACHE = _TransposeCache()
+
+
+class SpmmCsrFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, row_ptr, col_idx, values, m, k, b):
+        out = spmm_csr(row_ptr, col_idx, values, m, k, b)
+        ctx.save_for_backward(row_ptr, col_idx, values, b)
+        ctx.m, ctx.k = m, k
+        return out
+
+    @staticmethod
+    def backward(ctx, d_out):
+        row_ptr, col_idx, values, b = ctx.saved_tensors
+        d_out = d_out.contiguous()
+        d_values = d_b = None
+        if ctx.needs_input_grad[2]:
+            d_values = sddmm(row_ptr, col_idx, d_out, b)
+        if ctx.needs_input_grad[5]:
+            rp_t, ci_t, perm = TRANSPOSE_CACHE.get(row_ptr, col_idx, ctx.k)
+            vals_t = gather_values(perm, values)
+            d_b = spmm_csr(rp_t, ci_t, vals_t, ctx.k, ctx.m, d_out)
+        return None, None, d_values, None, None, d_b
+
+
+def spmm(a_csr_row_ptr, a_csr_col_idx, a_csr_values, a_num_rows, a_num_cols, b, *, out=None):
+    """`oneflow.spmm` with autograd: differentiable in `a_csr_values` and `b`.
+    `out=` (a preallocated result) is only accepted when no gradient is being recorded."""
+    if torch.is_grad_enabled() and (a_csr_values.requires_grad or b.requires_grad):
+        if out is not None:
+            raise RuntimeError("spmm: out= is not supported when gradients are required")
+        return SpmmCsrFunction.apply(a_csr_row_ptr, a_csr_col_idx, a_csr_values, int(a_num_rows),
+                                     int(a_num_cols), b)
+    return spmm_csr(a_csr_row_ptr, a_csr_col_idx, a_csr_values, a_num_rows, a_num_cols, b, out=out)
+
+
+__all__ = ["csr_transpose", "gather_values", "sddmm", "SpmmCsrFunction", "spmm", "TRANSPOSE_CACHE", "ops"]

@@ -148,3 +148,57 @@ def within_tolerance(c, c64, absum, rtol):
     bound = rtol * absum + 1e-30
     ok = err <= bound
     return bool(ok.all()), float((err / (absum + 1e-30)).max(initial=0.0))
+
+
+# ---- backward -----------------------------------------------------------
+def _lib_sddmm():
+    L = lib()
+    if not getattr(L, "_sddmm_set", False):
+        i64, p, c_int = ctypes.c_int64, ctypes.c_void_p, ctypes.c_int
+        L.orc_sddmm_f32.argtypes = [i64, p, p, p, i64, p, i64, p, i64, i64, c_int]
+        L.orc_sddmm_f64.argtypes = L.orc_sddmm_f32.argtypes
+        L._sddmm_set = True
+    return L
+
+
+def sddmm(row_ptr, col_idx, a, b, *, dtype="f32", row_begin=0, row_end=None, nthreads=None):
+    """out[j] = <a[row(j)-row_begin], b[col[j]]> in the operator's pairwise-leaf order.
+    a holds rows [row_begin, row_end); bf16 arrays are uint16 bit patterns."""
+    m = len(row_ptr) - 1
+    row_end = m if row_end is None else row_end
+    n = b.shape[1]
+    rp = np.ascontiguousarray(row_ptr, dtype=np.int64)
+    ci = np.ascontiguousarray(col_idx, dtype=np.int64)
+    nnz = int(rp[-1])
+    nt = nthreads or min(os.cpu_count() or 1, 16)
+    if dtype == "f64":
+        aa = np.ascontiguousarray(a, dtype=np.float64)
+        bb = np.ascontiguousarray(b, dtype=np.float64)
+        out = np.zeros(nnz, dtype=np.float64)
+        _lib_sddmm().orc_sddmm_f64(n, _p(rp), _p(ci), _p(aa), n, _p(bb), n, _p(out), row_begin,
+                                   row_end, nt)
+        return out
+    if dtype == "bf16":
+        aa, bb = bf16_bits_to_f32(np.asarray(a)), bf16_bits_to_f32(np.asarray(b))
+    else:
+        aa, bb = np.asarray(a).astype(np.float32), np.asarray(b).astype(np.float32)
+    aa, bb = np.ascontiguousarray(aa), np.ascontiguousarray(bb)
+    out = np.zeros(nnz, dtype=np.float32)
+    _lib_sddmm().orc_sddmm_f32(n, _p(rp), _p(ci), _p(aa), n, _p(bb), n, _p(out), row_begin, row_end, nt)
+    if dtype == "bf16":
+        return f32_to_bf16_bits(out)
+    if dtype == "f16":
+        return out.astype(np.float16)
+    return out
+
+
+def transpose(row_ptr, col_idx, k):
+    """CSR -> CSR of the transpose by a stable sort on the column (entries of each new row keep
+    ascending original row order).  Returns (row_ptr_T, col_idx_T = original rows, perm)."""
+    rp = np.asarray(row_ptr, dtype=np.int64)
+    ci = np.asarray(col_idx, dtype=np.int64)
+    rows = np.repeat(np.arange(len(rp) - 1, dtype=np.int64), np.diff(rp))
+    perm = np.argsort(ci, kind="stable")
+    rp_t = np.zeros(k + 1, dtype=np.int64)
+    rp_t[1:] = np.cumsum(np.bincount(ci, minlength=k))
+    return rp_t, rows[perm], perm

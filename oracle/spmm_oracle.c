@@ -154,3 +154,69 @@ void orc_spmm_f32_ref64(int64_t n, const int64_t* rp, const int64_t* col, const 
     }
   }
 }
+
+/* SDDMM (the values-gradient of C = A @ B): out[j] = <a[row(j) - row_begin, :], b[col[j], :]>
+ * in the operator's documented order (of-spmm_amd/csrc/spmm_backward.hip header): products
+ * rounded, 8-element leaves summed sequentially from +0, leaves zero-padded to a power of two
+ * and added pairwise level by level.  No SDDMM exists in the reference; the order is ours. */
+static int64_t pow2_at_least(int64_t x) {
+  int64_t p = 1;
+  while (p < x) p *= 2;
+  return p;
+}
+
+void orc_sddmm_f32(int64_t n, const int64_t* rp, const int64_t* col, const float* a, int64_t lda,
+                   const float* b, int64_t ldb, float* out, int64_t row_begin, int64_t row_end,
+                   int nthreads) {
+  const int64_t leaves = (n + 7) / 8, padded = pow2_at_least(leaves);
+#pragma omp parallel num_threads(nthreads)
+  {
+    float* leaf = (float*)__builtin_alloca(sizeof(float) * padded);
+#pragma omp for schedule(dynamic, 64)
+    for (int64_t r = row_begin; r < row_end; ++r) {
+      const float* ar = a + (r - row_begin) * lda;
+      for (int64_t j = rp[r]; j < rp[r + 1]; ++j) {
+        const float* br = b + col[j] * ldb;
+        for (int64_t l = 0; l < padded; ++l) {
+          float s = 0.0f;
+          for (int64_t e = 8 * l; e < 8 * l + 8 && e < n; ++e) {
+            const float p = ar[e] * br[e];
+            s = s + p;
+          }
+          leaf[l] = s;
+        }
+        for (int64_t w = 1; w < padded; w *= 2)
+          for (int64_t l = 0; l < padded; l += 2 * w) leaf[l] = leaf[l] + leaf[l + w];
+        out[j] = leaf[0];
+      }
+    }
+  }
+}
+
+void orc_sddmm_f64(int64_t n, const int64_t* rp, const int64_t* col, const double* a, int64_t lda,
+                   const double* b, int64_t ldb, double* out, int64_t row_begin, int64_t row_end,
+                   int nthreads) {
+  const int64_t leaves = (n + 7) / 8, padded = pow2_at_least(leaves);
+#pragma omp parallel num_threads(nthreads)
+  {
+    double* leaf = (double*)__builtin_alloca(sizeof(double) * padded);
+#pragma omp for schedule(dynamic, 64)
+    for (int64_t r = row_begin; r < row_end; ++r) {
+      const double* ar = a + (r - row_begin) * lda;
+      for (int64_t j = rp[r]; j < rp[r + 1]; ++j) {
+        const double* br = b + col[j] * ldb;
+        for (int64_t l = 0; l < padded; ++l) {
+          double s = 0.0;
+          for (int64_t e = 8 * l; e < 8 * l + 8 && e < n; ++e) {
+            const double p = ar[e] * br[e];
+            s = s + p;
+          }
+          leaf[l] = s;
+        }
+        for (int64_t w = 1; w < padded; w *= 2)
+          for (int64_t l = 0; l < padded; l += 2 * w) leaf[l] = leaf[l] + leaf[l + w];
+        out[j] = leaf[0];
+      }
+    }
+  }
+}
