@@ -37,13 +37,15 @@ __global__ void iota_kernel(I* __restrict__ out, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = (I)i;
 }
 
-// row_of[j] = r for j in [rp[r], rp[r+1]): one thread per row (rows are short on average; the
-// writes of one row are contiguous).
+// row_of[j] = r for j in [rp[r], rp[r+1]): one wave per row, lanes stride the row (a hub row
+// of 10^5-10^6 nonzeros must not be written by a single thread).
 template <typename I>
-__global__ void expand_rows_kernel(const I* __restrict__ rp, int64_t m, I* __restrict__ row_of) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(kBlock) expand_rows_kernel(const I* __restrict__ rp, int64_t m,
+                                                             I* __restrict__ row_of) {
+  const int64_t r = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   if (r >= m) return;
-  for (int64_t j = (int64_t)rp[r]; j < (int64_t)rp[r + 1]; ++j) row_of[j] = (I)r;
+  const int lane = threadIdx.x & 63;
+  for (int64_t j = (int64_t)rp[r] + lane; j < (int64_t)rp[r + 1]; j += 64) row_of[j] = (I)r;
 }
 
 // out_rp[c] = first position of column >= c in the sorted keys (binary search).
@@ -115,8 +117,8 @@ int transpose(hipStream_t s, int64_t m, int64_t k, int64_t nnz, const I* rp, con
   void* cub_tmp = static_cast<char*>(ws) + plan::align_up(4 * (size_t)nnz * sizeof(I), 256);
   hipLaunchKernelGGL((iota_kernel<I>), dim3(g_nnz), dim3(kBlock), 0, s, vals_in, nnz);
   OFX_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL((expand_rows_kernel<I>), dim3((unsigned)((m + kBlock - 1) / kBlock)),
-                     dim3(kBlock), 0, s, rp, m, row_of);
+  hipLaunchKernelGGL((expand_rows_kernel<I>), dim3((unsigned)((m + 3) / 4)), dim3(kBlock), 0, s,
+                     rp, m, row_of);
   OFX_HIP_CHECK(hipGetLastError());
   // stable LSD radix sort of (col, j): entries of one column keep ascending j == ascending row
   OFX_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub, col, keys_out, vals_in, out_perm,
@@ -207,38 +209,48 @@ __global__ void __launch_bounds__(kBlock)
   const T* arow = dC + lr * ldc;
 #pragma unroll
   for (int l = 0; l < L; ++l) load_leaf<T, ALIGNED>(arow, (int64_t)(gl * L + l) * kLeaf, n, a[l]);
-  for (int64_t j = j0; j < j1; j += U) {
-    const int cnt = (int)((j1 - j) < U ? (j1 - j) : U);
-    A bv[U][L][kLeaf];
+  const int gbase = lane & ~(LG - 1);
+  // Column indices come LG at a time (one coalesced load per group, then ds_bpermute), so the
+  // B-row loads of a batch never wait behind a dependent index load; lane t keeps the result of
+  // the batch's t-th nonzero and the group stores LG results with one coalesced store.
+  for (int64_t jb = j0; jb < j1; jb += LG) {
+    const int cnt = (int)((j1 - jb) < LG ? (j1 - jb) : LG);
+    const I myc = gl < cnt ? col[jb + gl] : I(0);
+    A res = A(0);
+    for (int k = 0; k < cnt; k += U) {
+      A bv[U][L][kLeaf];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (u < cnt) {
-        const T* brow = B + (int64_t)col[j + u] * ldb;
+      for (int u = 0; u < U; ++u) {
+        const int64_t cu = (int64_t)__shfl((int64_t)myc, gbase + ((k + u) & (LG - 1)), 64);
+        if (k + u < cnt) {
+          const T* brow = B + cu * ldb;
 #pragma unroll
-        for (int l = 0; l < L; ++l) load_leaf<T, ALIGNED>(brow, (int64_t)(gl * L + l) * kLeaf, n, bv[u][l]);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (u < cnt) {
-        A leaf[L];
-#pragma unroll
-        for (int l = 0; l < L; ++l) {
-          A s = A(0);
-#pragma unroll
-          for (int e = 0; e < kLeaf; ++e) s = s + a[l][e] * bv[u][l][e];
-          leaf[l] = s;
+          for (int l = 0; l < L; ++l) load_leaf<T, ALIGNED>(brow, (int64_t)(gl * L + l) * kLeaf, n, bv[u][l]);
         }
+      }
 #pragma unroll
-        for (int w = 1; w < L; w <<= 1)
+      for (int u = 0; u < U; ++u) {
+        if (k + u < cnt) {
+          A leaf[L];
 #pragma unroll
-          for (int l = 0; l < L; l += 2 * w) leaf[l] = leaf[l] + leaf[l + w];
-        A t = leaf[0];
+          for (int l = 0; l < L; ++l) {
+            A s = A(0);
 #pragma unroll
-        for (int w = 1; w < LG; w <<= 1) t = t + __shfl_xor(t, w, 64);
-        if (gl == 0) out[j + u] = Num<T>::store(t);
+            for (int e = 0; e < kLeaf; ++e) s = s + a[l][e] * bv[u][l][e];
+            leaf[l] = s;
+          }
+#pragma unroll
+          for (int w = 1; w < L; w <<= 1)
+#pragma unroll
+            for (int l = 0; l < L; l += 2 * w) leaf[l] = leaf[l] + leaf[l + w];
+          A t = leaf[0];
+#pragma unroll
+          for (int w = 1; w < LG; w <<= 1) t = t + __shfl_xor(t, w, 64);
+          if (gl == k + u) res = t;
+        }
       }
     }
+    if (gl < cnt) out[jb + gl] = Num<T>::store(res);
   }
 }
 
