@@ -258,6 +258,20 @@ int ofx_functional_spmm_csr_ex(void* stream, const ofx_tensor_desc* row_ptr,
                                ofx_tensor_desc* out, void* tmp, size_t tmp_bytes,
                                int64_t parallel_id, int64_t parallel_num, int out_split_axis,
                                int num_threads);
+/* Gradient functors (ops "sddmm_csr", "csr_transpose"; oneflow/user/ops/sddmm_op.cpp) through
+ * the same op-registry dispatch.  With tmp_size_out != NULL only the tmp-buffer size is
+ * computed (nothing runs).  Outputs: sddmm out [nnz] in b's dtype; transpose out_row_ptr [k+1],
+ * out_col_idx [nnz], out_perm [nnz] in the index dtype.                                      */
+int ofx_functional_sddmm_csr(void* stream, const ofx_tensor_desc* row_ptr,
+                             const ofx_tensor_desc* col_idx, const ofx_tensor_desc* a,
+                             const ofx_tensor_desc* b, int64_t a_num_rows, int64_t a_num_cols,
+                             ofx_tensor_desc* out, void* tmp, size_t tmp_bytes,
+                             size_t* tmp_size_out);
+int ofx_functional_csr_transpose(void* stream, const ofx_tensor_desc* row_ptr,
+                                 const ofx_tensor_desc* col_idx, int64_t a_num_rows,
+                                 int64_t a_num_cols, ofx_tensor_desc* out_row_ptr,
+                                 ofx_tensor_desc* out_col_idx, ofx_tensor_desc* out_perm,
+                                 void* tmp, size_t tmp_bytes, size_t* tmp_size_out);
 /* The op's registered SBP signatures and no-grad inputs, as text (tests / introspection). */
 int ofx_op_spmm_csr_sbp_signatures(char* buf, size_t len);
 

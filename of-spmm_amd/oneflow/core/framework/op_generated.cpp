@@ -19,4 +19,30 @@ REGISTER_USER_OP("spmm_csr")
     .SetDataTypeInferFn(SpmmCsrOp::InferDataType)
     .SetInputArgModifyFn(SpmmCsrOp::ModifyInputArg);
 
+REGISTER_USER_OP("sddmm_csr")
+    .Input("a_csr_row_ptr")
+    .Input("a_csr_col_idx")
+    .Input("a")
+    .Input("b")
+    .Output("out")
+    .Attr<int64_t>("a_num_rows", 0)
+    .Attr<int64_t>("a_num_cols", 0)
+    .SetLogicalTensorDescInferFn(SddmmCsrOp::InferLogicalTensorDesc)
+    .SetPhysicalTensorDescInferFn(SddmmCsrOp::InferPhysicalTensorDesc)
+    .SetGetSbpFn(SddmmCsrOp::GetSbp)
+    .SetDataTypeInferFn(SddmmCsrOp::InferDataType);
+
+REGISTER_USER_OP("csr_transpose")
+    .Input("a_csr_row_ptr")
+    .Input("a_csr_col_idx")
+    .Output("out_row_ptr")
+    .Output("out_col_idx")
+    .Output("out_perm")
+    .Attr<int64_t>("a_num_rows", 0)
+    .Attr<int64_t>("a_num_cols", 0)
+    .SetLogicalTensorDescInferFn(CsrTransposeOp::InferLogicalTensorDesc)
+    .SetPhysicalTensorDescInferFn(CsrTransposeOp::InferPhysicalTensorDesc)
+    .SetGetSbpFn(CsrTransposeOp::GetSbp)
+    .SetDataTypeInferFn(CsrTransposeOp::InferDataType);
+
 }  // namespace oneflow

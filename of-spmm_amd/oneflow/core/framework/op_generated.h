@@ -17,6 +17,23 @@ class SpmmCsrOp {
                                     const user_op::UserOpConfWrapper& conf);
 };
 
+// Gradient ops of spmm_csr.
+class SddmmCsrOp {
+ public:
+  static Maybe<void> InferLogicalTensorDesc(user_op::InferContext* ctx);
+  static Maybe<void> InferPhysicalTensorDesc(user_op::InferContext* ctx);
+  static Maybe<void> GetSbp(user_op::SbpContext* ctx);
+  static Maybe<void> InferDataType(user_op::InferContext* ctx);
+};
+
+class CsrTransposeOp {
+ public:
+  static Maybe<void> InferLogicalTensorDesc(user_op::InferContext* ctx);
+  static Maybe<void> InferPhysicalTensorDesc(user_op::InferContext* ctx);
+  static Maybe<void> GetSbp(user_op::SbpContext* ctx);
+  static Maybe<void> InferDataType(user_op::InferContext* ctx);
+};
+
 }  // namespace oneflow
 
 #endif  // OFX_ONEFLOW_SHIM_OP_GENERATED_H_

@@ -235,3 +235,104 @@ extern "C" int ofx_op_spmm_csr_sbp_signatures(char* buf, size_t len) {
   snprintf(buf, len, "%s", s.c_str());
   return OFX_OK;
 }
+
+// ---- gradient functors: functional::SddmmCsr / functional::CsrTranspose ----------------------
+// The grad function of spmm_csr calls these; the Python autograd binding
+// (oneflow_spmm/autograd.py) goes through the same entries.  Generic eager-local dispatch of a
+// registered user op: inference -> output check -> kernel choice (HOB on every arg's dtype) ->
+// tmp size or Compute.
+namespace oneflow {
+namespace {
+
+struct Arg {
+  const char* name;
+  const ofx_tensor_desc* d;
+};
+
+Maybe<void> RunUserOp(const std::string& op_name, const std::vector<Arg>& ins,
+                      const std::vector<Arg>& outs, const user_op::AttrMap& attrs, void* stream,
+                      void* tmp, size_t tmp_bytes, size_t* tmp_size_out) {
+  const user_op::OpRegistryResult* op = user_op::UserOpRegistryMgr::Get().GetOpRegistryResult(op_name);
+  CHECK_OR_RETURN(op != nullptr) << Error::RuntimeError() << "op " << op_name << " is not registered";
+  const int device = ins.front().d->device;
+  DescMap in;
+  for (const Arg& a : ins) {
+    CHECK_OR_RETURN(a.d != nullptr) << Error::RuntimeError() << op_name << ": NULL input " << a.name;
+    CHECK_OR_RETURN(a.d->ndim >= 1 && a.d->ndim <= 2)
+        << Error::RuntimeError() << op_name << ": " << a.name << " must be 1-D or 2-D";
+    CHECK_EQ_OR_RETURN(a.d->device, device)
+        << Error::RuntimeError() << op_name << ": expected all tensors on the same device";
+    in[{a.name, 0}] = user_op::TensorDesc(ShapeOf(a.d), (DataType)a.d->dtype);
+  }
+  user_op::InferContext ictx(in, attrs);
+  JUST(op->logical_infer(&ictx));
+  JUST(op->dtype_infer(&ictx));
+  user_op::KernelRegContext rc;
+  rc.device_type = device < 0 ? DeviceType::kCPU : DeviceType::kHIP;
+  for (const Arg& a : ins) rc.dtypes[{a.name, 0}] = (DataType)a.d->dtype;
+  for (const std::string& o : op->outputs) rc.dtypes[{o, 0}] = ictx.OutputTensorDesc(o, 0).data_type();
+  const user_op::OpKernelRegistryResult* reg = nullptr;
+  JUST(user_op::UserOpRegistryMgr::Get().GetOpKernelRegistryResult(op_name, rc, &reg));
+  if (tmp_size_out) {
+    user_op::InferSizeContext sc;
+    sc.descs = in;
+    sc.attrs = attrs;
+    *tmp_size_out = reg->infer_tmp_size ? reg->infer_tmp_size(&sc) : 0;
+    return Maybe<void>::Ok();
+  }
+  std::vector<std::unique_ptr<user_op::Tensor>> hold;
+  std::map<std::pair<std::string, int32_t>, user_op::Tensor*> tensors;
+  auto add = [&](const Arg& a) {
+    hold.emplace_back(new user_op::Tensor(ShapeOf(a.d), (DataType)a.d->dtype, a.d->data,
+                                          a.d->ndim == 2 ? a.d->stride[0] : -1));
+    tensors[{a.name, 0}] = hold.back().get();
+  };
+  for (const Arg& a : ins) add(a);
+  for (const Arg& o : outs) {
+    CHECK_OR_RETURN(o.d != nullptr) << Error::RuntimeError() << op_name << ": NULL output " << o.name;
+    const user_op::TensorDesc& want = ictx.OutputTensorDesc(o.name, 0);
+    CHECK_OR_RETURN(ShapeOf(o.d) == want.shape() && (DataType)o.d->dtype == want.data_type() &&
+                    o.d->device == device)
+        << Error::RuntimeError() << op_name << ": output " << o.name << " must be "
+        << want.shape().ToString() << " of dtype " << DataType_Name(want.data_type());
+    add(o);
+  }
+  user_op::Tensor t_tmp(Shape({(int64_t)tmp_bytes}), kChar, tmp);
+  if (tmp) tensors[{"tmp_buffer", 0}] = &t_tmp;
+  ep::CpuStream cpu_stream(0);
+  ep::HipStream hip_stream(stream, device);
+  ep::Stream* s = device < 0 ? static_cast<ep::Stream*>(&cpu_stream) : static_cast<ep::Stream*>(&hip_stream);
+  user_op::KernelComputeContext ctx(s, tensors, attrs, rc.device_type);
+  const user_op::OpKernel* kernel = GetKernel(reg);
+  try {
+    kernel->Compute(&ctx, nullptr, nullptr);
+  } catch (const KernelCheckError& e) {
+    return Maybe<void>("KernelCheckError", e.msg);
+  }
+  return Maybe<void>::Ok();
+}
+
+}  // namespace
+}  // namespace oneflow
+
+extern "C" int ofx_functional_sddmm_csr(void* stream, const ofx_tensor_desc* row_ptr,
+                                        const ofx_tensor_desc* col_idx, const ofx_tensor_desc* a,
+                                        const ofx_tensor_desc* b, int64_t a_num_rows,
+                                        int64_t a_num_cols, ofx_tensor_desc* out, void* tmp,
+                                        size_t tmp_bytes, size_t* tmp_size_out) {
+  return ToStatus(RunUserOp("sddmm_csr",
+                            {{"a_csr_row_ptr", row_ptr}, {"a_csr_col_idx", col_idx}, {"a", a}, {"b", b}},
+                            {{"out", out}}, {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols}},
+                            stream, tmp, tmp_bytes, tmp_size_out));
+}
+
+extern "C" int ofx_functional_csr_transpose(void* stream, const ofx_tensor_desc* row_ptr,
+                                            const ofx_tensor_desc* col_idx, int64_t a_num_rows,
+                                            int64_t a_num_cols, ofx_tensor_desc* out_row_ptr,
+                                            ofx_tensor_desc* out_col_idx, ofx_tensor_desc* out_perm,
+                                            void* tmp, size_t tmp_bytes, size_t* tmp_size_out) {
+  return ToStatus(RunUserOp("csr_transpose", {{"a_csr_row_ptr", row_ptr}, {"a_csr_col_idx", col_idx}},
+                            {{"out_row_ptr", out_row_ptr}, {"out_col_idx", out_col_idx}, {"out_perm", out_perm}},
+                            {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols}}, stream, tmp,
+                            tmp_bytes, tmp_size_out));
+}

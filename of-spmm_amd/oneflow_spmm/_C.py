@@ -113,6 +113,49 @@ def spmm_csr(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor,
     return out
 
 
+def _run_grad_op(fn, stream_of, ins, outs, extra):
+    """Two-phase call of a functional gradient entry: tmp size, then the run."""
+    size = ctypes.c_size_t(0)
+    descs_in = [ctypes.byref(desc(t)) for t in ins]
+    descs_out = [ctypes.byref(desc(t)) for t in outs]
+    check(fn(None, *descs_in, *extra, *descs_out, None, 0, ctypes.byref(size)), fn.__name__)
+    tmp = None
+    if size.value and stream_of.device.type != "cpu":
+        tmp = torch.empty(size.value, dtype=torch.uint8, device=stream_of.device)
+    check(fn(current_stream_handle(stream_of), *descs_in, *extra, *descs_out,
+             tmp.data_ptr() if tmp is not None else None, size.value if tmp is not None else 0,
+             None), fn.__name__)
+
+
+def sddmm_csr(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor, a: torch.Tensor,
+              b: torch.Tensor, a_num_rows: int, a_num_cols: int) -> torch.Tensor:
+    """out[j] = <a[row(j), :], b[col(j), :]> (op "sddmm_csr": the values-gradient of spmm_csr)."""
+    rp, ci = _prep(a_csr_row_ptr, "a_csr_row_ptr"), _prep(a_csr_col_idx, "a_csr_col_idx")
+    a, b = _prep(a, "a", matrix=True), _prep(b, "b", matrix=True)
+    if b.dim() == 2 and b.shape[1] == 0:  # empty inner dimension: every dot product is 0
+        out = torch.zeros(ci.numel(), dtype=b.dtype, device=b.device)
+    else:
+        out = torch.empty(ci.numel(), dtype=b.dtype, device=b.device)
+    if b.dim() == 2 and b.shape[1] == 0 and a.dim() == 2 and a.shape[1] == 0:
+        return out
+    _run_grad_op(LIB.ofx_functional_sddmm_csr, b, [rp, ci, a, b], [out],
+                 [int(a_num_rows), int(a_num_cols)])
+    return out
+
+
+def csr_transpose(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor, a_num_rows: int,
+                  a_num_cols: int):
+    """Structure of A^T (op "csr_transpose"): (row_ptr [K+1], col_idx [nnz], perm [nnz])."""
+    rp, ci = _prep(a_csr_row_ptr, "a_csr_row_ptr"), _prep(a_csr_col_idx, "a_csr_col_idx")
+    it, dev = rp.dtype, rp.device
+    rp_t = torch.empty(int(a_num_cols) + 1, dtype=it, device=dev)
+    ci_t = torch.empty(ci.numel(), dtype=it, device=dev)
+    perm = torch.empty(ci.numel(), dtype=it, device=dev)
+    _run_grad_op(LIB.ofx_functional_csr_transpose, rp, [rp, ci], [rp_t, ci_t, perm],
+                 [int(a_num_rows), int(a_num_cols)])
+    return rp_t, ci_t, perm
+
+
 def balanced_range(total: int, parts: int, idx: int) -> tuple[int, int]:
     lo, hi = ctypes.c_int64(), ctypes.c_int64()
     check(LIB.ofx_balanced_range(total, parts, idx, ctypes.byref(lo), ctypes.byref(hi)),

@@ -102,6 +102,10 @@ def _load():
         "ofx_functional_spmm_csr": ([p, pdesc, pdesc, pdesc, i64, i64, pdesc, pdesc, p, sz], i32),
         "ofx_functional_spmm_csr_ex": ([p, pdesc, pdesc, pdesc, i64, i64, pdesc, pdesc, p, sz, i64,
                                         i64, i32, i32], i32),
+        "ofx_functional_sddmm_csr": ([p, pdesc, pdesc, pdesc, pdesc, i64, i64, pdesc, p, sz,
+                                      ctypes.POINTER(sz)], i32),
+        "ofx_functional_csr_transpose": ([p, pdesc, pdesc, i64, i64, pdesc, pdesc, pdesc, p, sz,
+                                          ctypes.POINTER(sz)], i32),
         "ofx_op_spmm_csr_sbp_signatures": ([ctypes.c_char_p, sz], i32),
     }
     for name, (args, res) in sigs.items():

@@ -12,39 +12,20 @@ include/ofx_spmm.h).
 """
 from __future__ import annotations
 
-import ctypes
 from collections import OrderedDict
 
 import torch
 
-from . import ops
+from . import _C, ops
 from ._C import current_stream_handle, dtype_code, spmm_csr
 from ._lib import LIB, check
 
 
 # ---- building blocks ----------------------------------------------------------------------------
 def csr_transpose(row_ptr: torch.Tensor, col_idx: torch.Tensor, k: int):
-    """Structure of A^T: (row_ptr_T [k+1], col_idx_T [nnz] = rows of A, perm [nnz])."""
-    m = row_ptr.numel() - 1
-    nnz = col_idx.numel()
-    it = row_ptr.dtype
-    dev = row_ptr.device
-    rp_t = torch.empty(k + 1, dtype=it, device=dev)
-    ci_t = torch.empty(nnz, dtype=it, device=dev)
-    perm = torch.empty(nnz, dtype=it, device=dev)
-    idt = dtype_code(it)
-    ptr = lambda t: t.data_ptr() if t.numel() else None  # noqa: E731
-    if dev.type == "cpu":
-        check(LIB.ofx_csr_transpose_cpu(idt, m, k, nnz, row_ptr.data_ptr(), ptr(col_idx),
-                                        rp_t.data_ptr(), ptr(ci_t), ptr(perm)), "csr_transpose")
-        return rp_t, ci_t, perm
-    ws_bytes = ctypes.c_size_t(0)
-    check(LIB.ofx_csr_transpose_workspace_size(idt, m, k, nnz, ctypes.byref(ws_bytes)), "csr_transpose")
-    ws = torch.empty(max(ws_bytes.value, 1), dtype=torch.uint8, device=dev)
-    check(LIB.ofx_csr_transpose(current_stream_handle(row_ptr), idt, m, k, nnz, row_ptr.data_ptr(),
-                                ptr(col_idx), rp_t.data_ptr(), ptr(ci_t), ptr(perm),
-                                ws.data_ptr(), ws_bytes.value), "csr_transpose")
-    return rp_t, ci_t, perm
+    """Structure of A^T: (row_ptr_T [k+1], col_idx_T [nnz] = rows of A, perm [nnz]).
+    Op "csr_transpose" through the op layer (CPU or HIP kernel by device)."""
+    return _C.csr_transpose(row_ptr, col_idx, row_ptr.numel() - 1, k)
 
 
 def gather_values(perm: torch.Tensor, values: torch.Tensor) -> torch.Tensor:
@@ -60,34 +41,9 @@ def gather_values(perm: torch.Tensor, values: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def sddmm(row_ptr: torch.Tensor, col_idx: torch.Tensor, a: torch.Tensor, b: torch.Tensor, *,
-          row_begin: int = 0, row_end: int | None = None, num_threads: int = 0) -> torch.Tensor:
-    """out[j] = <a[row(j) - row_begin, :], b[col_idx[j], :]> for the nonzeros of rows
-    [row_begin, row_end) (other entries of `out` stay 0)."""
-    m = row_ptr.numel() - 1
-    row_end = m if row_end is None else row_end
-    n = b.shape[1]
-    k = b.shape[0]
-    nnz = col_idx.numel()
-    a = a if (a.dim() == 2 and a.stride(1) == 1) else a.contiguous()
-    b = b if (b.dim() == 2 and b.stride(1) == 1) else b.contiguous()
-    out = torch.zeros(nnz, dtype=b.dtype, device=b.device)
-    if nnz == 0 or row_end == row_begin or n == 0:
-        return out
-    idt, vdt = dtype_code(row_ptr.dtype), dtype_code(b.dtype)
-    if b.device.type == "cpu":
-        check(LIB.ofx_sddmm_csr_cpu(int(num_threads), idt, vdt, m, k, n, nnz, row_ptr.data_ptr(),
-                                    col_idx.data_ptr(), a.data_ptr(), a.stride(0), b.data_ptr(),
-                                    b.stride(0), out.data_ptr(), row_begin, row_end), "sddmm_csr")
-        return out
-    ws_bytes = ctypes.c_size_t(0)
-    check(LIB.ofx_sddmm_csr_workspace_size(idt, vdt, m, n, nnz, ctypes.byref(ws_bytes)), "sddmm_csr")
-    ws = torch.empty(max(ws_bytes.value, 1), dtype=torch.uint8, device=b.device)
-    check(LIB.ofx_sddmm_csr(current_stream_handle(b), idt, vdt, m, k, n, nnz, row_ptr.data_ptr(),
-                            col_idx.data_ptr(), a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
-                            out.data_ptr(), row_begin, row_end, ws.data_ptr(), ws_bytes.value),
-          "sddmm_csr")
-    return out
+def sddmm(row_ptr: torch.Tensor, col_idx: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """out[j] = <a[row(j), :], b[col_idx[j], :]>: op "sddmm_csr" through the op layer."""
+    return _C.sddmm_csr(row_ptr, col_idx, a, b, row_ptr.numel() - 1, b.shape[0])
 
 
 # ---- transpose cache (the sparsity pattern of a GNN graph is static across layers/steps) -------

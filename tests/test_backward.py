@@ -207,3 +207,22 @@ def test_gpu_autograd_bitexact_vs_oracle(device):
     assert len(fs.autograd.TRANSPOSE_CACHE.entries) == n_cached
     torch.cuda.synchronize()
     assert_bitwise(bb.grad, oracle.spmm(rt, ct, v.numpy()[perm], g.numpy()), "d b (cached)")
+
+
+def test_grad_ops_through_op_layer_errors_and_sbp():
+    rng = np.random.default_rng(9)
+    m, k, n = 10, 12, 6
+    rp, ci, v = random_csr(m, k, rng.integers(0, 4, size=m), rng)
+    a = random_dense(m, n, rng)
+    b = random_dense(k, n, rng)
+    with pytest.raises(RuntimeError, match="same number of columns"):
+        fs._C.sddmm_csr(rp, ci, a[:, :4].contiguous(), b, m, k)
+    with pytest.raises(RuntimeError, match="a_num_rows rows"):
+        fs._C.sddmm_csr(rp, ci, a[:5].contiguous(), b, m, k)
+    with pytest.raises(TypeError, match="a datatype"):
+        fs._C.sddmm_csr(rp, ci, a.double(), b, m, k)
+    with pytest.raises(RuntimeError, match="a_num_rows"):
+        fs._C.csr_transpose(rp, ci, m + 1, k)
+    assert fs._C.sddmm_csr(rp, ci, a[:, :0], b[:, :0], m, k).abs().sum() == 0
+    rt, ct, perm = fs._C.csr_transpose(rp, ci, m, k)
+    assert rt.shape == (k + 1,) and ct.shape == ci.shape and perm.dtype == rp.dtype
