@@ -159,6 +159,22 @@ int ofx_sddmm_csr_cpu(int num_threads, int idx_dtype, int val_dtype, int64_t m, 
                       const void* a, int64_t lda, const void* b, int64_t ldb, void* out,
                       int64_t row_begin, int64_t row_end);
 
+/* ---- COO (edge_index) -> CSR -----------------------------------------
+ * Canonical CSR from COO pairs: rows ascending, columns ascending; with merge_duplicates != 0,
+ * equal (row, col) entries become one whose value is their sum in input order (fp32 accumulation
+ * for 16-bit types), else duplicates are kept in input order.  values/out_values may both be
+ * NULL (structure only).  out_nnz: device int64 scalar (host int64* for the CPU version);
+ * bad_flag (device uint32, may be NULL) is set non-zero if an entry lies outside m x k.
+ * Outputs must hold nnz entries (the upper bound).  Device version: nnz < 2^31.            */
+int ofx_coo_to_csr_workspace_size(int idx_dtype, int64_t m, int64_t k, int64_t nnz, size_t* bytes);
+int ofx_coo_to_csr(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k, int64_t nnz,
+                   const void* row, const void* col, const void* values, int merge_duplicates,
+                   void* out_row_ptr, void* out_col_idx, void* out_values, void* out_nnz,
+                   void* bad_flag, void* workspace, size_t workspace_bytes);
+int ofx_coo_to_csr_cpu(int idx_dtype, int val_dtype, int64_t m, int64_t k, int64_t nnz,
+                       const void* row, const void* col, const void* values, int merge_duplicates,
+                       void* out_row_ptr, void* out_col_idx, void* out_values, int64_t* out_nnz);
+
 /* ---- row partition (BalancedSplitter) ---------------------------------------------------- */
 int ofx_balanced_range(int64_t total, int64_t parts, int64_t idx, int64_t* begin, int64_t* end);
 /* Rebase a row slice of a CSR: out_row_ptr[i] = row_ptr[row_begin + i] - row_ptr[row_begin],

@@ -258,3 +258,85 @@ extern "C" int ofx_sddmm_csr_cpu(int num_threads, int idx_dtype, int val_dtype, 
   else run((const int64_t*)nullptr);
   return OFX_OK;
 }
+
+// ---- COO -> CSR on the host (same output as csr_build.hip) ------------------------------------
+#include <algorithm>
+#include <numeric>
+
+namespace ofx {
+namespace {
+template <typename T, typename I>
+int64_t cpu_coo_to_csr(int64_t m, int64_t k, int64_t nnz, const I* row, const I* col, const T* val,
+                       int merge, I* out_rp, I* out_col, T* out_val) {
+#pragma clang fp contract(off)
+  using A = typename Num<T>::acc;
+  std::vector<int64_t> perm(nnz);
+  std::iota(perm.begin(), perm.end(), 0);
+  auto key = [&](int64_t i) { return (uint64_t)row[i] * (uint64_t)k + (uint64_t)col[i]; };
+  std::stable_sort(perm.begin(), perm.end(), [&](int64_t a, int64_t b) { return key(a) < key(b); });
+  int64_t o = 0;
+  std::vector<int64_t> cnt(m + 1, 0);
+  for (int64_t i = 0; i < nnz;) {
+    int64_t e = i + 1;
+    if (merge)
+      while (e < nnz && key(perm[e]) == key(perm[i])) ++e;
+    out_col[o] = col[perm[i]];
+    if (val) {
+      A acc = A(0);
+      for (int64_t q = i; q < e; ++q) acc = acc + Num<T>::load(val[perm[q]]);
+      out_val[o] = Num<T>::store(acc);
+    }
+    ++cnt[(int64_t)row[perm[i]] + 1];
+    ++o;
+    i = e;
+  }
+  for (int64_t r = 0; r < m; ++r) cnt[r + 1] += cnt[r];
+  for (int64_t r = 0; r <= m; ++r) out_rp[r] = (I)cnt[r];
+  return o;
+}
+}  // namespace
+}  // namespace ofx
+
+extern "C" int ofx_coo_to_csr_cpu(int idx_dtype, int val_dtype, int64_t m, int64_t k, int64_t nnz,
+                                  const void* row, const void* col, const void* values,
+                                  int merge_duplicates, void* out_row_ptr, void* out_col_idx,
+                                  void* out_values, int64_t* out_nnz) {
+  OFX_REQUIRE(m >= 0 && k >= 0 && nnz >= 0 && out_row_ptr && out_nnz &&
+                  (nnz == 0 || (row && col && out_col_idx)),
+              OFX_EINVAL, "coo_to_csr_cpu: bad arguments");
+  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "coo_to_csr_cpu: bad index dtype");
+  OFX_REQUIRE((values == nullptr) == (out_values == nullptr), OFX_EINVAL,
+              "coo_to_csr_cpu: values and out_values must both be given or both be NULL");
+  auto run = [&](auto* ip) -> int {
+    using I = std::remove_const_t<std::remove_pointer_t<decltype(ip)>>;
+    const I* r = (const I*)row;
+    const I* c = (const I*)col;
+    for (int64_t i = 0; i < nnz; ++i)
+      OFX_REQUIRE(r[i] >= 0 && r[i] < m && c[i] >= 0 && c[i] < k, OFX_EINVAL,
+                  "coo_to_csr_cpu: entry %lld (%lld, %lld) outside %lld x %lld", (long long)i,
+                  (long long)r[i], (long long)c[i], (long long)m, (long long)k);
+    const int vdt = values ? val_dtype : OFX_DT_FLOAT;
+    switch (vdt) {
+      case OFX_DT_FLOAT:
+        *out_nnz = cpu_coo_to_csr<float, I>(m, k, nnz, r, c, (const float*)values, merge_duplicates,
+                                            (I*)out_row_ptr, (I*)out_col_idx, (float*)out_values);
+        break;
+      case OFX_DT_DOUBLE:
+        *out_nnz = cpu_coo_to_csr<double, I>(m, k, nnz, r, c, (const double*)values, merge_duplicates,
+                                             (I*)out_row_ptr, (I*)out_col_idx, (double*)out_values);
+        break;
+      case OFX_DT_BFLOAT16:
+        *out_nnz = cpu_coo_to_csr<bf16, I>(m, k, nnz, r, c, (const bf16*)values, merge_duplicates,
+                                           (I*)out_row_ptr, (I*)out_col_idx, (bf16*)out_values);
+        break;
+      case OFX_DT_FLOAT16:
+        *out_nnz = cpu_coo_to_csr<f16, I>(m, k, nnz, r, c, (const f16*)values, merge_duplicates,
+                                          (I*)out_row_ptr, (I*)out_col_idx, (f16*)out_values);
+        break;
+      default: return fail(OFX_EUNSUPPORTED, "coo_to_csr_cpu: bad value dtype %d", vdt);
+    }
+    return OFX_OK;
+  };
+  if (idx_dtype == OFX_DT_INT32) return run((const int32_t*)nullptr);
+  return run((const int64_t*)nullptr);
+}

@@ -65,6 +65,9 @@ def _load():
         "ofx_sddmm_csr_workspace_size": ([i32, i32, i64, i64, i64, ctypes.POINTER(sz)], i32),
         "ofx_sddmm_csr": ([p, i32, i32, i64, i64, i64, i64, p, p, p, i64, p, i64, p, i64, i64, p, sz], i32),
         "ofx_sddmm_csr_cpu": ([i32, i32, i32, i64, i64, i64, i64, p, p, p, i64, p, i64, p, i64, i64], i32),
+        "ofx_coo_to_csr_workspace_size": ([i32, i64, i64, i64, ctypes.POINTER(sz)], i32),
+        "ofx_coo_to_csr": ([p, i32, i32, i64, i64, i64, p, p, p, i32, p, p, p, p, p, p, sz], i32),
+        "ofx_coo_to_csr_cpu": ([i32, i32, i64, i64, i64, p, p, p, i32, p, p, p, ctypes.POINTER(i64)], i32),
         "ofx_balanced_range": ([i64, i64, i64, ctypes.POINTER(i64), ctypes.POINTER(i64)], i32),
         "ofx_csr_row_slice": ([p, i32, p, i64, i64, p], i32),
         "ofx_csr_row_slice_host": ([i32, p, i64, i64, p, ctypes.POINTER(i64), ctypes.POINTER(i64)], i32),

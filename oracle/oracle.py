@@ -202,3 +202,46 @@ def transpose(row_ptr, col_idx, k):
     rp_t = np.zeros(k + 1, dtype=np.int64)
     rp_t[1:] = np.cumsum(np.bincount(ci, minlength=k))
     return rp_t, rows[perm], perm
+
+
+# ---- COO -> CSR -----------------------------------------------------------
+def coo_to_csr(row, col, values, m, k, merge=True, dtype="f32"):
+    """Canonical CSR from COO by a stable sort on (row, col); duplicates summed sequentially in
+    input order (fp32 for 16-bit types; bf16 as uint16 bits)."""
+    row = np.asarray(row, dtype=np.int64)
+    col = np.asarray(col, dtype=np.int64)
+    key = row * k + col
+    perm = np.argsort(key, kind="stable")
+    sk = key[perm]
+    heads = np.ones(len(sk), dtype=bool)
+    if merge and len(sk):
+        heads[1:] = sk[1:] != sk[:-1]
+    starts = np.nonzero(heads)[0]
+    ends = np.append(starts[1:], len(sk))
+    out_col = col[perm][starts]
+    out_row = row[perm][starts]
+    rp = np.zeros(m + 1, dtype=np.int64)
+    rp[1:] = np.cumsum(np.bincount(out_row, minlength=m))
+    out_val = None
+    if values is not None:
+        if dtype == "bf16":
+            v = bf16_bits_to_f32(np.asarray(values))
+        elif dtype == "f64":
+            v = np.asarray(values, dtype=np.float64)
+        else:
+            v = np.asarray(values).astype(np.float32)
+        acc_t = np.float64 if dtype == "f64" else np.float32
+        out = np.zeros(len(starts), dtype=acc_t)
+        vp = v[perm]
+        for i, (s, e) in enumerate(zip(starts, ends)):
+            a = acc_t(0)
+            for q in range(s, e):
+                a = acc_t(a + vp[q])
+            out[i] = a
+        if dtype == "bf16":
+            out_val = f32_to_bf16_bits(out)
+        elif dtype == "f16":
+            out_val = out.astype(np.float16)
+        else:
+            out_val = out
+    return rp, out_col, out_val
