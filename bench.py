@@ -45,7 +45,17 @@ def alg_bytes(rows: int, nnz: int, n: int, s_v: int, s_i: int = 4) -> int:
     return s_i * (rows + 1) + (s_i + s_v) * nnz + s_v * nnz * n + s_v * rows * n
 
 
+def _claim_stdout():
+    """Route fd 1 to stderr for the whole run (RCCL and the HIP runtime print banners on stdout)
+    and return a writer on the real stdout for the one JSON line of the bench contract."""
+    real = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
+    return os.fdopen(real, "w")
+
+
 def main():
+    out_stream = _claim_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -162,6 +172,12 @@ def main():
         if rowsplit:
             gather_ms.append(events[0].elapsed_time(events[1]))
     kern_ms = float(np.mean(spmm_ms))
+    gather_mean = float(np.mean(gather_ms)) if gather_ms else 0.0
+    phase = {"spmm_ms_max": kern_ms, "gather_ms_max": gather_mean}
+    if rowsplit and world > 1:
+        t = torch.tensor([kern_ms, gather_mean], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        phase = {"spmm_ms_max": float(t[0]), "gather_ms_max": float(t[1])}
     bytes_launch = alg_bytes(rows, nnz_local, n, s_v)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
 
@@ -202,9 +218,16 @@ def main():
                      "alg_bytes_per_launch": bytes_launch, "kernel_ms": round(kern_ms, 4)},
     }
     if rowsplit:
-        result["extra"] = {"allgather_ms_rank0": round(float(np.mean(gather_ms)), 4),
-                           "spmm_ms_rank0": round(kern_ms, 4),
-                           "rows_rank0": rows, "nnz_rank0": nnz_local}
+        result["extra"] = {
+            "allgather_ms_rank0": round(gather_mean, 4),
+            "spmm_ms_rank0": round(kern_ms, 4),
+            "allgather_ms_max": round(phase["gather_ms_max"], 4),
+            "spmm_ms_max": round(phase["spmm_ms_max"], 4),
+            # SpMM phase alone with the gathered B resident (SURVEY.md §8e reports it separately)
+            "spmm_phase_gflops_aggregate": round(flops / (phase["spmm_ms_max"] * 1e-3) / 1e9, 2),
+            "allgather_gbs_per_rank": round((rs.k_padded - rs.pad) * n * s_v / (phase["gather_ms_max"] * 1e-3) / 1e9, 2)
+            if phase["gather_ms_max"] > 0 else None,
+            "rows_rank0": rows, "nnz_rank0": nnz_local}
 
     # ---- CPU baseline: oracle restatement on the host cores (rank 0, N=1 only) ---------------
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
@@ -228,7 +251,7 @@ def main():
                                   "sample": f"full workload x{reps} runs ({t_cpu:.1f} s), oracle/spmm_oracle.c "
                                             f"OpenMP {threads} threads, same inputs and schedule"}
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=out_stream, flush=True)
     if rowsplit:
         rs.close()
         dist.destroy_process_group()
