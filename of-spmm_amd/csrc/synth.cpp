@@ -46,6 +46,16 @@ void fill_columns(int64_t k, double gamma, uint64_t seed, const int64_t* rp, int
     cdf[c] = acc;
   }
   const double W = acc;
+  // Bucket index over the CDF: bucket q covers targets [q*W/NB, (q+1)*W/NB); lo[q] = the first
+  // rank whose cdf exceeds the bucket's lower edge, so a search starts at lo[q] and ends by
+  // lo[q+1] + 1.  Same answer as a full binary search, O(1) expected steps on huge k.
+  const int64_t NB = k < (1 << 22) ? (k > 0 ? k : 1) : (1 << 22);
+  std::vector<int64_t> blo(NB + 1);
+  for (int64_t q = 0, r = 0; q <= NB; ++q) {
+    const double edge = (double)q / (double)NB * W;
+    while (r < k && cdf[r] <= edge) ++r;
+    blo[q] = r;
+  }
   const std::vector<int64_t> perm = permutation(k, seed);
   const uint64_t cs = splitmix64(seed ^ 0x636f6c756d6e73ull);
   const int64_t base = rp[row_begin];
@@ -62,9 +72,17 @@ void fill_columns(int64_t k, double gamma, uint64_t seed, const int64_t* rp, int
       for (int64_t j = 0; j < d; ++j) {
         const double uj = (double)(hash2(rs, (uint64_t)j) >> 11) * (1.0 / 9007199254740992.0);
         const double target = ((double)j + uj) / (double)d * W;
-        int64_t rank = (int64_t)(std::upper_bound(cdf.begin() + (prev + 1 < k ? prev + 1 : k - 1),
-                                                  cdf.end(), target) -
+        int64_t q = (int64_t)(target / W * (double)NB);
+        if (q < 0) q = 0;
+        if (q > NB - 1) q = NB - 1;
+        // first rank with cdf > target: search the bucket (one rank of slack on each side for
+        // edge rounding), fall back to the whole table if the bucket does not bracket it
+        const int64_t lo = blo[q] > 0 ? blo[q] - 1 : 0;
+        const int64_t hi = blo[q + 1] + 1 < k ? blo[q + 1] + 1 : k;
+        int64_t rank = (int64_t)(std::upper_bound(cdf.begin() + lo, cdf.begin() + hi, target) -
                                  cdf.begin());
+        if (!((rank == 0 || cdf[rank - 1] <= target) && (rank == k || cdf[rank] > target)))
+          rank = (int64_t)(std::upper_bound(cdf.begin(), cdf.end(), target) - cdf.begin());
         if (rank > k - 1) rank = k - 1;
         if (rank < prev + 1) rank = prev + 1;
         if (rank > k - d + j) rank = k - d + j;

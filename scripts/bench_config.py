@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Single-GPU throughput of one BASELINE config through the op layer, with a sampled bit-exact
+check against the oracle (first/last rows, a middle block and the heaviest rows).
+
+    python scripts/bench_config.py --config papers [--reps 5]
+
+Prints one JSON line: time, GFLOP/s, gather-model GB/s and fraction of 8 TB/s, and the check."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "of-spmm_amd"), ROOT]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="papers")
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--threads", type=int, default=16)
+    args = ap.parse_args()
+    import oneflow_spmm as fs
+    from oneflow_spmm import synth
+    from bench import alg_bytes
+    from oracle import oracle
+
+    cfg = synth.CONFIGS[args.config]
+    m, k, nnz, n, dt = cfg["m"], cfg["k"], cfg["nnz"], cfg["n"], cfg["dtype"]
+    dev = torch.device("cuda", 0)
+    t0 = time.time()
+    rp_full = synth.row_ptr(m, k, nnz)
+    cols = synth.columns(m, k, rp_full, threads=args.threads)
+    vals = synth.values(0, nnz, dt)
+    t_gen = time.time() - t0
+    d_rp = torch.from_numpy(rp_full.astype(np.int32 if nnz < 2**31 else np.int64)).to(dev)
+    d_ci = torch.from_numpy(cols).to(dev)
+    d_v = vals.to(dev)
+    d_b = synth.dense(0, k, n, dt, device=dev)
+    out = torch.empty((m, n), dtype=dt, device=dev)
+    fs.spmm(d_rp, d_ci, d_v, m, k, d_b, out=out)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ts = []
+    for _ in range(args.reps):
+        e0.record()
+        fs.spmm(d_rp, d_ci, d_v, m, k, d_b, out=out)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    ms = float(np.median(ts))
+    sv = d_b.element_size()
+    nbytes = alg_bytes(m, nnz, n, sv)
+    # sampled check (bit-exact vs oracle with the operator's schedule)
+    deg = np.diff(rp_full)
+    heavy = np.argsort(deg)[-20:]
+    ranges = [(0, 2000), (m // 2, m // 2 + 2000), (m - 2000, m)] + [(int(r), int(r) + 1) for r in heavy]
+    b_rows_needed = None  # oracle reads B rows through col; copy B to host once
+    b_host = d_b.cpu()
+    b_np = b_host.numpy() if dt != torch.bfloat16 else b_host.view(torch.int16).numpy().view(np.uint16)
+    v_np = vals.numpy() if dt != torch.bfloat16 else vals.view(torch.int16).numpy().view(np.uint16)
+    dname = {torch.float32: "f32", torch.bfloat16: "bf16", torch.float16: "f16", torch.float64: "f64"}[dt]
+    ok = True
+    for lo, hi in ranges:
+        ref = oracle.spmm(rp_full, cols, v_np, b_np, dtype=dname, row_begin=lo, row_end=hi,
+                          nthreads=args.threads)
+        got = out[lo:hi].cpu()
+        got = got.numpy() if dt != torch.bfloat16 else got.view(torch.int16).numpy().view(np.uint16)
+        ok = ok and np.array_equal(np.ascontiguousarray(got).view(np.uint8),
+                                   np.ascontiguousarray(ref).view(np.uint8))
+    del b_rows_needed
+    print(json.dumps({
+        "config": args.config, "m": m, "nnz": nnz, "n": n, "dtype": dname,
+        "max_degree": int(deg.max()), "gen_s": round(t_gen, 1), "ms": round(ms, 3),
+        "gflops": round(2.0 * nnz * n / (ms * 1e-3) / 1e9, 1),
+        "gather_model_gbs": round(nbytes / (ms * 1e-3) / 1e9, 1),
+        "frac_of_8tbs": round(nbytes / (ms * 1e-3) / 8e12, 4),
+        "sampled_rows_bitexact": bool(ok), "sampled_ranges": len(ranges)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
