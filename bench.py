@@ -64,6 +64,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--variant", type=int, default=0, help="force a kernel variant (VEC*100+LPR)")
+    ap.add_argument("--comm", choices=["rccl", "rccl-p2p"], default=None,
+                    help="all-gather schedule for N>1 (default: measured at setup, faster kept)")
     ap.add_argument("--force-rowsplit", action="store_true",
                     help="run the N>1 code path (RCCL all-gather + local SpMM) even with one rank")
     args = ap.parse_args()
@@ -125,6 +127,10 @@ def main():
         d_ci = rs.remap_columns(d_ci)
         klo, khi = rs.k_range
         rs.shard_view().copy_(synth.dense(klo, khi, n, dt, device=device))
+        # ring vs direct point-to-point all-gather: measured here (untimed), faster one kept
+        comm_times = rs.tune_comm() if not args.comm else {}
+        if args.comm:
+            rs.comm_kind = args.comm
 
         def step():
             rs(d_rp, d_ci, d_v, out=out)
@@ -227,7 +233,9 @@ def main():
             "spmm_phase_gflops_aggregate": round(flops / (phase["spmm_ms_max"] * 1e-3) / 1e9, 2),
             "allgather_gbs_per_rank": round((rs.k_padded - rs.pad) * n * s_v / (phase["gather_ms_max"] * 1e-3) / 1e9, 2)
             if phase["gather_ms_max"] > 0 else None,
-            "rows_rank0": rows, "nnz_rank0": nnz_local}
+            "rows_rank0": rows, "nnz_rank0": nnz_local,
+            "allgather_schedule": rs.comm_kind,
+            "allgather_tune_ms": {kk: round(vv, 4) for kk, vv in comm_times.items()}}
 
     # ---- CPU baseline: oracle restatement on the host cores (rank 0, N=1 only) ---------------
     if world == 1 and rank == 0 and not args.no_cpu_baseline:

@@ -217,6 +217,9 @@ int ofx_comm_init_rank(void** comm, int nranks, const void* uid, int rank);
 int ofx_comm_destroy(void* comm);
 /* out[r*count .. (r+1)*count) = in of rank r; count in elements of dtype. */
 int ofx_allgather(void* stream, const void* in, void* out, size_t count, int dtype, void* comm);
+/* The same all-gather as grouped point-to-point send/recv with every peer (in place: this
+ * rank's slot of `buf` is the send buffer).  Same result bytes as ofx_allgather.           */
+int ofx_allgather_p2p(void* stream, void* buf, size_t count, int dtype, void* comm);
 
 /* ---- synthetic power-law CSR (deterministic, counter-based) ---------------- */
 /* row_ptr_out: int64[m+1].  Degrees of a Chung–Lu power law (exponent gamma), rows permuted. */

@@ -72,3 +72,29 @@ extern "C" int ofx_allgather(void* stream, const void* in, void* out, size_t cou
                                static_cast<hipStream_t>(stream)));
   return OFX_OK;
 }
+
+// All-gather as grouped point-to-point transfers: every rank sends its slot to every peer and
+// receives every peer's slot directly (one xGMI link per peer on a fully connected MI355X node),
+// instead of RCCL's ring/tree schedule.  `buf` holds nranks slots of `count` elements; this
+// rank's slot (rank * count) is the send buffer (in place).  Same bytes as ofx_allgather.
+extern "C" int ofx_allgather_p2p(void* stream, void* buf, size_t count, int dtype, void* comm) {
+  ncclDataType_t t;
+  OFX_REQUIRE(nccl_dtype(dtype, &t), OFX_EUNSUPPORTED, "allgather_p2p: unsupported dtype %d", dtype);
+  OFX_REQUIRE(comm && (count == 0 || buf), OFX_EINVAL, "allgather_p2p: NULL argument");
+  ncclComm_t c = static_cast<ncclComm_t>(comm);
+  int nranks = 0, rank = 0;
+  OFX_NCCL_CHECK(ncclCommCount(c, &nranks));
+  OFX_NCCL_CHECK(ncclCommUserRank(c, &rank));
+  const size_t esz = (size_t)(dtype == OFX_DT_DOUBLE || dtype == OFX_DT_INT64 ? 8
+                              : (dtype == OFX_DT_FLOAT16 || dtype == OFX_DT_BFLOAT16 ? 2 : 4));
+  char* base = static_cast<char*>(buf);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  OFX_NCCL_CHECK(ncclGroupStart());
+  for (int d = 1; d < nranks; ++d) {  // peers in a rotated order so links are loaded evenly
+    const int to = (rank + d) % nranks, from = (rank - d + nranks) % nranks;
+    OFX_NCCL_CHECK(ncclSend(base + (size_t)rank * count * esz, count, t, to, c, s));
+    OFX_NCCL_CHECK(ncclRecv(base + (size_t)from * count * esz, count, t, from, c, s));
+  }
+  OFX_NCCL_CHECK(ncclGroupEnd());
+  return OFX_OK;
+}

@@ -71,9 +71,11 @@ class RowSplitSpmm:
                                             self.device)
         if comm == "auto":
             comm = "rccl" if self.device.type == "cuda" else "torch"
+        if comm not in ("rccl", "rccl-p2p", "torch"):
+            raise ValueError(f"RowSplitSpmm: unknown comm {comm!r}")
         self.comm_kind = comm
         self._comm = None
-        if comm == "rccl":
+        if comm.startswith("rccl"):
             self._init_rccl()
         self.ev = None
 
@@ -89,6 +91,29 @@ class RowSplitSpmm:
         check(LIB.ofx_set_device(self.device.index if self.device.index is not None else 0), "set_device")
         check(LIB.ofx_comm_init_rank(ctypes.byref(comm), self.world, uid, self.rank), "comm_init_rank")
         self._comm = comm
+
+    def tune_comm(self, reps: int = 3) -> dict:
+        """Times the ring all-gather and the point-to-point one on this node (same bytes) and
+        keeps the faster; the timings are max-reduced over ranks, so every rank makes the
+        same choice.  Returns the timings (ms)."""
+        if not self.comm_kind.startswith("rccl") or self.world == 1:
+            return {}
+        times = {}
+        for kind in ("rccl", "rccl-p2p"):
+            self.comm_kind = kind
+            self.all_gather_b()
+            torch.cuda.synchronize(self.device)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                self.all_gather_b()
+            e1.record()
+            torch.cuda.synchronize(self.device)
+            t = torch.tensor([e0.elapsed_time(e1) / reps], dtype=torch.float64, device=self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            times[kind] = float(t.item())
+        self.comm_kind = min(times, key=times.get)
+        return times
 
     def close(self):
         if self._comm is not None:
@@ -120,6 +145,10 @@ class RowSplitSpmm:
             s = current_stream_handle(self.gathered)
             check(LIB.ofx_allgather(s, slot.data_ptr(), self.gathered.data_ptr(), count,
                                     dtype_code(self.dtype), self._comm), "allgather")
+        elif self.comm_kind == "rccl-p2p":
+            s = current_stream_handle(self.gathered)
+            check(LIB.ofx_allgather_p2p(s, self.gathered.data_ptr(), count, dtype_code(self.dtype),
+                                        self._comm), "allgather_p2p")
         else:
             parts = list(self.gathered.view(self.world, self.pad, self.n).unbind(0))
             dist.all_gather(parts, slot.clone(), group=self.group)  # views: lands in place

@@ -1,0 +1,95 @@
+"""Multi-rank RCCL path on whatever GPUs the box has: 2 processes share the visible GPU(s)
+(rank r on device r % ndev), torch.distributed/gloo is only the bootstrap store, the RCCL
+communicator and both all-gather schedules (ring ncclAllGather, grouped send/recv) go through the
+C-ABI.  Every rank's output rows are compared bit-exactly with the oracle in the parent.
+RCCL may refuse two ranks on one device ("Duplicate GPU"): the test then skips, the 2-rank
+semantics stay covered by tests/test_distributed_gloo.py."""
+import os
+import socket
+import traceback
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from helpers import assert_bitwise, oracle_spmm, power_law_degrees, random_csr, random_dense
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, kind, rp, ci, v, b, q):
+    try:
+        import torch.distributed as dist
+        from oneflow_spmm.distributed import RowSplitSpmm
+
+        ndev = torch.cuda.device_count()
+        device = torch.device("cuda", rank % ndev)
+        torch.cuda.set_device(device)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                                world_size=world)
+        m, k, n = rp.numel() - 1, b.shape[0], b.shape[1]
+        try:
+            rs = RowSplitSpmm(m, k, n, ci.numel(), torch.float32, torch.int32, device,
+                              comm="rccl" if kind == "tune" else kind, local_csr=False)
+        except Exception as e:  # OfxError(OFX_ECOMM) when RCCL rejects the layout
+            q.put((rank, "skip", str(e)))
+            dist.destroy_process_group()
+            return
+        lo, hi = rs.k_range
+        rs.shard_view().copy_(b[lo:hi].to(device))
+        times = rs.tune_comm(reps=2) if kind == "tune" else {}
+        if kind == "tune":  # the tuning gathers wrote the same bytes; reset the foreign slots
+            rs.gathered.zero_()
+            rs.shard_view().copy_(b[lo:hi].to(device))
+        out = rs(rp.to(device), rs.remap_columns(ci.to(device)), v.to(device))
+        torch.cuda.synchronize()
+        q.put((rank, "ok", (rs.row_range, out.cpu(), rs.comm_kind, times)))
+        rs.close()
+        dist.destroy_process_group()
+    except Exception:
+        q.put((rank, "err", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("kind", ["rccl", "rccl-p2p", "tune"])
+def test_row_split_two_ranks(kind):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rng = np.random.default_rng(29)
+    m, k, n = 1001, 999, 64          # K % 2 != 0: exercises the padded slots
+    rp, ci, v = random_csr(m, k, power_law_degrees(m, 30000, k, rng), rng)
+    b = random_dense(k, n, rng)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    env_old = os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, rp, ci, v, b, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    if env_old is None:
+        os.environ.pop("HSA_ENABLE_IPC_MODE_LEGACY", None)
+    errs = [r for r in res if r[1] == "err"]
+    assert not errs, errs[0][2]
+    skips = [r for r in res if r[1] == "skip"]
+    if skips:
+        pytest.skip(f"RCCL refused this rank layout: {skips[0][2][:200]}")
+    ref = oracle_spmm(rp, ci, v, b)
+    kinds = set()
+    for _, _, ((lo, hi), out, ck, times) in res:
+        assert_bitwise(out, ref[lo:hi], f"{kind} rows [{lo},{hi})")
+        kinds.add(ck)
+        if kind == "tune":
+            assert set(times) == {"rccl", "rccl-p2p"}
+    assert len(kinds) == 1  # every rank made the same choice
