@@ -47,37 +47,91 @@ class RowSplitSpmm:
 
     Call with this rank's *local* CSR slice (row_ptr rebased to 0, columns already remapped with
     `remap_columns`) — or construct with `local_csr=False` and pass the full CSR (Broadcast SBP);
-    the kernel then computes the row range itself (the OpKernelCache path)."""
+    the kernel then computes the row range itself (the OpKernelCache path).
+
+    pipeline = C > 1 splits the dense columns into C blocks of N/C: the gathered buffer is laid
+    out block-major [C, K_pad, N/C], block c+1 is all-gathered on a side stream while the SpMM of
+    block c runs (out[:, block c] written through ldc = N).  Output columns are independent and
+    every block runs the full-N hub schedule (split = default_split(N)), so the result is
+    bit-identical to C = 1."""
 
     def __init__(self, m: int, k: int, n: int, nnz_local: int, dtype: torch.dtype,
                  idx_dtype: torch.dtype, device: torch.device, group=None,
-                 comm: str = "auto", local_csr: bool = True):
+                 comm: str = "auto", local_csr: bool = True, pipeline: int = 1):
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.m, self.k, self.n = m, k, n
         self.dtype, self.device = dtype, torch.device(device)
+        self.idx_dtype, self.nnz_local = idx_dtype, nnz_local
         self.row_range = balanced_range(m, self.world, self.rank)
         self.k_range = balanced_range(k, self.world, self.rank)
         self.pad = math.ceil(k / self.world) if k else 0
         self.k_padded = self.pad * self.world
         self.local_csr = local_csr
-        self.gathered = torch.zeros((self.k_padded, n), dtype=dtype, device=self.device)
-        rows_local = self.row_range[1] - self.row_range[0]
-        m_kernel = rows_local if local_csr else m
-        self.kernel = None
-        if self.device.type == "cuda":
-            self.kernel = ops.SpmmCsrKernel(m_kernel, self.k_padded, n, nnz_local, idx_dtype, dtype,
-                                            self.device)
+        # every block keeps the hub schedule of the full width (bit-identity across pipelines)
+        self.options = ops.make_options(split=ops.default_split(n))
         if comm == "auto":
             comm = "rccl" if self.device.type == "cuda" else "torch"
         if comm not in ("rccl", "rccl-p2p", "torch"):
             raise ValueError(f"RowSplitSpmm: unknown comm {comm!r}")
         self.comm_kind = comm
         self._comm = None
+        self.comm_stream = None
+        if self.device.type == "cuda":
+            self.comm_stream = torch.cuda.Stream(self.device)
+        self.gathered = None
+        self.set_pipeline(pipeline)
         if comm.startswith("rccl"):
             self._init_rccl()
-        self.ev = None
+
+    # -- layout ----------------------------------------------------------------------------------
+    def set_pipeline(self, chunks: int):
+        """(Re)lay out the gathered buffer for `chunks` column blocks, keeping this rank's shard."""
+        if chunks < 1 or self.n % chunks:
+            raise ValueError(f"RowSplitSpmm: pipeline {chunks} must divide n={self.n}")
+        shard = self.shard() if self.gathered is not None else None
+        self.gathered = None
+        self.chunks, self.nc = chunks, self.n // chunks
+        self.gathered = torch.zeros((chunks, self.k_padded, self.nc), dtype=self.dtype,
+                                    device=self.device)
+        self.chunk_events = ([torch.cuda.Event() for _ in range(chunks)]
+                             if self.device.type == "cuda" else None)
+        rows_local = self.row_range[1] - self.row_range[0]
+        m_kernel = rows_local if self.local_csr else self.m
+        self.kernel = None
+        if self.device.type == "cuda":
+            self.kernel = ops.SpmmCsrKernel(m_kernel, self.k_padded, self.nc, self.nnz_local,
+                                            self.idx_dtype, self.dtype, self.device, self.options)
+        if shard is not None:
+            self.load_shard(shard)
+
+    def block(self, c: int) -> torch.Tensor:
+        """Gathered B, column block c: [K_pad, N/C] contiguous."""
+        return self.gathered[c]
+
+    def shard_view(self) -> torch.Tensor:
+        """This rank's B shard inside the gathered buffer (write b here: in-place all-gather).
+        Only for pipeline 1, where the buffer is plain [K_pad, N]; use load_shard otherwise."""
+        if self.chunks != 1:
+            raise RuntimeError("shard_view: the gathered buffer is block-major; use load_shard")
+        lo, hi = self.k_range
+        return self.gathered[0][self.rank * self.pad: self.rank * self.pad + (hi - lo)]
+
+    def load_shard(self, b_shard: torch.Tensor):
+        """Writes this rank's rows of B ([K_r, N]) into its slot of every column block."""
+        lo, hi = self.k_range
+        r0 = self.rank * self.pad
+        for c in range(self.chunks):
+            self.gathered[c, r0:r0 + (hi - lo)].copy_(b_shard[:, c * self.nc:(c + 1) * self.nc])
+
+    def shard(self) -> torch.Tensor:
+        lo, hi = self.k_range
+        r0 = self.rank * self.pad
+        return torch.cat([self.gathered[c, r0:r0 + (hi - lo)] for c in range(self.chunks)], dim=1)
+
+    def remap_columns(self, col_idx: torch.Tensor) -> torch.Tensor:
+        return padded_owner_remap(col_idx, self.k, self.world)
 
     # -- communicator (EagerNcclCommMgr::CreateNcclComm pattern: rank 0 makes the id) --------
     def _init_rccl(self):
@@ -92,29 +146,6 @@ class RowSplitSpmm:
         check(LIB.ofx_comm_init_rank(ctypes.byref(comm), self.world, uid, self.rank), "comm_init_rank")
         self._comm = comm
 
-    def tune_comm(self, reps: int = 3) -> dict:
-        """Times the ring all-gather and the point-to-point one on this node (same bytes) and
-        keeps the faster; the timings are max-reduced over ranks, so every rank makes the
-        same choice.  Returns the timings (ms)."""
-        if not self.comm_kind.startswith("rccl") or self.world == 1:
-            return {}
-        times = {}
-        for kind in ("rccl", "rccl-p2p"):
-            self.comm_kind = kind
-            self.all_gather_b()
-            torch.cuda.synchronize(self.device)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(reps):
-                self.all_gather_b()
-            e1.record()
-            torch.cuda.synchronize(self.device)
-            t = torch.tensor([e0.elapsed_time(e1) / reps], dtype=torch.float64, device=self.device)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-            times[kind] = float(t.item())
-        self.comm_kind = min(times, key=times.get)
-        return times
-
     def close(self):
         if self._comm is not None:
             check(LIB.ofx_comm_destroy(self._comm), "comm_destroy")
@@ -126,51 +157,111 @@ class RowSplitSpmm:
         except Exception:
             pass
 
-    # -- layout helpers ----------------------------------------------------------------------
-    def shard_view(self) -> torch.Tensor:
-        """This rank's B shard inside the gathered buffer (write b here: in-place all-gather)."""
-        lo, hi = self.k_range
-        return self.gathered[self.rank * self.pad: self.rank * self.pad + (hi - lo)]
-
-    def remap_columns(self, col_idx: torch.Tensor) -> torch.Tensor:
-        return padded_owner_remap(col_idx, self.k, self.world)
-
     # -- the collective ------------------------------------------------------------------------
-    def all_gather_b(self, b_shard: torch.Tensor | None = None):
-        slot = self.gathered[self.rank * self.pad:(self.rank + 1) * self.pad]
-        if b_shard is not None and b_shard.data_ptr() != slot.data_ptr():
-            slot[: b_shard.shape[0]].copy_(b_shard)
-        count = self.pad * self.n
-        if self.comm_kind == "rccl":
-            s = current_stream_handle(self.gathered)
-            check(LIB.ofx_allgather(s, slot.data_ptr(), self.gathered.data_ptr(), count,
-                                    dtype_code(self.dtype), self._comm), "allgather")
-        elif self.comm_kind == "rccl-p2p":
-            s = current_stream_handle(self.gathered)
-            check(LIB.ofx_allgather_p2p(s, self.gathered.data_ptr(), count, dtype_code(self.dtype),
-                                        self._comm), "allgather_p2p")
-        else:
-            parts = list(self.gathered.view(self.world, self.pad, self.n).unbind(0))
+    def gather_block(self, c: int, stream=None):
+        """All-gather column block c in place (each rank's slot is its send buffer)."""
+        blk = self.gathered[c]
+        slot = blk[self.rank * self.pad:(self.rank + 1) * self.pad]
+        count = self.pad * self.nc
+        if self.comm_kind == "torch":
+            parts = list(blk.view(self.world, self.pad, self.nc).unbind(0))
             dist.all_gather(parts, slot.clone(), group=self.group)  # views: lands in place
+            return
+        s = stream if stream is not None else current_stream_handle(blk)
+        if self.comm_kind == "rccl":
+            check(LIB.ofx_allgather(s, slot.data_ptr(), blk.data_ptr(), count,
+                                    dtype_code(self.dtype), self._comm), "allgather")
+        else:
+            check(LIB.ofx_allgather_p2p(s, blk.data_ptr(), count, dtype_code(self.dtype),
+                                        self._comm), "allgather_p2p")
+
+    def all_gather_b(self, b_shard: torch.Tensor | None = None):
+        if b_shard is not None:
+            self.load_shard(b_shard)
+        for c in range(self.chunks):
+            self.gather_block(c)
+
+    def compute_block(self, c, row_ptr, col_idx, values, out, stream=None):
+        lo, hi = self.row_range
+        rb, re = (0, hi - lo) if self.local_csr else (lo, hi)
+        o = out[:, c * self.nc:(c + 1) * self.nc]
+        if self.kernel is not None:
+            self.kernel(row_ptr, col_idx, values, self.gathered[c], o, rb, re, stream=stream)
+        else:
+            m_kernel = hi - lo if self.local_csr else self.m
+            ops.spmm_csr_cpu(row_ptr, col_idx, values, self.gathered[c], m_kernel, self.k_padded,
+                             out=o, row_begin=rb, row_end=re, options=self.options)
+
+    def compute(self, row_ptr, col_idx, values, out):
+        """The local SpMM over the gathered B (B resident; no communication)."""
+        for c in range(self.chunks):
+            self.compute_block(c, row_ptr, col_idx, values, out)
+        return out
 
     # -- one step ------------------------------------------------------------------------------
     def __call__(self, row_ptr, col_idx, values, b_shard=None, out=None, events=None):
-        """events: optional (start, mid, end) torch.cuda.Event to time gather / SpMM."""
+        """Gather + local SpMM.  events: optional (start, mid, end) torch.cuda.Event; with
+        pipeline 1 they bracket the gather and the SpMM, pipelined `mid` marks the last gather."""
         lo, hi = self.row_range
         if out is None:
             out = torch.empty((hi - lo, self.n), dtype=self.dtype, device=self.device)
+        if b_shard is not None:
+            self.load_shard(b_shard)
+        pipelined = self.chunks > 1 and self.comm_stream is not None and self.comm_kind != "torch"
         if events:
             events[0].record()
-        self.all_gather_b(b_shard)
-        if events:
-            events[1].record()
-        rb, re = (0, hi - lo) if self.local_csr else (lo, hi)
-        if self.kernel is not None:
-            self.kernel(row_ptr, col_idx, values, self.gathered, out, rb, re)
+        if not pipelined:
+            self.all_gather_b()
+            if events:
+                events[1].record()
+            self.compute(row_ptr, col_idx, values, out)
         else:
-            m_kernel = hi - lo if self.local_csr else self.m
-            ops.spmm_csr_cpu(row_ptr, col_idx, values, self.gathered, m_kernel, self.k_padded,
-                             out=out, row_begin=rb, row_end=re)
+            cur = torch.cuda.current_stream(self.device)
+            cs = self.comm_stream
+            cs.wait_stream(cur)  # the previous step's reads of the blocks / shard writes are done
+            side = ctypes.c_void_p(cs.cuda_stream)
+            for c in range(self.chunks):
+                self.gather_block(c, stream=side)
+                self.chunk_events[c].record(cs)
+            if events:
+                events[1].record(cs)
+            for c in range(self.chunks):
+                cur.wait_event(self.chunk_events[c])
+                self.compute_block(c, row_ptr, col_idx, values, out)
+            # the caching allocator must not recycle these while the side stream uses them
+            self.gathered.record_stream(cs)
         if events:
             events[2].record()
         return out
+
+    # -- schedule choice -------------------------------------------------------------------------
+    def tune(self, row_ptr, col_idx, values, out, pipelines=(1, 2, 4), reps: int = 3) -> dict:
+        """Times every (all-gather schedule, pipeline depth) on this node with the real step and
+        keeps the fastest.  Timings are max-reduced over ranks, so all ranks choose the same.
+        Every candidate produces the same bytes.  Returns {"<comm>/p<C>": ms}."""
+        if self.world == 1 or not self.comm_kind.startswith("rccl"):
+            return {}
+        times = {}
+        for chunks in pipelines:
+            if self.n % chunks:
+                continue
+            self.set_pipeline(chunks)
+            for kind in ("rccl", "rccl-p2p"):
+                self.comm_kind = kind
+                self(row_ptr, col_idx, values, out=out)
+                torch.cuda.synchronize(self.device)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(reps):
+                    self(row_ptr, col_idx, values, out=out)
+                e1.record()
+                torch.cuda.synchronize(self.device)
+                t = torch.tensor([e0.elapsed_time(e1) / reps], dtype=torch.float64,
+                                 device=self.device)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+                times[f"{kind}/p{chunks}"] = float(t.item())
+        best = min(times, key=times.get)
+        kind, p = best.split("/p")
+        self.comm_kind = kind
+        self.set_pipeline(int(p))
+        return times

@@ -17,7 +17,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, m, k, n, local_csr, q):
+def _worker(rank, world, port, m, k, n, local_csr, pipeline, density, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     import sys
@@ -31,7 +31,7 @@ def _worker(rank, world, port, m, k, n, local_csr, q):
         from tests.helpers import power_law_degrees, random_csr, random_dense
 
         rng = np.random.default_rng(1234)
-        rp, ci, v = random_csr(m, k, power_law_degrees(m, 30 * m, k, rng), rng)
+        rp, ci, v = random_csr(m, k, power_law_degrees(m, density * m, k, rng), rng)
         b = random_dense(k, n, rng)
         full = oracle.spmm(rp.numpy(), ci.numpy(), v.numpy(), b.numpy())
         lo, hi = oracle.balanced_range(m, world, rank)
@@ -41,18 +41,20 @@ def _worker(rank, world, port, m, k, n, local_csr, q):
         else:
             lrp, lci, lv = rp, ci, v
         rs = RowSplitSpmm(m, k, n, lci.numel(), torch.float32, torch.int32, "cpu",
-                          local_csr=local_csr)
+                          local_csr=local_csr, pipeline=pipeline)
         assert rs.row_range == (lo, hi)
         klo, khi = rs.k_range
         assert (klo, khi) == oracle.balanced_range(k, world, rank)
-        rs.shard_view().copy_(b[klo:khi])
+        rs.load_shard(b[klo:khi])
         out = rs(lrp, rs.remap_columns(lci), lv)
         ok = np.array_equal(out.numpy().view(np.uint32), full[lo:hi].view(np.uint32))
-        # the gathered buffer holds every shard at its padded slot
-        g = rs.gathered.view(world, rs.pad, n)
-        for r in range(world):
-            a, e = oracle.balanced_range(k, world, r)
-            ok = ok and torch.equal(g[r, : e - a], b[a:e])
+        # the gathered buffer holds every shard at its padded slot, in every column block
+        nc = n // pipeline
+        for c in range(pipeline):
+            g = rs.block(c).view(world, rs.pad, nc)
+            for r in range(world):
+                a, e = oracle.balanced_range(k, world, r)
+                ok = ok and torch.equal(g[r, : e - a], b[a:e, c * nc:(c + 1) * nc])
         # a second step with a new dense operand passed as a separate shard tensor
         b2 = random_dense(k, n, np.random.default_rng(99))
         out2 = rs(lrp, rs.remap_columns(lci), lv, b_shard=b2[klo:khi])
@@ -69,10 +71,23 @@ def _worker(rank, world, port, m, k, n, local_csr, q):
     (3, 500, 400, 8, True),
 ])
 def test_row_split_gloo(world, m, k, n, local_csr):
+    _run(world, m, k, n, local_csr, 1, 30)
+
+
+@pytest.mark.parametrize("world,m,k,n,local_csr,pipeline", [
+    (2, 400, 3001, 128, True, 4),   # hub rows > 2 x default_split(128) = 1024: blocks keep it
+    (3, 301, 2999, 128, False, 2),
+])
+def test_row_split_pipelined_gloo(world, m, k, n, local_csr, pipeline):
+    """Column-block pipelining: same bytes as pipeline 1 / the oracle with the full-N schedule."""
+    _run(world, m, k, n, local_csr, pipeline, 60)
+
+
+def _run(world, m, k, n, local_csr, pipeline, density):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, m, k, n, local_csr, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, m, k, n, local_csr, pipeline, density, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -273,8 +273,8 @@ def test_row_split_rccl_single_rank(device):
                             device_id=device)
     try:
         rng = np.random.default_rng(17)
-        m, k, n = 777, 555, 64
-        rp, ci, v = random_csr(m, k, power_law_degrees(m, 20000, k, rng), rng)
+        m, k, n = 777, 3555, 128
+        rp, ci, v = random_csr(m, k, power_law_degrees(m, 60000, k, rng), rng)
         b = random_dense(k, n, rng)
         rs = RowSplitSpmm(m, k, n, ci.numel(), torch.float32, torch.int32, device)
         assert rs.comm_kind == "rccl"
@@ -282,6 +282,15 @@ def test_row_split_rccl_single_rank(device):
         out = rs(rp.to(device), rs.remap_columns(ci.to(device)), v.to(device))
         torch.cuda.synchronize()
         assert_bitwise(out, oracle_spmm(rp, ci, v, b), "rccl row split")
+        # column-block pipeline on the side stream (ring and point-to-point schedules)
+        for kind, chunks in (("rccl", 4), ("rccl-p2p", 2)):
+            rs.comm_kind = kind
+            rs.set_pipeline(chunks)
+            out2 = torch.full_like(out, float("nan"))
+            for _ in range(3):  # back-to-back steps: stream ordering between them
+                rs(rp.to(device), rs.remap_columns(ci.to(device)), v.to(device), out=out2)
+            torch.cuda.synchronize()
+            assert_bitwise(out2, oracle_spmm(rp, ci, v, b), f"{kind} pipeline {chunks}")
         rs.close()
     finally:
         dist.destroy_process_group()
