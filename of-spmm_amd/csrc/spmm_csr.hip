@@ -446,7 +446,10 @@ int launch_typed(const Launch& L) {
   // variant = VEC * 100 + LPR forces a configuration (tuning / tests); 0 = auto.
   const int forced_vec = L.sched.variant > 0 ? L.sched.variant / 100 : 0;
   const int forced_lpr = L.sched.variant > 0 ? L.sched.variant % 100 : 0;
-  const int vec = pick_vec((int)sizeof(T), L, forced_vec);
+  // fp32 rows of <= 64 B: one element per lane over 16 lanes beats 4 lanes of float4 (+9% on
+  // products-shaped N=16, scripts/ab.py); wider rows keep the widest vector
+  const int vec = (!forced_vec && sizeof(T) == 4 && L.n <= 16) ? 1
+                                                                 : pick_vec((int)sizeof(T), L, forced_vec);
   OFX_REQUIRE(vec > 0, OFX_EINVAL,
               "spmm_csr: variant %d not applicable (n=%lld ldb=%lld ldc=%lld or pointer alignment)",
               L.sched.variant, (long long)L.n, (long long)L.ldb, (long long)L.ldc);

@@ -30,12 +30,14 @@ def main():
     ap.add_argument("--variants", default="0,432,264,464,232")
     ap.add_argument("--split", type=int, default=0)
     ap.add_argument("--heavy", type=int, default=0, help="0 default, <0 off")
+    ap.add_argument("--n", type=int, default=0, help="override the dense width")
     args = ap.parse_args()
     from oneflow_spmm import ops, synth
     from bench import alg_bytes
 
     cfg = synth.CONFIGS[args.config]
     m, k, nnz, n, dt = cfg["m"], cfg["k"], cfg["nnz"], cfg["n"], cfg["dtype"]
+    n = args.n or n
     dev = torch.device("cuda", 0)
     rp, ci, v = synth.csr(m, k, nnz, val_dtype=dt, threads=16)
     rp, ci, v = rp.to(dev), ci.to(dev), v.to(dev)
