@@ -113,6 +113,26 @@ int ofx_spmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t 
                  int64_t row_end, void* workspace, size_t workspace_bytes,
                  const ofx_spmm_options* opts);
 
+/* Fused epilogue: out = act(A @ B + bias), bit-identical to the
+ * composition spmm_csr -> bias_add (BroadcastElementwiseBinary kAdd over axis 1,
+ * oneflow/user/kernels/bias_add_kernel.cpp:25-53) -> relu (UnaryFunctor<kRelu>,
+ * oneflow/core/ep/common/primitive/unary_functor.h:146-156): the row sum is rounded to T,
+ * the bias added in the accumulation type and rounded to T again, relu maps x <= 0 to +0.
+ * `bias` is T[n] on the device or NULL; `activation` is OFX_ACT_*.  Same workspace as
+ * ofx_spmm_csr.                                                                             */
+#define OFX_ACT_NONE 0
+#define OFX_ACT_RELU 1
+int ofx_spmm_csr_fused(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k, int64_t n,
+                       int64_t nnz, const void* row_ptr, const void* col_idx, const void* values,
+                       const void* b, int64_t ldb, void* c, int64_t ldc, int64_t row_begin,
+                       int64_t row_end, const void* bias, int activation, void* workspace,
+                       size_t workspace_bytes, const ofx_spmm_options* opts);
+int ofx_spmm_csr_fused_cpu(int num_threads, int idx_dtype, int val_dtype, int64_t m, int64_t k,
+                           int64_t n, int64_t nnz, const void* row_ptr, const void* col_idx,
+                           const void* values, const void* b, int64_t ldb, void* c, int64_t ldc,
+                           int64_t row_begin, int64_t row_end, const void* bias, int activation,
+                           const ofx_spmm_options* opts);
+
 /* Device-side structural check of a CSR (row_ptr monotone, row_ptr[0]==0, row_ptr[m]==nnz,
  * 0 <= col < k).  Writes a 32-bit error code to *flag_dev (0 = ok, 1 = bad row_ptr,
  * 2 = column out of range) asynchronously on `stream`.                                     */
@@ -277,6 +297,15 @@ int ofx_functional_spmm_csr_ex(void* stream, const ofx_tensor_desc* row_ptr,
                                ofx_tensor_desc* out, void* tmp, size_t tmp_bytes,
                                int64_t parallel_id, int64_t parallel_num, int out_split_axis,
                                int num_threads);
+/* Op "fused_spmm_csr" (relu?(A @ b + bias?), oneflow/user/ops/fused_spmm_op.cpp mirror) through
+ * the op-registry dispatch; bias may be NULL (optional input absent).  With tmp_size_out !=
+ * NULL only the tmp-buffer size is computed (nothing runs).                                  */
+int ofx_functional_fused_spmm_csr(void* stream, const ofx_tensor_desc* row_ptr,
+                                  const ofx_tensor_desc* col_idx, const ofx_tensor_desc* values,
+                                  const ofx_tensor_desc* b, const ofx_tensor_desc* bias,
+                                  int64_t a_num_rows, int64_t a_num_cols, int relu,
+                                  ofx_tensor_desc* out, void* tmp, size_t tmp_bytes,
+                                  size_t* tmp_size_out);
 /* Gradient functors (ops "sddmm_csr", "csr_transpose"; oneflow/user/ops/sddmm_op.cpp) through
  * the same op-registry dispatch.  With tmp_size_out != NULL only the tmp-buffer size is
  * computed (nothing runs).  Outputs: sddmm out [nnz] in b's dtype; transpose out_row_ptr [k+1],

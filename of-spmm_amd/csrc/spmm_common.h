@@ -73,6 +73,19 @@ struct Num<f16> {
   OFX_HD static f16 store(float a) { return f16{f32_to_f16(a)}; }
 };
 
+// Epilogue of the fused op (include/ofx_spmm.h ofx_spmm_csr_fused): the composition
+// spmm_csr -> bias_add -> relu, each step rounding to T as the separate ops would
+// (bias_add: oneflow/user/kernels/bias_add_kernel.cpp:25-53; relu:
+// oneflow/core/ep/common/primitive/unary_functor.h:146-156, x <= 0 -> +0, NaN passes).
+template <typename T>
+OFX_HD T epilogue(typename Num<T>::acc acc, const T* bias, int64_t c, int act) {
+  T y = Num<T>::store(acc);
+  if (bias) y = Num<T>::store(Num<T>::load(y) + Num<T>::load(bias[c]));
+  if (act == OFX_ACT_RELU && Num<T>::load(y) <= typename Num<T>::acc(0))
+    y = Num<T>::store(typename Num<T>::acc(0));
+  return y;
+}
+
 OFX_HD int dtype_size(int dt) {
   switch (dt) {
     case OFX_DT_FLOAT: return 4;

@@ -35,7 +35,7 @@ void row_sum(const I* col, const T* val, const T* B, int64_t ldb, int64_t n, int
 template <typename T, typename I>
 int cpu_spmm(int nthreads, int64_t n, const I* rp, const I* col, const T* val, const T* B,
              int64_t ldb, T* C, int64_t ldc, int64_t row_begin, int64_t row_end,
-             const Schedule& s) {
+             const Schedule& s, const T* bias, int act) {
 #pragma clang fp contract(off)
   using A = typename Num<T>::acc;
   const int64_t rows = row_end - row_begin;
@@ -60,7 +60,7 @@ int cpu_spmm(int nthreads, int64_t n, const I* rp, const I* col, const T* val, c
         }
       }
       T* out = C + g * ldc;
-      for (int64_t c = 0; c < n; ++c) out[c] = Num<T>::store(acc[c]);
+      for (int64_t c = 0; c < n; ++c) out[c] = epilogue<T>(acc[c], bias, c, act);
     }
   }
   return OFX_OK;
@@ -69,22 +69,23 @@ int cpu_spmm(int nthreads, int64_t n, const I* rp, const I* col, const T* val, c
 template <typename I>
 int cpu_dispatch(int nthreads, int val_dtype, int64_t n, const void* rp, const void* col,
                  const void* val, const void* b, int64_t ldb, void* c, int64_t ldc,
-                 int64_t row_begin, int64_t row_end, const Schedule& s) {
+                 int64_t row_begin, int64_t row_end, const Schedule& s, const void* bias,
+                 int act) {
   const I* r = static_cast<const I*>(rp);
   const I* ci = static_cast<const I*>(col);
   switch (val_dtype) {
     case OFX_DT_FLOAT:
       return cpu_spmm<float, I>(nthreads, n, r, ci, (const float*)val, (const float*)b, ldb,
-                                (float*)c, ldc, row_begin, row_end, s);
+                                (float*)c, ldc, row_begin, row_end, s, (const float*)bias, act);
     case OFX_DT_DOUBLE:
       return cpu_spmm<double, I>(nthreads, n, r, ci, (const double*)val, (const double*)b, ldb,
-                                 (double*)c, ldc, row_begin, row_end, s);
+                                 (double*)c, ldc, row_begin, row_end, s, (const double*)bias, act);
     case OFX_DT_BFLOAT16:
       return cpu_spmm<bf16, I>(nthreads, n, r, ci, (const bf16*)val, (const bf16*)b, ldb,
-                               (bf16*)c, ldc, row_begin, row_end, s);
+                               (bf16*)c, ldc, row_begin, row_end, s, (const bf16*)bias, act);
     case OFX_DT_FLOAT16:
       return cpu_spmm<f16, I>(nthreads, n, r, ci, (const f16*)val, (const f16*)b, ldb, (f16*)c,
-                              ldc, row_begin, row_end, s);
+                              ldc, row_begin, row_end, s, (const f16*)bias, act);
     default: return fail(OFX_EUNSUPPORTED, "spmm_csr_cpu: unsupported value dtype %d", val_dtype);
   }
 }
@@ -94,11 +95,12 @@ int cpu_dispatch(int nthreads, int val_dtype, int64_t n, const void* rp, const v
 
 using namespace ofx;
 
-extern "C" int ofx_spmm_csr_cpu(int num_threads, int idx_dtype, int val_dtype, int64_t m,
-                                int64_t k, int64_t n, int64_t nnz, const void* row_ptr,
-                                const void* col_idx, const void* values, const void* b,
-                                int64_t ldb, void* c, int64_t ldc, int64_t row_begin,
-                                int64_t row_end, const ofx_spmm_options* opts) {
+namespace ofx {
+namespace {
+int spmm_cpu_entry(int num_threads, int idx_dtype, int val_dtype, int64_t m, int64_t k, int64_t n,
+                   int64_t nnz, const void* row_ptr, const void* col_idx, const void* values,
+                   const void* b, int64_t ldb, void* c, int64_t ldc, int64_t row_begin,
+                   int64_t row_end, const void* bias, int act, const ofx_spmm_options* opts) {
   OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED,
               "spmm_csr_cpu: index dtype %d is not int32/int64", idx_dtype);
   OFX_REQUIRE(is_value_dtype(val_dtype), OFX_EUNSUPPORTED,
@@ -108,6 +110,8 @@ extern "C" int ofx_spmm_csr_cpu(int num_threads, int idx_dtype, int val_dtype, i
               "spmm_csr_cpu: row range [%lld, %lld) outside [0, %lld)", (long long)row_begin,
               (long long)row_end, (long long)m);
   OFX_REQUIRE(ldb >= n && ldc >= n, OFX_EINVAL, "spmm_csr_cpu: ldb/ldc < n");
+  OFX_REQUIRE(act == OFX_ACT_NONE || act == OFX_ACT_RELU, OFX_EINVAL,
+              "spmm_csr_cpu: unknown activation %d", act);
   if (row_end == row_begin || n == 0) return OFX_OK;
   OFX_REQUIRE(row_ptr && c && (nnz == 0 || (col_idx && values && b)), OFX_EINVAL,
               "spmm_csr_cpu: NULL pointer");
@@ -115,9 +119,30 @@ extern "C" int ofx_spmm_csr_cpu(int num_threads, int idx_dtype, int val_dtype, i
   const Schedule s = resolve_schedule(n, opts);
   if (idx_dtype == OFX_DT_INT32)
     return cpu_dispatch<int32_t>(nt, val_dtype, n, row_ptr, col_idx, values, b, ldb, c, ldc,
-                                 row_begin, row_end, s);
+                                 row_begin, row_end, s, bias, act);
   return cpu_dispatch<int64_t>(nt, val_dtype, n, row_ptr, col_idx, values, b, ldb, c, ldc,
-                               row_begin, row_end, s);
+                               row_begin, row_end, s, bias, act);
+}
+}  // namespace
+}  // namespace ofx
+
+extern "C" int ofx_spmm_csr_cpu(int num_threads, int idx_dtype, int val_dtype, int64_t m,
+                                int64_t k, int64_t n, int64_t nnz, const void* row_ptr,
+                                const void* col_idx, const void* values, const void* b,
+                                int64_t ldb, void* c, int64_t ldc, int64_t row_begin,
+                                int64_t row_end, const ofx_spmm_options* opts) {
+  return spmm_cpu_entry(num_threads, idx_dtype, val_dtype, m, k, n, nnz, row_ptr, col_idx, values,
+                        b, ldb, c, ldc, row_begin, row_end, nullptr, OFX_ACT_NONE, opts);
+}
+
+extern "C" int ofx_spmm_csr_fused_cpu(int num_threads, int idx_dtype, int val_dtype, int64_t m,
+                                      int64_t k, int64_t n, int64_t nnz, const void* row_ptr,
+                                      const void* col_idx, const void* values, const void* b,
+                                      int64_t ldb, void* c, int64_t ldc, int64_t row_begin,
+                                      int64_t row_end, const void* bias, int activation,
+                                      const ofx_spmm_options* opts) {
+  return spmm_cpu_entry(num_threads, idx_dtype, val_dtype, m, k, n, nnz, row_ptr, col_idx, values,
+                        b, ldb, c, ldc, row_begin, row_end, bias, activation, opts);
 }
 
 // ---- BalancedSplitter (oneflow/core/common/balanced_splitter.cpp:20-40) -------------------

@@ -182,10 +182,16 @@ __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* _
 }
 
 template <typename T, int VEC, bool NT>
-__device__ __forceinline__ void store_row(T* __restrict__ p, const typename Num<T>::acc (&acc)[VEC]) {
+__device__ __forceinline__ void store_row(T* __restrict__ p, const typename Num<T>::acc (&acc)[VEC],
+                                          const T* __restrict__ bias, int act) {
   Pack<T, VEC> o;
+  if (bias == nullptr && act == OFX_ACT_NONE) {  // uniform: the plain op pays one branch
 #pragma unroll
-  for (int e = 0; e < VEC; ++e) o.v[e] = Num<T>::store(acc[e]);
+    for (int e = 0; e < VEC; ++e) o.v[e] = Num<T>::store(acc[e]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) o.v[e] = epilogue<T>(acc[e], bias, e, act);
+  }
   if constexpr (NT && (sizeof(o) == 16 || sizeof(o) == 8 || sizeof(o) == 4 || sizeof(o) == 2)) {
     using R = typename RawVec<sizeof(o)>::type;
     __builtin_nontemporal_store(__builtin_bit_cast(R, o), reinterpret_cast<R*>(p));
@@ -209,7 +215,8 @@ __global__ void __launch_bounds__(64 * K::WPB)
                      T* __restrict__ C, int64_t ldc, int64_t row_begin, int64_t nrows, int64_t n,
                      int64_t chunk, const unsigned long long* __restrict__ counters,
                      const int64_t* __restrict__ items, const int64_t* __restrict__ order,
-                     typename Num<T>::acc* __restrict__ part) {
+                     typename Num<T>::acc* __restrict__ part, const T* __restrict__ bias,
+                     int act) {
   using A = typename Num<T>::acc;
   constexpr int VEC = K::VEC, LPR = K::LPR, kWaves = K::WPB;
   constexpr int GPW = 64 / LPR;
@@ -257,7 +264,7 @@ __global__ void __launch_bounds__(64 * K::WPB)
       if (c >= 0)
         store_partial<A, VEC>(part + g * n + cc, acc);
       else
-        store_row<T, VEC, K::NT>(C + lr * ldc + cc, acc);
+        store_row<T, VEC, K::NT>(C + lr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
     }
   }
 }
@@ -267,7 +274,7 @@ __global__ void __launch_bounds__(kBlock)
     spmm_reduce_kernel(const unsigned long long* __restrict__ counters,
                        const int64_t* __restrict__ hubs,
                        const typename Num<T>::acc* __restrict__ part, T* __restrict__ C,
-                       int64_t ldc, int64_t n) {
+                       int64_t ldc, int64_t n, const T* __restrict__ bias, int act) {
 #pragma clang fp contract(off)
   using A = typename Num<T>::acc;
   constexpr int kPre = 16;  // partial rows in flight per thread (the adds stay in chunk order)
@@ -288,7 +295,7 @@ __global__ void __launch_bounds__(kBlock)
         for (int u = 0; u < kPre; ++u) acc = acc + v[u];
       }
       for (; q < nc; ++q) acc = acc + p[q * n];
-      C[lr * ldc + c] = Num<T>::store(acc);
+      C[lr * ldc + c] = epilogue<T>(acc, bias, c, act);
     }
   }
 }
@@ -340,6 +347,8 @@ struct Launch {
   Schedule sched;
   void* ws;
   size_t ws_bytes;
+  const void* bias;  // fused epilogue (T[n] or NULL) and OFX_ACT_*
+  int act;
 };
 
 int pick_vec(int elem_bytes, const Launch& L, int forced_vec) {
@@ -392,12 +401,13 @@ int launch_cfg(const Launch& L) {
               (long long)L.nrows);
   hipLaunchKernelGGL((spmm_main_kernel<T, I, K>), dim3((unsigned)grid), dim3(64 * K::WPB), 0,
                      L.stream, rp, col, val, B, L.ldb, C, L.ldc, L.row_begin, L.nrows, L.n,
-                     plan ? L.sched.chunk : INT64_MAX, counters, items, order, part);
+                     plan ? L.sched.chunk : INT64_MAX, counters, items, order, part,
+                     static_cast<const T*>(L.bias), L.act);
   OFX_HIP_CHECK(hipGetLastError());
   if (plan && w.max_hubs > 0) {
     const int64_t rgrid = w.max_hubs < kMaxReduceBlocks ? w.max_hubs : kMaxReduceBlocks;
     hipLaunchKernelGGL((spmm_reduce_kernel<T>), dim3((unsigned)rgrid), dim3(kBlock), 0, L.stream,
-                       counters, hub, part, C, L.ldc, L.n);
+                       counters, hub, part, C, L.ldc, L.n, static_cast<const T*>(L.bias), L.act);
     OFX_HIP_CHECK(hipGetLastError());
   }
   return OFX_OK;
@@ -512,11 +522,13 @@ extern "C" int ofx_spmm_csr_workspace_size(int idx_dtype, int val_dtype, int64_t
   return OFX_OK;
 }
 
-extern "C" int ofx_spmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k,
-                            int64_t n, int64_t nnz, const void* row_ptr, const void* col_idx,
-                            const void* values, const void* b, int64_t ldb, void* c, int64_t ldc,
-                            int64_t row_begin, int64_t row_end, void* workspace,
-                            size_t workspace_bytes, const ofx_spmm_options* opts) {
+namespace ofx {
+namespace {
+int spmm_entry(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k, int64_t n,
+               int64_t nnz, const void* row_ptr, const void* col_idx, const void* values,
+               const void* b, int64_t ldb, void* c, int64_t ldc, int64_t row_begin,
+               int64_t row_end, const void* bias, int act, void* workspace,
+               size_t workspace_bytes, const ofx_spmm_options* opts) {
   int rc = check_common(idx_dtype, val_dtype, m, k, n, nnz);
   if (rc) return rc;
   OFX_REQUIRE(0 <= row_begin && row_begin <= row_end && row_end <= m, OFX_EINVAL,
@@ -524,15 +536,41 @@ extern "C" int ofx_spmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t 
               (long long)row_end, (long long)m);
   OFX_REQUIRE(ldb >= n && ldc >= n, OFX_EINVAL, "spmm_csr: ldb=%lld / ldc=%lld < n=%lld",
               (long long)ldb, (long long)ldc, (long long)n);
+  OFX_REQUIRE(act == OFX_ACT_NONE || act == OFX_ACT_RELU, OFX_EINVAL,
+              "spmm_csr: unknown activation %d", act);
   const int64_t nrows = row_end - row_begin;
   if (nrows == 0 || n == 0) return OFX_OK;  // nothing to write
   OFX_REQUIRE(row_ptr && c, OFX_EINVAL, "spmm_csr: NULL row_ptr or output");
   OFX_REQUIRE(nnz == 0 || (col_idx && values && b), OFX_EINVAL,
               "spmm_csr: NULL col_idx/values/b with nnz=%lld", (long long)nnz);
   Launch L{static_cast<hipStream_t>(stream), row_ptr, col_idx, values, b, c, ldb, ldc,
-           row_begin, nrows, n, nnz, resolve_schedule(n, opts), workspace, workspace_bytes};
+           row_begin, nrows, n, nnz, resolve_schedule(n, opts), workspace, workspace_bytes,
+           bias, act};
   if (idx_dtype == OFX_DT_INT32) return launch_idx<int32_t>(val_dtype, L);
   return launch_idx<int64_t>(val_dtype, L);
+}
+}  // namespace
+}  // namespace ofx
+
+extern "C" int ofx_spmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k,
+                            int64_t n, int64_t nnz, const void* row_ptr, const void* col_idx,
+                            const void* values, const void* b, int64_t ldb, void* c, int64_t ldc,
+                            int64_t row_begin, int64_t row_end, void* workspace,
+                            size_t workspace_bytes, const ofx_spmm_options* opts) {
+  return spmm_entry(stream, idx_dtype, val_dtype, m, k, n, nnz, row_ptr, col_idx, values, b, ldb,
+                    c, ldc, row_begin, row_end, nullptr, OFX_ACT_NONE, workspace, workspace_bytes,
+                    opts);
+}
+
+extern "C" int ofx_spmm_csr_fused(void* stream, int idx_dtype, int val_dtype, int64_t m,
+                                  int64_t k, int64_t n, int64_t nnz, const void* row_ptr,
+                                  const void* col_idx, const void* values, const void* b,
+                                  int64_t ldb, void* c, int64_t ldc, int64_t row_begin,
+                                  int64_t row_end, const void* bias, int activation,
+                                  void* workspace, size_t workspace_bytes,
+                                  const ofx_spmm_options* opts) {
+  return spmm_entry(stream, idx_dtype, val_dtype, m, k, n, nnz, row_ptr, col_idx, values, b, ldb,
+                    c, ldc, row_begin, row_end, bias, activation, workspace, workspace_bytes, opts);
 }
 
 extern "C" int ofx_csr_validate(void* stream, int idx_dtype, int64_t m, int64_t k, int64_t nnz,

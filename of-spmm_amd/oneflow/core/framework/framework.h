@@ -286,6 +286,8 @@ class InferContext {
   InferContext(std::map<std::pair<std::string, int32_t>, TensorDesc> in, AttrMap attrs)
       : in_(std::move(in)), attrs_(std::move(attrs)) {}
   const TensorDesc& InputTensorDesc(const std::string& n, int32_t i) const { return in_.at({n, i}); }
+  // optional inputs (oneflow/core/framework/infer_util.h:71)
+  bool has_input(const std::string& n, int32_t i) const { return in_.count({n, i}) > 0; }
   const Shape& InputShape(const std::string& n, int32_t i) const { return in_.at({n, i}).shape(); }
   DataType InputDType(const std::string& n, int32_t i) const { return in_.at({n, i}).data_type(); }
   TensorDesc* MutOutputTensorDesc(const std::string& n, int32_t i) { return &out_[{n, i}]; }
@@ -327,13 +329,32 @@ class SbpSignatureBuilder {
   SbpSignature sig_;
 };
 
+// user_op_conf() of an SbpContext: which (optional) inputs the op instance has
+// (oneflow/core/framework/user_op_conf.h:58).
+class UserOpConfView {
+ public:
+  explicit UserOpConfView(std::vector<std::string> present = {}) : present_(std::move(present)) {}
+  bool has_input(const std::string& n, int32_t) const {
+    for (const auto& p : present_)
+      if (p == n) return true;
+    return false;
+  }
+
+ private:
+  std::vector<std::string> present_;
+};
+
 class SbpContext {
  public:
+  SbpContext() = default;
+  explicit SbpContext(UserOpConfView conf) : conf_(std::move(conf)) {}
+  const UserOpConfView& user_op_conf() const { return conf_; }
   SbpSignatureBuilder NewBuilder() { return SbpSignatureBuilder(&sigs_); }
   const std::vector<SbpSignature>& signatures() const { return sigs_; }
 
  private:
   std::vector<SbpSignature> sigs_;
+  UserOpConfView conf_;
 };
 
 struct InputArgModifier {
@@ -487,7 +508,7 @@ class OpKernelRegistry {
 // Op schema registration (what the ODS tblgen output registers in op_generated.cpp).
 struct OpRegistryResult {
   std::string op_type_name;
-  std::vector<std::string> inputs, outputs;
+  std::vector<std::string> inputs, optional_inputs, outputs;
   std::vector<std::pair<std::string, int64_t>> attrs;  // name, default
   std::function<Maybe<void>(InferContext*)> logical_infer, physical_infer, dtype_infer;
   std::function<Maybe<void>(SbpContext*)> get_sbp;
@@ -498,6 +519,10 @@ class OpRegistry {
   explicit OpRegistry(std::string op) { r_.op_type_name = std::move(op); }
   OpRegistry& Input(const std::string& n) {
     r_.inputs.push_back(n);
+    return *this;
+  }
+  OpRegistry& OptionalInput(const std::string& n) {
+    r_.optional_inputs.push_back(n);
     return *this;
   }
   OpRegistry& Output(const std::string& n) {

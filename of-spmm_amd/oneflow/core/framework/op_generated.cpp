@@ -19,6 +19,22 @@ REGISTER_USER_OP("spmm_csr")
     .SetDataTypeInferFn(SpmmCsrOp::InferDataType)
     .SetInputArgModifyFn(SpmmCsrOp::ModifyInputArg);
 
+REGISTER_USER_OP("fused_spmm_csr")
+    .Input("a_csr_row_ptr")
+    .Input("a_csr_col_idx")
+    .Input("a_csr_values")
+    .Input("b")
+    .OptionalInput("bias")
+    .Output("out")
+    .Attr<int64_t>("a_num_rows", 0)
+    .Attr<int64_t>("a_num_cols", 0)
+    .Attr<bool>("relu", false)
+    .SetLogicalTensorDescInferFn(FusedSpmmCsrOp::InferLogicalTensorDesc)
+    .SetPhysicalTensorDescInferFn(FusedSpmmCsrOp::InferPhysicalTensorDesc)
+    .SetGetSbpFn(FusedSpmmCsrOp::GetSbp)
+    .SetDataTypeInferFn(FusedSpmmCsrOp::InferDataType)
+    .SetInputArgModifyFn(FusedSpmmCsrOp::ModifyInputArg);
+
 REGISTER_USER_OP("sddmm_csr")
     .Input("a_csr_row_ptr")
     .Input("a_csr_col_idx")

@@ -17,6 +17,17 @@ class SpmmCsrOp {
                                     const user_op::UserOpConfWrapper& conf);
 };
 
+// Fused epilogue variant.
+class FusedSpmmCsrOp {
+ public:
+  static Maybe<void> InferLogicalTensorDesc(user_op::InferContext* ctx);
+  static Maybe<void> InferPhysicalTensorDesc(user_op::InferContext* ctx);
+  static Maybe<void> GetSbp(user_op::SbpContext* ctx);
+  static Maybe<void> InferDataType(user_op::InferContext* ctx);
+  static Maybe<void> ModifyInputArg(const user_op::GetInputArgModifier& GetInputArgModifierFn,
+                                    const user_op::UserOpConfWrapper& conf);
+};
+
 // Gradient ops of spmm_csr.
 class SddmmCsrOp {
  public:

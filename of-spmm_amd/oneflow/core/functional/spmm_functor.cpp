@@ -336,3 +336,21 @@ extern "C" int ofx_functional_csr_transpose(void* stream, const ofx_tensor_desc*
                             {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols}}, stream, tmp,
                             tmp_bytes, tmp_size_out));
 }
+
+// functional::FusedSpmmCsr: relu?(A @ b + bias?) through op
+// "fused_spmm_csr"; `bias` may be NULL (the optional input is then absent).
+extern "C" int ofx_functional_fused_spmm_csr(void* stream, const ofx_tensor_desc* row_ptr,
+                                             const ofx_tensor_desc* col_idx,
+                                             const ofx_tensor_desc* values,
+                                             const ofx_tensor_desc* b, const ofx_tensor_desc* bias,
+                                             int64_t a_num_rows, int64_t a_num_cols, int relu,
+                                             ofx_tensor_desc* out, void* tmp, size_t tmp_bytes,
+                                             size_t* tmp_size_out) {
+  std::vector<Arg> ins = {{"a_csr_row_ptr", row_ptr}, {"a_csr_col_idx", col_idx},
+                          {"a_csr_values", values}, {"b", b}};
+  if (bias != nullptr) ins.push_back({"bias", bias});
+  return ToStatus(RunUserOp("fused_spmm_csr", ins, {{"out", out}},
+                            {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols},
+                             {"relu", relu ? 1 : 0}},
+                            stream, tmp, tmp_bytes, tmp_size_out));
+}

@@ -40,6 +40,61 @@ std::shared_ptr<user_op::OpKernelCache> CreateSpmmCsrOpKernelCache(user_op::Kern
 
 int DtCode(DataType dt) { return static_cast<int>(dt); }
 
+// Shared body of "spmm_csr" and "fused_spmm_csr": bias (optional T[N]) and relu are the fused
+// epilogue; the plain op passes none (ofx_spmm_csr_fused with NULL/none == ofx_spmm_csr).
+template <DeviceType device_type>
+void ComputeSpmmCsr(user_op::KernelComputeContext* ctx, const user_op::OpKernelCache* cache,
+                    const user_op::Tensor* bias, bool relu, const char* op_name) {
+  const user_op::Tensor* row_ptr = ctx->Tensor4ArgNameAndIndex("a_csr_row_ptr", 0);
+  const user_op::Tensor* col_idx = ctx->Tensor4ArgNameAndIndex("a_csr_col_idx", 0);
+  const user_op::Tensor* values = ctx->Tensor4ArgNameAndIndex("a_csr_values", 0);
+  const user_op::Tensor* b = ctx->Tensor4ArgNameAndIndex("b", 0);
+  user_op::Tensor* out = ctx->Tensor4ArgNameAndIndex("out", 0);
+  const int64_t m = ctx->Attr<int64_t>("a_num_rows");
+  const int64_t k = ctx->Attr<int64_t>("a_num_cols");
+  OFX_KERNEL_CHECK(b->shape_view().NumAxes() == 2, "b Numdims should be equal to 2. ");
+  OFX_KERNEL_CHECK(out->shape_view().NumAxes() == 2, "out Numdims should be equal to 2. ");
+  OFX_KERNEL_CHECK(out->data_type() == b->data_type(), "out datatype should be equal to b. ");
+  const int64_t n = out->shape_view().At(1);
+  const int64_t nnz = col_idx->shape_view().elem_cnt();
+  int64_t row_begin = 0;
+  int64_t row_end = m;
+  if (cache != nullptr) {
+    const auto* range = dynamic_cast<const SpmmCsrOpKernelCache*>(cache);
+    OFX_KERNEL_CHECK(range != nullptr, "unexpected kernel cache type");
+    row_begin = range->lower();
+    row_end = range->upper();
+  }
+  OFX_KERNEL_CHECK(out->shape_view().At(0) == row_end - row_begin,
+                   "out rows " << out->shape_view().At(0) << " != row range "
+                               << row_end - row_begin);
+  if (bias != nullptr)
+    OFX_KERNEL_CHECK(bias->shape_view().elem_cnt() == n && bias->data_type() == b->data_type(),
+                     "bias must be [" << n << "] of b's dtype");
+  const int idx_dt = DtCode(row_ptr->data_type());
+  const int val_dt = DtCode(values->data_type());
+  const void* bias_ptr = bias ? bias->dptr() : nullptr;
+  const int act = relu ? OFX_ACT_RELU : OFX_ACT_NONE;
+  int rc;
+  if (device_type == DeviceType::kHIP) {
+    user_op::Tensor* tmp = ctx->Tensor4ArgNameAndIndex("tmp_buffer", 0);
+    void* ws = tmp ? tmp->mut_dptr() : nullptr;
+    const size_t ws_bytes = tmp ? (size_t)tmp->shape_view().elem_cnt() : 0;
+    void* stream = ctx->stream()->As<ep::HipStream>()->hip_stream();
+    rc = ofx_spmm_csr_fused(stream, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
+                            col_idx->dptr(), values->dptr(), b->dptr(), b->row_stride(),
+                            out->mut_dptr(), out->row_stride(), row_begin, row_end, bias_ptr, act,
+                            ws, ws_bytes, nullptr);
+  } else {
+    const int threads = ctx->stream()->As<ep::CpuStream>()->num_threads();
+    rc = ofx_spmm_csr_fused_cpu(threads, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
+                                col_idx->dptr(), values->dptr(), b->dptr(), b->row_stride(),
+                                out->mut_dptr(), out->row_stride(), row_begin, row_end, bias_ptr,
+                                act, nullptr);
+  }
+  OFX_KERNEL_CHECK(rc == OFX_OK, op_name << " kernel failed (" << rc << "): " << ofx_last_error());
+}
+
 template <DeviceType device_type>
 class SpmmCsrKernel final : public user_op::OpKernel, public user_op::CudaGraphSupport {
  public:
@@ -57,47 +112,29 @@ class SpmmCsrKernel final : public user_op::OpKernel, public user_op::CudaGraphS
   using user_op::OpKernel::Compute;
   void Compute(user_op::KernelComputeContext* ctx, user_op::OpKernelState*,
                const user_op::OpKernelCache* cache) const override {
-    const user_op::Tensor* row_ptr = ctx->Tensor4ArgNameAndIndex("a_csr_row_ptr", 0);
-    const user_op::Tensor* col_idx = ctx->Tensor4ArgNameAndIndex("a_csr_col_idx", 0);
-    const user_op::Tensor* values = ctx->Tensor4ArgNameAndIndex("a_csr_values", 0);
-    const user_op::Tensor* b = ctx->Tensor4ArgNameAndIndex("b", 0);
-    user_op::Tensor* out = ctx->Tensor4ArgNameAndIndex("out", 0);
-    const int64_t m = ctx->Attr<int64_t>("a_num_rows");
-    const int64_t k = ctx->Attr<int64_t>("a_num_cols");
-    OFX_KERNEL_CHECK(b->shape_view().NumAxes() == 2, "b Numdims should be equal to 2. ");
-    OFX_KERNEL_CHECK(out->shape_view().NumAxes() == 2, "out Numdims should be equal to 2. ");
-    OFX_KERNEL_CHECK(out->data_type() == b->data_type(), "out datatype should be equal to b. ");
-    const int64_t n = out->shape_view().At(1);
-    const int64_t nnz = col_idx->shape_view().elem_cnt();
-    int64_t row_begin = 0;
-    int64_t row_end = m;
-    if (cache != nullptr) {
-      const auto* range = dynamic_cast<const SpmmCsrOpKernelCache*>(cache);
-      OFX_KERNEL_CHECK(range != nullptr, "unexpected kernel cache type");
-      row_begin = range->lower();
-      row_end = range->upper();
-    }
-    OFX_KERNEL_CHECK(out->shape_view().At(0) == row_end - row_begin,
-                     "out rows " << out->shape_view().At(0) << " != row range "
-                                 << row_end - row_begin);
-    const int idx_dt = DtCode(row_ptr->data_type());
-    const int val_dt = DtCode(values->data_type());
-    int rc;
-    if (device_type == DeviceType::kHIP) {
-      user_op::Tensor* tmp = ctx->Tensor4ArgNameAndIndex("tmp_buffer", 0);
-      void* ws = tmp ? tmp->mut_dptr() : nullptr;
-      const size_t ws_bytes = tmp ? (size_t)tmp->shape_view().elem_cnt() : 0;
-      void* stream = ctx->stream()->As<ep::HipStream>()->hip_stream();
-      rc = ofx_spmm_csr(stream, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(), col_idx->dptr(),
-                        values->dptr(), b->dptr(), b->row_stride(), out->mut_dptr(),
-                        out->row_stride(), row_begin, row_end, ws, ws_bytes, nullptr);
-    } else {
-      const int threads = ctx->stream()->As<ep::CpuStream>()->num_threads();
-      rc = ofx_spmm_csr_cpu(threads, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
-                            col_idx->dptr(), values->dptr(), b->dptr(), b->row_stride(),
-                            out->mut_dptr(), out->row_stride(), row_begin, row_end, nullptr);
-    }
-    OFX_KERNEL_CHECK(rc == OFX_OK, "spmm_csr kernel failed (" << rc << "): " << ofx_last_error());
+    ComputeSpmmCsr<device_type>(ctx, cache, nullptr, false, "spmm_csr");
+  }
+};
+
+template <DeviceType device_type>
+class FusedSpmmCsrKernel final : public user_op::OpKernel, public user_op::CudaGraphSupport {
+ public:
+  FusedSpmmCsrKernel() = default;
+  ~FusedSpmmCsrKernel() override = default;
+
+  std::shared_ptr<user_op::OpKernelCache> InitOpKernelCache(
+      user_op::KernelCacheContext* ctx) const override {
+    return CreateSpmmCsrOpKernelCache(ctx);
+  }
+
+  bool AlwaysComputeWhenAllOutputsEmpty() const override { return false; }
+
+ private:
+  using user_op::OpKernel::Compute;
+  void Compute(user_op::KernelComputeContext* ctx, user_op::OpKernelState*,
+               const user_op::OpKernelCache* cache) const override {
+    ComputeSpmmCsr<device_type>(ctx, cache, ctx->Tensor4ArgNameAndIndex("bias", 0),
+                                ctx->Attr<bool>("relu"), "fused_spmm_csr");
   }
 };
 
@@ -114,9 +151,9 @@ size_t InferSpmmCsrTmpSize(user_op::InferSizeContext* ctx) {
 
 }  // namespace
 
-#define REGISTER_SPMM_CSR_KERNEL(device, dtype, itype)                                         \
-  REGISTER_USER_KERNEL("spmm_csr")                                                            \
-      .SetCreateFn<SpmmCsrKernel<device>>()                                                   \
+#define REGISTER_SPMM_CSR_KERNEL_OF(op, kernel, device, dtype, itype)                          \
+  REGISTER_USER_KERNEL(op)                                                                    \
+      .SetCreateFn<kernel<device>>()                                                          \
       .SetIsMatchedHob((user_op::HobDeviceType() == device)                                   \
                        && (user_op::HobDataType("out", 0) == dtype)                           \
                        && (user_op::HobDataType("a_csr_row_ptr", 0) == itype))                \
@@ -125,6 +162,10 @@ size_t InferSpmmCsrTmpSize(user_op::InferSizeContext* ctx) {
                                    InferSpmmCsrTmpSize)                                       \
                              : std::function<size_t(user_op::InferSizeContext*)>(             \
                                    [](user_op::InferSizeContext*) -> size_t { return 0; }));
+
+#define REGISTER_SPMM_CSR_KERNEL(device, dtype, itype)                                     \
+  REGISTER_SPMM_CSR_KERNEL_OF("spmm_csr", SpmmCsrKernel, device, dtype, itype)            \
+  REGISTER_SPMM_CSR_KERNEL_OF("fused_spmm_csr", FusedSpmmCsrKernel, device, dtype, itype)
 
 #define REGISTER_SPMM_CSR_KERNEL_ALL_INDEX(device, dtype) \
   REGISTER_SPMM_CSR_KERNEL(device, dtype, kInt32)         \

@@ -113,6 +113,40 @@ def spmm_csr(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor,
     return out
 
 
+def fused_spmm_csr(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor,
+                   a_csr_values: torch.Tensor, a_num_rows: int, a_num_cols: int, b: torch.Tensor,
+                   bias: torch.Tensor | None = None, *, relu: bool = False,
+                   out: torch.Tensor | None = None) -> torch.Tensor:
+    """Op "fused_spmm_csr": relu?(A @ b + bias?) in one kernel, the same bits as
+    spmm_csr -> bias_add -> relu run separately."""
+    rp = _prep(a_csr_row_ptr, "a_csr_row_ptr")
+    ci = _prep(a_csr_col_idx, "a_csr_col_idx")
+    vals = _prep(a_csr_values, "a_csr_values")
+    bb = _prep(b, "b", matrix=True)
+    bs = _prep(bias, "bias") if bias is not None else None
+    d_rp, d_ci, d_v, d_b = desc(rp), desc(ci), desc(vals), desc(bb)
+    d_bias = ctypes.byref(desc(bs)) if bs is not None else None
+    od = TensorDesc()
+    check(LIB.ofx_functional_spmm_csr_infer(ctypes.byref(d_rp), ctypes.byref(d_ci), ctypes.byref(d_v),
+                                            int(a_num_rows), int(a_num_cols), ctypes.byref(d_b),
+                                            ctypes.byref(od)), "fused_spmm_csr")
+    if out is None:
+        out = torch.empty((od.shape[0], od.shape[1]), dtype=_DT_TO_TORCH[od.dtype], device=bb.device)
+    d_o = desc(out)
+    args = (ctypes.byref(d_rp), ctypes.byref(d_ci), ctypes.byref(d_v), ctypes.byref(d_b), d_bias,
+            int(a_num_rows), int(a_num_cols), 1 if relu else 0, ctypes.byref(d_o))
+    size = ctypes.c_size_t(0)
+    check(LIB.ofx_functional_fused_spmm_csr(None, *args, None, 0, ctypes.byref(size)), "fused_spmm_csr")
+    tmp = None
+    if size.value and bb.device.type != "cpu":
+        tmp = torch.empty(size.value, dtype=torch.uint8, device=bb.device)
+    check(LIB.ofx_functional_fused_spmm_csr(current_stream_handle(bb), *args,
+                                            tmp.data_ptr() if tmp is not None else None,
+                                            size.value if tmp is not None else 0, None),
+          "fused_spmm_csr")
+    return out
+
+
 def _run_grad_op(fn, stream_of, ins, outs, extra):
     """Two-phase call of a functional gradient entry: tmp size, then the run."""
     size = ctypes.c_size_t(0)

@@ -103,4 +103,48 @@ def spmm(a_csr_row_ptr, a_csr_col_idx, a_csr_values, a_num_rows, a_num_cols, b, 
     return spmm_csr(a_csr_row_ptr, a_csr_col_idx, a_csr_values, a_num_rows, a_num_cols, b, out=out)
 
 
-__all__ = ["csr_transpose", "gather_values", "sddmm", "SpmmCsrFunction", "spmm", "TRANSPOSE_CACHE", "ops"]
+class FusedSpmmCsrFunction(torch.autograd.Function):
+    """relu?(A @ b + bias?).  Backward as the unfused graph's: relu_grad from the output
+    (dy where y > 0, oneflow/core/autograd/gradient_funcs/activation.cpp:195-205), bias_add
+    grad = column sum of the masked gradient (gradient_funcs/bias_add.cpp:62), then the
+    spmm_csr gradients."""
+
+    @staticmethod
+    def forward(ctx, row_ptr, col_idx, values, m, k, b, bias, relu):
+        out = _C.fused_spmm_csr(row_ptr, col_idx, values, m, k, b, bias, relu=relu)
+        ctx.save_for_backward(row_ptr, col_idx, values, b, out if relu else None)
+        ctx.m, ctx.k, ctx.relu, ctx.has_bias = m, k, relu, bias is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, d_out):
+        row_ptr, col_idx, values, b, out = ctx.saved_tensors
+        g = d_out.contiguous()
+        if ctx.relu:
+            g = torch.where(out > 0, g, torch.zeros_like(g))
+        d_bias = g.sum(0) if ctx.has_bias and ctx.needs_input_grad[6] else None
+        d_values = d_b = None
+        if ctx.needs_input_grad[2]:
+            d_values = sddmm(row_ptr, col_idx, g, b)
+        if ctx.needs_input_grad[5]:
+            rp_t, ci_t, perm = TRANSPOSE_CACHE.get(row_ptr, col_idx, ctx.k)
+            d_b = spmm_csr(rp_t, ci_t, gather_values(perm, values), ctx.k, ctx.m, g)
+        return None, None, d_values, None, None, d_b, d_bias, None
+
+
+def fused_spmm(a_csr_row_ptr, a_csr_col_idx, a_csr_values, a_num_rows, a_num_cols, b, bias=None,
+               *, relu=False, out=None):
+    """A GCN layer's aggregation + bias + activation: relu?(A @ b + bias?) with autograd."""
+    needs = (a_csr_values.requires_grad or b.requires_grad or
+             (bias is not None and bias.requires_grad))
+    if torch.is_grad_enabled() and needs:
+        if out is not None:
+            raise RuntimeError("fused_spmm: out= is not supported when gradients are required")
+        return FusedSpmmCsrFunction.apply(a_csr_row_ptr, a_csr_col_idx, a_csr_values,
+                                          int(a_num_rows), int(a_num_cols), b, bias, bool(relu))
+    return _C.fused_spmm_csr(a_csr_row_ptr, a_csr_col_idx, a_csr_values, a_num_rows, a_num_cols, b,
+                             bias, relu=relu, out=out)
+
+
+__all__ = ["csr_transpose", "gather_values", "sddmm", "SpmmCsrFunction", "spmm", "TRANSPOSE_CACHE", "ops",
+           "FusedSpmmCsrFunction", "fused_spmm"]

@@ -46,15 +46,19 @@ class SpmmCsrKernel:
         self.workspace = torch.empty(max(ws, 1), dtype=torch.uint8, device=device)
         self.ws_bytes = ws
 
-    def __call__(self, row_ptr, col_idx, values, b, out, row_begin=0, row_end=None, stream=None):
+    def __call__(self, row_ptr, col_idx, values, b, out, row_begin=0, row_end=None, stream=None,
+                 bias=None, relu=False):
+        """bias / relu: the fused epilogue (ofx_spmm_csr_fused); none = the plain op."""
         row_end = self.m if row_end is None else row_end
         s = stream if stream is not None else current_stream_handle(b)
-        check(LIB.ofx_spmm_csr(s, self.idx_dt, self.val_dt, self.m, self.k, self.n, self.nnz,
-                               row_ptr.data_ptr(), col_idx.data_ptr() if col_idx.numel() else None,
-                               values.data_ptr() if values.numel() else None,
-                               b.data_ptr() if b.numel() else None, b.stride(0), out.data_ptr(),
-                               out.stride(0), row_begin, row_end, self.workspace.data_ptr(),
-                               self.ws_bytes, ctypes.byref(self.options) if self.options else None),
+        check(LIB.ofx_spmm_csr_fused(s, self.idx_dt, self.val_dt, self.m, self.k, self.n, self.nnz,
+                                     row_ptr.data_ptr(), col_idx.data_ptr() if col_idx.numel() else None,
+                                     values.data_ptr() if values.numel() else None,
+                                     b.data_ptr() if b.numel() else None, b.stride(0), out.data_ptr(),
+                                     out.stride(0), row_begin, row_end,
+                                     bias.data_ptr() if bias is not None else None, 1 if relu else 0,
+                                     self.workspace.data_ptr(), self.ws_bytes,
+                                     ctypes.byref(self.options) if self.options else None),
               "spmm_csr")
         return out
 
@@ -72,18 +76,19 @@ def spmm_csr_device(row_ptr, col_idx, values, b, m, k, *, out=None, row_begin=0,
 
 
 def spmm_csr_cpu(row_ptr, col_idx, values, b, m, k, *, out=None, row_begin=0, row_end=None,
-                 options: Options | None = None, num_threads: int = 0):
-    """The DeviceType::kCPU kernel (C-ABI ofx_spmm_csr_cpu), host tensors."""
+                 options: Options | None = None, num_threads: int = 0, bias=None, relu=False):
+    """The DeviceType::kCPU kernel (C-ABI ofx_spmm_csr_fused_cpu), host tensors."""
     row_end = m if row_end is None else row_end
     if out is None:
         out = torch.empty((row_end - row_begin, b.shape[1]), dtype=b.dtype)
-    check(LIB.ofx_spmm_csr_cpu(int(num_threads), dtype_code(row_ptr.dtype), dtype_code(b.dtype), m, k,
-                               b.shape[1], col_idx.numel(), row_ptr.data_ptr(),
-                               col_idx.data_ptr() if col_idx.numel() else None,
-                               values.data_ptr() if values.numel() else None,
-                               b.data_ptr() if b.numel() else None, b.stride(0), out.data_ptr(),
-                               out.stride(0), row_begin, row_end,
-                               ctypes.byref(options) if options else None), "spmm_csr_cpu")
+    check(LIB.ofx_spmm_csr_fused_cpu(int(num_threads), dtype_code(row_ptr.dtype), dtype_code(b.dtype),
+                                     m, k, b.shape[1], col_idx.numel(), row_ptr.data_ptr(),
+                                     col_idx.data_ptr() if col_idx.numel() else None,
+                                     values.data_ptr() if values.numel() else None,
+                                     b.data_ptr() if b.numel() else None, b.stride(0), out.data_ptr(),
+                                     out.stride(0), row_begin, row_end,
+                                     bias.data_ptr() if bias is not None else None, 1 if relu else 0,
+                                     ctypes.byref(options) if options else None), "spmm_csr_cpu")
     return out
 
 

@@ -125,6 +125,32 @@ def spmm(row_ptr, col_idx, values, b, *, dtype="f32", row_begin=0, row_end=None,
     return out
 
 
+def bias_act(out, bias=None, activation="none", *, dtype="f32"):
+    """The composition spmm_csr -> bias_add -> relu applied to an oracle SpMM result, each op
+    rounding to the storage dtype as the separate OneFlow kernels do:
+      bias_add  BroadcastElementwiseBinary kAdd of out[M,N] and bias[1,N,1]-broadcast
+                (oneflow/user/kernels/bias_add_kernel.cpp:25-53): one add, one rounding;
+      relu      UnaryFunctor<kRelu> (oneflow/core/ep/common/primitive/unary_functor.h:146-156):
+                src <= 0 -> 0 (so -0 -> +0), otherwise src (NaN passes).
+    bf16 arrays are uint16 bit patterns; the add is done in fp32 and rounded once (exact for
+    two 16-bit operands: fp32 holds >= 2p+2 bits, so the double rounding is innocuous)."""
+    y = np.array(out, copy=True)
+    if bias is not None:
+        bias = np.asarray(bias)
+        if dtype == "bf16":
+            y = f32_to_bf16_bits(bf16_bits_to_f32(y) + bf16_bits_to_f32(bias)[None, :])
+        elif dtype == "f16":
+            y = (y.astype(np.float32) + bias.astype(np.float32)[None, :]).astype(np.float16)
+        else:
+            y = y + bias.astype(y.dtype)[None, :]
+    if activation == "relu":
+        f = bf16_bits_to_f32(y) if dtype == "bf16" else y
+        y = np.where(f <= 0, np.zeros_like(y), y)
+    elif activation != "none":
+        raise ValueError(f"oracle: unknown activation {activation!r}")
+    return y
+
+
 def ref64(row_ptr, col_idx, values_f32, b_f32, *, row_begin=0, row_end=None, nthreads=None):
     """fp64 product C64 and |.|-sum bound of an fp32 (or upcast 16-bit) problem."""
     m = len(row_ptr) - 1

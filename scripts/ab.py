@@ -4,7 +4,8 @@
     python scripts/ab.py [--config products] [--rounds 8] [--reps 5] [--variants 0,264,432,...]
 
 Variant codes: 0 = the op's auto choice; VEC*100+LPR forces (VEC, LPR); "ordered" = no hub split;
-a suffix "h<thr>" sets the heavy-row threshold (h-1 = off), e.g. 10002h256.
+a suffix "h<thr>" sets the heavy-row threshold (h-1 = off), e.g. 10002h256; a prefix "f" runs
+the fused epilogue (bias + relu) with that variant, e.g. f0 (not compared for bit identity).
 Prints per-variant median/min ms and gather-model GB/s; checks every variant is bit-identical to
 the auto variant on the first round.
 """
@@ -44,12 +45,14 @@ def main():
     b = synth.dense(0, k, n, dt, device=dev)
     s_v = b.element_size()
     nbytes = alg_bytes(m, nnz, n, s_v)
-    kernels, outs = {}, {}
+    kernels, outs, fused = {}, {}, {}
+    bias = synth.dense(0, 1, n, dt, device=dev)[0]
     for name in args.variants.split(","):
+        fused[name] = name.startswith("f")
         if name == "ordered":
             opts = ops.make_options(ordered=True)
         else:
-            vv, _, h = name.partition("h")
+            vv, _, h = name.lstrip("f").partition("h")
             opts = ops.make_options(variant=int(vv), split=args.split, heavy=int(h) if h else args.heavy)
         kernels[name] = ops.SpmmCsrKernel(m, k, n, nnz, torch.int32, dt, dev, opts)
         outs[name] = torch.empty((m, n), dtype=dt, device=dev)
@@ -57,17 +60,20 @@ def main():
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for r in range(args.rounds):
         for name, kern in kernels.items():
-            kern(rp, ci, v, b, outs[name])  # warm
+            epi = dict(bias=bias, relu=True) if fused[name] else {}
+            kern(rp, ci, v, b, outs[name], **epi)  # warm
             torch.cuda.synchronize()
             e0.record()
             for _ in range(args.reps):
-                kern(rp, ci, v, b, outs[name])
+                kern(rp, ci, v, b, outs[name], **epi)
             e1.record()
             torch.cuda.synchronize()
             times[name].append(e0.elapsed_time(e1) / args.reps)
         if r == 0:
             ref = outs[next(iter(outs))]
             for name, o in outs.items():
+                if fused[name]:
+                    continue
                 same = torch.equal(o.view(torch.uint8), ref.view(torch.uint8))
                 print(f"[ab] {name}: bit-identical to first variant: {same}", flush=True)
     for name, t in times.items():
