@@ -136,7 +136,7 @@ def main():
             rs.comm_kind = args.comm or rs.comm_kind
             rs.set_pipeline(args.pipeline or 1)
         else:
-            comm_times = rs.tune(d_rp, d_ci, d_v, out)
+            comm_times = rs.tune(d_rp, d_ci, d_v, out, force=args.force_rowsplit)
 
         def step():
             rs(d_rp, d_ci, d_v, out=out)

@@ -291,6 +291,14 @@ def test_row_split_rccl_single_rank(device):
                 rs(rp.to(device), rs.remap_columns(ci.to(device)), v.to(device), out=out2)
             torch.cuda.synchronize()
             assert_bitwise(out2, oracle_spmm(rp, ci, v, b), f"{kind} pipeline {chunks}")
+        # the setup-time choice runs every candidate step and keeps one; output stays exact
+        times = rs.tune(rp.to(device), rs.remap_columns(ci.to(device)), v.to(device), out2,
+                        reps=1, force=True)
+        assert len(times) == 6 and f"{rs.comm_kind}/p{rs.chunks}" in times
+        out2.fill_(float("nan"))
+        rs(rp.to(device), rs.remap_columns(ci.to(device)), v.to(device), out=out2)
+        torch.cuda.synchronize()
+        assert_bitwise(out2, oracle_spmm(rp, ci, v, b), "after tune")
         rs.close()
     finally:
         dist.destroy_process_group()
