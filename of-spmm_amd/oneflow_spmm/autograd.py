@@ -51,6 +51,7 @@ class _TransposeCache:
     def __init__(self, capacity: int = 4):
         self.capacity = capacity
         self.entries: OrderedDict = OrderedDict()
+        self.value_entries: OrderedDict = OrderedDict()
 
     def get(self, row_ptr, col_idx, k):
         key = (row_ptr.data_ptr(), col_idx.data_ptr(), row_ptr._version, col_idx._version,
@@ -65,6 +66,24 @@ class _TransposeCache:
         while len(self.entries) > self.capacity:
             self.entries.popitem(last=False)
         return t
+
+
+    def values_t(self, row_ptr, col_idx, values, k):
+        """A^T's values = values[perm].  Edge weights of a GNN (e.g. GCN normalisation) are
+        usually constant across steps, so the gathered copy is kept too, keyed on the values
+        tensor's storage and version (an in-place update invalidates it)."""
+        rp_t, ci_t, perm = self.get(row_ptr, col_idx, k)
+        key = (row_ptr.data_ptr(), col_idx.data_ptr(), row_ptr._version, col_idx._version, k,
+               values.data_ptr(), values._version, values.dtype, values.numel(), str(values.device))
+        hit = self.value_entries.get(key)
+        if hit is not None:
+            self.value_entries.move_to_end(key)
+            return rp_t, ci_t, hit[1]
+        vals_t = gather_values(perm, values)
+        self.value_entries[key] = (values, vals_t)  # holds values: its storage cannot be reused
+        while len(self.value_entries) > self.capacity:
+            self.value_entries.popitem(last=False)
+        return rp_t, ci_t, vals_t
 
 
 TRANSPOSE_CACHE = _TransposeCache()
@@ -86,8 +105,7 @@ class SpmmCsrFunction(torch.autograd.Function):
         if ctx.needs_input_grad[2]:
             d_values = sddmm(row_ptr, col_idx, d_out, b)
         if ctx.needs_input_grad[5]:
-            rp_t, ci_t, perm = TRANSPOSE_CACHE.get(row_ptr, col_idx, ctx.k)
-            vals_t = gather_values(perm, values)
+            rp_t, ci_t, vals_t = TRANSPOSE_CACHE.values_t(row_ptr, col_idx, values.detach(), ctx.k)
             d_b = spmm_csr(rp_t, ci_t, vals_t, ctx.k, ctx.m, d_out)
         return None, None, d_values, None, None, d_b
 
@@ -127,8 +145,8 @@ class FusedSpmmCsrFunction(torch.autograd.Function):
         if ctx.needs_input_grad[2]:
             d_values = sddmm(row_ptr, col_idx, g, b)
         if ctx.needs_input_grad[5]:
-            rp_t, ci_t, perm = TRANSPOSE_CACHE.get(row_ptr, col_idx, ctx.k)
-            d_b = spmm_csr(rp_t, ci_t, gather_values(perm, values), ctx.k, ctx.m, g)
+            rp_t, ci_t, vals_t = TRANSPOSE_CACHE.values_t(row_ptr, col_idx, values.detach(), ctx.k)
+            d_b = spmm_csr(rp_t, ci_t, vals_t, ctx.k, ctx.m, g)
         return None, None, d_values, None, None, d_b, d_bias, None
 
 

@@ -226,3 +226,24 @@ def test_grad_ops_through_op_layer_errors_and_sbp():
     assert fs._C.sddmm_csr(rp, ci, a[:, :0], b[:, :0], m, k).abs().sum() == 0
     rt, ct, perm = fs._C.csr_transpose(rp, ci, m, k)
     assert rt.shape == (k + 1,) and ct.shape == ci.shape and perm.dtype == rp.dtype
+
+
+def test_transposed_values_cache_follows_inplace_updates():
+    """dB uses A^T's values from a cache keyed on the values' storage and version: an in-place
+    update of the values (an optimizer step on edge weights) must be seen by the next backward."""
+    from oneflow_spmm.autograd import TRANSPOSE_CACHE
+    rng = np.random.default_rng(31)
+    m, k, n = 40, 30, 8
+    rp, ci, v = random_csr(m, k, rng.integers(0, 6, size=m), rng)
+    b = random_dense(k, n, rng)
+    g = torch.from_numpy(rng.uniform(-1, 1, (m, n)).astype(np.float32))
+    vv = v.clone().requires_grad_(True)
+    rt, ct, perm = oracle.transpose(rp.numpy(), ci.numpy(), k)
+    for step in range(3):
+        bb = b.clone().requires_grad_(True)
+        fs.spmm(rp, ci, vv, m, k, bb).backward(g)
+        ref_db = oracle.spmm(rt, ct, vv.detach().numpy()[perm], g.numpy())
+        assert_bitwise(bb.grad, ref_db, f"dB step {step}")
+        with torch.no_grad():
+            vv.mul_(0.5).add_(0.25)
+    assert len(TRANSPOSE_CACHE.value_entries) <= TRANSPOSE_CACHE.capacity
