@@ -268,9 +268,18 @@ Schedule sddmm_schedule(int64_t n) {
   return resolve_schedule(n, nullptr);
 }
 
+#ifndef OFX_SD_U
+#define OFX_SD_U 0
+#endif
+#ifndef OFX_SD_LG8
+#define OFX_SD_LG8 8
+#endif
+#ifndef OFX_SD_LG16
+#define OFX_SD_LG16 16
+#endif
 template <typename T, typename I, int LG, int L, bool ALIGNED>
 int sddmm_cfg(const SddmmArgs& a) {
-  constexpr int U = L >= 4 ? 2 : 4;
+  constexpr int U = OFX_SD_U > 0 ? OFX_SD_U : (L >= 4 ? 2 : 4);
   constexpr int64_t GPB = (kBlock / 64) * (64 / LG);
   const Schedule sched = sddmm_schedule(a.n);
   const plan::WsLayout w = plan::ws_layout(a.nrows, a.nnz, 0, 0, sched);
@@ -299,8 +308,8 @@ int sddmm_aligned(const SddmmArgs& a) {
   if (leaves <= 1) return sddmm_cfg<T, I, 1, 1, ALIGNED>(a);
   if (leaves <= 2) return sddmm_cfg<T, I, 2, 1, ALIGNED>(a);
   if (leaves <= 4) return sddmm_cfg<T, I, 4, 1, ALIGNED>(a);
-  if (leaves <= 8) return sddmm_cfg<T, I, 8, 1, ALIGNED>(a);
-  if (leaves <= 16) return sddmm_cfg<T, I, 16, 1, ALIGNED>(a);
+  if (leaves <= 8) return sddmm_cfg<T, I, OFX_SD_LG8, 8 / OFX_SD_LG8, ALIGNED>(a);
+  if (leaves <= 16) return sddmm_cfg<T, I, OFX_SD_LG16, 16 / OFX_SD_LG16, ALIGNED>(a);
   if (leaves <= 32) return sddmm_cfg<T, I, 32, 1, ALIGNED>(a);
   if (leaves <= 64) return sddmm_cfg<T, I, 64, 1, ALIGNED>(a);
   if (leaves <= 128) return sddmm_cfg<T, I, 64, 2, ALIGNED>(a);

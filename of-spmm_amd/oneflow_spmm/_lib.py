@@ -8,7 +8,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libofx_spmm.so")
+# OFX_SPMM_LIB: A/B timing of alternative builds of the same sources (scripts/); the default is
+# the in-tree library next to this file.
+LIB_PATH = os.environ.get("OFX_SPMM_LIB") or os.path.join(_HERE, "libofx_spmm.so")
 
 # OneFlow DataType codes (oneflow/core/common/data_type.proto:4-26)
 DT_FLOAT, DT_DOUBLE, DT_INT32, DT_INT64, DT_FLOAT16, DT_BFLOAT16 = 2, 3, 5, 6, 9, 11

@@ -31,35 +31,42 @@ def timed(fn, reps=10):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="products")
+    ap.add_argument("--n", type=int, default=0, help="override the dense width")
+    ap.add_argument("--only", default="", help="comma list of phases (transpose,gather,sddmm,db,fwd)")
     args = ap.parse_args()
     import oneflow_spmm as fs
     from oneflow_spmm import autograd as ag
     from oneflow_spmm import synth
     cfg = synth.CONFIGS[args.config]
     m, k, nnz, n, dt = cfg["m"], cfg["k"], cfg["nnz"], cfg["n"], cfg["dtype"]
+    n = args.n or n
     dev = torch.device("cuda", 0)
     rp, ci, v = synth.csr(m, k, nnz, val_dtype=dt, threads=16)
     rp, ci, v = rp.to(dev), ci.to(dev), v.to(dev)
     b = synth.dense(0, k, n, dt, device=dev)
     g = synth.dense(0, m, n, dt, device=dev, seed=7)
     sv = b.element_size()
-    res = {"config": args.config}
-    t = timed(lambda: fs.csr_transpose(rp, ci, k), reps=3)
-    res["transpose_ms"] = t
-    rt, ct, perm = fs.csr_transpose(rp, ci, k)
-    t = timed(lambda: ag.gather_values(perm, v))
-    res["gather_values_ms"] = t
-    t = timed(lambda: fs.sddmm(rp, ci, g, b))
-    sd_bytes = 4 * (m + 1) + 4 * nnz + sv * nnz * n + sv * m * n + sv * nnz
-    res["sddmm_ms"] = t
-    res["sddmm_gbs"] = sd_bytes / (t * 1e-3) / 1e9
-    vt = ag.gather_values(perm, v)
-    t = timed(lambda: fs.spmm_csr(rt, ct, vt, k, m, g))
-    db_bytes = 4 * (k + 1) + (4 + sv) * nnz + sv * nnz * n + sv * k * n
-    res["db_spmm_ms"] = t
-    res["db_spmm_gbs"] = db_bytes / (t * 1e-3) / 1e9
-    t = timed(lambda: fs.spmm_csr(rp, ci, v, m, k, b))
-    res["forward_ms"] = t
+    res = {"config": args.config, "n": n}
+    only = set(args.only.split(",")) if args.only else {"transpose", "gather", "sddmm", "db", "fwd"}
+    if only & {"transpose", "gather", "db"}:
+        t = timed(lambda: fs.csr_transpose(rp, ci, k), reps=3)
+        res["transpose_ms"] = t
+        rt, ct, perm = fs.csr_transpose(rp, ci, k)
+    if "gather" in only:
+        res["gather_values_ms"] = timed(lambda: ag.gather_values(perm, v))
+    if "sddmm" in only:
+        t = timed(lambda: fs.sddmm(rp, ci, g, b))
+        sd_bytes = 4 * (m + 1) + 4 * nnz + sv * nnz * n + sv * m * n + sv * nnz
+        res["sddmm_ms"] = t
+        res["sddmm_gbs"] = sd_bytes / (t * 1e-3) / 1e9
+    if "db" in only:
+        vt = ag.gather_values(perm, v)
+        t = timed(lambda: fs.spmm_csr(rt, ct, vt, k, m, g))
+        db_bytes = 4 * (k + 1) + (4 + sv) * nnz + sv * nnz * n + sv * k * n
+        res["db_spmm_ms"] = t
+        res["db_spmm_gbs"] = db_bytes / (t * 1e-3) / 1e9
+    if "fwd" in only:
+        res["forward_ms"] = timed(lambda: fs.spmm_csr(rp, ci, v, m, k, b))
     print(json.dumps({kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in res.items()}))
 
 
