@@ -24,6 +24,11 @@ CONFIGS = {
     "reddit": dict(m=232_965, k=232_965, nnz=114_615_892, n=256, dtype=torch.bfloat16),
     "papers": dict(m=111_059_956, k=111_059_956, nnz=1_615_685_872, n=128, dtype=torch.float32),
 }
+# Not a BASELINE config: the maximum-size case of the int64 index path (nnz > 2^31 - 1, so
+# row_ptr offsets and every nonzero position past 2^31 need 64-bit indices end to end).
+EXTRA_CONFIGS = {
+    "int64_max": dict(m=40_000_000, k=40_000_000, nnz=2_300_000_000, n=16, dtype=torch.float32),
+}
 
 
 @dataclass

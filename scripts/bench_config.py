@@ -29,15 +29,17 @@ def main():
     from bench import alg_bytes
     from oracle import oracle
 
-    cfg = synth.CONFIGS[args.config]
+    cfg = {**synth.CONFIGS, **synth.EXTRA_CONFIGS}[args.config]
     m, k, nnz, n, dt = cfg["m"], cfg["k"], cfg["nnz"], cfg["n"], cfg["dtype"]
     dev = torch.device("cuda", 0)
     t0 = time.time()
     rp_full = synth.row_ptr(m, k, nnz)
-    cols = synth.columns(m, k, rp_full, threads=args.threads)
+    wide = nnz >= 2**31 or k >= 2**31
+    cols = synth.columns(m, k, rp_full, threads=args.threads,
+                         idx_dtype=np.int64 if wide else np.int32)
     vals = synth.values(0, nnz, dt)
     t_gen = time.time() - t0
-    d_rp = torch.from_numpy(rp_full.astype(np.int32 if nnz < 2**31 else np.int64)).to(dev)
+    d_rp = torch.from_numpy(rp_full.astype(np.int64 if wide else np.int32)).to(dev)
     d_ci = torch.from_numpy(cols).to(dev)
     d_v = vals.to(dev)
     d_b = synth.dense(0, k, n, dt, device=dev)
@@ -59,6 +61,9 @@ def main():
     deg = np.diff(rp_full)
     heavy = np.argsort(deg)[-20:]
     ranges = [(0, 2000), (m // 2, m // 2 + 2000), (m - 2000, m)] + [(int(r), int(r) + 1) for r in heavy]
+    if wide and nnz > 2**31:  # rows whose nonzeros straddle position 2^31
+        rc = int(np.searchsorted(rp_full, 2**31, side="right")) - 1
+        ranges.append((max(rc - 1000, 0), min(rc + 1000, m)))
     b_rows_needed = None  # oracle reads B rows through col; copy B to host once
     b_host = d_b.cpu()
     b_np = b_host.numpy() if dt != torch.bfloat16 else b_host.view(torch.int16).numpy().view(np.uint16)
@@ -75,6 +80,7 @@ def main():
     del b_rows_needed
     print(json.dumps({
         "config": args.config, "m": m, "nnz": nnz, "n": n, "dtype": dname,
+        "index": "int64" if wide else "int32",
         "max_degree": int(deg.max()), "gen_s": round(t_gen, 1), "ms": round(ms, 3),
         "gflops": round(2.0 * nnz * n / (ms * 1e-3) / 1e9, 1),
         "gather_model_gbs": round(nbytes / (ms * 1e-3) / 1e9, 1),
