@@ -10,7 +10,8 @@ from collections import defaultdict
 
 
 def short(name):
-    name = name.replace("void ", "").replace("ofx::(anonymous namespace)::", "")
+    name = name.replace("void ", "").replace("(anonymous namespace)::", "")
+    name = name.replace("ofx::plan::", "").replace("ofx::", "")
     return name.split("(")[0]
 
 
