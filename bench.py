@@ -68,6 +68,8 @@ def main():
                     help="all-gather schedule for N>1 (default: measured at setup, faster kept)")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="column blocks for gather/SpMM overlap at N>1 (default: measured)")
+    ap.add_argument("--exchange", choices=["auto", "allgather", "halo"], default="auto",
+                    help="B exchange for N>1 (default: measured at setup)")
     ap.add_argument("--force-rowsplit", action="store_true",
                     help="run the N>1 code path (RCCL all-gather + local SpMM) even with one rank")
     args = ap.parse_args()
@@ -126,20 +128,22 @@ def main():
                 kern(d_rp, d_ci, d_v, d_b, out)
     else:
         rs = RowSplitSpmm(m, k, n, nnz_local, dt, torch.int32, device)
-        d_ci = rs.remap_columns(d_ci)
         klo, khi = rs.k_range
         rs.load_shard(synth.dense(klo, khi, n, dt, device=device))
-        # all-gather schedule (ring / point-to-point) x pipeline depth (column blocks gathered
-        # while the previous block computes): measured here, untimed, fastest kept (same bytes)
+        rs.bind(d_rp, d_ci, d_v, halo=args.exchange in ("auto", "halo"))
+        # exchange: all-gather (ring / point-to-point) x pipeline depth (column blocks gathered
+        # while the previous block computes), or halo-only rows; measured here, untimed, the
+        # fastest kept (every candidate gives the same bytes)
         comm_times = {}
-        if args.comm or args.pipeline:
+        if args.comm or args.pipeline or args.exchange != "auto":
+            rs.exchange = "halo" if args.exchange == "halo" else "allgather"
             rs.comm_kind = args.comm or rs.comm_kind
             rs.set_pipeline(args.pipeline or 1)
         else:
-            comm_times = rs.tune(d_rp, d_ci, d_v, out, force=args.force_rowsplit)
+            comm_times = rs.tune(out, force=args.force_rowsplit)
 
         def step():
-            rs(d_rp, d_ci, d_v, out=out)
+            rs.step(out)
 
     # ---- warmup + timed region -----------------------------------------------------------------
     for _ in range(args.warmup):
@@ -179,9 +183,9 @@ def main():
             events[2].record()
         else:
             events[0].record()
-            rs.all_gather_b()
+            rs.gather_phase()
             events[1].record()
-            rs.compute(d_rp, d_ci, d_v, out)
+            rs.compute_phase(out)
             events[2].record()
         torch.cuda.synchronize()
         spmm_ms.append(events[1].elapsed_time(events[2]))
@@ -206,7 +210,7 @@ def main():
             events[2].record()
         else:
             events[1].record()
-            rs.compute(d_rp, d_ci, d_v, out)
+            rs.compute_phase(out)
             events[2].record()
         torch.cuda.synchronize()
         cold.append(events[1].elapsed_time(events[2]))
@@ -265,10 +269,15 @@ def main():
             "spmm_ms_max": round(phase["spmm_ms_max"], 4),
             # SpMM phase alone with the gathered B resident (SURVEY.md §8e reports it separately)
             "spmm_phase_gflops_aggregate": round(flops / (phase["spmm_ms_max"] * 1e-3) / 1e9, 2),
-            "allgather_gbs_per_rank": round((rs.k_padded - rs.pad) * n * s_v / (phase["gather_ms_max"] * 1e-3) / 1e9, 2)
+            "allgather_gbs_per_rank": round(((rs.halo.halo_rows if rs.exchange == "halo" else
+                                              rs.k_padded - rs.pad) * n * s_v) /
+                                            (phase["gather_ms_max"] * 1e-3) / 1e9, 2)
             if phase["gather_ms_max"] > 0 else None,
             "rows_rank0": rows, "nnz_rank0": nnz_local,
-            "allgather_schedule": rs.comm_kind, "pipeline_blocks": rs.chunks,
+            "exchange": rs.exchange, "allgather_schedule": rs.comm_kind,
+            "pipeline_blocks": rs.chunks,
+            "halo_rows_received": rs.halo.halo_rows if rs.halo is not None else None,
+            "remote_rows_total": (rs.k - (khi - klo)),
             "allgather_tune_ms": {kk: round(vv, 4) for kk, vv in comm_times.items()},
             "nnz_per_rank_max_over_mean": round(float(nz[0]) / (float(nz[1]) / world), 4)})
 

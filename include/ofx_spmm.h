@@ -240,6 +240,18 @@ int ofx_allgather(void* stream, const void* in, void* out, size_t count, int dty
 /* The same all-gather as grouped point-to-point send/recv with every peer (in place: this
  * rank's slot of `buf` is the send buffer).  Same result bytes as ofx_allgather.           */
 int ofx_allgather_p2p(void* stream, void* buf, size_t count, int dtype, void* comm);
+/* Halo exchange: grouped send/recv of B rows with per-peer counts, the
+ * ShuffleData pattern of oneflow/user/kernels/data_shuffle_kernel.cu:119-135.  Counts and
+ * offsets are in rows of n elements (host arrays, one entry per rank); this rank's entry and
+ * zero counts are skipped.                                                                  */
+int ofx_exchange_rows(void* stream, void* comm, int dtype, int64_t n, const void* send_buf,
+                      const int64_t* send_counts, const int64_t* send_offsets, void* recv_buf,
+                      const int64_t* recv_counts, const int64_t* recv_offsets);
+/* Row gather on the device: dst[i, :] = src[idx[i], :] for i < count, rows of row_bytes bytes,
+ * strides in bytes (packs the halo rows a peer requested into one send buffer).             */
+int ofx_gather_rows(void* stream, int idx_dtype, int64_t count, int64_t row_bytes,
+                    const void* idx, const void* src, int64_t src_stride_bytes, void* dst,
+                    int64_t dst_stride_bytes);
 
 /* ---- synthetic power-law CSR (deterministic, counter-based) ---------------- */
 /* row_ptr_out: int64[m+1].  Degrees of a Chung–Lu power law (exponent gamma), rows permuted. */

@@ -13,6 +13,7 @@
 #include <cstring>
 
 #include "ofx_internal.h"
+#include "spmm_common.h"
 
 #define OFX_NCCL_CHECK(expr)                                                                   \
   do {                                                                                         \
@@ -85,8 +86,7 @@ extern "C" int ofx_allgather_p2p(void* stream, void* buf, size_t count, int dtyp
   int nranks = 0, rank = 0;
   OFX_NCCL_CHECK(ncclCommCount(c, &nranks));
   OFX_NCCL_CHECK(ncclCommUserRank(c, &rank));
-  const size_t esz = (size_t)(dtype == OFX_DT_DOUBLE || dtype == OFX_DT_INT64 ? 8
-                              : (dtype == OFX_DT_FLOAT16 || dtype == OFX_DT_BFLOAT16 ? 2 : 4));
+  const size_t esz = (size_t)ofx::dtype_size(dtype);
   char* base = static_cast<char*>(buf);
   hipStream_t s = static_cast<hipStream_t>(stream);
   OFX_NCCL_CHECK(ncclGroupStart());
@@ -94,6 +94,41 @@ extern "C" int ofx_allgather_p2p(void* stream, void* buf, size_t count, int dtyp
     const int to = (rank + d) % nranks, from = (rank - d + nranks) % nranks;
     OFX_NCCL_CHECK(ncclSend(base + (size_t)rank * count * esz, count, t, to, c, s));
     OFX_NCCL_CHECK(ncclRecv(base + (size_t)from * count * esz, count, t, from, c, s));
+  }
+  OFX_NCCL_CHECK(ncclGroupEnd());
+  return OFX_OK;
+}
+
+// Halo exchange of B rows: grouped point-to-point send/recv with
+// per-peer row counts, the pattern of ShuffleData in
+// oneflow/user/kernels/data_shuffle_kernel.cu:119-135 (ncclGroupStart; ncclSend/ncclRecv per
+// peer; ncclGroupEnd).  Counts and offsets are in rows of `n` elements, host arrays of nranks;
+// this rank's own entry and zero counts are skipped (both sides agree by construction).
+extern "C" int ofx_exchange_rows(void* stream, void* comm, int dtype, int64_t n,
+                                 const void* send_buf, const int64_t* send_counts,
+                                 const int64_t* send_offsets, void* recv_buf,
+                                 const int64_t* recv_counts, const int64_t* recv_offsets) {
+  ncclDataType_t t;
+  OFX_REQUIRE(nccl_dtype(dtype, &t), OFX_EUNSUPPORTED, "exchange_rows: unsupported dtype %d", dtype);
+  OFX_REQUIRE(comm && send_counts && send_offsets && recv_counts && recv_offsets && n >= 0,
+              OFX_EINVAL, "exchange_rows: NULL argument");
+  ncclComm_t c = static_cast<ncclComm_t>(comm);
+  int nranks = 0, rank = 0;
+  OFX_NCCL_CHECK(ncclCommCount(c, &nranks));
+  OFX_NCCL_CHECK(ncclCommUserRank(c, &rank));
+  const size_t row_bytes = (size_t)n * (size_t)ofx::dtype_size(dtype);
+  const char* sb = static_cast<const char*>(send_buf);
+  char* rb = static_cast<char*>(recv_buf);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  OFX_NCCL_CHECK(ncclGroupStart());
+  for (int d = 1; d < nranks; ++d) {
+    const int to = (rank + d) % nranks, from = (rank - d + nranks) % nranks;
+    if (send_counts[to] > 0)
+      OFX_NCCL_CHECK(ncclSend(sb + (size_t)send_offsets[to] * row_bytes,
+                              (size_t)(send_counts[to] * n), t, to, c, s));
+    if (recv_counts[from] > 0)
+      OFX_NCCL_CHECK(ncclRecv(rb + (size_t)recv_offsets[from] * row_bytes,
+                              (size_t)(recv_counts[from] * n), t, from, c, s));
   }
   OFX_NCCL_CHECK(ncclGroupEnd());
   return OFX_OK;

@@ -1,0 +1,92 @@
+// rows.hip — row gather for the halo exchange: dst[i, :] = src[idx[i], :].
+//
+// Packs the B rows a peer asked for into one contiguous send buffer per step (the pack step of
+// ShuffleData's callers, oneflow/user/kernels/data_shuffle_kernel.cu:356-497, which gather
+// embedding rows by id before the grouped send).  HBM-bound: row_bytes read + written per row.
+// Lane groups of LPR lanes copy one row with the widest aligned word (16 B when the row size,
+// strides and base pointers allow it, else 4 B, else 1 B); groups stride over the rows.
+#include <hip/hip_runtime.h>
+
+#include "ofx_internal.h"
+#include "spmm_common.h"
+
+namespace ofx {
+namespace {
+
+constexpr int kBlock = 256;
+
+template <typename W, int LPR, typename I>
+__global__ void __launch_bounds__(kBlock)
+    gather_rows_kernel(const I* __restrict__ idx, int64_t count, int64_t words,
+                       const char* __restrict__ src, int64_t src_stride, char* __restrict__ dst,
+                       int64_t dst_stride) {
+  constexpr int GPB = kBlock / LPR;
+  const int gl = threadIdx.x % LPR;
+  for (int64_t i = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR; i < count;
+       i += (int64_t)gridDim.x * GPB) {
+    const W* s = reinterpret_cast<const W*>(src + (int64_t)idx[i] * src_stride);
+    W* d = reinterpret_cast<W*>(dst + i * dst_stride);
+    for (int64_t w = gl; w < words; w += LPR) d[w] = s[w];
+  }
+}
+
+template <typename W, typename I>
+int launch(hipStream_t s, const I* idx, int64_t count, int64_t row_bytes, const void* src,
+           int64_t src_stride, void* dst, int64_t dst_stride) {
+  const int64_t words = row_bytes / (int64_t)sizeof(W);
+  int lpr = 1;
+  while (lpr < 64 && lpr < words) lpr *= 2;
+  const int64_t gpb = kBlock / lpr;
+  const unsigned grid = (unsigned)std::min<int64_t>((count + gpb - 1) / gpb, 65536);
+  auto go = [&](auto k) {
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, s, idx, count, words,
+                       static_cast<const char*>(src), src_stride, static_cast<char*>(dst),
+                       dst_stride);
+  };
+  switch (lpr) {
+    case 1: go(gather_rows_kernel<W, 1, I>); break;
+    case 2: go(gather_rows_kernel<W, 2, I>); break;
+    case 4: go(gather_rows_kernel<W, 4, I>); break;
+    case 8: go(gather_rows_kernel<W, 8, I>); break;
+    case 16: go(gather_rows_kernel<W, 16, I>); break;
+    case 32: go(gather_rows_kernel<W, 32, I>); break;
+    default: go(gather_rows_kernel<W, 64, I>); break;
+  }
+  OFX_HIP_CHECK(hipGetLastError());
+  return OFX_OK;
+}
+
+template <typename I>
+int dispatch(hipStream_t s, const I* idx, int64_t count, int64_t row_bytes, const void* src,
+             int64_t src_stride, void* dst, int64_t dst_stride) {
+  auto aligned = [&](int64_t a) {
+    return row_bytes % a == 0 && src_stride % a == 0 && dst_stride % a == 0 &&
+           (uintptr_t)src % a == 0 && (uintptr_t)dst % a == 0;
+  };
+  if (aligned(16)) return launch<uint4>(s, idx, count, row_bytes, src, src_stride, dst, dst_stride);
+  if (aligned(4)) return launch<uint32_t>(s, idx, count, row_bytes, src, src_stride, dst, dst_stride);
+  return launch<unsigned char>(s, idx, count, row_bytes, src, src_stride, dst, dst_stride);
+}
+
+}  // namespace
+}  // namespace ofx
+
+using namespace ofx;
+
+extern "C" int ofx_gather_rows(void* stream, int idx_dtype, int64_t count, int64_t row_bytes,
+                               const void* idx, const void* src, int64_t src_stride_bytes,
+                               void* dst, int64_t dst_stride_bytes) {
+  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "gather_rows: bad index dtype %d",
+              idx_dtype);
+  OFX_REQUIRE(count >= 0 && row_bytes >= 0 && src_stride_bytes >= row_bytes &&
+                  dst_stride_bytes >= row_bytes,
+              OFX_EINVAL, "gather_rows: bad sizes");
+  if (count == 0 || row_bytes == 0) return OFX_OK;
+  OFX_REQUIRE(idx && src && dst, OFX_EINVAL, "gather_rows: NULL pointer");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (idx_dtype == OFX_DT_INT32)
+    return dispatch(s, static_cast<const int32_t*>(idx), count, row_bytes, src, src_stride_bytes,
+                    dst, dst_stride_bytes);
+  return dispatch(s, static_cast<const int64_t*>(idx), count, row_bytes, src, src_stride_bytes, dst,
+                  dst_stride_bytes);
+}

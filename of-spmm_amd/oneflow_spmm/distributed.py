@@ -42,6 +42,84 @@ def padded_owner_remap(col_idx: torch.Tensor, k: int, world: int) -> torch.Tenso
     return (c + shift).to(col_idx.dtype)
 
 
+def _exchange_lists(send: list, group, device) -> list:
+    """Setup-time all-to-all of variable-length int64 lists through torch.distributed (the
+    counts first, then point-to-point transfers); send[p] goes to rank p, result[p] came from p."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
+        else torch.device("cpu")
+    counts = torch.tensor([t.numel() for t in send], dtype=torch.int64, device=dev)
+    allc = [torch.zeros(world, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(allc, counts, group=group)
+    recv_counts = [int(allc[p][rank]) for p in range(world)]
+    out = [torch.empty(c, dtype=torch.int64, device=dev) for c in recv_counts]
+    ops_ = []
+    for p in range(world):
+        if p == rank:
+            continue
+        if send[p].numel():
+            ops_.append(dist.P2POp(dist.isend, send[p].to(dev).contiguous(), dist.get_global_rank(group, p) if group else p, group))
+        if recv_counts[p]:
+            ops_.append(dist.P2POp(dist.irecv, out[p], dist.get_global_rank(group, p) if group else p, group))
+    if ops_:
+        for r in dist.batch_isend_irecv(ops_):
+            r.wait()
+    return [t.to(device) for t in out]
+
+
+class HaloPlan:
+    """Halo-only exchange of B, built once per graph from this rank's
+    column indices: each rank receives only the B rows its rows reference, from their owners
+    (BalancedSplitter(K, G) shards), and sends the rows its peers asked for.
+
+    Compact B layout on this rank: [own shard rows (K_r) | rows from peer p, p ascending, each
+    block in ascending global row order].  `cols` = the column indices remapped into it.  The
+    SpMM reads B rows from wherever they live, so the result bits are those of the all-gather.
+    """
+
+    def __init__(self, col_idx: torch.Tensor, k: int, world: int, rank: int, group, device):
+        lo, hi = balanced_range(k, world, rank)
+        self.k_own = hi - lo
+        starts = torch.tensor([balanced_range(k, world, r)[0] for r in range(world)],
+                              dtype=torch.int64, device=col_idx.device)
+        c = col_idx.to(torch.int64)
+        uniq = torch.unique(c)  # sorted
+        owner = torch.searchsorted(starts, uniq, right=True) - 1
+        counts = torch.bincount(owner, minlength=world).cpu()
+        first = torch.zeros(world + 1, dtype=torch.int64)
+        first[1:] = torch.cumsum(counts, 0)
+        need = [uniq[first[p]:first[p + 1]] for p in range(world)]
+        need[rank] = need[rank][:0]
+        self.recv_counts = [int(counts[p]) if p != rank else 0 for p in range(world)]
+        roff, acc = [0] * world, 0
+        for p in range(world):
+            roff[p] = acc
+            acc += self.recv_counts[p]
+        self.recv_offsets, self.halo_rows = roff, acc
+        self.k_compact = self.k_own + acc
+        # remap every nonzero: own -> c - lo; remote from p -> K_r + roff[p] + rank within need[p]
+        pos = torch.searchsorted(uniq, c)
+        own_ = torch.searchsorted(starts, c, right=True) - 1
+        base = torch.tensor([self.k_own + roff[p] - int(first[p]) for p in range(world)],
+                            dtype=torch.int64, device=c.device)
+        remote = base[own_] + pos
+        self.cols = torch.where(own_ == rank, c - lo, remote).to(col_idx.dtype)
+        # what my peers need from me: their lists, as rows of my shard
+        asked = _exchange_lists(need, group, device)
+        self.send_counts = [int(t.numel()) if p != rank else 0 for p, t in enumerate(asked)]
+        soff, acc = [0] * world, 0
+        for p in range(world):
+            soff[p] = acc
+            acc += self.send_counts[p]
+        self.send_offsets, self.send_rows = soff, acc
+        parts = [asked[p] - lo for p in range(world) if p != rank and asked[p].numel()]
+        self.send_idx = (torch.cat(parts) if parts else torch.zeros(0, dtype=torch.int64)).to(device)
+        as_c = lambda v: (ctypes.c_int64 * world)(*v)  # noqa: E731
+        self._c = (as_c(self.send_counts), as_c(self.send_offsets), as_c(self.recv_counts),
+                   as_c(self.recv_offsets))
+        self.remote_rows_total = k - self.k_own
+
+
 class RowSplitSpmm:
     """out[rows of this rank] = A[rows of this rank, :] @ all_gather(b shards).
 
@@ -81,6 +159,9 @@ class RowSplitSpmm:
         if self.device.type == "cuda":
             self.comm_stream = torch.cuda.Stream(self.device)
         self.gathered = None
+        self.halo = None
+        self.exchange = "allgather"
+        self._bound = None
         self.set_pipeline(pipeline)
         if comm.startswith("rccl"):
             self._init_rccl()
@@ -124,6 +205,8 @@ class RowSplitSpmm:
         r0 = self.rank * self.pad
         for c in range(self.chunks):
             self.gathered[c, r0:r0 + (hi - lo)].copy_(b_shard[:, c * self.nc:(c + 1) * self.nc])
+        if self.halo is not None:
+            self.compact[: self.halo.k_own].copy_(b_shard)
 
     def shard(self) -> torch.Tensor:
         lo, hi = self.k_range
@@ -234,36 +317,161 @@ class RowSplitSpmm:
             events[2].record()
         return out
 
+    # -- bound form: this rank's CSR once, every exchange layout prepared ------------------------
+    def bind(self, row_ptr, col_idx, values, halo: bool = True):
+        """Binds this rank's CSR (`col_idx` in global B row ids; the local slice, or the full CSR
+        when local_csr=False).  Remaps the columns for the all-gather layout and, with halo=True,
+        builds the halo plan; `step()` then runs whichever exchange is selected."""
+        cols = {"allgather": self.remap_columns(col_idx)}
+        if halo:
+            if self.local_csr:
+                mine = col_idx
+            else:
+                lo, hi = self.row_range
+                j0, j1 = int(row_ptr[lo]), int(row_ptr[hi])
+                mine = col_idx[j0:j1]
+            self.halo = HaloPlan(mine, self.k, self.world, self.rank, self.group, self.device)
+            hc = self.halo.cols
+            if not self.local_csr:  # full-length array, entries outside this rank's rows unused
+                full = torch.zeros_like(col_idx)
+                full[j0:j1] = hc
+                hc = full
+            cols["halo"] = hc
+            self.compact = torch.zeros((self.halo.k_compact, self.n), dtype=self.dtype,
+                                       device=self.device)
+            self.send_buf = torch.empty((self.halo.send_rows, self.n), dtype=self.dtype,
+                                        device=self.device)
+            rows_local = self.row_range[1] - self.row_range[0]
+            self.halo_kernel = None
+            if self.device.type == "cuda":
+                self.halo_kernel = ops.SpmmCsrKernel(rows_local if self.local_csr else self.m,
+                                                     self.halo.k_compact, self.n, col_idx.numel(),
+                                                     self.idx_dtype, self.dtype, self.device,
+                                                     self.options)
+            self.compact[: self.halo.k_own].copy_(self.shard())
+        self._bound = (row_ptr, cols, values)
+
+    def halo_exchange(self, b_shard=None):
+        """Pack the rows each peer asked for, then grouped send/recv into the compact buffer."""
+        h = self.halo
+        if b_shard is not None:
+            self.compact[: h.k_own].copy_(b_shard)
+        if self.comm_kind == "torch":
+            if h.send_rows:
+                torch.index_select(self.compact, 0, h.send_idx, out=self.send_buf)
+            reqs = []
+            for p in range(self.world):
+                gp = dist.get_global_rank(self.group, p) if self.group else p
+                if h.send_counts[p]:
+                    o = h.send_offsets[p]
+                    reqs.append(dist.P2POp(dist.isend, self.send_buf[o:o + h.send_counts[p]], gp, self.group))
+                if h.recv_counts[p]:
+                    o = h.k_own + h.recv_offsets[p]
+                    reqs.append(dist.P2POp(dist.irecv, self.compact[o:o + h.recv_counts[p]], gp, self.group))
+            if reqs:
+                for r in dist.batch_isend_irecv(reqs):
+                    r.wait()
+            return
+        s = current_stream_handle(self.compact)
+        esz = self.compact.element_size()
+        if h.send_rows:
+            check(LIB.ofx_gather_rows(s, dtype_code(torch.int64), h.send_rows, self.n * esz,
+                                      h.send_idx.data_ptr(), self.compact.data_ptr(),
+                                      self.compact.stride(0) * esz, self.send_buf.data_ptr(),
+                                      self.send_buf.stride(0) * esz), "gather_rows")
+        sc, so, rc, ro = h._c
+        check(LIB.ofx_exchange_rows(s, self._comm, dtype_code(self.dtype), self.n,
+                                    self.send_buf.data_ptr() if h.send_rows else None, sc, so,
+                                    self.compact.data_ptr() + h.k_own * self.n * esz, rc, ro),
+              "exchange_rows")
+
+    def halo_compute(self, out):
+        row_ptr, cols, values = self._bound
+        lo, hi = self.row_range
+        rb, re = (0, hi - lo) if self.local_csr else (lo, hi)
+        if self.halo_kernel is not None:
+            self.halo_kernel(row_ptr, cols["halo"], values, self.compact, out, rb, re)
+        else:
+            m_kernel = hi - lo if self.local_csr else self.m
+            ops.spmm_csr_cpu(row_ptr, cols["halo"], values, self.compact, m_kernel,
+                             self.halo.k_compact, out=out, row_begin=rb, row_end=re,
+                             options=self.options)
+        return out
+
+    def step(self, out, b_shard=None, events=None):
+        """One exchange + local SpMM over the bound CSR with the selected exchange."""
+        row_ptr, cols, values = self._bound
+        if self.exchange == "halo":
+            if events:
+                events[0].record()
+            self.halo_exchange(b_shard)
+            if events:
+                events[1].record()
+            self.halo_compute(out)
+            if events:
+                events[2].record()
+            return out
+        if b_shard is not None:
+            self.load_shard(b_shard)
+        return self(row_ptr, cols["allgather"], values, out=out, events=events)
+
+    def gather_phase(self):
+        """The exchange alone (phase timing)."""
+        if self.exchange == "halo":
+            self.halo_exchange()
+        else:
+            self.all_gather_b()
+
+    def compute_phase(self, out):
+        """The local SpMM alone with the exchanged B resident (phase timing)."""
+        if self.exchange == "halo":
+            return self.halo_compute(out)
+        row_ptr, cols, values = self._bound
+        return self.compute(row_ptr, cols["allgather"], values, out)
+
     # -- schedule choice -------------------------------------------------------------------------
-    def tune(self, row_ptr, col_idx, values, out, pipelines=(1, 2, 4), reps: int = 3,
-             force: bool = False) -> dict:
-        """Times every (all-gather schedule, pipeline depth) on this node with the real step and
-        keeps the fastest.  Timings are max-reduced over ranks, so all ranks choose the same.
-        Every candidate produces the same bytes.  Returns {"<comm>/p<C>": ms}.  One rank has
-        nothing to gather, so it keeps its setting unless `force` (tests)."""
+    def tune(self, out, pipelines=(1, 2, 4), reps: int = 3, force: bool = False) -> dict:
+        """Times every exchange on this node with the real step over the bound CSR: all-gather
+        (ring / point-to-point) x pipeline depth, and the halo exchange if built.  Keeps the
+        fastest.  Timings are max-reduced over ranks, so all ranks choose the same; every
+        candidate produces the same bytes.  Returns {"<comm>/p<C>" | "halo": ms}.  One rank has
+        nothing to exchange, so it keeps its setting unless `force` (tests)."""
+        if self._bound is None:
+            raise RuntimeError("tune: bind() the CSR first")
         if not self.comm_kind.startswith("rccl") or (self.world == 1 and not force):
             return {}
+
+        def measure():
+            self.step(out)
+            torch.cuda.synchronize(self.device)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                self.step(out)
+            e1.record()
+            torch.cuda.synchronize(self.device)
+            t = torch.tensor([e0.elapsed_time(e1) / reps], dtype=torch.float64, device=self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            return float(t.item())
+
         times = {}
+        self.exchange = "allgather"
         for chunks in pipelines:
             if self.n % chunks:
                 continue
             self.set_pipeline(chunks)
             for kind in ("rccl", "rccl-p2p"):
                 self.comm_kind = kind
-                self(row_ptr, col_idx, values, out=out)
-                torch.cuda.synchronize(self.device)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(reps):
-                    self(row_ptr, col_idx, values, out=out)
-                e1.record()
-                torch.cuda.synchronize(self.device)
-                t = torch.tensor([e0.elapsed_time(e1) / reps], dtype=torch.float64,
-                                 device=self.device)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-                times[f"{kind}/p{chunks}"] = float(t.item())
+                times[f"{kind}/p{chunks}"] = measure()
+        if self.halo is not None:
+            self.exchange, self.comm_kind = "halo", "rccl"
+            times["halo"] = measure()
         best = min(times, key=times.get)
-        kind, p = best.split("/p")
-        self.comm_kind = kind
-        self.set_pipeline(int(p))
+        if best == "halo":
+            self.exchange, self.comm_kind = "halo", "rccl"
+            self.set_pipeline(1)
+        else:
+            kind, p = best.split("/p")
+            self.exchange, self.comm_kind = "allgather", kind
+            self.set_pipeline(int(p))
         return times

@@ -1,6 +1,7 @@
 """CPU multi-process (gloo) tests of the row-split wrapper: BalancedSplitter rows, padded in-place
 all-gather of the Split(0) dense shards, column remap, local SpMM — bit-exact against the
-oracle's full product.  The same code path runs RCCL on GPUs (comm="rccl")."""
+oracle's full product; column-block pipelining; the halo-only exchange (bound form).  The same
+code path runs RCCL on GPUs (comm="rccl")."""
 import os
 import socket
 
@@ -60,6 +61,19 @@ def _worker(rank, world, port, m, k, n, local_csr, pipeline, density, q):
         out2 = rs(lrp, rs.remap_columns(lci), lv, b_shard=b2[klo:khi])
         full2 = oracle.spmm(rp.numpy(), ci.numpy(), v.numpy(), b2.numpy())
         ok = ok and np.array_equal(out2.numpy().view(np.uint32), full2[lo:hi].view(np.uint32))
+        # the bound form with the halo-only exchange: same bytes
+        rs.bind(lrp, lci, lv, halo=True)
+        h = rs.halo
+        ok = ok and h.k_compact == (khi - klo) + h.halo_rows and h.halo_rows <= k - (khi - klo)
+        rs.exchange = "halo"
+        out3 = torch.full_like(out2, float("nan"))
+        rs.step(out3, b_shard=b[klo:khi])
+        ok = ok and np.array_equal(out3.numpy().view(np.uint32), full[lo:hi].view(np.uint32))
+        # every halo row holds the B row it stands for
+        uniq = torch.unique((lci if local_csr else lci[int(lrp[lo]):int(lrp[hi])]).long())
+        ok = ok and torch.equal(rs.compact[: h.k_own], b[klo:khi])
+        remote = uniq[(uniq < klo) | (uniq >= khi)]
+        ok = ok and torch.equal(rs.compact[h.k_own:], b[remote])
         q.put((rank, bool(ok)))
     finally:
         dist.destroy_process_group()
@@ -95,3 +109,55 @@ def _run(world, m, k, n, local_csr, pipeline, density):
     results = dict(q.get(timeout=5) for _ in range(world))
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert results == {r: True for r in range(world)}, results
+
+
+def _banded_worker(rank, world, port, q):
+    """A graph with locality (every row references columns within +-w of itself): the halo
+    exchange moves only the band edges instead of the whole B."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    import sys
+    for p in (root, os.path.join(root, "of-spmm_amd")):
+        sys.path.insert(0, p)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oneflow_spmm import ops
+        from oneflow_spmm.distributed import RowSplitSpmm
+        from oracle import oracle
+        m = k = 3000
+        n, w = 32, 20
+        rng = np.random.default_rng(77)
+        rows = [np.unique(np.clip(r + rng.integers(-w, w + 1, size=8), 0, k - 1)) for r in range(m)]
+        rp = torch.tensor(np.concatenate([[0], np.cumsum([len(x) for x in rows])]), dtype=torch.int32)
+        ci = torch.tensor(np.concatenate(rows), dtype=torch.int32)
+        v = torch.from_numpy(rng.uniform(-1, 1, ci.numel()).astype(np.float32))
+        b = torch.from_numpy(rng.uniform(-1, 1, (k, n)).astype(np.float32))
+        full = oracle.spmm(rp.numpy(), ci.numpy(), v.numpy(), b.numpy())
+        lo, hi = oracle.balanced_range(m, world, rank)
+        lrp, n0, n1 = ops.csr_row_slice(rp, lo, hi)
+        rs = RowSplitSpmm(m, k, n, n1 - n0, torch.float32, torch.int32, "cpu")
+        klo, khi = rs.k_range
+        rs.load_shard(b[klo:khi])
+        rs.bind(lrp, ci[n0:n1], v[n0:n1], halo=True)
+        rs.exchange = "halo"
+        out = rs.step(torch.empty((hi - lo, n)))
+        ok = np.array_equal(out.numpy().view(np.uint32), full[lo:hi].view(np.uint32))
+        ok = ok and 0 < rs.halo.halo_rows <= 2 * w * (world - 1)
+        q.put((rank, bool(ok), rs.halo.halo_rows))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_halo_exchange_moves_only_the_band_edges(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_banded_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    res = [q.get(timeout=5) for _ in range(world)]
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(ok for _, ok, _ in res), res

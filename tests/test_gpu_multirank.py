@@ -37,32 +37,35 @@ def _worker(rank, world, port, kind, rp, ci, v, b, q):
         m, k, n = rp.numel() - 1, b.shape[0], b.shape[1]
         try:
             rs = RowSplitSpmm(m, k, n, ci.numel(), torch.float32, torch.int32, device,
-                              comm="rccl" if kind == "tune" else kind, local_csr=False)
+                              comm="rccl" if kind in ("tune", "halo") else kind, local_csr=False)
         except Exception as e:  # OfxError(OFX_ECOMM) when RCCL rejects the layout
             q.put((rank, "skip", str(e)))
             dist.destroy_process_group()
             return
         lo, hi = rs.k_range
         rs.load_shard(b[lo:hi].to(device))
-        d_rp, d_ci, d_v = rp.to(device), rs.remap_columns(ci.to(device)), v.to(device)
         out = torch.empty((rs.row_range[1] - rs.row_range[0], n), device=device)
-        times = rs.tune(d_rp, d_ci, d_v, out, reps=2) if kind == "tune" else {}
-        if kind == "tune":  # re-lay out: clear the foreign slots, so the step must gather them
-            rs.set_pipeline(rs.chunks)
-            sh = rs.shard()
-            rs.gathered.zero_()
-            rs.load_shard(sh)
+        rs.bind(rp.to(device), ci.to(device), v.to(device), halo=kind in ("tune", "halo"))
+        if kind == "halo":
+            rs.exchange = "halo"
+        times = rs.tune(out, reps=2) if kind == "tune" else {}
+        # clear everything received, so the checked step must exchange it again
+        sh = rs.shard()
+        rs.gathered.zero_()
+        if rs.halo is not None:
+            rs.compact.zero_()
+        rs.load_shard(sh)
         out.zero_()
-        out = rs(d_rp, d_ci, d_v, out=out)
+        rs.step(out)
         torch.cuda.synchronize()
-        q.put((rank, "ok", (rs.row_range, out.cpu(), rs.comm_kind, times)))
+        q.put((rank, "ok", (rs.row_range, out.cpu(), (rs.exchange, rs.comm_kind, rs.chunks), times)))
         rs.close()
         dist.destroy_process_group()
     except Exception:
         q.put((rank, "err", traceback.format_exc()))
 
 
-@pytest.mark.parametrize("kind", ["rccl", "rccl-p2p", "tune"])
+@pytest.mark.parametrize("kind", ["rccl", "rccl-p2p", "halo", "tune"])
 def test_row_split_two_ranks(kind):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -96,5 +99,5 @@ def test_row_split_two_ranks(kind):
         assert_bitwise(out, ref[lo:hi], f"{kind} rows [{lo},{hi})")
         kinds.add(ck)
         if kind == "tune":
-            assert {t.split("/")[0] for t in times} == {"rccl", "rccl-p2p"}
+            assert {t.split("/")[0] for t in times} == {"rccl", "rccl-p2p", "halo"}
     assert len(kinds) == 1  # every rank made the same choice

@@ -292,13 +292,16 @@ def test_row_split_rccl_single_rank(device):
             torch.cuda.synchronize()
             assert_bitwise(out2, oracle_spmm(rp, ci, v, b), f"{kind} pipeline {chunks}")
         # the setup-time choice runs every candidate step and keeps one; output stays exact
-        times = rs.tune(rp.to(device), rs.remap_columns(ci.to(device)), v.to(device), out2,
-                        reps=1, force=True)
-        assert len(times) == 6 and f"{rs.comm_kind}/p{rs.chunks}" in times
-        out2.fill_(float("nan"))
-        rs(rp.to(device), rs.remap_columns(ci.to(device)), v.to(device), out=out2)
-        torch.cuda.synchronize()
-        assert_bitwise(out2, oracle_spmm(rp, ci, v, b), "after tune")
+        rs.bind(rp.to(device), ci.to(device), v.to(device), halo=True)
+        assert rs.halo.halo_rows == 0 and rs.halo.k_compact == k  # one rank owns every row
+        times = rs.tune(out2, reps=1, force=True)
+        assert len(times) == 7 and "halo" in times
+        for exchange in ("allgather", "halo"):
+            rs.exchange = exchange
+            out2.fill_(float("nan"))
+            rs.step(out2)
+            torch.cuda.synchronize()
+            assert_bitwise(out2, oracle_spmm(rp, ci, v, b), f"after tune, {exchange}")
         rs.close()
     finally:
         dist.destroy_process_group()
