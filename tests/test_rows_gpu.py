@@ -1,0 +1,42 @@
+"""ofx_gather_rows (the halo pack kernel, csrc/rows.hip): dst[i] = src[idx[i]] byte-exact against
+torch.index_select, for 16-B, 4-B and 1-B word paths, strided rows and both index dtypes."""
+import numpy as np
+import pytest
+import torch
+
+from oneflow_spmm._C import current_stream_handle, dtype_code
+from oneflow_spmm._lib import LIB, check
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("idx_dtype", [torch.int32, torch.int64])
+@pytest.mark.parametrize("n,dtype,pad", [(128, torch.float32, 0), (3, torch.float32, 0),
+                                         (7, torch.bfloat16, 0), (64, torch.float32, 5),
+                                         (1, torch.bfloat16, 3), (300, torch.float64, 0)])
+def test_gather_rows_matches_index_select(device, idx_dtype, n, dtype, pad):
+    rng = np.random.default_rng(n + pad)
+    k, count = 5000, 3333
+    src_full = torch.from_numpy(rng.standard_normal((k, n + pad))).to(dtype).to(device)
+    src = src_full[:, :n]
+    idx = torch.from_numpy(rng.integers(0, k, count)).to(idx_dtype).to(device)
+    dst_full = torch.full((count, n + pad), 7, dtype=dtype, device=device)
+    dst = dst_full[:, :n]
+    esz = src.element_size()
+    check(LIB.ofx_gather_rows(current_stream_handle(src), dtype_code(idx_dtype), count, n * esz,
+                              idx.data_ptr(), src.data_ptr(), src.stride(0) * esz, dst.data_ptr(),
+                              dst.stride(0) * esz), "gather_rows")
+    torch.cuda.synchronize()
+    want = torch.index_select(src, 0, idx.long())
+    assert torch.equal(dst.contiguous().view(torch.uint8), want.contiguous().view(torch.uint8))
+    if pad:
+        assert (dst_full[:, n:] == 7).all()  # row padding untouched
+
+
+def test_gather_rows_empty_and_errors(device):
+    x = torch.zeros(4, 4, device=device)
+    check(LIB.ofx_gather_rows(None, dtype_code(torch.int64), 0, 16, None, None, 16, None, 16), "empty")
+    assert LIB.ofx_gather_rows(None, dtype_code(torch.float32), 1, 16, x.data_ptr(), x.data_ptr(),
+                               16, x.data_ptr(), 16) != 0
+    assert LIB.ofx_gather_rows(None, dtype_code(torch.int64), 1, 32, x.data_ptr(), x.data_ptr(),
+                               16, x.data_ptr(), 16) != 0  # stride < row
