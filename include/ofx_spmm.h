@@ -240,6 +240,21 @@ int ofx_allgather(void* stream, const void* in, void* out, size_t count, int dty
 /* The same all-gather as grouped point-to-point send/recv with every peer (in place: this
  * rank's slot of `buf` is the send buffer).  Same result bytes as ofx_allgather.           */
 int ofx_allgather_p2p(void* stream, void* buf, size_t count, int dtype, void* comm);
+/* One row-split step on this rank: in-place all-gather of the padded B shards
+ * in b_gathered [k_padded, n] (k_padded = ranks * P; this rank's rows already at
+ * [rank * P, rank * P + K_r)), then the local SpMM of this rank's m_local rows (row_ptr rebased
+ * to 0, columns remapped by ofx_padded_owner_remap).  `workspace` as ofx_spmm_csr for
+ * (m_local, k_padded, n, nnz_local).                                                         */
+int ofx_spmm_rowsplit(void* stream, void* comm, int idx_dtype, int val_dtype, int64_t m_local,
+                      int64_t k_padded, int64_t n, int64_t nnz_local, const void* row_ptr,
+                      const void* col_idx, const void* values, void* b_gathered, void* c,
+                      int64_t ldc, void* workspace, size_t workspace_bytes,
+                      const ofx_spmm_options* opts);
+/* Column c of B -> its row in the padded gathered buffer: c + max(owner(c) - k % world, 0)
+ * when k % world > 0, c otherwise; owner from BalancedSplitter(k, world)
+ * (oneflow/core/common/balanced_splitter.cpp:20-40).                                         */
+int ofx_padded_owner_remap(void* stream, int idx_dtype, int64_t nnz, int64_t k, int64_t world,
+                           const void* col_in, void* col_out);
 /* Halo exchange: grouped send/recv of B rows with per-peer counts, the
  * ShuffleData pattern of oneflow/user/kernels/data_shuffle_kernel.cu:119-135.  Counts and
  * offsets are in rows of n elements (host arrays, one entry per rank); this rank's entry and

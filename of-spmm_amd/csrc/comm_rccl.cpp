@@ -133,3 +133,33 @@ extern "C" int ofx_exchange_rows(void* stream, void* comm, int dtype, int64_t n,
   OFX_NCCL_CHECK(ncclGroupEnd());
   return OFX_OK;
 }
+
+// One step of the row-split operator on this rank (SURVEY.md §8b "ofx_spmm_rowsplit"): the
+// S(0) -> B boxing of b as an in-place all-gather of the padded shards (each rank has written
+// its rows at [rank * P, rank * P + K_r) of b_gathered), then the local SpMM of this rank's rows
+// (CSR slice with row_ptr rebased to 0 and columns remapped by ofx_padded_owner_remap).  The
+// same two launches RowSplitSpmm issues; stream-ordered, no host synchronisation.
+extern "C" int ofx_spmm_rowsplit(void* stream, void* comm, int idx_dtype, int val_dtype,
+                                 int64_t m_local, int64_t k_padded, int64_t n, int64_t nnz_local,
+                                 const void* row_ptr, const void* col_idx, const void* values,
+                                 void* b_gathered, void* c, int64_t ldc, void* workspace,
+                                 size_t workspace_bytes, const ofx_spmm_options* opts) {
+  OFX_REQUIRE(comm && k_padded >= 0 && n >= 0, OFX_EINVAL, "spmm_rowsplit: bad arguments");
+  int nranks = 0, rank = 0;
+  ncclComm_t cm = static_cast<ncclComm_t>(comm);
+  OFX_NCCL_CHECK(ncclCommCount(cm, &nranks));
+  OFX_NCCL_CHECK(ncclCommUserRank(cm, &rank));
+  OFX_REQUIRE(k_padded % nranks == 0, OFX_EINVAL,
+              "spmm_rowsplit: k_padded=%lld is not a multiple of %d ranks", (long long)k_padded,
+              nranks);
+  const int64_t pad = k_padded / nranks;
+  const size_t esz = (size_t)ofx::dtype_size(val_dtype);
+  if (pad * n > 0) {
+    char* slot = static_cast<char*>(b_gathered) + (size_t)(rank * pad * n) * esz;
+    const int rc = ofx_allgather(stream, slot, b_gathered, (size_t)(pad * n), val_dtype, comm);
+    if (rc) return rc;
+  }
+  return ofx_spmm_csr(stream, idx_dtype, val_dtype, m_local, k_padded, n, nnz_local, row_ptr,
+                      col_idx, values, b_gathered, n, c, ldc, 0, m_local, workspace,
+                      workspace_bytes, opts);
+}

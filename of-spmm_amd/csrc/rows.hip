@@ -90,3 +90,46 @@ extern "C" int ofx_gather_rows(void* stream, int idx_dtype, int64_t count, int64
   return dispatch(s, static_cast<const int64_t*>(idx), count, row_bytes, src, src_stride_bytes, dst,
                   dst_stride_bytes);
 }
+
+// ---- padded-owner column remap (row split) -----------------------------------
+// Column c of B lives in shard owner(c) = BalancedSplitter(k, world) and, in the padded gathered
+// buffer [world * P, n] (P = ceil(k / world)), at row c + max(owner(c) - extra, 0) where
+// extra = k % world > 0 (the first `extra` shards hold P rows, the rest P - 1, each padded to
+// P); with extra == 0 every shard holds exactly P rows and c stays.
+namespace ofx {
+namespace {
+template <typename I>
+__global__ void padded_remap_kernel(const I* __restrict__ in, I* __restrict__ out, int64_t nnz,
+                                    int64_t base, int64_t extra) {
+  const int64_t big = extra * (base + 1);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nnz; j += stride) {
+    const int64_t c = (int64_t)in[j];
+    const int64_t owner = c < big ? c / (base + 1) : extra + (c - big) / (base > 0 ? base : 1);
+    // extra == 0: P == base, every shard fills its slot, nothing moves
+    out[j] = (I)(c + (extra > 0 && owner > extra ? owner - extra : 0));
+  }
+}
+}  // namespace
+}  // namespace ofx
+
+extern "C" int ofx_padded_owner_remap(void* stream, int idx_dtype, int64_t nnz, int64_t k,
+                                      int64_t world, const void* col_in, void* col_out) {
+  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "padded_owner_remap: bad index dtype");
+  OFX_REQUIRE(nnz >= 0 && k >= 0 && world > 0, OFX_EINVAL, "padded_owner_remap: bad sizes");
+  if (nnz == 0) return OFX_OK;
+  OFX_REQUIRE(col_in && col_out, OFX_EINVAL, "padded_owner_remap: NULL pointer");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t base = k / world, extra = k % world;
+  const unsigned grid = (unsigned)std::min<int64_t>((nnz + kBlock - 1) / kBlock, 65536);
+  if (idx_dtype == OFX_DT_INT32)
+    hipLaunchKernelGGL(padded_remap_kernel<int32_t>, dim3(grid), dim3(kBlock), 0, s,
+                       static_cast<const int32_t*>(col_in), static_cast<int32_t*>(col_out), nnz,
+                       base, extra);
+  else
+    hipLaunchKernelGGL(padded_remap_kernel<int64_t>, dim3(grid), dim3(kBlock), 0, s,
+                       static_cast<const int64_t*>(col_in), static_cast<int64_t*>(col_out), nnz,
+                       base, extra);
+  OFX_HIP_CHECK(hipGetLastError());
+  return OFX_OK;
+}

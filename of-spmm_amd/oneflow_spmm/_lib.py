@@ -104,6 +104,8 @@ def _load():
         "ofx_allgather": ([p, p, p, sz, i32, p], i32),
         "ofx_allgather_p2p": ([p, p, sz, i32, p], i32),
         "ofx_exchange_rows": ([p, p, i32, i64, p, p, p, p, p, p], i32),
+        "ofx_spmm_rowsplit": ([p, p, i32, i32, i64, i64, i64, i64, p, p, p, p, p, i64, p, sz, popt], i32),
+        "ofx_padded_owner_remap": ([p, i32, i64, i64, i64, p, p], i32),
         "ofx_gather_rows": ([p, i32, i64, i64, p, p, i64, p, i64], i32),
         "ofx_synth_row_ptr": ([i64, i64, i64, ctypes.c_double, u64, p], i32),
         "ofx_synth_columns": ([i64, i64, ctypes.c_double, u64, p, i64, i64, i32, p, i32], i32),

@@ -214,7 +214,17 @@ class RowSplitSpmm:
         return torch.cat([self.gathered[c, r0:r0 + (hi - lo)] for c in range(self.chunks)], dim=1)
 
     def remap_columns(self, col_idx: torch.Tensor) -> torch.Tensor:
-        return padded_owner_remap(col_idx, self.k, self.world)
+        """Global B row ids -> rows of the padded gathered buffer (HIP kernel on the device)."""
+        if col_idx.device.type != "cuda":
+            return padded_owner_remap(col_idx, self.k, self.world)
+        col_idx = col_idx.contiguous()
+        out = torch.empty_like(col_idx)
+        check(LIB.ofx_padded_owner_remap(current_stream_handle(col_idx), dtype_code(col_idx.dtype),
+                                         col_idx.numel(), self.k, self.world,
+                                         col_idx.data_ptr() if col_idx.numel() else None,
+                                         out.data_ptr() if col_idx.numel() else None),
+              "padded_owner_remap")
+        return out
 
     # -- communicator (EagerNcclCommMgr::CreateNcclComm pattern: rank 0 makes the id) --------
     def _init_rccl(self):
@@ -291,6 +301,21 @@ class RowSplitSpmm:
         if b_shard is not None:
             self.load_shard(b_shard)
         pipelined = self.chunks > 1 and self.comm_stream is not None and self.comm_kind != "torch"
+        if (not pipelined and not events and self.chunks == 1 and self.comm_kind == "rccl"
+                and self.local_csr and self.kernel is not None):
+            # the whole step in one C-ABI call: in-place all-gather + local SpMM
+            kern = self.kernel
+            blk = self.gathered[0]
+            check(LIB.ofx_spmm_rowsplit(current_stream_handle(blk), self._comm, kern.idx_dt,
+                                        kern.val_dt, hi - lo, self.k_padded, self.n, kern.nnz,
+                                        row_ptr.data_ptr(),
+                                        col_idx.data_ptr() if col_idx.numel() else None,
+                                        values.data_ptr() if values.numel() else None,
+                                        blk.data_ptr(), out.data_ptr(), out.stride(0),
+                                        kern.workspace.data_ptr(), kern.ws_bytes,
+                                        ctypes.byref(kern.options) if kern.options else None),
+                  "spmm_rowsplit")
+            return out
         if events:
             events[0].record()
         if not pipelined:

@@ -40,3 +40,17 @@ def test_gather_rows_empty_and_errors(device):
                                16, x.data_ptr(), 16) != 0
     assert LIB.ofx_gather_rows(None, dtype_code(torch.int64), 1, 32, x.data_ptr(), x.data_ptr(),
                                16, x.data_ptr(), 16) != 0  # stride < row
+
+
+@pytest.mark.parametrize("k,world", [(2449029, 8), (999, 2), (1000, 4), (7, 3), (5, 8)])
+@pytest.mark.parametrize("idx_dtype", [torch.int32, torch.int64])
+def test_device_padded_remap_matches_host(device, k, world, idx_dtype):
+    from oneflow_spmm.distributed import padded_owner_remap
+    rng = np.random.default_rng(k)
+    col = torch.from_numpy(rng.integers(0, k, 20000)).to(idx_dtype)
+    out = torch.empty_like(col, device=device)
+    d = col.to(device)
+    check(LIB.ofx_padded_owner_remap(None, dtype_code(idx_dtype), col.numel(), k, world,
+                                     d.data_ptr(), out.data_ptr()), "remap")
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), padded_owner_remap(col, k, world))
