@@ -311,6 +311,22 @@ def main():
         result["extra"]["cpu_1thread"] = {
             "value": round(2.0 * float(rp_np[r1]) * n / t_1 / 1e9, 3), "unit": "GFLOP/s", "cores": 1,
             "sample": f"rows [0,{r1}) = {int(rp_np[r1])} nnz, one run ({t_1:.1f} s)"}
+        # the operator's own DeviceType::kCPU kernel (SURVEY.md §8d's a2), same threads, through
+        # the op layer on host tensors; bit-identical to the GPU result by contract
+        h_rp = torch.from_numpy(rp_full.astype(np.int32))
+        h_ci, h_b = torch.from_numpy(cols), synth.dense(0, k, n, dt)
+        h_out = torch.empty((m, n), dtype=dt)
+        fs.spmm_csr(h_rp, h_ci, vals, m, k, h_b, out=h_out, num_threads=threads)
+        reps2, t_a2 = 0, 0.0
+        while t_a2 < 5.0 and reps2 < 3:
+            t1 = time.perf_counter()
+            fs.spmm_csr(h_rp, h_ci, vals, m, k, h_b, out=h_out, num_threads=threads)
+            t_a2 += time.perf_counter() - t1
+            reps2 += 1
+        result["extra"]["cpu_op_kernel"] = {
+            "value": round(flops * reps2 / t_a2 / 1e9, 3), "unit": "GFLOP/s", "cores": threads,
+            "sample": f"full workload x{reps2} runs ({t_a2:.1f} s), ofx_spmm_csr_cpu via the op layer",
+            "bitexact_vs_gpu": bool(torch.equal(h_out.view(torch.uint8), out.cpu().view(torch.uint8)))}
     if rank == 0:
         print(json.dumps(result), file=out_stream, flush=True)
     if rowsplit:
