@@ -83,6 +83,7 @@ def _worker(rank, world, port, m, k, n, local_csr, pipeline, density, q):
     (2, 301, 257, 16, True),    # K % G != 0 -> padded shards + remap
     (2, 300, 256, 32, False),   # full CSR broadcast, kernel computes the row range
     (3, 500, 400, 8, True),
+    (4, 603, 1001, 16, True),   # 4 ranks: K % 4 = 1, one long shard and three short ones
 ])
 def test_row_split_gloo(world, m, k, n, local_csr):
     _run(world, m, k, n, local_csr, 1, 30)
@@ -148,7 +149,7 @@ def _banded_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_halo_exchange_moves_only_the_band_edges(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
