@@ -1,0 +1,64 @@
+/* A plain-C host of the C-ABI (include/ofx_spmm.h), as a non-Python caller (cgo / JNI / a C++
+ * framework) would bind it: CPU kernel, fused epilogue, balanced ranges, row slices, error
+ * reporting.  Built and run by tests/test_native_abi.py with gcc; no GPU needed. */
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "ofx_spmm.h"
+
+static int fails = 0;
+#define EXPECT(c)                                              \
+  do {                                                         \
+    if (!(c)) {                                                \
+      fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c); \
+      ++fails;                                                 \
+    }                                                          \
+  } while (0)
+
+int main(void) {
+  /* A = [[1, 0, 2], [0, 3, 0]] (CSR), B = [[1, 0], [0, 1], [1, 1]] */
+  const int32_t rp[3] = {0, 2, 3};
+  const int32_t col[3] = {0, 2, 1};
+  const float val[3] = {1.f, 2.f, 3.f};
+  const float b[6] = {1.f, 0.f, 0.f, 1.f, 1.f, 1.f};
+  float c[4];
+  memset(c, 0xff, sizeof(c));
+  EXPECT(ofx_spmm_csr_cpu(1, OFX_DT_INT32, OFX_DT_FLOAT, 2, 3, 2, 3, rp, col, val, b, 2, c, 2, 0, 2,
+                          NULL) == OFX_OK);
+  EXPECT(c[0] == 3.f && c[1] == 2.f && c[2] == 0.f && c[3] == 3.f);
+
+  /* fused: relu(A @ B + bias), bias = [-3, -1] -> [[0, 1], [0, 2]]; -0 -> +0 */
+  const float bias[2] = {-3.f, -1.f};
+  EXPECT(ofx_spmm_csr_fused_cpu(1, OFX_DT_INT32, OFX_DT_FLOAT, 2, 3, 2, 3, rp, col, val, b, 2, c, 2,
+                                0, 2, bias, OFX_ACT_RELU, NULL) == OFX_OK);
+  EXPECT(c[0] == 0.f && !signbit(c[0]) && c[1] == 1.f && c[2] == 0.f && c[3] == 2.f);
+
+  /* one row of the global form: row range [1, 2) into a 1-row output */
+  float c1[2] = {0, 0};
+  EXPECT(ofx_spmm_csr_cpu(1, OFX_DT_INT32, OFX_DT_FLOAT, 2, 3, 2, 3, rp, col, val, b, 2, c1, 2, 1, 2,
+                          NULL) == OFX_OK);
+  EXPECT(c1[0] == 0.f && c1[1] == 3.f);
+
+  /* BalancedSplitter(10, 4): 3, 3, 2, 2 */
+  int64_t lo, hi;
+  EXPECT(ofx_balanced_range(10, 4, 1, &lo, &hi) == OFX_OK && lo == 3 && hi == 6);
+  EXPECT(ofx_balanced_range(10, 4, 3, &lo, &hi) == OFX_OK && lo == 8 && hi == 10);
+
+  /* row slice of the CSR: rows [1, 2) -> row_ptr [0, 1], nnz range [2, 3) */
+  int32_t out_rp[2];
+  int64_t n0, n1;
+  EXPECT(ofx_csr_row_slice_host(OFX_DT_INT32, rp, 1, 2, out_rp, &n0, &n1) == OFX_OK);
+  EXPECT(out_rp[0] == 0 && out_rp[1] == 1 && n0 == 2 && n1 == 3);
+
+  /* errors: a status code plus a thread-local message, never an abort */
+  EXPECT(ofx_spmm_csr_cpu(1, OFX_DT_FLOAT, OFX_DT_FLOAT, 2, 3, 2, 3, rp, col, val, b, 2, c, 2, 0, 2,
+                          NULL) == OFX_EUNSUPPORTED);
+  EXPECT(strlen(ofx_last_error()) > 0);
+  EXPECT(ofx_spmm_csr_cpu(1, OFX_DT_INT32, OFX_DT_FLOAT, 2, 3, 2, 3, rp, col, val, b, 1, c, 2, 0, 2,
+                          NULL) == OFX_EINVAL); /* ldb < n */
+  EXPECT(ofx_spmm_default_split(128) == 512);
+
+  printf("%s %d failures\n", fails ? "FAIL" : "OK", fails);
+  return fails ? 1 : 0;
+}
