@@ -327,6 +327,21 @@ def main():
             "value": round(flops * reps2 / t_a2 / 1e9, 3), "unit": "GFLOP/s", "cores": threads,
             "sample": f"full workload x{reps2} runs ({t_a2:.1f} s), ofx_spmm_csr_cpu via the op layer",
             "bitexact_vs_gpu": bool(torch.equal(h_out.view(torch.uint8), out.cpu().view(torch.uint8)))}
+        del h_rp, h_ci, h_b, h_out
+        # BASELINE configs[0]: the Cora-shaped problem on the OneFlow CPU op path (plumbing)
+        cc = synth.CONFIGS["cora"]
+        c_rp, c_ci, c_v = synth.csr(cc["m"], cc["k"], cc["nnz"], threads=threads)
+        c_b = synth.dense(0, cc["k"], cc["n"], cc["dtype"])
+        cora = {}
+        for nt in (1, threads):
+            fs.spmm_csr(c_rp, c_ci, c_v, cc["m"], cc["k"], c_b, num_threads=nt)
+            ts = []
+            for _ in range(50):
+                t1 = time.perf_counter()
+                fs.spmm_csr(c_rp, c_ci, c_v, cc["m"], cc["k"], c_b, num_threads=nt)
+                ts.append(time.perf_counter() - t1)
+            cora[f"ms_{nt}_threads"] = round(float(np.median(ts)) * 1e3, 4)
+        result["extra"]["cora_cpu_op_path"] = cora
     if rank == 0:
         print(json.dumps(result), file=out_stream, flush=True)
     if rowsplit:
