@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--split", type=int, default=0)
     ap.add_argument("--heavy", type=int, default=0, help="0 default, <0 off")
     ap.add_argument("--n", type=int, default=0, help="override the dense width")
+    ap.add_argument("--share-out", action="store_true",
+                    help="one output buffer for all variants (papers scale); identity by checksum")
     args = ap.parse_args()
     from oneflow_spmm import ops, synth
     from bench import alg_bytes
@@ -55,21 +57,31 @@ def main():
             vv, _, h = name.lstrip("f").partition("h")
             opts = ops.make_options(variant=int(vv), split=args.split, heavy=int(h) if h else args.heavy)
         kernels[name] = ops.SpmmCsrKernel(m, k, n, nnz, torch.int32, dt, dev, opts)
-        outs[name] = torch.empty((m, n), dtype=dt, device=dev)
+        if args.share_out and outs:
+            outs[name] = next(iter(outs.values()))
+        else:
+            outs[name] = torch.empty((m, n), dtype=dt, device=dev)
     times = {name: [] for name in kernels}
+    sums = {}
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for r in range(args.rounds):
         for name, kern in kernels.items():
             epi = dict(bias=bias, relu=True) if fused[name] else {}
             kern(rp, ci, v, b, outs[name], **epi)  # warm
             torch.cuda.synchronize()
+            if args.share_out and r == 0:
+                sums[name] = int(outs[name].view(torch.int32).sum(dtype=torch.int64).item())
             e0.record()
             for _ in range(args.reps):
                 kern(rp, ci, v, b, outs[name], **epi)
             e1.record()
             torch.cuda.synchronize()
             times[name].append(e0.elapsed_time(e1) / args.reps)
-        if r == 0:
+        if r == 0 and args.share_out:
+            first = next(iter(sums.values()))
+            for name, cs in sums.items():
+                print(f"[ab] {name}: checksum equal to first variant: {cs == first}", flush=True)
+        elif r == 0:
             ref = outs[next(iter(outs))]
             for name, o in outs.items():
                 if fused[name]:
