@@ -349,6 +349,7 @@ struct Launch {
   size_t ws_bytes;
   const void* bias;  // fused epilogue (T[n] or NULL) and OFX_ACT_*
   int act;
+  int64_t b_rows;  // k: rows of B (cache-footprint choice of load hints)
 };
 
 int pick_vec(int elem_bytes, const Launch& L, int forced_vec) {
@@ -413,14 +414,22 @@ int launch_cfg(const Launch& L) {
   return OFX_OK;
 }
 
+// B far larger than the Infinity Cache (> 1 GiB): the col/val/C streams are loaded and stored
+// non-temporally so they do not evict the hot (hub) B rows that still hit on-die.  Measured
+// (scripts/ab.py, bit-identical): papers-scale -1.8%, products -0.3%; with B at cache size
+// (1M power-law, 256 MB) the same hint costs +8%, hence the threshold.
+constexpr int64_t kNtBytes = int64_t(1) << 30;
+
 template <typename T, typename I, int VEC>
-int launch_vec(const Launch& L, int lpr) {
+int launch_vec(const Launch& L, int lpr, bool nt) {
   switch (lpr) {
     case 4: return launch_cfg<T, I, Cfg<VEC, 4>>(L);
     case 8: return launch_cfg<T, I, Cfg<VEC, 8>>(L);
     case 16: return launch_cfg<T, I, Cfg<VEC, 16>>(L);
-    case 32: return launch_cfg<T, I, Cfg<VEC, 32>>(L);
-    case 64: return launch_cfg<T, I, Cfg<VEC, 64>>(L);
+    case 32:
+      return nt ? launch_cfg<T, I, Cfg<VEC, 32, 8, 4, true>>(L) : launch_cfg<T, I, Cfg<VEC, 32>>(L);
+    case 64:
+      return nt ? launch_cfg<T, I, Cfg<VEC, 64, 8, 4, true>>(L) : launch_cfg<T, I, Cfg<VEC, 64>>(L);
     default: return fail(OFX_EINVAL, "spmm_csr: unsupported lanes-per-row %d", lpr);
   }
 }
@@ -464,14 +473,15 @@ int launch_typed(const Launch& L) {
               "spmm_csr: variant %d not applicable (n=%lld ldb=%lld ldc=%lld or pointer alignment)",
               L.sched.variant, (long long)L.n, (long long)L.ldb, (long long)L.ldc);
   const int lpr = forced_lpr ? forced_lpr : pick_lpr(L.n, vec);
+  const bool nt = (L.b_rows * L.ldb * (int64_t)sizeof(T)) > kNtBytes;
   switch (vec) {
-    case 1: return launch_vec<T, I, 1>(L, lpr);
-    case 2: return launch_vec<T, I, 2>(L, lpr);
+    case 1: return launch_vec<T, I, 1>(L, lpr, nt);
+    case 2: return launch_vec<T, I, 2>(L, lpr, nt);
     case 4:
-      if constexpr (sizeof(T) <= 4) return launch_vec<T, I, 4>(L, lpr);
+      if constexpr (sizeof(T) <= 4) return launch_vec<T, I, 4>(L, lpr, nt);
       break;
     case 8:
-      if constexpr (sizeof(T) == 2) return launch_vec<T, I, 8>(L, lpr);
+      if constexpr (sizeof(T) == 2) return launch_vec<T, I, 8>(L, lpr, nt);
       break;
   }
   return fail(OFX_EINVAL, "spmm_csr: unsupported vector width %d", vec);
@@ -545,7 +555,7 @@ int spmm_entry(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k,
               "spmm_csr: NULL col_idx/values/b with nnz=%lld", (long long)nnz);
   Launch L{static_cast<hipStream_t>(stream), row_ptr, col_idx, values, b, c, ldb, ldc,
            row_begin, nrows, n, nnz, resolve_schedule(n, opts), workspace, workspace_bytes,
-           bias, act};
+           bias, act, k};
   if (idx_dtype == OFX_DT_INT32) return launch_idx<int32_t>(val_dtype, L);
   return launch_idx<int64_t>(val_dtype, L);
 }
