@@ -43,28 +43,27 @@ def padded_owner_remap(col_idx: torch.Tensor, k: int, world: int) -> torch.Tenso
 
 
 def _exchange_lists(send: list, group, device) -> list:
-    """Setup-time all-to-all of variable-length int64 lists through torch.distributed (the
-    counts first, then point-to-point transfers); send[p] goes to rank p, result[p] came from p."""
+    """Setup-time all-to-all of variable-length int64 lists (send[p] goes to rank p, result[p]
+    came from p) built from all_gather alone — the most portable collective across gloo and
+    RCCL; the lists are padded to the longest rank's total for the exchange."""
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
         else torch.device("cpu")
     counts = torch.tensor([t.numel() for t in send], dtype=torch.int64, device=dev)
     allc = [torch.zeros(world, dtype=torch.int64, device=dev) for _ in range(world)]
     dist.all_gather(allc, counts, group=group)
-    recv_counts = [int(allc[p][rank]) for p in range(world)]
-    out = [torch.empty(c, dtype=torch.int64, device=dev) for c in recv_counts]
-    ops_ = []
-    for p in range(world):
-        if p == rank:
-            continue
-        if send[p].numel():
-            ops_.append(dist.P2POp(dist.isend, send[p].to(dev).contiguous(), dist.get_global_rank(group, p) if group else p, group))
-        if recv_counts[p]:
-            ops_.append(dist.P2POp(dist.irecv, out[p], dist.get_global_rank(group, p) if group else p, group))
-    if ops_:
-        for r in dist.batch_isend_irecv(ops_):
-            r.wait()
-    return [t.to(device) for t in out]
+    cmat = torch.stack(allc).cpu()  # cmat[src, dst] = length of src's list for dst
+    width = int(cmat.sum(1).max())
+    mine = torch.zeros(max(width, 1), dtype=torch.int64, device=dev)
+    flat = torch.cat([t.to(dev, torch.int64) for t in send]) if width else mine[:0]
+    mine[: flat.numel()] = flat
+    every = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(every, mine, group=group)
+    out = []
+    for src in range(world):
+        off = int(cmat[src, :rank].sum())
+        out.append(every[src][off: off + int(cmat[src, rank])].to(device))
+    return out
 
 
 class HaloPlan:
