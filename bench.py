@@ -127,7 +127,11 @@ def main():
             def step():
                 kern(d_rp, d_ci, d_v, d_b, out)
     else:
-        rs = RowSplitSpmm(m, k, n, nnz_local, dt, torch.int32, device)
+        try:
+            rs = RowSplitSpmm(m, k, n, nnz_local, dt, torch.int32, device)
+        except fs.OfxError as e:  # own RCCL communicator refused: torch.distributed's (also RCCL)
+            log(f"[bench] native RCCL communicator unavailable ({e}); using torch.distributed")
+            rs = RowSplitSpmm(m, k, n, nnz_local, dt, torch.int32, device, comm="torch")
         klo, khi = rs.k_range
         rs.load_shard(synth.dense(klo, khi, n, dt, device=device))
         rs.bind(d_rp, d_ci, d_v, halo=args.exchange in ("auto", "halo"))
