@@ -288,26 +288,33 @@ def main():
     # ---- CPU baseline: oracle restatement on the host cores (rank 0, N=1 only) ---------------
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         from oracle import oracle
-        rp_np = rp_full
-        ci_np = cols.astype(np.int64)
+        # bounded sample: the first rows holding <= 130M nonzeros (all of products; rows are
+        # randomly permuted, so a leading block is representative), B whole on the host
+        r_s = m if nnz <= 130_000_000 else int(np.searchsorted(rp_full, 130_000_000, side="right")) - 1
+        nnz_s = int(rp_full[r_s])
+        flops_s = 2.0 * nnz_s * n
+        what = "full workload" if r_s == m else f"rows [0,{r_s}) = {nnz_s} nnz"
+        rp_np = rp_full[: r_s + 1]
+        ci_np = cols[:nnz_s].astype(np.int64)
         v_np = vals.numpy() if dt != torch.bfloat16 else vals.view(torch.int16).numpy().view(np.uint16)
-        b_np = synth.dense(0, k, n, dt)
-        b_np = b_np.numpy() if dt != torch.bfloat16 else b_np.view(torch.int16).numpy().view(np.uint16)
+        v_np = v_np[:nnz_s]
+        h_b = synth.dense(0, k, n, dt)
+        b_np = h_b.numpy() if dt != torch.bfloat16 else h_b.view(torch.int16).numpy().view(np.uint16)
         dname = result["dtype"]
-        oracle.spmm(rp_np, ci_np, v_np, b_np, dtype=dname, nthreads=threads, row_end=min(m, 100000))
+        oracle.spmm(rp_np, ci_np, v_np, b_np, dtype=dname, nthreads=threads, row_end=min(r_s, 100000))
         reps, t_cpu = 0, 0.0
         while t_cpu < 10.0 and reps < 5:
             t1 = time.perf_counter()
             oracle.spmm(rp_np, ci_np, v_np, b_np, dtype=dname, nthreads=threads)
             t_cpu += time.perf_counter() - t1
             reps += 1
-        cpu_gflops = flops * reps / t_cpu / 1e9
+        cpu_gflops = flops_s * reps / t_cpu / 1e9
         result["cpu_baseline"] = {"value": round(cpu_gflops, 3), "unit": "GFLOP/s", "cores": threads,
                                   "kind": "port",
-                                  "sample": f"full workload x{reps} runs ({t_cpu:.1f} s), oracle/spmm_oracle.c "
+                                  "sample": f"{what} x{reps} runs ({t_cpu:.1f} s), oracle/spmm_oracle.c "
                                             f"OpenMP {threads} threads, same inputs and schedule"}
         # single thread (OneFlow's default CPU_THREADING_RUNTIME=SEQ) on the first
-        # rows holding ~1/16 of the nonzeros (rows are randomly permuted: a representative block)
+        # rows holding ~1/16 of the sample's nonzeros
         r1 = int(np.searchsorted(rp_np, rp_np[-1] // 16))
         t1 = time.perf_counter()
         oracle.spmm(rp_np, ci_np, v_np, b_np, dtype=dname, nthreads=1, row_end=r1)
@@ -315,22 +322,25 @@ def main():
         result["extra"]["cpu_1thread"] = {
             "value": round(2.0 * float(rp_np[r1]) * n / t_1 / 1e9, 3), "unit": "GFLOP/s", "cores": 1,
             "sample": f"rows [0,{r1}) = {int(rp_np[r1])} nnz, one run ({t_1:.1f} s)"}
-        # the operator's own DeviceType::kCPU kernel (SURVEY.md §8d's a2), same threads, through
-        # the op layer on host tensors; bit-identical to the GPU result by contract
+        del ci_np, b_np
+        # the operator's own DeviceType::kCPU kernel (SURVEY.md §8d's a2), same threads and
+        # sample, on host tensors; bit-identical to the GPU result by contract
         h_rp = torch.from_numpy(rp_full.astype(np.int32))
-        h_ci, h_b = torch.from_numpy(cols), synth.dense(0, k, n, dt)
-        h_out = torch.empty((m, n), dtype=dt)
-        fs.spmm_csr(h_rp, h_ci, vals, m, k, h_b, out=h_out, num_threads=threads)
+        h_ci = torch.from_numpy(cols)
+        h_out = torch.empty((r_s, n), dtype=dt)
+        kw = dict(out=h_out, row_end=r_s, num_threads=threads)
+        ops.spmm_csr_cpu(h_rp, h_ci, vals, h_b, m, k, **kw)
         reps2, t_a2 = 0, 0.0
         while t_a2 < 5.0 and reps2 < 3:
             t1 = time.perf_counter()
-            fs.spmm_csr(h_rp, h_ci, vals, m, k, h_b, out=h_out, num_threads=threads)
+            ops.spmm_csr_cpu(h_rp, h_ci, vals, h_b, m, k, **kw)
             t_a2 += time.perf_counter() - t1
             reps2 += 1
         result["extra"]["cpu_op_kernel"] = {
-            "value": round(flops * reps2 / t_a2 / 1e9, 3), "unit": "GFLOP/s", "cores": threads,
-            "sample": f"full workload x{reps2} runs ({t_a2:.1f} s), ofx_spmm_csr_cpu via the op layer",
-            "bitexact_vs_gpu": bool(torch.equal(h_out.view(torch.uint8), out.cpu().view(torch.uint8)))}
+            "value": round(flops_s * reps2 / t_a2 / 1e9, 3), "unit": "GFLOP/s", "cores": threads,
+            "sample": f"{what} x{reps2} runs ({t_a2:.1f} s), ofx_spmm_csr_cpu (the kCPU kernel)",
+            "bitexact_vs_gpu": bool(torch.equal(h_out.view(torch.uint8),
+                                                out[:r_s].cpu().view(torch.uint8)))}
         del h_rp, h_ci, h_b, h_out
         # BASELINE configs[0]: the Cora-shaped problem on the OneFlow CPU op path (plumbing)
         cc = synth.CONFIGS["cora"]
