@@ -142,6 +142,24 @@ def main():
                    "padded_remap": remap}, f)
     manifest["files"]["partition.json"] = hashlib.sha256(
         open(os.path.join(HERE, "partition.json"), "rb").read()).hexdigest()
+
+    # fused epilogue fixtures (op fused_spmm_csr): relu(A @ B + bias) from scipy's fp64 product,
+    # numpy's bias add and max(x, 0); exact mode (integers, every step exact in fp32) and a
+    # random fp32 case (tolerance).  Separate RNG, so the fixtures above are unchanged.
+    frng = np.random.default_rng(20261016)
+    for name, exact in (("fused_exact", True), ("fused_f32", False)):
+        m, k, n = 300, 250, 24
+        deg = frng.integers(0, 15, size=m)
+        deg[7] = 0
+        rp, c, v = make_csr(m, k, deg, frng, exact=exact)
+        b = dense(k, n, frng, exact=exact)
+        bias = (frng.integers(-8, 9, size=n) if exact else frng.uniform(-1, 1, size=n)).astype(np.float32)
+        e64, absum, _ = expected(rp, c, v, b, m, k)
+        relu = np.maximum(e64 + bias.astype(np.float64)[None, :], 0.0)
+        path = os.path.join(HERE, f"{name}.npz")
+        np.savez_compressed(path, row_ptr=rp, col_idx=c, values=v, b=b, bias=bias, m=m, k=k,
+                            expected_relu_f64=relu, absum=absum)
+        manifest["files"][f"{name}.npz"] = hashlib.sha256(open(path, "rb").read()).hexdigest()
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
     print("wrote", len(manifest["files"]), "fixtures")

@@ -11,7 +11,9 @@ import pytest
 from oracle import oracle
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-CASES = sorted(glob.glob(os.path.join(GOLD, "*.npz")))
+CASES = sorted(p for p in glob.glob(os.path.join(GOLD, "*.npz"))
+               if not os.path.basename(p).startswith("fused_"))
+FUSED = sorted(glob.glob(os.path.join(GOLD, "fused_*.npz")))
 
 
 def test_manifest_hashes():
@@ -87,3 +89,25 @@ def test_bf16_rounding_helpers():
     assert np.isnan(back[-1]) and np.isinf(back[-2])
     assert oracle.default_split(128) == 512 and oracle.default_split(1) == 8192
     assert oracle.default_split(256) == 256 and oracle.default_split(1024) == 128
+
+
+@pytest.mark.parametrize("path", FUSED, ids=[os.path.basename(p) for p in FUSED])
+def test_oracle_bias_act_matches_fused_fixture(path):
+    """oracle.bias_act(oracle.spmm(.)) against scipy's fp64 product + bias, relu; exact mode
+    bit for bit, fp32 within 1e-5 of the |.|-sum (bias add and relu are 1-Lipschitz, one more
+    rounding); and the operator's CPU op path equals the oracle composition bit for bit."""
+    import torch
+
+    from oneflow_spmm import _C
+    z = np.load(path)
+    rp, c, v, b, bias = z["row_ptr"], z["col_idx"], z["values"], z["b"], z["bias"]
+    want, absum = z["expected_relu_f64"], z["absum"]
+    got = oracle.bias_act(oracle.spmm(rp, c, v, b, nthreads=4), bias, "relu")
+    if "exact" in path:
+        np.testing.assert_array_equal(got, want.astype(np.float32))
+    else:
+        bound = 1e-5 * (absum + np.abs(bias.astype(np.float64))[None, :]) + 1e-30
+        assert (np.abs(got.astype(np.float64) - want) <= bound).all()
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+    op = _C.fused_spmm_csr(t(rp), t(c), t(v), int(z["m"]), int(z["k"]), t(b), t(bias), relu=True)
+    np.testing.assert_array_equal(op.numpy().view(np.uint32), got.view(np.uint32))
