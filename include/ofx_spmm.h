@@ -349,6 +349,8 @@ int ofx_functional_csr_transpose(void* stream, const ofx_tensor_desc* row_ptr,
                                  void* tmp, size_t tmp_bytes, size_t* tmp_size_out);
 /* The op's registered SBP signatures and no-grad inputs, as text (tests / introspection). */
 int ofx_op_spmm_csr_sbp_signatures(char* buf, size_t len);
+/* Same for any registered op; optional_inputs = comma-separated optional inputs present.   */
+int ofx_op_sbp_signatures(const char* op_name, const char* optional_inputs, char* buf, size_t len);
 
 #ifdef __cplusplus
 }

@@ -208,11 +208,26 @@ extern "C" int ofx_functional_spmm_csr(void* stream, const ofx_tensor_desc* row_
                                     out, tmp, tmp_bytes, 0, 1, -1, 0);
 }
 
-// SBP signatures of the op, for the tests: "arg:sbp,arg:sbp;..." into buf.
-extern "C" int ofx_op_spmm_csr_sbp_signatures(char* buf, size_t len) {
-  const user_op::OpRegistryResult* op = user_op::UserOpRegistryMgr::Get().GetOpRegistryResult("spmm_csr");
-  OFX_REQUIRE(op && buf && len > 0, OFX_EINVAL, "spmm_csr not registered or NULL buffer");
-  user_op::SbpContext ctx;
+// SBP signatures of a registered op, for the tests: "arg:sbp,arg:sbp;...|no_grad:..." into buf.
+// `optional_inputs`: comma-separated optional inputs the op instance has (e.g. "bias").
+extern "C" int ofx_op_sbp_signatures(const char* op_name, const char* optional_inputs, char* buf,
+                                     size_t len) {
+  OFX_REQUIRE(op_name && buf && len > 0, OFX_EINVAL, "op_sbp_signatures: NULL argument");
+  const user_op::OpRegistryResult* op = user_op::UserOpRegistryMgr::Get().GetOpRegistryResult(op_name);
+  OFX_REQUIRE(op, OFX_EINVAL, "op %s is not registered", op_name);
+  std::vector<std::string> present;
+  if (optional_inputs) {
+    std::string all(optional_inputs), cur;
+    for (char ch : all + ",") {
+      if (ch == ',') {
+        if (!cur.empty()) present.push_back(cur);
+        cur.clear();
+      } else {
+        cur += ch;
+      }
+    }
+  }
+  user_op::SbpContext ctx{user_op::UserOpConfView(present)};
   int rc = ToStatus(op->get_sbp(&ctx));
   if (rc) return rc;
   std::string s;
@@ -223,8 +238,10 @@ extern "C" int ofx_op_spmm_csr_sbp_signatures(char* buf, size_t len) {
   // input-arg modifiers: which inputs have requires_grad disabled
   std::map<std::string, user_op::InputArgModifier> mods;
   user_op::GetInputArgModifier get = [&](const std::string& n, int32_t) { return &mods[n]; };
-  rc = ToStatus(op->input_modify(get, user_op::UserOpConfWrapper()));
-  if (rc) return rc;
+  if (op->input_modify) {
+    rc = ToStatus(op->input_modify(get, user_op::UserOpConfWrapper()));
+    if (rc) return rc;
+  }
   s += "|no_grad:";
   bool first = true;
   for (const auto& kv : mods)
@@ -234,6 +251,10 @@ extern "C" int ofx_op_spmm_csr_sbp_signatures(char* buf, size_t len) {
     }
   snprintf(buf, len, "%s", s.c_str());
   return OFX_OK;
+}
+
+extern "C" int ofx_op_spmm_csr_sbp_signatures(char* buf, size_t len) {
+  return ofx_op_sbp_signatures("spmm_csr", nullptr, buf, len);
 }
 
 // ---- gradient functors: functional::SddmmCsr / functional::CsrTranspose ----------------------

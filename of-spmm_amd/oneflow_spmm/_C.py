@@ -197,7 +197,7 @@ def balanced_range(total: int, parts: int, idx: int) -> tuple[int, int]:
     return lo.value, hi.value
 
 
-def sbp_signatures() -> str:
+def sbp_signatures(op: str = "spmm_csr", optional_inputs: str = "") -> str:
     buf = ctypes.create_string_buffer(4096)
-    check(LIB.ofx_op_spmm_csr_sbp_signatures(buf, len(buf)), "sbp")
+    check(LIB.ofx_op_sbp_signatures(op.encode(), optional_inputs.encode(), buf, len(buf)), "sbp")
     return buf.value.decode()

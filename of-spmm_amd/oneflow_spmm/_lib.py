@@ -123,6 +123,7 @@ def _load():
         "ofx_functional_csr_transpose": ([p, pdesc, pdesc, i64, i64, pdesc, pdesc, pdesc, p, sz,
                                           ctypes.POINTER(sz)], i32),
         "ofx_op_spmm_csr_sbp_signatures": ([ctypes.c_char_p, sz], i32),
+        "ofx_op_sbp_signatures": ([ctypes.c_char_p, ctypes.c_char_p, p, sz], i32),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)

@@ -47,6 +47,21 @@ def test_sbp_signatures_and_no_grad_inputs():
     assert mods == "no_grad:a_csr_col_idx,a_csr_row_ptr"
 
 
+def test_fused_op_sbp_with_and_without_bias():
+    def parse(s):
+        sigs, mods = s.split("|")
+        return [dict(kv.split(":") for kv in sig.split(",")) for sig in sigs.split(";")], mods
+    rows, mods = parse(fs._C.sbp_signatures("fused_spmm_csr", "bias"))
+    base = {"a_csr_row_ptr": "B", "a_csr_col_idx": "B", "a_csr_values": "B"}
+    assert {**base, "b": "B", "bias": "B", "out": "S(0)"} in rows
+    assert {**base, "b": "S(1)", "bias": "S(0)", "out": "S(1)"} in rows
+    assert mods == "no_grad:a_csr_col_idx,a_csr_row_ptr"
+    rows, _ = parse(fs._C.sbp_signatures("fused_spmm_csr", ""))
+    assert all("bias" not in r for r in rows) and {**base, "b": "B", "out": "S(0)"} in rows
+    with pytest.raises(fs.OfxError, match="not registered"):
+        fs._C.sbp_signatures("no_such_op")
+
+
 def _small():
     rng = np.random.default_rng(0)
     rp, ci, v = random_csr(6, 9, rng.integers(0, 4, size=6), rng)
