@@ -331,3 +331,49 @@ def test_hipgraph_capture_replay(device):
     torch.cuda.synchronize()
     ref = oracle_spmm(rp.cpu(), ci.cpu(), v.cpu(), b.cpu())
     assert_bitwise(out, ref, "graph replay")
+
+
+def test_row_split_step_hipgraph_capture(device):
+    """The whole row-split step (RCCL exchange + local SpMM; the pipelined form on two streams;
+    the halo form) is capture-safe: capture once, load a new B shard, replay, same bits."""
+    import socket
+
+    import torch.distributed as dist
+    from oneflow_spmm.distributed import RowSplitSpmm
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=device)
+    try:
+        rng = np.random.default_rng(41)
+        m, k, n = 3000, 2500, 128
+        rp, ci, v = random_csr(m, k, power_law_degrees(m, 90000, k, rng), rng)
+        b1, b2 = random_dense(k, n, rng), random_dense(k, n, rng)
+        rs = RowSplitSpmm(m, k, n, ci.numel(), torch.float32, torch.int32, device)
+        rs.load_shard(b1.to(device))
+        rs.bind(rp.to(device), ci.to(device), v.to(device), halo=True)
+        out = torch.empty((m, n), device=device)
+        for exchange, chunks in (("allgather", 1), ("allgather", 2), ("halo", 1)):
+            rs.exchange = exchange
+            rs.set_pipeline(chunks)
+            rs.load_shard(b1.to(device))
+            side = torch.cuda.Stream(device)
+            side.wait_stream(torch.cuda.current_stream(device))
+            with torch.cuda.stream(side):
+                rs.step(out)  # warm, outside the capture
+            torch.cuda.current_stream(device).wait_stream(side)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                rs.step(out)
+            rs.load_shard(b2.to(device))
+            out.fill_(float("nan"))
+            g.replay()
+            torch.cuda.synchronize()
+            assert_bitwise(out, oracle_spmm(rp, ci, v, b2), f"graph replay {exchange}/p{chunks}")
+            del g
+        rs.close()
+    finally:
+        dist.destroy_process_group()
