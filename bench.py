@@ -68,7 +68,7 @@ def main():
                     help="all-gather schedule for N>1 (default: measured at setup, faster kept)")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="column blocks for gather/SpMM overlap at N>1 (default: measured)")
-    ap.add_argument("--exchange", choices=["auto", "allgather", "halo"], default="auto",
+    ap.add_argument("--exchange", choices=["auto", "allgather", "halo", "nsplit"], default="auto",
                     help="B exchange for N>1 (default: measured at setup)")
     ap.add_argument("--force-rowsplit", action="store_true",
                     help="run the N>1 code path (RCCL all-gather + local SpMM) even with one rank")
@@ -134,13 +134,19 @@ def main():
             rs = RowSplitSpmm(m, k, n, nnz_local, dt, torch.int32, device, comm="torch")
         klo, khi = rs.k_range
         rs.load_shard(synth.dense(klo, khi, n, dt, device=device))
-        rs.bind(d_rp, d_ci, d_v, halo=args.exchange in ("auto", "halo"))
+        full = None
+        if args.exchange in ("auto", "nsplit") and n % world == 0:
+            # the column-split candidate needs the whole CSR on every rank
+            f_ci = torch.from_numpy(synth.columns(m, k, rp_full, threads=threads)).to(device)
+            full = (torch.from_numpy(rp_full.astype(np.int32)).to(device), f_ci,
+                    synth.values(0, nnz, dt).to(device))
+        rs.bind(d_rp, d_ci, d_v, halo=args.exchange in ("auto", "halo"), full_csr=full)
         # exchange: all-gather (ring / point-to-point) x pipeline depth (column blocks gathered
         # while the previous block computes), or halo-only rows; measured here, untimed, the
         # fastest kept (every candidate gives the same bytes)
         comm_times = {}
         if args.comm or args.pipeline or args.exchange != "auto":
-            rs.exchange = "halo" if args.exchange == "halo" else "allgather"
+            rs.exchange = args.exchange if args.exchange in ("halo", "nsplit") else "allgather"
             rs.comm_kind = args.comm or rs.comm_kind
             rs.set_pipeline(args.pipeline or 1)
         else:
@@ -273,8 +279,9 @@ def main():
             "spmm_ms_max": round(phase["spmm_ms_max"], 4),
             # SpMM phase alone with the gathered B resident (SURVEY.md §8e reports it separately)
             "spmm_phase_gflops_aggregate": round(flops / (phase["spmm_ms_max"] * 1e-3) / 1e9, 2),
-            "allgather_gbs_per_rank": round(((rs.halo.halo_rows if rs.exchange == "halo" else
-                                              rs.k_padded - rs.pad) * n * s_v) /
+            "allgather_gbs_per_rank": round(((rs.halo.halo_rows * n if rs.exchange == "halo" else
+                                              (k - (khi - klo)) * (n // world) if rs.exchange == "nsplit"
+                                              else (rs.k_padded - rs.pad) * n) * s_v) /
                                             (phase["gather_ms_max"] * 1e-3) / 1e9, 2)
             if phase["gather_ms_max"] > 0 else None,
             "rows_rank0": rows, "nnz_rank0": nnz_local,

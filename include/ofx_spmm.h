@@ -263,7 +263,8 @@ int ofx_exchange_rows(void* stream, void* comm, int dtype, int64_t n, const void
                       const int64_t* send_counts, const int64_t* send_offsets, void* recv_buf,
                       const int64_t* recv_counts, const int64_t* recv_offsets);
 /* Row gather on the device: dst[i, :] = src[idx[i], :] for i < count, rows of row_bytes bytes,
- * strides in bytes (packs the halo rows a peer requested into one send buffer).             */
+ * strides in bytes (packs the halo rows a peer requested into one send buffer).  idx == NULL
+ * is the identity: a strided 2-D copy (column-block packing of the N-split exchange).        */
 int ofx_gather_rows(void* stream, int idx_dtype, int64_t count, int64_t row_bytes,
                     const void* idx, const void* src, int64_t src_stride_bytes, void* dst,
                     int64_t dst_stride_bytes);

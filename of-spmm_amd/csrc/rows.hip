@@ -24,7 +24,8 @@ __global__ void __launch_bounds__(kBlock)
   const int gl = threadIdx.x % LPR;
   for (int64_t i = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR; i < count;
        i += (int64_t)gridDim.x * GPB) {
-    const W* s = reinterpret_cast<const W*>(src + (int64_t)idx[i] * src_stride);
+    const int64_t r = idx ? (int64_t)idx[i] : i;  // NULL index: a plain strided row copy
+    const W* s = reinterpret_cast<const W*>(src + r * src_stride);
     W* d = reinterpret_cast<W*>(dst + i * dst_stride);
     for (int64_t w = gl; w < words; w += LPR) d[w] = s[w];
   }
@@ -82,7 +83,7 @@ extern "C" int ofx_gather_rows(void* stream, int idx_dtype, int64_t count, int64
                   dst_stride_bytes >= row_bytes,
               OFX_EINVAL, "gather_rows: bad sizes");
   if (count == 0 || row_bytes == 0) return OFX_OK;
-  OFX_REQUIRE(idx && src && dst, OFX_EINVAL, "gather_rows: NULL pointer");
+  OFX_REQUIRE(src && dst, OFX_EINVAL, "gather_rows: NULL pointer");
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (idx_dtype == OFX_DT_INT32)
     return dispatch(s, static_cast<const int32_t*>(idx), count, row_bytes, src, src_stride_bytes,

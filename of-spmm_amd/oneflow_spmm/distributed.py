@@ -119,6 +119,115 @@ class HaloPlan:
         self.remote_rows_total = k - self.k_own
 
 
+def _copy_rows(dst: torch.Tensor, src: torch.Tensor):
+    """dst[i, :] = src[i, :] for two 2-D row-strided views of one shape (HIP on the device)."""
+    rows, w = src.shape
+    if rows == 0 or w == 0:
+        return
+    if dst.device.type != "cuda":
+        dst.copy_(src)
+        return
+    esz = src.element_size()
+    check(LIB.ofx_gather_rows(current_stream_handle(dst), dtype_code(torch.int64), rows, w * esz,
+                              None, src.data_ptr(), src.stride(0) * esz, dst.data_ptr(),
+                              dst.stride(0) * esz), "copy_rows")
+
+
+def _torch_exchange(send, send_counts, send_offsets, recv, recv_counts, recv_offsets, group):
+    """Grouped point-to-point rows exchange through torch.distributed (the CPU/gloo path of
+    ofx_exchange_rows; same counts/offsets convention, rows of the buffers' width)."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    reqs = []
+    for p in range(world):
+        if p == rank:
+            continue
+        gp = dist.get_global_rank(group, p) if group else p
+        if send_counts[p]:
+            o = send_offsets[p]
+            reqs.append(dist.P2POp(dist.isend, send[o:o + send_counts[p]], gp, group))
+        if recv_counts[p]:
+            o = recv_offsets[p]
+            reqs.append(dist.P2POp(dist.irecv, recv[o:o + recv_counts[p]], gp, group))
+    if reqs:
+        for r in dist.batch_isend_irecv(reqs):
+            r.wait()
+
+
+class NSplitPlan:
+    """The same S(0) -> S(0) step by a split of the dense COLUMNS (SURVEY.md §8e alternative
+    (ii); the op's (B, B, B, S(1)) -> S(1) signature in the middle):
+
+      1. all-to-all B from row shards to column blocks: rank q gets every rank's rows of
+         B[:, q-block] (|B|(G-1)/G^2 per rank instead of the all-gather's |B|(G-1)/G);
+      2. SpMM of ALL rows of A against this rank's N/G columns (the full CSR is bound);
+      3. all-to-all C back from column blocks to this rank's rows.
+
+    Every output column is summed in the same order with the full-width hub schedule
+    (split = default_split(N)), so the bits equal the row split's.  Needs N % G == 0."""
+
+    def __init__(self, owner, row_ptr, col_idx, values):
+        o = owner
+        G, r = o.world, o.rank
+        self.ng = o.n // G
+        self.k_rng = [balanced_range(o.k, G, p) for p in range(G)]
+        self.m_rng = [balanced_range(o.m, G, p) for p in range(G)]
+        k_r = self.k_rng[r][1] - self.k_rng[r][0]
+        m_r = self.m_rng[r][1] - self.m_rng[r][0]
+        self.k_r, self.m_r = k_r, m_r
+        dev, dt = o.device, o.dtype
+        self.shard = torch.zeros((k_r, o.n), dtype=dt, device=dev)
+        self.send_b = torch.empty((G * k_r, self.ng), dtype=dt, device=dev)
+        self.b_cols = torch.zeros((o.k, self.ng), dtype=dt, device=dev)
+        self.c_cols = torch.empty((o.m, self.ng), dtype=dt, device=dev)
+        self.recv_c = torch.empty((G * m_r, self.ng), dtype=dt, device=dev)
+        self.csr = (row_ptr, col_idx, values)
+        z = lambda f: [f(p) if p != r else 0 for p in range(G)]  # noqa: E731
+        self.b_counts = (z(lambda p: k_r), z(lambda p: p * k_r),
+                         z(lambda p: self.k_rng[p][1] - self.k_rng[p][0]), z(lambda p: self.k_rng[p][0]))
+        self.c_counts = (z(lambda p: self.m_rng[p][1] - self.m_rng[p][0]), z(lambda p: self.m_rng[p][0]),
+                         z(lambda p: m_r), z(lambda p: p * m_r))
+        as_c = lambda v: (ctypes.c_int64 * G)(*v)  # noqa: E731
+        self._cb = tuple(as_c(v) for v in self.b_counts)
+        self._cc = tuple(as_c(v) for v in self.c_counts)
+        self.kernel = None
+        if dev.type == "cuda":
+            self.kernel = ops.SpmmCsrKernel(o.m, o.k, self.ng, col_idx.numel(), o.idx_dtype, dt,
+                                            dev, o.options)
+
+    def _exchange(self, owner, send, counts, c_counts, recv):
+        if owner.comm_kind == "torch":
+            _torch_exchange(send, counts[0], counts[1], recv, counts[2], counts[3], owner.group)
+            return
+        sc, so, rc, ro = c_counts
+        check(LIB.ofx_exchange_rows(current_stream_handle(recv), owner._comm,
+                                    dtype_code(owner.dtype), self.ng, send.data_ptr(), sc, so,
+                                    recv.data_ptr(), rc, ro), "exchange_rows")
+
+    def exchange_b(self, owner):
+        G, r, ng = owner.world, owner.rank, self.ng
+        for q in range(G):
+            if q != r:
+                _copy_rows(self.send_b[q * self.k_r:(q + 1) * self.k_r], self.shard[:, q * ng:(q + 1) * ng])
+        lo, hi = self.k_rng[r]
+        _copy_rows(self.b_cols[lo:hi], self.shard[:, r * ng:(r + 1) * ng])
+        self._exchange(owner, self.send_b, self.b_counts, self._cb, self.b_cols)
+
+    def compute_and_return(self, owner, out):
+        G, r, ng = owner.world, owner.rank, self.ng
+        rp, ci, v = self.csr
+        if self.kernel is not None:
+            self.kernel(rp, ci, v, self.b_cols, self.c_cols)
+        else:
+            ops.spmm_csr_cpu(rp, ci, v, self.b_cols, owner.m, owner.k, out=self.c_cols,
+                             options=owner.options)
+        self._exchange(owner, self.c_cols, self.c_counts, self._cc, self.recv_c)
+        lo, hi = self.m_rng[r]
+        for p in range(G):
+            src = self.c_cols[lo:hi] if p == r else self.recv_c[p * self.m_r:(p + 1) * self.m_r]
+            _copy_rows(out[:, p * ng:(p + 1) * ng], src)
+        return out
+
+
 class RowSplitSpmm:
     """out[rows of this rank] = A[rows of this rank, :] @ all_gather(b shards).
 
@@ -159,6 +268,7 @@ class RowSplitSpmm:
             self.comm_stream = torch.cuda.Stream(self.device)
         self.gathered = None
         self.halo = None
+        self.ns = None
         self.exchange = "allgather"
         self._bound = None
         self.set_pipeline(pipeline)
@@ -206,6 +316,8 @@ class RowSplitSpmm:
             self.gathered[c, r0:r0 + (hi - lo)].copy_(b_shard[:, c * self.nc:(c + 1) * self.nc])
         if self.halo is not None:
             self.compact[: self.halo.k_own].copy_(b_shard)
+        if self.ns is not None:
+            self.ns.shard.copy_(b_shard)
 
     def shard(self) -> torch.Tensor:
         lo, hi = self.k_range
@@ -342,11 +454,15 @@ class RowSplitSpmm:
         return out
 
     # -- bound form: this rank's CSR once, every exchange layout prepared ------------------------
-    def bind(self, row_ptr, col_idx, values, halo: bool = True):
+    def bind(self, row_ptr, col_idx, values, halo: bool = True, full_csr=None):
         """Binds this rank's CSR (`col_idx` in global B row ids; the local slice, or the full CSR
         when local_csr=False).  Remaps the columns for the all-gather layout and, with halo=True,
-        builds the halo plan; `step()` then runs whichever exchange is selected."""
+        builds the halo plan; with `full_csr=(row_ptr, col_idx, values)` of the WHOLE matrix (and
+        N % G == 0) also the column-split plan.  `step()` then runs the selected exchange."""
         cols = {"allgather": self.remap_columns(col_idx)}
+        if full_csr is not None and self.n % self.world == 0:
+            self.ns = NSplitPlan(self, *full_csr)
+            self.ns.shard.copy_(self.shard())
         if halo:
             if self.local_csr:
                 mine = col_idx
@@ -383,18 +499,8 @@ class RowSplitSpmm:
         if self.comm_kind == "torch":
             if h.send_rows:
                 torch.index_select(self.compact, 0, h.send_idx, out=self.send_buf)
-            reqs = []
-            for p in range(self.world):
-                gp = dist.get_global_rank(self.group, p) if self.group else p
-                if h.send_counts[p]:
-                    o = h.send_offsets[p]
-                    reqs.append(dist.P2POp(dist.isend, self.send_buf[o:o + h.send_counts[p]], gp, self.group))
-                if h.recv_counts[p]:
-                    o = h.k_own + h.recv_offsets[p]
-                    reqs.append(dist.P2POp(dist.irecv, self.compact[o:o + h.recv_counts[p]], gp, self.group))
-            if reqs:
-                for r in dist.batch_isend_irecv(reqs):
-                    r.wait()
+            _torch_exchange(self.send_buf, h.send_counts, h.send_offsets, self.compact,
+                            h.recv_counts, [h.k_own + o for o in h.recv_offsets], self.group)
             return
         s = current_stream_handle(self.compact)
         esz = self.compact.element_size()
@@ -425,6 +531,18 @@ class RowSplitSpmm:
     def step(self, out, b_shard=None, events=None):
         """One exchange + local SpMM over the bound CSR with the selected exchange."""
         row_ptr, cols, values = self._bound
+        if self.exchange == "nsplit":
+            if b_shard is not None:
+                self.ns.shard.copy_(b_shard)
+            if events:
+                events[0].record()
+            self.ns.exchange_b(self)
+            if events:
+                events[1].record()
+            self.ns.compute_and_return(self, out)
+            if events:
+                events[2].record()
+            return out
         if self.exchange == "halo":
             if events:
                 events[0].record()
@@ -443,6 +561,8 @@ class RowSplitSpmm:
         """The exchange alone (phase timing)."""
         if self.exchange == "halo":
             self.halo_exchange()
+        elif self.exchange == "nsplit":
+            self.ns.exchange_b(self)
         else:
             self.all_gather_b()
 
@@ -450,15 +570,17 @@ class RowSplitSpmm:
         """The local SpMM alone with the exchanged B resident (phase timing)."""
         if self.exchange == "halo":
             return self.halo_compute(out)
+        if self.exchange == "nsplit":  # local SpMM + the return all-to-all of C
+            return self.ns.compute_and_return(self, out)
         row_ptr, cols, values = self._bound
         return self.compute(row_ptr, cols["allgather"], values, out)
 
     # -- schedule choice -------------------------------------------------------------------------
     def tune(self, out, pipelines=(1, 2, 4), reps: int = 3, force: bool = False) -> dict:
         """Times every exchange on this node with the real step over the bound CSR: all-gather
-        (ring / point-to-point) x pipeline depth, and the halo exchange if built.  Keeps the
+        (ring / point-to-point) x pipeline depth, the halo exchange and the column split if built.  Keeps the
         fastest.  Timings are max-reduced over ranks, so all ranks choose the same; every
-        candidate produces the same bytes.  Returns {"<comm>/p<C>" | "halo": ms}.  One rank has
+        candidate produces the same bytes.  Returns {"<comm>/p<C>" | "halo" | "nsplit": ms}.  One rank has
         nothing to exchange, so it keeps its setting unless `force` (tests)."""
         if self._bound is None:
             raise RuntimeError("tune: bind() the CSR first")
@@ -490,9 +612,12 @@ class RowSplitSpmm:
         if self.halo is not None:
             self.exchange, self.comm_kind = "halo", "rccl"
             times["halo"] = measure()
+        if self.ns is not None:
+            self.exchange, self.comm_kind = "nsplit", "rccl"
+            times["nsplit"] = measure()
         best = min(times, key=times.get)
-        if best == "halo":
-            self.exchange, self.comm_kind = "halo", "rccl"
+        if best in ("halo", "nsplit"):
+            self.exchange, self.comm_kind = best, "rccl"
             self.set_pipeline(1)
         else:
             kind, p = best.split("/p")

@@ -74,6 +74,14 @@ def _worker(rank, world, port, m, k, n, local_csr, pipeline, density, q):
         ok = ok and torch.equal(rs.compact[: h.k_own], b[klo:khi])
         remote = uniq[(uniq < klo) | (uniq >= khi)]
         ok = ok and torch.equal(rs.compact[h.k_own:], b[remote])
+        # the column split (all-to-all of B to column blocks, SpMM of all rows, C back): same bytes
+        if n % world == 0:
+            rs.bind(lrp, lci, lv, halo=False, full_csr=(rp, ci, v))
+            rs.exchange = "nsplit"
+            out4 = torch.full_like(out2, float("nan"))
+            rs.step(out4, b_shard=b2[klo:khi])
+            ok = ok and np.array_equal(out4.numpy().view(np.uint32), full2[lo:hi].view(np.uint32))
+            ok = ok and torch.equal(rs.ns.b_cols, b2[:, rank * (n // world):(rank + 1) * (n // world)])
         q.put((rank, bool(ok)))
     finally:
         dist.destroy_process_group()

@@ -37,7 +37,8 @@ def _worker(rank, world, port, kind, rp, ci, v, b, q):
         m, k, n = rp.numel() - 1, b.shape[0], b.shape[1]
         try:
             rs = RowSplitSpmm(m, k, n, ci.numel(), torch.float32, torch.int32, device,
-                              comm="rccl" if kind in ("tune", "halo") else kind, local_csr=False)
+                              comm="rccl" if kind in ("tune", "halo", "nsplit") else kind,
+                              local_csr=False)
         except Exception as e:  # OfxError(OFX_ECOMM) when RCCL rejects the layout
             q.put((rank, "skip", str(e)))
             dist.destroy_process_group()
@@ -45,15 +46,18 @@ def _worker(rank, world, port, kind, rp, ci, v, b, q):
         lo, hi = rs.k_range
         rs.load_shard(b[lo:hi].to(device))
         out = torch.empty((rs.row_range[1] - rs.row_range[0], n), device=device)
-        rs.bind(rp.to(device), ci.to(device), v.to(device), halo=kind in ("tune", "halo"))
-        if kind == "halo":
-            rs.exchange = "halo"
+        d = (rp.to(device), ci.to(device), v.to(device))
+        rs.bind(*d, halo=kind in ("tune", "halo"), full_csr=d if kind in ("tune", "nsplit") else None)
+        if kind in ("halo", "nsplit"):
+            rs.exchange = kind
         times = rs.tune(out, reps=2) if kind == "tune" else {}
         # clear everything received, so the checked step must exchange it again
         sh = rs.shard()
         rs.gathered.zero_()
         if rs.halo is not None:
             rs.compact.zero_()
+        if rs.ns is not None:
+            rs.ns.b_cols.zero_()
         rs.load_shard(sh)
         out.zero_()
         rs.step(out)
@@ -65,7 +69,7 @@ def _worker(rank, world, port, kind, rp, ci, v, b, q):
         q.put((rank, "err", traceback.format_exc()))
 
 
-@pytest.mark.parametrize("kind", ["rccl", "rccl-p2p", "halo", "tune"])
+@pytest.mark.parametrize("kind", ["rccl", "rccl-p2p", "halo", "nsplit", "tune"])
 def test_row_split_two_ranks(kind):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -99,5 +103,5 @@ def test_row_split_two_ranks(kind):
         assert_bitwise(out, ref[lo:hi], f"{kind} rows [{lo},{hi})")
         kinds.add(ck)
         if kind == "tune":
-            assert {t.split("/")[0] for t in times} == {"rccl", "rccl-p2p", "halo"}
+            assert {t.split("/")[0] for t in times} == {"rccl", "rccl-p2p", "halo", "nsplit"}
     assert len(kinds) == 1  # every rank made the same choice
