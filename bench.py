@@ -68,8 +68,9 @@ def main():
                     help="all-gather schedule for N>1 (default: measured at setup, faster kept)")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="column blocks for gather/SpMM overlap at N>1 (default: measured)")
-    ap.add_argument("--exchange", choices=["auto", "allgather", "halo", "nsplit"], default="auto",
-                    help="B exchange for N>1 (default: measured at setup)")
+    ap.add_argument("--exchange", default="auto",
+                    help="B exchange for N>1: auto | allgather | halo | nsplit | grid<R>x<C> "
+                         "(default: measured at setup)")
     ap.add_argument("--force-rowsplit", action="store_true",
                     help="run the N>1 code path (RCCL all-gather + local SpMM) even with one rank")
     args = ap.parse_args()
@@ -135,8 +136,8 @@ def main():
         klo, khi = rs.k_range
         rs.load_shard(synth.dense(klo, khi, n, dt, device=device))
         full = None
-        if args.exchange in ("auto", "nsplit") and n % world == 0:
-            # the column-split candidate needs the whole CSR on every rank
+        if args.exchange == "auto" or args.exchange == "nsplit" or args.exchange.startswith("grid"):
+            # the grid / column-split candidates need the whole CSR on every rank
             f_ci = torch.from_numpy(synth.columns(m, k, rp_full, threads=threads)).to(device)
             full = (torch.from_numpy(rp_full.astype(np.int32)).to(device), f_ci,
                     synth.values(0, nnz, dt).to(device))
@@ -146,7 +147,9 @@ def main():
         # fastest kept (every candidate gives the same bytes)
         comm_times = {}
         if args.comm or args.pipeline or args.exchange != "auto":
-            rs.exchange = args.exchange if args.exchange in ("halo", "nsplit") else "allgather"
+            rs.exchange = args.exchange if args.exchange != "auto" else "allgather"
+            if rs.exchange not in ("allgather", "halo") and rs.exchange not in rs.grids:
+                raise SystemExit(f"--exchange {rs.exchange}: not available (grids: {list(rs.grids)})")
             rs.comm_kind = args.comm or rs.comm_kind
             rs.set_pipeline(args.pipeline or 1)
         else:
@@ -227,6 +230,9 @@ def main():
     del scratch
     cold_ms = float(np.median(cold))
     bytes_launch = alg_bytes(rows, nnz_local, n, s_v)
+    if rowsplit and rs.exchange in rs.grids:  # the grid's SpMM: its row group x N/C columns
+        gp = rs.grids[rs.exchange]
+        bytes_launch = alg_bytes(gp.ghi - gp.glo, int(rp_full[gp.ghi] - rp_full[gp.glo]), gp.ng, s_v)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
 
     # HBM-side traffic of the dominant kernel per launch from the committed rocprofv3 PMC summary
@@ -279,8 +285,10 @@ def main():
             "spmm_ms_max": round(phase["spmm_ms_max"], 4),
             # SpMM phase alone with the gathered B resident (SURVEY.md §8e reports it separately)
             "spmm_phase_gflops_aggregate": round(flops / (phase["spmm_ms_max"] * 1e-3) / 1e9, 2),
+            # B bytes this rank receives in the exchange phase / its time
             "allgather_gbs_per_rank": round(((rs.halo.halo_rows * n if rs.exchange == "halo" else
-                                              (k - (khi - klo)) * (n // world) if rs.exchange == "nsplit"
+                                              rs.grids[rs.exchange].exchange_rows()[0] *
+                                              rs.grids[rs.exchange].ng if rs.exchange in rs.grids
                                               else (rs.k_padded - rs.pad) * n) * s_v) /
                                             (phase["gather_ms_max"] * 1e-3) / 1e9, 2)
             if phase["gather_ms_max"] > 0 else None,

@@ -153,46 +153,75 @@ def _torch_exchange(send, send_counts, send_offsets, recv, recv_counts, recv_off
             r.wait()
 
 
-class NSplitPlan:
-    """The same S(0) -> S(0) step by a split of the dense COLUMNS (SURVEY.md §8e alternative
-    (ii); the op's (B, B, B, S(1)) -> S(1) signature in the middle):
+class GridPlan:
+    """The S(0) -> S(0) step on a 2-D grid of the G ranks: R row groups x C column blocks (R*C = G,
+    C | N).  Rank p sits in row group g = p // C at column c = p % C; its row group holds the rows
+    of ranks g*C .. g*C+C-1 (a contiguous range of OneFlow's S(0) split).
 
-      1. all-to-all B from row shards to column blocks: rank q gets every rank's rows of
-         B[:, q-block] (|B|(G-1)/G^2 per rank instead of the all-gather's |B|(G-1)/G);
-      2. SpMM of ALL rows of A against this rank's N/G columns (the full CSR is bound);
-      3. all-to-all C back from column blocks to this rank's rows.
+      1. B from row shards to column blocks: every rank sends block c(p) = p % C of its shard to
+         each peer p and receives every rank's rows of B[:, its block] (|B|(G-1)/(G*C) per rank;
+         the all-gather moves |B|(G-1)/G, the pure column split (C = G) |B|(G-1)/G^2);
+      2. SpMM of the row group's rows of A against the N/C columns (the op's S(1) signature
+         inside the group; global-form launch on the whole CSR, no slice copy);
+      3. C back inside the row group: each member gets its own rows of every block.
 
-    Every output column is summed in the same order with the full-width hub schedule
-    (split = default_split(N)), so the bits equal the row split's.  Needs N % G == 0."""
+    C = 1 is the all-gather itself; C = G is the column split of SURVEY.md §8e alternative (ii)
+    ("nsplit").  In between, traffic falls by C while the SpMM's row width shrinks only to N/C
+    (the gather runs 512-B rows at 7.7 TB/s but 64-B rows at ~3.9), so the best grid depends on
+    the links and N: `tune()` measures every one.  Every output column is summed in the same order
+    with the full-width hub schedule (split = default_split(N)), so the bits are the row split's."""
 
-    def __init__(self, owner, row_ptr, col_idx, values):
+    def __init__(self, owner, cn, row_ptr, col_idx, values):
         o = owner
         G, r = o.world, o.rank
-        self.ng = o.n // G
+        if cn < 1 or G % cn or o.n % cn:
+            raise ValueError(f"GridPlan: {cn} column blocks must divide world {G} and n {o.n}")
+        self.cn, self.rg = cn, G // cn
+        self.g, self.c = divmod(r, cn)
+        self.ng = nb = o.n // cn
         self.k_rng = [balanced_range(o.k, G, p) for p in range(G)]
         self.m_rng = [balanced_range(o.m, G, p) for p in range(G)]
+        members = range(self.g * cn, self.g * cn + cn)
+        self.glo, self.ghi = self.m_rng[members[0]][0], self.m_rng[members[-1]][1]
         k_r = self.k_rng[r][1] - self.k_rng[r][0]
         m_r = self.m_rng[r][1] - self.m_rng[r][0]
         self.k_r, self.m_r = k_r, m_r
         dev, dt = o.device, o.dtype
         self.shard = torch.zeros((k_r, o.n), dtype=dt, device=dev)
-        self.send_b = torch.empty((G * k_r, self.ng), dtype=dt, device=dev)
-        self.b_cols = torch.zeros((o.k, self.ng), dtype=dt, device=dev)
-        self.c_cols = torch.empty((o.m, self.ng), dtype=dt, device=dev)
-        self.recv_c = torch.empty((G * m_r, self.ng), dtype=dt, device=dev)
+        self.send_b = torch.empty((cn * k_r, nb), dtype=dt, device=dev)  # shard, block-major
+        self.b_cols = torch.zeros((o.k, nb), dtype=dt, device=dev)
+        self.c_grp = torch.empty((self.ghi - self.glo, nb), dtype=dt, device=dev)
+        self.recv_c = torch.empty((cn * m_r, nb), dtype=dt, device=dev)
         self.csr = (row_ptr, col_idx, values)
-        z = lambda f: [f(p) if p != r else 0 for p in range(G)]  # noqa: E731
-        self.b_counts = (z(lambda p: k_r), z(lambda p: p * k_r),
-                         z(lambda p: self.k_rng[p][1] - self.k_rng[p][0]), z(lambda p: self.k_rng[p][0]))
-        self.c_counts = (z(lambda p: self.m_rng[p][1] - self.m_rng[p][0]), z(lambda p: self.m_rng[p][0]),
-                         z(lambda p: m_r), z(lambda p: p * m_r))
+        peer = [p != r for p in range(G)]
+        mate = [p != r and p // cn == self.g for p in range(G)]
+        m_of = lambda p: self.m_rng[p][1] - self.m_rng[p][0]  # noqa: E731
+        # (send counts, send offsets, recv counts, recv offsets), in rows of nb elements
+        self.b_counts = ([k_r if peer[p] else 0 for p in range(G)],
+                         [(p % cn) * k_r if peer[p] else 0 for p in range(G)],
+                         [self.k_rng[p][1] - self.k_rng[p][0] if peer[p] else 0 for p in range(G)],
+                         [self.k_rng[p][0] if peer[p] else 0 for p in range(G)])
+        self.c_counts = ([m_of(p) if mate[p] else 0 for p in range(G)],
+                         [self.m_rng[p][0] - self.glo if mate[p] else 0 for p in range(G)],
+                         [m_r if mate[p] else 0 for p in range(G)],
+                         [(p % cn) * m_r if mate[p] else 0 for p in range(G)])
         as_c = lambda v: (ctypes.c_int64 * G)(*v)  # noqa: E731
         self._cb = tuple(as_c(v) for v in self.b_counts)
         self._cc = tuple(as_c(v) for v in self.c_counts)
+        # blocks some peer needs: all of them once there are other row groups
+        self.packed = [b for b in range(cn) if b != self.c or self.rg > 1]
         self.kernel = None
         if dev.type == "cuda":
-            self.kernel = ops.SpmmCsrKernel(o.m, o.k, self.ng, col_idx.numel(), o.idx_dtype, dt,
+            self.kernel = ops.SpmmCsrKernel(o.m, o.k, nb, col_idx.numel(), o.idx_dtype, dt,
                                             dev, o.options)
+
+    @property
+    def name(self) -> str:
+        return "nsplit" if self.rg == 1 else f"grid{self.rg}x{self.cn}"
+
+    def exchange_rows(self) -> tuple:
+        """Rows of N/C elements this rank receives per step: (B rows, C rows)."""
+        return sum(self.b_counts[2]), sum(self.c_counts[2])
 
     def _exchange(self, owner, send, counts, c_counts, recv):
         if owner.comm_kind == "torch":
@@ -204,28 +233,32 @@ class NSplitPlan:
                                     recv.data_ptr(), rc, ro), "exchange_rows")
 
     def exchange_b(self, owner):
-        G, r, ng = owner.world, owner.rank, self.ng
-        for q in range(G):
-            if q != r:
-                _copy_rows(self.send_b[q * self.k_r:(q + 1) * self.k_r], self.shard[:, q * ng:(q + 1) * ng])
-        lo, hi = self.k_rng[r]
-        _copy_rows(self.b_cols[lo:hi], self.shard[:, r * ng:(r + 1) * ng])
+        nb, k_r = self.ng, self.k_r
+        for b in self.packed:
+            _copy_rows(self.send_b[b * k_r:(b + 1) * k_r], self.shard[:, b * nb:(b + 1) * nb])
+        lo, hi = self.k_rng[owner.rank]
+        _copy_rows(self.b_cols[lo:hi], self.shard[:, self.c * nb:(self.c + 1) * nb])
         self._exchange(owner, self.send_b, self.b_counts, self._cb, self.b_cols)
 
     def compute_and_return(self, owner, out):
-        G, r, ng = owner.world, owner.rank, self.ng
+        nb, r = self.ng, owner.rank
         rp, ci, v = self.csr
         if self.kernel is not None:
-            self.kernel(rp, ci, v, self.b_cols, self.c_cols)
+            self.kernel(rp, ci, v, self.b_cols, self.c_grp, self.glo, self.ghi)
         else:
-            ops.spmm_csr_cpu(rp, ci, v, self.b_cols, owner.m, owner.k, out=self.c_cols,
-                             options=owner.options)
-        self._exchange(owner, self.c_cols, self.c_counts, self._cc, self.recv_c)
+            ops.spmm_csr_cpu(rp, ci, v, self.b_cols, owner.m, owner.k, out=self.c_grp,
+                             row_begin=self.glo, row_end=self.ghi, options=owner.options)
+        if self.cn > 1:
+            self._exchange(owner, self.c_grp, self.c_counts, self._cc, self.recv_c)
         lo, hi = self.m_rng[r]
-        for p in range(G):
-            src = self.c_cols[lo:hi] if p == r else self.recv_c[p * self.m_r:(p + 1) * self.m_r]
-            _copy_rows(out[:, p * ng:(p + 1) * ng], src)
+        for b in range(self.cn):
+            src = (self.c_grp[lo - self.glo:hi - self.glo] if b == self.c
+                   else self.recv_c[b * self.m_r:(b + 1) * self.m_r])
+            _copy_rows(out[:, b * nb:(b + 1) * nb], src)
         return out
+
+
+NSplitPlan = GridPlan  # the C = G grid (kept name: SURVEY.md §8e alternative (ii))
 
 
 class RowSplitSpmm:
@@ -268,7 +301,8 @@ class RowSplitSpmm:
             self.comm_stream = torch.cuda.Stream(self.device)
         self.gathered = None
         self.halo = None
-        self.ns = None
+        self.ns = None      # the column split (C = G grid), when bound
+        self.grids = {}     # name -> GridPlan (every R x C grid with C > 1), when bound
         self.exchange = "allgather"
         self._bound = None
         self.set_pipeline(pipeline)
@@ -316,8 +350,8 @@ class RowSplitSpmm:
             self.gathered[c, r0:r0 + (hi - lo)].copy_(b_shard[:, c * self.nc:(c + 1) * self.nc])
         if self.halo is not None:
             self.compact[: self.halo.k_own].copy_(b_shard)
-        if self.ns is not None:
-            self.ns.shard.copy_(b_shard)
+        for gp in self.grids.values():
+            gp.shard.copy_(b_shard)
 
     def shard(self) -> torch.Tensor:
         lo, hi = self.k_range
@@ -457,12 +491,21 @@ class RowSplitSpmm:
     def bind(self, row_ptr, col_idx, values, halo: bool = True, full_csr=None):
         """Binds this rank's CSR (`col_idx` in global B row ids; the local slice, or the full CSR
         when local_csr=False).  Remaps the columns for the all-gather layout and, with halo=True,
-        builds the halo plan; with `full_csr=(row_ptr, col_idx, values)` of the WHOLE matrix (and
-        N % G == 0) also the column-split plan.  `step()` then runs the selected exchange."""
+        builds the halo plan; with `full_csr=(row_ptr, col_idx, values)` of the WHOLE matrix also
+        the grid plans: R x C for every C > 1 dividing both G and N (C = G is the column split,
+        "nsplit").  `step()` then runs the selected exchange."""
         cols = {"allgather": self.remap_columns(col_idx)}
-        if full_csr is not None and self.n % self.world == 0:
-            self.ns = NSplitPlan(self, *full_csr)
-            self.ns.shard.copy_(self.shard())
+        self.grids, self.ns = {}, None
+        if full_csr is not None:
+            shard = self.shard()
+            cands = {c for c in range(2, self.world + 1) if self.world % c == 0}
+            cands.add(self.world)  # one rank: the 1 x 1 "column split" (tests)
+            for cn in sorted(cands):
+                if self.n % cn == 0:
+                    gp = GridPlan(self, cn, *full_csr)
+                    gp.shard.copy_(shard)
+                    self.grids[gp.name] = gp
+            self.ns = self.grids.get("nsplit")
         if halo:
             if self.local_csr:
                 mine = col_idx
@@ -531,15 +574,16 @@ class RowSplitSpmm:
     def step(self, out, b_shard=None, events=None):
         """One exchange + local SpMM over the bound CSR with the selected exchange."""
         row_ptr, cols, values = self._bound
-        if self.exchange == "nsplit":
+        if self.exchange in self.grids:
+            gp = self.grids[self.exchange]
             if b_shard is not None:
-                self.ns.shard.copy_(b_shard)
+                gp.shard.copy_(b_shard)
             if events:
                 events[0].record()
-            self.ns.exchange_b(self)
+            gp.exchange_b(self)
             if events:
                 events[1].record()
-            self.ns.compute_and_return(self, out)
+            gp.compute_and_return(self, out)
             if events:
                 events[2].record()
             return out
@@ -561,8 +605,8 @@ class RowSplitSpmm:
         """The exchange alone (phase timing)."""
         if self.exchange == "halo":
             self.halo_exchange()
-        elif self.exchange == "nsplit":
-            self.ns.exchange_b(self)
+        elif self.exchange in self.grids:
+            self.grids[self.exchange].exchange_b(self)
         else:
             self.all_gather_b()
 
@@ -570,18 +614,19 @@ class RowSplitSpmm:
         """The local SpMM alone with the exchanged B resident (phase timing)."""
         if self.exchange == "halo":
             return self.halo_compute(out)
-        if self.exchange == "nsplit":  # local SpMM + the return all-to-all of C
-            return self.ns.compute_and_return(self, out)
+        if self.exchange in self.grids:  # local SpMM + the return of C inside the row group
+            return self.grids[self.exchange].compute_and_return(self, out)
         row_ptr, cols, values = self._bound
         return self.compute(row_ptr, cols["allgather"], values, out)
 
     # -- schedule choice -------------------------------------------------------------------------
     def tune(self, out, pipelines=(1, 2, 4), reps: int = 3, force: bool = False) -> dict:
         """Times every exchange on this node with the real step over the bound CSR: all-gather
-        (ring / point-to-point) x pipeline depth, the halo exchange and the column split if built.  Keeps the
-        fastest.  Timings are max-reduced over ranks, so all ranks choose the same; every
-        candidate produces the same bytes.  Returns {"<comm>/p<C>" | "halo" | "nsplit": ms}.  One rank has
-        nothing to exchange, so it keeps its setting unless `force` (tests)."""
+        (ring / point-to-point) x pipeline depth, the halo exchange and the grid plans if built.
+        Keeps the fastest.  Timings are max-reduced over ranks, so all ranks choose the same; every
+        candidate produces the same bytes.  Returns {"<comm>/p<C>" | "halo" | "nsplit" |
+        "grid<R>x<C>": ms}.  One rank has nothing to exchange, so it keeps its setting unless
+        `force` (tests)."""
         if self._bound is None:
             raise RuntimeError("tune: bind() the CSR first")
         if not self.comm_kind.startswith("rccl") or (self.world == 1 and not force):
@@ -612,11 +657,11 @@ class RowSplitSpmm:
         if self.halo is not None:
             self.exchange, self.comm_kind = "halo", "rccl"
             times["halo"] = measure()
-        if self.ns is not None:
-            self.exchange, self.comm_kind = "nsplit", "rccl"
-            times["nsplit"] = measure()
+        for name in self.grids:
+            self.exchange, self.comm_kind = name, "rccl"
+            times[name] = measure()
         best = min(times, key=times.get)
-        if best in ("halo", "nsplit"):
+        if best == "halo" or best in self.grids:
             self.exchange, self.comm_kind = best, "rccl"
             self.set_pipeline(1)
         else:

@@ -5,7 +5,13 @@ gathered layout) times the full gathered B, exactly what rank r's kernel does af
 exchange.  Reports per-rank ms and the whole-job SpMM-phase GFLOP/s = 2*nnz*N / max_r(ms)
 (the exchange itself needs the G GPUs and is not included).
 
-    python scripts/rank_local.py --config products --world 8
+--cn C > 1 measures the R x C grid exchange (distributed.GridPlan, R = G/C) instead: per row
+group, the SpMM of the group's rows (global-form launch on the whole CSR) against one N/C column
+block of B, plus the rank-local copies of its step (packing the shard into C blocks, unpacking C
+blocks of its output rows).  Those are the grid's compute phase; its two exchanges move
+(G-1)/G * |B|/C and (C-1)/C * |C|/G per rank.
+
+    python scripts/rank_local.py --config products --world 8 [--cn 4]
 """
 import argparse
 import json
@@ -24,7 +30,10 @@ def main():
     ap.add_argument("--config", default="products")
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--cn", type=int, default=1)
     args = ap.parse_args()
+    if args.cn > 1:
+        return grid(args)
     from oneflow_spmm import _C, ops, synth
     from oneflow_spmm.distributed import padded_owner_remap
 
@@ -63,6 +72,68 @@ def main():
     worst = max(x["ms"] for x in res)
     print(json.dumps({"config": args.config, "world": G, "per_rank": res, "max_ms": worst,
                       "spmm_phase_gflops_aggregate": round(2.0 * nnz * n / (worst * 1e-3) / 1e9, 1)}))
+
+
+def _median_ms(fn, reps):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return float(np.median(ts))
+
+
+def grid(args):
+    from oneflow_spmm import _C, ops, synth
+    from oneflow_spmm.distributed import _copy_rows
+
+    cfg = synth.CONFIGS[args.config]
+    m, k, nnz, n, dt = cfg["m"], cfg["k"], cfg["nnz"], cfg["n"], cfg["dtype"]
+    G, C = args.world, args.cn
+    R, nb = G // C, n // C
+    assert G % C == 0 and n % C == 0
+    dev = torch.device("cuda", 0)
+    rp = synth.row_ptr(m, k, nnz)
+    d_rp = torch.from_numpy(rp.astype(np.int32)).to(dev)
+    d_ci = torch.from_numpy(synth.columns(m, k, rp, threads=16)).to(dev)
+    d_v = synth.values(0, nnz, dt).to(dev)
+    b_blk = synth.dense(0, k, n, dt, device=dev)[:, :nb].contiguous()
+    opts = ops.make_options(split=ops.default_split(n))
+    kern = ops.SpmmCsrKernel(m, k, nb, nnz, torch.int32, dt, dev, opts)
+    # rank-local copies of a step, sized for rank 0 (the largest shard / row range)
+    k0 = _C.balanced_range(k, G, 0)[1]
+    m0 = _C.balanced_range(m, G, 0)[1]
+    shard = torch.zeros((k0, n), dtype=dt, device=dev)
+    send_b = torch.empty((C * k0, nb), dtype=dt, device=dev)
+    recv_c = torch.empty((C * m0, nb), dtype=dt, device=dev)
+    out = torch.empty((m0, n), dtype=dt, device=dev)
+
+    def copies():
+        for b in range(C):
+            _copy_rows(send_b[b * k0:(b + 1) * k0], shard[:, b * nb:(b + 1) * nb])
+        for b in range(C):
+            _copy_rows(out[:, b * nb:(b + 1) * nb], recv_c[b * m0:(b + 1) * m0])
+    copy_ms = _median_ms(copies, args.reps)
+    res = []
+    for g in range(R):
+        lo = _C.balanced_range(m, G, g * C)[0]
+        hi = _C.balanced_range(m, G, g * C + C - 1)[1]
+        c_grp = torch.empty((hi - lo, nb), dtype=dt, device=dev)
+        ms = _median_ms(lambda: kern(d_rp, d_ci, d_v, b_blk, c_grp, lo, hi), args.reps)
+        res.append({"row_group": g, "rows": hi - lo, "nnz": int(rp[hi] - rp[lo]), "ms": round(ms, 4)})
+        del c_grp
+    worst = max(x["ms"] for x in res)
+    s_v = torch.empty(0, dtype=dt).element_size()
+    print(json.dumps({"config": args.config, "world": G, "grid": f"{R}x{C}", "block_n": nb,
+                      "per_row_group": res, "max_spmm_ms": worst, "local_copies_ms": round(copy_ms, 4),
+                      "b_bytes_received_per_rank": (k - k0) * nb * s_v,
+                      "c_bytes_received_per_rank": (C - 1) * m0 * nb * s_v,
+                      "spmm_phase_gflops_aggregate": round(2.0 * nnz * n / ((worst + copy_ms) * 1e-3) / 1e9, 1)}))
 
 
 if __name__ == "__main__":

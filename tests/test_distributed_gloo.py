@@ -74,14 +74,21 @@ def _worker(rank, world, port, m, k, n, local_csr, pipeline, density, q):
         ok = ok and torch.equal(rs.compact[: h.k_own], b[klo:khi])
         remote = uniq[(uniq < klo) | (uniq >= khi)]
         ok = ok and torch.equal(rs.compact[h.k_own:], b[remote])
-        # the column split (all-to-all of B to column blocks, SpMM of all rows, C back): same bytes
-        if n % world == 0:
-            rs.bind(lrp, lci, lv, halo=False, full_csr=(rp, ci, v))
-            rs.exchange = "nsplit"
+        # the grids (B to column blocks, SpMM of the row group's rows, C back inside the group;
+        # the column split is the 1 x G grid): same bytes
+        rs.bind(lrp, lci, lv, halo=False, full_csr=(rp, ci, v))
+        want = {("nsplit" if c == world else f"grid{world // c}x{c}") for c in range(2, world + 1)
+                if world % c == 0 and n % c == 0}
+        ok = ok and set(rs.grids) == want and (rs.ns is not None) == (n % world == 0)
+        for name, gp in rs.grids.items():
+            rs.exchange = name
             out4 = torch.full_like(out2, float("nan"))
             rs.step(out4, b_shard=b2[klo:khi])
             ok = ok and np.array_equal(out4.numpy().view(np.uint32), full2[lo:hi].view(np.uint32))
-            ok = ok and torch.equal(rs.ns.b_cols, b2[:, rank * (n // world):(rank + 1) * (n // world)])
+            nb = n // gp.cn
+            ok = ok and torch.equal(gp.b_cols, b2[:, gp.c * nb:(gp.c + 1) * nb])
+            ok = ok and (gp.glo, gp.ghi) == (oracle.balanced_range(m, world, gp.g * gp.cn)[0],
+                                             oracle.balanced_range(m, world, gp.g * gp.cn + gp.cn - 1)[1])
         q.put((rank, bool(ok)))
     finally:
         dist.destroy_process_group()
@@ -92,6 +99,7 @@ def _worker(rank, world, port, m, k, n, local_csr, pipeline, density, q):
     (2, 300, 256, 32, False),   # full CSR broadcast, kernel computes the row range
     (3, 500, 400, 8, True),
     (4, 603, 1001, 16, True),   # 4 ranks: K % 4 = 1, one long shard and three short ones
+    (6, 700, 1003, 12, False),  # 6 ranks: grids 3x2, 2x3 and the 1x6 column split
 ])
 def test_row_split_gloo(world, m, k, n, local_csr):
     _run(world, m, k, n, local_csr, 1, 30)
