@@ -136,12 +136,14 @@ def main():
         klo, khi = rs.k_range
         rs.load_shard(synth.dense(klo, khi, n, dt, device=device))
         full = None
-        if args.exchange == "auto" or args.exchange == "nsplit" or args.exchange.startswith("grid"):
+        pinned_sub = int(args.exchange.split("/s")[1]) if "/s" in args.exchange else 1
+        if args.exchange == "auto" or args.exchange.startswith(("nsplit", "grid")):
             # the grid / column-split candidates need the whole CSR on every rank
             f_ci = torch.from_numpy(synth.columns(m, k, rp_full, threads=threads)).to(device)
             full = (torch.from_numpy(rp_full.astype(np.int32)).to(device), f_ci,
                     synth.values(0, nnz, dt).to(device))
-        rs.bind(d_rp, d_ci, d_v, halo=args.exchange in ("auto", "halo"), full_csr=full)
+        rs.bind(d_rp, d_ci, d_v, halo=args.exchange in ("auto", "halo"), full_csr=full,
+                grid_subs=tuple(sorted({1, 2, pinned_sub})))
         # exchange: all-gather (ring / point-to-point) x pipeline depth (column blocks gathered
         # while the previous block computes), or halo-only rows; measured here, untimed, the
         # fastest kept (every candidate gives the same bytes)
@@ -232,7 +234,8 @@ def main():
     bytes_launch = alg_bytes(rows, nnz_local, n, s_v)
     if rowsplit and rs.exchange in rs.grids:  # the grid's SpMM: its row group x N/C columns
         gp = rs.grids[rs.exchange]
-        bytes_launch = alg_bytes(gp.ghi - gp.glo, int(rp_full[gp.ghi] - rp_full[gp.glo]), gp.ng, s_v)
+        bytes_launch = gp.sub * alg_bytes(gp.ghi - gp.glo, int(rp_full[gp.ghi] - rp_full[gp.glo]),
+                                          gp.w, s_v)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
 
     # HBM-side traffic of the dominant kernel per launch from the committed rocprofv3 PMC summary
@@ -287,8 +290,8 @@ def main():
             "spmm_phase_gflops_aggregate": round(flops / (phase["spmm_ms_max"] * 1e-3) / 1e9, 2),
             # B bytes this rank receives in the exchange phase / its time
             "allgather_gbs_per_rank": round(((rs.halo.halo_rows * n if rs.exchange == "halo" else
-                                              rs.grids[rs.exchange].exchange_rows()[0] *
-                                              rs.grids[rs.exchange].ng if rs.exchange in rs.grids
+                                              rs.grids[rs.exchange].exchange_rows()[0]
+                                              if rs.exchange in rs.grids
                                               else (rs.k_padded - rs.pad) * n) * s_v) /
                                             (phase["gather_ms_max"] * 1e-3) / 1e9, 2)
             if phase["gather_ms_max"] > 0 else None,

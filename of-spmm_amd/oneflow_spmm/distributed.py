@@ -168,17 +168,27 @@ class GridPlan:
     C = 1 is the all-gather itself; C = G is the column split of SURVEY.md §8e alternative (ii)
     ("nsplit").  In between, traffic falls by C while the SpMM's row width shrinks only to N/C
     (the gather runs 512-B rows at 7.7 TB/s but 64-B rows at ~3.9), so the best grid depends on
-    the links and N: `tune()` measures every one.  Every output column is summed in the same order
-    with the full-width hub schedule (split = default_split(N)), so the bits are the row split's."""
+    the links and N: `tune()` measures every one.
 
-    def __init__(self, owner, cn, row_ptr, col_idx, values):
+    sub = S > 1 pipelines the step over S column sub-blocks of N/(C*S): the B exchange of
+    sub-block s+1 and the C return of sub-block s-1 run on the side stream while the SpMM of
+    sub-block s runs (the all-gather's column-block pipelining).  Buffers are
+    sub-block-major so every exchange is contiguous per peer:
+      send_b [S][C][k_r][w]   (w = N/(C*S); block b, sub-block s = columns b*N/C + s*w ..)
+      b_cols [S][K][w]        c_grp [S][group rows][w]        recv_c [S][C][m_r][w]
+    Every output column is summed in the same order with the full-width hub schedule
+    (split = default_split(N)), so the bits are the row split's for every (C, S)."""
+
+    def __init__(self, owner, cn, row_ptr, col_idx, values, sub: int = 1):
         o = owner
         G, r = o.world, o.rank
-        if cn < 1 or G % cn or o.n % cn:
-            raise ValueError(f"GridPlan: {cn} column blocks must divide world {G} and n {o.n}")
-        self.cn, self.rg = cn, G // cn
+        if cn < 1 or G % cn or sub < 1 or o.n % (cn * sub):
+            raise ValueError(f"GridPlan: {cn} column blocks must divide world {G}, and {cn} x {sub} "
+                             f"sub-blocks n {o.n}")
+        self.cn, self.rg, self.sub = cn, G // cn, sub
         self.g, self.c = divmod(r, cn)
-        self.ng = nb = o.n // cn
+        self.ng = o.n // cn
+        self.w = w = self.ng // sub
         self.k_rng = [balanced_range(o.k, G, p) for p in range(G)]
         self.m_rng = [balanced_range(o.m, G, p) for p in range(G)]
         members = range(self.g * cn, self.g * cn + cn)
@@ -186,75 +196,133 @@ class GridPlan:
         k_r = self.k_rng[r][1] - self.k_rng[r][0]
         m_r = self.m_rng[r][1] - self.m_rng[r][0]
         self.k_r, self.m_r = k_r, m_r
+        m_g = self.ghi - self.glo
         dev, dt = o.device, o.dtype
         self.shard = torch.zeros((k_r, o.n), dtype=dt, device=dev)
-        self.send_b = torch.empty((cn * k_r, nb), dtype=dt, device=dev)  # shard, block-major
-        self.b_cols = torch.zeros((o.k, nb), dtype=dt, device=dev)
-        self.c_grp = torch.empty((self.ghi - self.glo, nb), dtype=dt, device=dev)
-        self.recv_c = torch.empty((cn * m_r, nb), dtype=dt, device=dev)
+        self.send_b = torch.empty((sub, cn, k_r, w), dtype=dt, device=dev)
+        self.b_cols = torch.zeros((sub, o.k, w), dtype=dt, device=dev)
+        self.c_grp = torch.empty((sub, m_g, w), dtype=dt, device=dev)
+        self.recv_c = torch.empty((sub, cn, m_r, w), dtype=dt, device=dev)
         self.csr = (row_ptr, col_idx, values)
         peer = [p != r for p in range(G)]
         mate = [p != r and p // cn == self.g for p in range(G)]
         m_of = lambda p: self.m_rng[p][1] - self.m_rng[p][0]  # noqa: E731
-        # (send counts, send offsets, recv counts, recv offsets), in rows of nb elements
-        self.b_counts = ([k_r if peer[p] else 0 for p in range(G)],
-                         [(p % cn) * k_r if peer[p] else 0 for p in range(G)],
-                         [self.k_rng[p][1] - self.k_rng[p][0] if peer[p] else 0 for p in range(G)],
-                         [self.k_rng[p][0] if peer[p] else 0 for p in range(G)])
-        self.c_counts = ([m_of(p) if mate[p] else 0 for p in range(G)],
-                         [self.m_rng[p][0] - self.glo if mate[p] else 0 for p in range(G)],
-                         [m_r if mate[p] else 0 for p in range(G)],
-                         [(p % cn) * m_r if mate[p] else 0 for p in range(G)])
+        # per sub-block: (send counts, send offsets, recv counts, recv offsets) in rows of w
+        # elements, offsets from the start of the buffer (sub-block s adds s * its stride)
+        self.b_counts, self.c_counts = [], []
+        for s in range(sub):
+            self.b_counts.append((
+                [k_r if peer[p] else 0 for p in range(G)],
+                [(s * cn + p % cn) * k_r if peer[p] else 0 for p in range(G)],
+                [self.k_rng[p][1] - self.k_rng[p][0] if peer[p] else 0 for p in range(G)],
+                [s * o.k + self.k_rng[p][0] if peer[p] else 0 for p in range(G)]))
+            self.c_counts.append((
+                [m_of(p) if mate[p] else 0 for p in range(G)],
+                [s * m_g + self.m_rng[p][0] - self.glo if mate[p] else 0 for p in range(G)],
+                [m_r if mate[p] else 0 for p in range(G)],
+                [(s * cn + p % cn) * m_r if mate[p] else 0 for p in range(G)]))
         as_c = lambda v: (ctypes.c_int64 * G)(*v)  # noqa: E731
-        self._cb = tuple(as_c(v) for v in self.b_counts)
-        self._cc = tuple(as_c(v) for v in self.c_counts)
+        self._cb = [tuple(as_c(v) for v in t) for t in self.b_counts]
+        self._cc = [tuple(as_c(v) for v in t) for t in self.c_counts]
         # blocks some peer needs: all of them once there are other row groups
         self.packed = [b for b in range(cn) if b != self.c or self.rg > 1]
         self.kernel = None
+        self.events = None
         if dev.type == "cuda":
-            self.kernel = ops.SpmmCsrKernel(o.m, o.k, nb, col_idx.numel(), o.idx_dtype, dt,
+            self.kernel = ops.SpmmCsrKernel(o.m, o.k, w, col_idx.numel(), o.idx_dtype, dt,
                                             dev, o.options)
+            self.events = ([torch.cuda.Event() for _ in range(sub)],
+                           [torch.cuda.Event() for _ in range(sub)])
 
     @property
     def name(self) -> str:
-        return "nsplit" if self.rg == 1 else f"grid{self.rg}x{self.cn}"
+        base = "nsplit" if self.rg == 1 else f"grid{self.rg}x{self.cn}"
+        return base if self.sub == 1 else f"{base}/s{self.sub}"
 
     def exchange_rows(self) -> tuple:
-        """Rows of N/C elements this rank receives per step: (B rows, C rows)."""
-        return sum(self.b_counts[2]), sum(self.c_counts[2])
+        """Elements this rank receives per step: (of B, of C)."""
+        return (sum(sum(t[2]) for t in self.b_counts) * self.w,
+                sum(sum(t[2]) for t in self.c_counts) * self.w)
 
-    def _exchange(self, owner, send, counts, c_counts, recv):
+    def _cols(self, b, s):
+        lo = b * self.ng + s * self.w
+        return slice(lo, lo + self.w)
+
+    def _exchange(self, owner, send, counts, c_counts, recv, stream=None):
         if owner.comm_kind == "torch":
-            _torch_exchange(send, counts[0], counts[1], recv, counts[2], counts[3], owner.group)
+            _torch_exchange(send.view(-1, self.w), counts[0], counts[1], recv.view(-1, self.w),
+                            counts[2], counts[3], owner.group)
             return
         sc, so, rc, ro = c_counts
-        check(LIB.ofx_exchange_rows(current_stream_handle(recv), owner._comm,
-                                    dtype_code(owner.dtype), self.ng, send.data_ptr(), sc, so,
-                                    recv.data_ptr(), rc, ro), "exchange_rows")
+        s = stream if stream is not None else current_stream_handle(recv)
+        check(LIB.ofx_exchange_rows(s, owner._comm, dtype_code(owner.dtype), self.w,
+                                    send.data_ptr(), sc, so, recv.data_ptr(), rc, ro),
+              "exchange_rows")
 
-    def exchange_b(self, owner):
-        nb, k_r = self.ng, self.k_r
-        for b in self.packed:
-            _copy_rows(self.send_b[b * k_r:(b + 1) * k_r], self.shard[:, b * nb:(b + 1) * nb])
+    def _pack(self, owner):
         lo, hi = self.k_rng[owner.rank]
-        _copy_rows(self.b_cols[lo:hi], self.shard[:, self.c * nb:(self.c + 1) * nb])
-        self._exchange(owner, self.send_b, self.b_counts, self._cb, self.b_cols)
+        for s in range(self.sub):
+            for b in self.packed:
+                _copy_rows(self.send_b[s, b], self.shard[:, self._cols(b, s)])
+            _copy_rows(self.b_cols[s, lo:hi], self.shard[:, self._cols(self.c, s)])
 
-    def compute_and_return(self, owner, out):
-        nb, r = self.ng, owner.rank
+    def _spmm(self, owner, s):
         rp, ci, v = self.csr
         if self.kernel is not None:
-            self.kernel(rp, ci, v, self.b_cols, self.c_grp, self.glo, self.ghi)
+            self.kernel(rp, ci, v, self.b_cols[s], self.c_grp[s], self.glo, self.ghi)
         else:
-            ops.spmm_csr_cpu(rp, ci, v, self.b_cols, owner.m, owner.k, out=self.c_grp,
+            ops.spmm_csr_cpu(rp, ci, v, self.b_cols[s], owner.m, owner.k, out=self.c_grp[s],
                              row_begin=self.glo, row_end=self.ghi, options=owner.options)
-        if self.cn > 1:
-            self._exchange(owner, self.c_grp, self.c_counts, self._cc, self.recv_c)
-        lo, hi = self.m_rng[r]
-        for b in range(self.cn):
-            src = (self.c_grp[lo - self.glo:hi - self.glo] if b == self.c
-                   else self.recv_c[b * self.m_r:(b + 1) * self.m_r])
-            _copy_rows(out[:, b * nb:(b + 1) * nb], src)
+
+    def _unpack(self, owner, out):
+        lo, hi = self.m_rng[owner.rank]
+        for s in range(self.sub):
+            for b in range(self.cn):
+                src = (self.c_grp[s, lo - self.glo:hi - self.glo] if b == self.c
+                       else self.recv_c[s, b])
+                _copy_rows(out[:, self._cols(b, s)], src)
+
+    def exchange_b(self, owner):
+        """Phase 1 alone, every sub-block, on the current stream (phase timing)."""
+        self._pack(owner)
+        for s in range(self.sub):
+            self._exchange(owner, self.send_b, self.b_counts[s], self._cb[s], self.b_cols)
+
+    def compute_and_return(self, owner, out):
+        """Phases 2 and 3 on the current stream, B exchanged (phase timing)."""
+        for s in range(self.sub):
+            self._spmm(owner, s)
+            if self.cn > 1:
+                self._exchange(owner, self.c_grp, self.c_counts[s], self._cc[s], self.recv_c)
+        self._unpack(owner, out)
+        return out
+
+    def step(self, owner, out):
+        """The whole step; with sub-blocks on a GPU, exchanges on the side stream overlap the
+        SpMMs (HIP events order them)."""
+        if self.sub == 1 or self.kernel is None or owner.comm_kind == "torch":
+            self.exchange_b(owner)
+            return self.compute_and_return(owner, out)
+        cur = torch.cuda.current_stream(owner.device)
+        cs = owner.comm_stream
+        side = ctypes.c_void_p(cs.cuda_stream)
+        ev_b, ev_c = self.events
+        self._pack(owner)
+        cs.wait_stream(cur)  # packed shard; the previous step's reads of c_grp/recv_c are done
+        for s in range(self.sub):
+            self._exchange(owner, self.send_b, self.b_counts[s], self._cb[s], self.b_cols, side)
+            ev_b[s].record(cs)
+        for s in range(self.sub):
+            cur.wait_event(ev_b[s])
+            self._spmm(owner, s)
+            if self.cn > 1:
+                ev_c[s].record(cur)
+                cs.wait_event(ev_c[s])
+                self._exchange(owner, self.c_grp, self.c_counts[s], self._cc[s], self.recv_c, side)
+        cur.wait_stream(cs)
+        self._unpack(owner, out)
+        for t in (self.send_b, self.b_cols, self.c_grp, self.recv_c):
+            t.record_stream(cs)
         return out
 
 
@@ -488,12 +556,13 @@ class RowSplitSpmm:
         return out
 
     # -- bound form: this rank's CSR once, every exchange layout prepared ------------------------
-    def bind(self, row_ptr, col_idx, values, halo: bool = True, full_csr=None):
+    def bind(self, row_ptr, col_idx, values, halo: bool = True, full_csr=None, grid_subs=(1,)):
         """Binds this rank's CSR (`col_idx` in global B row ids; the local slice, or the full CSR
         when local_csr=False).  Remaps the columns for the all-gather layout and, with halo=True,
         builds the halo plan; with `full_csr=(row_ptr, col_idx, values)` of the WHOLE matrix also
-        the grid plans: R x C for every C > 1 dividing both G and N (C = G is the column split,
-        "nsplit").  `step()` then runs the selected exchange."""
+        the grid plans: R x C for every C > 1 dividing G, times every sub-block depth S in
+        `grid_subs` with C*S | N (C = G is the column split, "nsplit").  `step()` then runs the
+        selected exchange."""
         cols = {"allgather": self.remap_columns(col_idx)}
         self.grids, self.ns = {}, None
         if full_csr is not None:
@@ -501,10 +570,11 @@ class RowSplitSpmm:
             cands = {c for c in range(2, self.world + 1) if self.world % c == 0}
             cands.add(self.world)  # one rank: the 1 x 1 "column split" (tests)
             for cn in sorted(cands):
-                if self.n % cn == 0:
-                    gp = GridPlan(self, cn, *full_csr)
-                    gp.shard.copy_(shard)
-                    self.grids[gp.name] = gp
+                for sub in grid_subs:
+                    if self.n % (cn * sub) == 0:
+                        gp = GridPlan(self, cn, *full_csr, sub=sub)
+                        gp.shard.copy_(shard)
+                        self.grids[gp.name] = gp
             self.ns = self.grids.get("nsplit")
         if halo:
             if self.local_csr:
@@ -578,14 +648,13 @@ class RowSplitSpmm:
             gp = self.grids[self.exchange]
             if b_shard is not None:
                 gp.shard.copy_(b_shard)
-            if events:
-                events[0].record()
+            if not events:
+                return gp.step(self, out)
+            events[0].record()
             gp.exchange_b(self)
-            if events:
-                events[1].record()
+            events[1].record()
             gp.compute_and_return(self, out)
-            if events:
-                events[2].record()
+            events[2].record()
             return out
         if self.exchange == "halo":
             if events:
@@ -624,8 +693,8 @@ class RowSplitSpmm:
         """Times every exchange on this node with the real step over the bound CSR: all-gather
         (ring / point-to-point) x pipeline depth, the halo exchange and the grid plans if built.
         Keeps the fastest.  Timings are max-reduced over ranks, so all ranks choose the same; every
-        candidate produces the same bytes.  Returns {"<comm>/p<C>" | "halo" | "nsplit" |
-        "grid<R>x<C>": ms}.  One rank has nothing to exchange, so it keeps its setting unless
+        candidate produces the same bytes.  Returns {"<comm>/p<C>" | "halo" | "nsplit[/s<S>]" |
+        "grid<R>x<C>[/s<S>]": ms}.  One rank has nothing to exchange, so it keeps its setting unless
         `force` (tests)."""
         if self._bound is None:
             raise RuntimeError("tune: bind() the CSR first")

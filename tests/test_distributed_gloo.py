@@ -76,9 +76,10 @@ def _worker(rank, world, port, m, k, n, local_csr, pipeline, density, q):
         ok = ok and torch.equal(rs.compact[h.k_own:], b[remote])
         # the grids (B to column blocks, SpMM of the row group's rows, C back inside the group;
         # the column split is the 1 x G grid): same bytes
-        rs.bind(lrp, lci, lv, halo=False, full_csr=(rp, ci, v))
-        want = {("nsplit" if c == world else f"grid{world // c}x{c}") for c in range(2, world + 1)
-                if world % c == 0 and n % c == 0}
+        # (and S = 2 sub-blocks, the pipelined form's layout)
+        rs.bind(lrp, lci, lv, halo=False, full_csr=(rp, ci, v), grid_subs=(1, 2))
+        want = {("nsplit" if c == world else f"grid{world // c}x{c}") + ("" if s == 1 else f"/s{s}")
+                for c in range(2, world + 1) for s in (1, 2) if world % c == 0 and n % (c * s) == 0}
         ok = ok and set(rs.grids) == want and (rs.ns is not None) == (n % world == 0)
         for name, gp in rs.grids.items():
             rs.exchange = name
@@ -86,7 +87,9 @@ def _worker(rank, world, port, m, k, n, local_csr, pipeline, density, q):
             rs.step(out4, b_shard=b2[klo:khi])
             ok = ok and np.array_equal(out4.numpy().view(np.uint32), full2[lo:hi].view(np.uint32))
             nb = n // gp.cn
-            ok = ok and torch.equal(gp.b_cols, b2[:, gp.c * nb:(gp.c + 1) * nb])
+            for s in range(gp.sub):
+                c0 = gp.c * nb + s * gp.w
+                ok = ok and torch.equal(gp.b_cols[s], b2[:, c0:c0 + gp.w])
             ok = ok and (gp.glo, gp.ghi) == (oracle.balanced_range(m, world, gp.g * gp.cn)[0],
                                              oracle.balanced_range(m, world, gp.g * gp.cn + gp.cn - 1)[1])
         q.put((rank, bool(ok)))

@@ -293,11 +293,11 @@ def test_row_split_rccl_single_rank(device):
             assert_bitwise(out2, oracle_spmm(rp, ci, v, b), f"{kind} pipeline {chunks}")
         # the setup-time choice runs every candidate step and keeps one; output stays exact
         d = (rp.to(device), ci.to(device), v.to(device))
-        rs.bind(*d, halo=True, full_csr=d)
+        rs.bind(*d, halo=True, full_csr=d, grid_subs=(1, 4))
         assert rs.halo.halo_rows == 0 and rs.halo.k_compact == k  # one rank owns every row
         times = rs.tune(out2, reps=1, force=True)
-        assert len(times) == 8 and "halo" in times and "nsplit" in times
-        for exchange in ("allgather", "halo", "nsplit"):
+        assert len(times) == 9 and "halo" in times and "nsplit" in times and "nsplit/s4" in times
+        for exchange in ("allgather", "halo", "nsplit", "nsplit/s4"):
             rs.exchange = exchange
             out2.fill_(float("nan"))
             rs.step(out2)
@@ -355,9 +355,10 @@ def test_row_split_step_hipgraph_capture(device):
         rs = RowSplitSpmm(m, k, n, ci.numel(), torch.float32, torch.int32, device)
         rs.load_shard(b1.to(device))
         d = (rp.to(device), ci.to(device), v.to(device))
-        rs.bind(*d, halo=True, full_csr=d)
+        rs.bind(*d, halo=True, full_csr=d, grid_subs=(1, 2))
         out = torch.empty((m, n), device=device)
-        for exchange, chunks in (("allgather", 1), ("allgather", 2), ("halo", 1), ("nsplit", 1)):
+        for exchange, chunks in (("allgather", 1), ("allgather", 2), ("halo", 1), ("nsplit", 1),
+                                 ("nsplit/s2", 1)):
             rs.exchange = exchange
             rs.set_pipeline(chunks)
             rs.load_shard(b1.to(device))
