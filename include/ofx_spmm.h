@@ -90,6 +90,12 @@ typedef struct ofx_spmm_options {
                             * > t first, then the rest in index order;                       *
                             * t = this; 0 = auto (5x mean degree); < 0 = index order.  No    *
                             * numeric effect.                                                */
+  int32_t planned;         /* != 0: the workspace already holds the work list that           *
+                            * ofx_spmm_csr_plan built for this row_ptr (unchanged since),    *
+                            * row range, m, n, nnz and options; the launch skips planning.   *
+                            * Only for a static graph (the plan-once / compute-many pattern  *
+                            * of a bound CSR).  No numeric effect.                           */
+  int32_t reserved;        /* 0                                                              */
 } ofx_spmm_options;
 
 /* The default split threshold for dense width n (a fixed function of n; part of the numeric
@@ -112,6 +118,16 @@ int ofx_spmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t 
                  const void* b, int64_t ldb, void* c, int64_t ldc, int64_t row_begin,
                  int64_t row_end, void* workspace, size_t workspace_bytes,
                  const ofx_spmm_options* opts);
+
+/* Plans rows [row_begin, row_end) into `workspace` (the hub chunks and degree-binned work list
+ * every ofx_spmm_csr launch otherwise builds first: three small kernels over row_ptr), so that
+ * launches with opts->planned != 0 on the same row_ptr, range, shapes and options skip it.
+ * Asynchronous on `stream`; the same workspace size as ofx_spmm_csr.  A problem that needs no
+ * plan (workspace size 0) is a no-op.  No reference counterpart (OneFlow re-plans per call); the
+ * pattern is cuSPARSE's SpMM_preprocess.                                                     */
+int ofx_spmm_csr_plan(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k, int64_t n,
+                      int64_t nnz, const void* row_ptr, int64_t row_begin, int64_t row_end,
+                      void* workspace, size_t workspace_bytes, const ofx_spmm_options* opts);
 
 /* Fused epilogue: out = act(A @ B + bias), bit-identical to the
  * composition spmm_csr -> bias_add (BroadcastElementwiseBinary kAdd over axis 1,

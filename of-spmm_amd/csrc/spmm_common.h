@@ -122,11 +122,13 @@ struct Schedule {
   int64_t heavy;  // degree-bin threshold for the device work order (no numeric effect);
                   // 0 = auto, INT64_MAX = off
   int32_t variant;
+  int32_t planned;  // the workspace holds this launch's plan (ofx_spmm_csr_plan): skip planning
 };
 
 static inline Schedule resolve_schedule(int64_t n, const ofx_spmm_options* o) {
   Schedule s;
   s.variant = o ? o->variant : 0;
+  s.planned = o ? o->planned : 0;
   const int64_t h = o ? o->heavy_threshold : 0;
   s.heavy = h > 0 ? h : (h < 0 ? INT64_MAX : 0);  // 0 = auto (device launch: 5x mean degree)
   if (o && o->ordered) {

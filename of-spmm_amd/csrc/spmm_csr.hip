@@ -269,7 +269,16 @@ __global__ void __launch_bounds__(64 * K::WPB)
   }
 }
 
-template <typename T>
+// ---- hub reduce: C[hub row] = ((0 + part[chunk 0]) + part[chunk 1]) + ... (chunk order) ---------
+// One group of L lanes per hub (64/L hubs per wave); each lane owns VEC consecutive columns and
+// reads them as one 16-B vector per partial row, kPre partial rows in flight before the in-order
+// adds.  Memory-level parallelism is what bounds this pass (Reddit: ~450k chunk partials of 1 KB):
+// a 256-thread block per hub with 4-B loads ran at 3.1 TB/s; 16-B loads over 64/L hubs per wave
+// keep 4x the bytes in flight (Reddit 148 -> 125 us, products unchanged at 33 us; a separate
+// one-lane-per-column kernel with 64 partials in flight for hubs of > 64 chunks measured slower
+// for both, 45 / 147 us, and was dropped).
+
+template <typename T, int VEC, int L>
 __global__ void __launch_bounds__(kBlock)
     spmm_reduce_kernel(const unsigned long long* __restrict__ counters,
                        const int64_t* __restrict__ hubs,
@@ -277,27 +286,78 @@ __global__ void __launch_bounds__(kBlock)
                        int64_t ldc, int64_t n, const T* __restrict__ bias, int act) {
 #pragma clang fp contract(off)
   using A = typename Num<T>::acc;
-  constexpr int kPre = 16;  // partial rows in flight per thread (the adds stay in chunk order)
+  using P = Pack<A, VEC>;
+  constexpr int kPre = 16;  // partial rows in flight per lane (the adds stay in chunk order)
   const int64_t nhubs = (int64_t)counters[1];
-  for (int64_t h = blockIdx.x; h < nhubs; h += gridDim.x) {
+  const int gl = threadIdx.x % L;
+  const int64_t groups = (int64_t)gridDim.x * (kBlock / L);
+  for (int64_t h = (int64_t)blockIdx.x * (kBlock / L) + threadIdx.x / L; h < nhubs; h += groups) {
     const int64_t lr = hubs[3 * h + 0];
     const int64_t slot = hubs[3 * h + 1];
     const int64_t nc = hubs[3 * h + 2];
-    for (int64_t c = threadIdx.x; c < n; c += kBlock) {
+    for (int64_t c = (int64_t)gl * VEC; c < n; c += (int64_t)L * VEC) {
       const A* p = part + slot * n + c;
-      A acc = A(0);
+      A acc[VEC];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) acc[e] = A(0);
       int64_t q = 0;
       for (; q + kPre <= nc; q += kPre) {
-        A v[kPre];
+        P v[kPre];
 #pragma unroll
-        for (int u = 0; u < kPre; ++u) v[u] = p[(q + u) * n];
+        for (int u = 0; u < kPre; ++u) v[u] = *reinterpret_cast<const P*>(p + (q + u) * n);
 #pragma unroll
-        for (int u = 0; u < kPre; ++u) acc = acc + v[u];
+        for (int u = 0; u < kPre; ++u) {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + v[u].v[e];
+        }
       }
-      for (; q < nc; ++q) acc = acc + p[q * n];
-      C[lr * ldc + c] = epilogue<T>(acc, bias, c, act);
+      for (; q < nc; ++q) {
+        const P v = *reinterpret_cast<const P*>(p + q * n);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + v.v[e];
+      }
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) C[lr * ldc + c + e] = epilogue<T>(acc[e], bias, c + e, act);
     }
   }
+}
+
+template <typename T, int VEC>
+int launch_reduce_vec(hipStream_t s, int64_t max_hubs, int64_t n,
+                      const unsigned long long* counters, const int64_t* hubs,
+                      const typename Num<T>::acc* part, T* C, int64_t ldc, const T* bias, int act) {
+  const int64_t lanes = (n + VEC - 1) / VEC;
+  int l = 4;
+  while (l < 64 && l < lanes) l *= 2;
+  const int64_t per_block = kBlock / l;
+  int64_t grid = (max_hubs + per_block - 1) / per_block;
+  if (grid > kMaxReduceBlocks) grid = kMaxReduceBlocks;
+#define OFX_REDUCE(LL)                                                                        \
+  hipLaunchKernelGGL((spmm_reduce_kernel<T, VEC, LL>), dim3((unsigned)grid), dim3(kBlock), 0, s, \
+                     counters, hubs, part, C, ldc, n, bias, act)
+  switch (l) {
+    case 4: OFX_REDUCE(4); break;
+    case 8: OFX_REDUCE(8); break;
+    case 16: OFX_REDUCE(16); break;
+    case 32: OFX_REDUCE(32); break;
+    default: OFX_REDUCE(64); break;
+  }
+#undef OFX_REDUCE
+  OFX_HIP_CHECK(hipGetLastError());
+  return OFX_OK;
+}
+
+// 16-B partial loads when every partial row starts 16-B aligned (the workspace base is 256-B
+// aligned and rows are n accumulators apart), else one accumulator per lane.
+template <typename T>
+int launch_reduce(hipStream_t s, int64_t max_hubs, int64_t n, const unsigned long long* counters,
+                  const int64_t* hubs, const typename Num<T>::acc* part, T* C, int64_t ldc,
+                  const T* bias, int act) {
+  using A = typename Num<T>::acc;
+  constexpr int kVec = 16 / (int)sizeof(A);
+  if ((n * (int64_t)sizeof(A)) % 16 == 0)
+    return launch_reduce_vec<T, kVec>(s, max_hubs, n, counters, hubs, part, C, ldc, bias, act);
+  return launch_reduce_vec<T, 1>(s, max_hubs, n, counters, hubs, part, C, ldc, bias, act);
 }
 
 // ---- validation / slicing / synthetic dense ------------------------------------------------
@@ -388,9 +448,13 @@ int launch_cfg(const Launch& L) {
     OFX_REQUIRE(L.ws != nullptr && L.ws_bytes >= w.total, OFX_EWORKSPACE,
                 "spmm_csr: workspace of %zu bytes is smaller than the %zu bytes required",
                 L.ws_bytes, w.total);
-    const int rc = launch_plan<I>(L.stream, rp, L.row_begin, L.nrows, L.nnz, L.sched, w,
-                                  static_cast<char*>(L.ws), &wl);
-    if (rc) return rc;
+    if (L.sched.planned) {
+      plan::worklist_of(w, static_cast<char*>(L.ws), &wl);
+    } else {
+      const int rc = launch_plan<I>(L.stream, rp, L.row_begin, L.nrows, L.nnz, L.sched, w,
+                                    static_cast<char*>(L.ws), &wl);
+      if (rc) return rc;
+    }
   }
   unsigned long long* counters = wl.counters;
   int64_t *hub = wl.hubs, *items = wl.items, *order = wl.order;
@@ -405,12 +469,9 @@ int launch_cfg(const Launch& L) {
                      plan ? L.sched.chunk : INT64_MAX, counters, items, order, part,
                      static_cast<const T*>(L.bias), L.act);
   OFX_HIP_CHECK(hipGetLastError());
-  if (plan && w.max_hubs > 0) {
-    const int64_t rgrid = w.max_hubs < kMaxReduceBlocks ? w.max_hubs : kMaxReduceBlocks;
-    hipLaunchKernelGGL((spmm_reduce_kernel<T>), dim3((unsigned)rgrid), dim3(kBlock), 0, L.stream,
-                       counters, hub, part, C, L.ldc, L.n, static_cast<const T*>(L.bias), L.act);
-    OFX_HIP_CHECK(hipGetLastError());
-  }
+  if (plan && w.max_hubs > 0)
+    return launch_reduce<T>(L.stream, w.max_hubs, L.n, counters, hub, part, C, L.ldc,
+                            static_cast<const T*>(L.bias), L.act);
   return OFX_OK;
 }
 
@@ -570,6 +631,34 @@ extern "C" int ofx_spmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t 
   return spmm_entry(stream, idx_dtype, val_dtype, m, k, n, nnz, row_ptr, col_idx, values, b, ldb,
                     c, ldc, row_begin, row_end, nullptr, OFX_ACT_NONE, workspace, workspace_bytes,
                     opts);
+}
+
+extern "C" int ofx_spmm_csr_plan(void* stream, int idx_dtype, int val_dtype, int64_t m,
+                                 int64_t k, int64_t n, int64_t nnz, const void* row_ptr,
+                                 int64_t row_begin, int64_t row_end, void* workspace,
+                                 size_t workspace_bytes, const ofx_spmm_options* opts) {
+  int rc = check_common(idx_dtype, val_dtype, m, k, n, nnz);
+  if (rc) return rc;
+  OFX_REQUIRE(0 <= row_begin && row_begin <= row_end && row_end <= m, OFX_EINVAL,
+              "spmm_csr_plan: row range [%lld, %lld) outside [0, %lld)", (long long)row_begin,
+              (long long)row_end, (long long)m);
+  const int64_t nrows = row_end - row_begin;
+  if (nrows == 0 || n == 0) return OFX_OK;  // the launch writes nothing either
+  const Schedule s = resolve_schedule(n, opts);
+  const plan::WsLayout w = plan::ws_layout(nrows, nnz, n, acc_bytes_of(val_dtype), s);
+  if (w.total == 0) return OFX_OK;  // identity work list: nothing to plan
+  OFX_REQUIRE(row_ptr != nullptr, OFX_EINVAL, "spmm_csr_plan: NULL row_ptr");
+  OFX_REQUIRE(workspace != nullptr && workspace_bytes >= w.total, OFX_EWORKSPACE,
+              "spmm_csr_plan: workspace of %zu bytes is smaller than the %zu bytes required",
+              workspace_bytes, w.total);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  plan::WorkList wl{};
+  char* ws = static_cast<char*>(workspace);
+  if (idx_dtype == OFX_DT_INT32)
+    return plan::launch_plan<int32_t>(st, static_cast<const int32_t*>(row_ptr), row_begin, nrows,
+                                      nnz, s, w, ws, &wl);
+  return plan::launch_plan<int64_t>(st, static_cast<const int64_t*>(row_ptr), row_begin, nrows,
+                                    nnz, s, w, ws, &wl);
 }
 
 extern "C" int ofx_spmm_csr_fused(void* stream, int idx_dtype, int val_dtype, int64_t m,

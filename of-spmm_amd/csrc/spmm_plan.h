@@ -230,6 +230,15 @@ struct WorkList {
   void* part;
 };
 
+// The work list's pointers inside workspace `ws` laid out as `w` (a plan built earlier).
+inline void worklist_of(const WsLayout& w, char* ws, WorkList* wl) {
+  wl->counters = reinterpret_cast<unsigned long long*>(ws + w.counters);
+  wl->hubs = reinterpret_cast<int64_t*>(ws + w.hubs);
+  wl->items = reinterpret_cast<int64_t*>(ws + w.items);
+  wl->order = reinterpret_cast<int64_t*>(ws + w.order);
+  wl->part = ws + w.part;
+}
+
 // Launches plan_count / plan_scan / plan_write on `stream` into workspace `ws` laid out as `w`.
 template <typename I>
 int launch_plan(hipStream_t stream, const I* rp, int64_t row_begin, int64_t nrows, int64_t nnz,
@@ -241,11 +250,7 @@ int launch_plan(hipStream_t stream, const I* rp, int64_t row_begin, int64_t nrow
     const int64_t mean = nrows > 0 ? (nnz + nrows - 1) / nrows : 1;
     heavy = 5 * mean < 16 ? 16 : 5 * mean;
   }
-  wl->counters = reinterpret_cast<unsigned long long*>(ws + w.counters);
-  wl->hubs = reinterpret_cast<int64_t*>(ws + w.hubs);
-  wl->items = reinterpret_cast<int64_t*>(ws + w.items);
-  wl->order = reinterpret_cast<int64_t*>(ws + w.order);
-  wl->part = ws + w.part;
+  worklist_of(w, ws, wl);
   auto* block_tot = reinterpret_cast<int64_t*>(ws + w.block_tot);
   const unsigned pgrid = (unsigned)w.plan_blocks;
   hipLaunchKernelGGL((spmm_plan_count_kernel<I>), dim3(pgrid), dim3(kBlock), 0, stream, rp,

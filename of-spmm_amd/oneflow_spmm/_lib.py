@@ -31,7 +31,8 @@ class OfxError(RuntimeError):
 class Options(ctypes.Structure):
     _fields_ = [("split_threshold", ctypes.c_int64), ("chunk", ctypes.c_int64),
                 ("ordered", ctypes.c_int32), ("variant", ctypes.c_int32),
-                ("heavy_threshold", ctypes.c_int64)]
+                ("heavy_threshold", ctypes.c_int64), ("planned", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 class TensorDesc(ctypes.Structure):
@@ -57,6 +58,7 @@ def _load():
         "ofx_spmm_csr_workspace_size": ([i32, i32, i64, i64, i64, i64, popt, ctypes.POINTER(sz)], i32),
         "ofx_spmm_csr": ([p, i32, i32, i64, i64, i64, i64, p, p, p, p, i64, p, i64, i64, i64, p, sz,
                           popt], i32),
+        "ofx_spmm_csr_plan": ([p, i32, i32, i64, i64, i64, i64, p, i64, i64, p, sz, popt], i32),
         "ofx_spmm_csr_fused": ([p, i32, i32, i64, i64, i64, i64, p, p, p, p, i64, p, i64, i64, i64,
                                 p, i32, p, sz, popt], i32),
         "ofx_spmm_csr_fused_cpu": ([i32, i32, i32, i64, i64, i64, i64, p, p, p, p, i64, p, i64, i64,

@@ -230,7 +230,7 @@ class GridPlan:
         self.events = None
         if dev.type == "cuda":
             self.kernel = ops.SpmmCsrKernel(o.m, o.k, w, col_idx.numel(), o.idx_dtype, dt,
-                                            dev, o.options)
+                                            dev, o.options).plan(row_ptr, self.glo, self.ghi)
             self.events = ([torch.cuda.Event() for _ in range(sub)],
                            [torch.cuda.Event() for _ in range(sub)])
 
@@ -269,7 +269,7 @@ class GridPlan:
     def _spmm(self, owner, s):
         rp, ci, v = self.csr
         if self.kernel is not None:
-            self.kernel(rp, ci, v, self.b_cols[s], self.c_grp[s], self.glo, self.ghi)
+            self.kernel(rp, ci, v, self.b_cols[s], self.c_grp[s], self.glo, self.ghi, planned=True)
         else:
             ops.spmm_csr_cpu(rp, ci, v, self.b_cols[s], owner.m, owner.k, out=self.c_grp[s],
                              row_begin=self.glo, row_end=self.ghi, options=owner.options)
@@ -373,6 +373,7 @@ class RowSplitSpmm:
         self.grids = {}     # name -> GridPlan (every R x C grid with C > 1), when bound
         self.exchange = "allgather"
         self._bound = None
+        self.kernel = None
         self.set_pipeline(pipeline)
         if comm.startswith("rccl"):
             self._init_rccl()
@@ -395,8 +396,19 @@ class RowSplitSpmm:
         if self.device.type == "cuda":
             self.kernel = ops.SpmmCsrKernel(m_kernel, self.k_padded, self.nc, self.nnz_local,
                                             self.idx_dtype, self.dtype, self.device, self.options)
+            if self._bound is not None:
+                self.kernel.plan(self._bound[0], *self._rows())
         if shard is not None:
             self.load_shard(shard)
+
+    def _rows(self):
+        """The kernel's row range: local rows of a local CSR, or this rank's rows of the full one."""
+        lo, hi = self.row_range
+        return (0, hi - lo) if self.local_csr else (lo, hi)
+
+    def _planned(self, row_ptr) -> bool:
+        """Launches over the bound CSR reuse the plan built at bind()."""
+        return self._bound is not None and row_ptr is self._bound[0]
 
     def block(self, c: int) -> torch.Tensor:
         """Gathered B, column block c: [K_pad, N/C] contiguous."""
@@ -489,10 +501,11 @@ class RowSplitSpmm:
 
     def compute_block(self, c, row_ptr, col_idx, values, out, stream=None):
         lo, hi = self.row_range
-        rb, re = (0, hi - lo) if self.local_csr else (lo, hi)
+        rb, re = self._rows()
         o = out[:, c * self.nc:(c + 1) * self.nc]
         if self.kernel is not None:
-            self.kernel(row_ptr, col_idx, values, self.gathered[c], o, rb, re, stream=stream)
+            self.kernel(row_ptr, col_idx, values, self.gathered[c], o, rb, re, stream=stream,
+                        planned=self._planned(row_ptr))
         else:
             m_kernel = hi - lo if self.local_csr else self.m
             ops.spmm_csr_cpu(row_ptr, col_idx, values, self.gathered[c], m_kernel, self.k_padded,
@@ -519,6 +532,7 @@ class RowSplitSpmm:
             # the whole step in one C-ABI call: in-place all-gather + local SpMM
             kern = self.kernel
             blk = self.gathered[0]
+            opts = kern.launch_options(row_ptr, 0, hi - lo, self._planned(row_ptr))
             check(LIB.ofx_spmm_rowsplit(current_stream_handle(blk), self._comm, kern.idx_dt,
                                         kern.val_dt, hi - lo, self.k_padded, self.n, kern.nnz,
                                         row_ptr.data_ptr(),
@@ -526,7 +540,7 @@ class RowSplitSpmm:
                                         values.data_ptr() if values.numel() else None,
                                         blk.data_ptr(), out.data_ptr(), out.stride(0),
                                         kern.workspace.data_ptr(), kern.ws_bytes,
-                                        ctypes.byref(kern.options) if kern.options else None),
+                                        ctypes.byref(opts) if opts else None),
                   "spmm_rowsplit")
             return out
         if events:
@@ -600,9 +614,11 @@ class RowSplitSpmm:
                 self.halo_kernel = ops.SpmmCsrKernel(rows_local if self.local_csr else self.m,
                                                      self.halo.k_compact, self.n, col_idx.numel(),
                                                      self.idx_dtype, self.dtype, self.device,
-                                                     self.options)
+                                                     self.options).plan(row_ptr, *self._rows())
             self.compact[: self.halo.k_own].copy_(self.shard())
         self._bound = (row_ptr, cols, values)
+        if self.kernel is not None:
+            self.kernel.plan(row_ptr, *self._rows())
 
     def halo_exchange(self, b_shard=None):
         """Pack the rows each peer asked for, then grouped send/recv into the compact buffer."""
@@ -633,7 +649,7 @@ class RowSplitSpmm:
         lo, hi = self.row_range
         rb, re = (0, hi - lo) if self.local_csr else (lo, hi)
         if self.halo_kernel is not None:
-            self.halo_kernel(row_ptr, cols["halo"], values, self.compact, out, rb, re)
+            self.halo_kernel(row_ptr, cols["halo"], values, self.compact, out, rb, re, planned=True)
         else:
             m_kernel = hi - lo if self.local_csr else self.m
             ops.spmm_csr_cpu(row_ptr, cols["halo"], values, self.compact, m_kernel,

@@ -16,9 +16,11 @@ INT64_MAX = (1 << 63) - 1
 
 
 def make_options(split: int = 0, chunk: int = 0, ordered: bool = False, variant: int = 0,
-                 heavy: int = 0) -> Options:
-    """heavy: rows longer than this (not split) are scheduled first; 0 = default, <0 = off."""
-    return Options(int(split), int(chunk), 1 if ordered else 0, int(variant), int(heavy))
+                 heavy: int = 0, planned: bool = False) -> Options:
+    """heavy: rows longer than this (not split) are scheduled first; 0 = default, <0 = off.
+    planned: the workspace holds ofx_spmm_csr_plan's work list (see SpmmCsrKernel.plan)."""
+    return Options(int(split), int(chunk), 1 if ordered else 0, int(variant), int(heavy),
+                   1 if planned else 0, 0)
 
 
 def default_split(n: int) -> int:
@@ -35,7 +37,12 @@ def workspace_size(idx_dtype: torch.dtype, val_dtype: torch.dtype, m: int, k: in
 
 
 class SpmmCsrKernel:
-    """Holds the workspace for repeated launches of one problem shape (the OneFlow tmp buffer)."""
+    """Holds the workspace for repeated launches of one problem shape (the OneFlow tmp buffer).
+
+    plan(row_ptr, row_begin, row_end) builds the work list once (ofx_spmm_csr_plan) for a static
+    graph; launches with planned=True on that same row_ptr tensor and row range then skip the
+    three planning kernels.  The caller promises row_ptr's contents have not changed (a bound
+    CSR); the tensor identity and range are checked here."""
 
     def __init__(self, m: int, k: int, n: int, nnz: int, idx_dtype: torch.dtype,
                  val_dtype: torch.dtype, device, options: Options | None = None):
@@ -45,12 +52,38 @@ class SpmmCsrKernel:
         ws = workspace_size(idx_dtype, val_dtype, m, k, n, nnz, options)
         self.workspace = torch.empty(max(ws, 1), dtype=torch.uint8, device=device)
         self.ws_bytes = ws
+        self._planned_for = None
+        self._planned_opts = None
+
+    def plan(self, row_ptr, row_begin=0, row_end=None, stream=None):
+        row_end = self.m if row_end is None else row_end
+        s = stream if stream is not None else current_stream_handle(row_ptr)
+        check(LIB.ofx_spmm_csr_plan(s, self.idx_dt, self.val_dt, self.m, self.k, self.n, self.nnz,
+                                    row_ptr.data_ptr(), row_begin, row_end,
+                                    self.workspace.data_ptr(), self.ws_bytes,
+                                    ctypes.byref(self.options) if self.options else None),
+              "spmm_csr_plan")
+        o = self.options or Options()
+        self._planned_opts = Options(o.split_threshold, o.chunk, o.ordered, o.variant,
+                                     o.heavy_threshold, 1, 0)
+        self._planned_for = (row_ptr.data_ptr(), row_ptr.numel(), row_begin, row_end)
+        return self
+
+    def launch_options(self, row_ptr, row_begin, row_end, planned: bool):
+        """The options struct of one launch (the planned form after a matching plan())."""
+        if not planned:
+            return self.options
+        if self._planned_for != (row_ptr.data_ptr(), row_ptr.numel(), row_begin, row_end):
+            raise RuntimeError("SpmmCsrKernel: planned launch without a plan() of this row_ptr "
+                               "and row range")
+        return self._planned_opts
 
     def __call__(self, row_ptr, col_idx, values, b, out, row_begin=0, row_end=None, stream=None,
-                 bias=None, relu=False):
+                 bias=None, relu=False, planned: bool = False):
         """bias / relu: the fused epilogue (ofx_spmm_csr_fused); none = the plain op."""
         row_end = self.m if row_end is None else row_end
         s = stream if stream is not None else current_stream_handle(b)
+        opts = self.launch_options(row_ptr, row_begin, row_end, planned)
         check(LIB.ofx_spmm_csr_fused(s, self.idx_dt, self.val_dt, self.m, self.k, self.n, self.nnz,
                                      row_ptr.data_ptr(), col_idx.data_ptr() if col_idx.numel() else None,
                                      values.data_ptr() if values.numel() else None,
@@ -58,7 +91,7 @@ class SpmmCsrKernel:
                                      out.stride(0), row_begin, row_end,
                                      bias.data_ptr() if bias is not None else None, 1 if relu else 0,
                                      self.workspace.data_ptr(), self.ws_bytes,
-                                     ctypes.byref(self.options) if self.options else None),
+                                     ctypes.byref(opts) if opts else None),
               "spmm_csr")
         return out
 

@@ -308,6 +308,57 @@ def test_row_split_rccl_single_rank(device):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("dtype", ["f32", "f64", "bf16"])
+@pytest.mark.parametrize("n", [3, 64, 256])
+@pytest.mark.parametrize("epi", [False, True])
+def test_deep_and_shallow_hub_reduce(device, dtype, n, epi):
+    """Both hub-reduce kernels: shallow hubs (<= 64 chunks: 16-B vectors, many hubs per wave)
+    and deep hubs (> 64 chunks: one lane per column, 64 partials in flight, LDS-compacted hub
+    list), with the fused bias + relu epilogue, 16-B and scalar partial rows (n = 3)."""
+    rng = np.random.default_rng(70 + n)
+    split = ops.default_split(n)
+    m, k = 700, max(4096, 160 * split)
+    deg = rng.integers(0, 20, size=m)
+    deg[[3, 100, 650]] = [150 * split + 7, 65 * split, 64 * split + split - 1]  # deep x2, shallow
+    deg[200:260] = rng.integers(split + 1, 5 * split, size=60)  # many shallow hubs
+    deg = np.minimum(deg, k)
+    rp, ci, v = random_csr(m, k, deg, rng, torch.int32, DTYPES[dtype])
+    b = random_dense(k, n, rng, DTYPES[dtype])
+    bias = random_dense(1, n, rng, DTYPES[dtype])[0] if epi else None
+    kern = ops.SpmmCsrKernel(m, k, n, ci.numel(), torch.int32, DTYPES[dtype], device)
+    out = torch.full((m, n), float("nan"), dtype=DTYPES[dtype], device=device)
+    kern(rp.to(device), ci.to(device), v.to(device), b.to(device), out,
+         bias=bias.to(device) if epi else None, relu=epi)
+    torch.cuda.synchronize()
+    ref = oracle_spmm(rp, ci, v, b)
+    if epi:
+        ref = oracle.bias_act(ref, to_oracle(bias), "relu", dtype=dtype)
+    assert_bitwise(out, ref, f"{dtype} n={n} epilogue={epi}")
+
+
+@pytest.mark.parametrize("idx", [torch.int32, torch.int64])
+def test_plan_once_compute_many(device, idx):
+    """ofx_spmm_csr_plan builds the work list once; planned launches (hub chunks, degree bins,
+    a row range of the full CSR) give the same bits as self-planning ones for new B each time."""
+    rng = np.random.default_rng(51)
+    m, k, n = 40000, 30000, 64
+    deg = power_law_degrees(m, 900000, k, rng)
+    rp, ci, v = random_csr(m, k, deg, rng, idx)
+    assert int(np.diff(rp.numpy()).max()) > ops.default_split(n)  # hub rows are split
+    d_rp, d_ci, d_v = rp.to(device), ci.to(device), v.to(device)
+    for rb, re in ((0, m), (1234, 38000)):
+        kern = ops.SpmmCsrKernel(m, k, n, ci.numel(), idx, torch.float32, device).plan(d_rp, rb, re)
+        for it in range(3):
+            b = random_dense(k, n, np.random.default_rng(60 + it))
+            out = torch.full((re - rb, n), float("nan"), device=device)
+            kern(d_rp, d_ci, d_v, b.to(device), out, rb, re, planned=True)
+            torch.cuda.synchronize()
+            ref = oracle.spmm(rp.numpy(), ci.numpy(), v.numpy(), b.numpy(), row_begin=rb, row_end=re)
+            assert_bitwise(out, ref, f"planned launch {it} rows [{rb},{re})")
+        with pytest.raises(RuntimeError):  # a planned launch needs a plan of this range
+            kern(d_rp, d_ci, d_v, b.to(device), out[:10], 0, 10, planned=True)
+
+
 def test_hipgraph_capture_replay(device):
     """The op launches are capture-safe (no allocation / sync inside): capture into a graph,
     replay on new data, same bits as eager."""
