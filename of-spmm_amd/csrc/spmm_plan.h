@@ -37,6 +37,7 @@ constexpr int kPlanRowsPerThread = 4;
 constexpr int64_t kPlanRows = (int64_t)kBlock * kPlanRowsPerThread;
 constexpr int kBins = 2;
 constexpr int kPlanVals = 2 + kBins;  // hubs, chunks, bins...
+constexpr int64_t kOwnItems = 8;      // hubs with more chunks get their items written wave-wide
 
 template <typename I>
 __device__ __forceinline__ int plan_row(const I* __restrict__ rp, int64_t row_begin, int64_t nrows,
@@ -118,32 +119,41 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
+// One block: each thread owns a run of `per` consecutive plan blocks, sums it, one block-wide
+// scan of the 256 run totals gives the run offsets, then each thread rewrites its run as
+// exclusive offsets.  (A Hillis-Steele block scan per tile of 256 plan blocks took 21 us at
+// products scale: ten tiles x eight barrier steps.)
 __global__ void __launch_bounds__(kBlock)
     spmm_plan_scan_kernel(int64_t* __restrict__ block_tot, int64_t nblocks,
                           unsigned long long* __restrict__ counters) {
-  int64_t carry[kPlanVals];
+  const int64_t per = (nblocks + kBlock - 1) / kBlock;
+  const int64_t b0 = (int64_t)threadIdx.x * per;
+  const int64_t b1 = b0 + per < nblocks ? b0 + per : nblocks;
+  int64_t v[kPlanVals], tot[kPlanVals];
 #pragma unroll
-  for (int i = 0; i < kPlanVals; ++i) carry[i] = 0;
-  for (int64_t b0 = 0; b0 < nblocks; b0 += kBlock) {
-    const int64_t b = b0 + threadIdx.x;
-    int64_t v[kPlanVals], tot[kPlanVals];
+  for (int i = 0; i < kPlanVals; ++i) v[i] = 0;
+#pragma unroll 8
+  for (int64_t b = b0; b < b1; ++b) {
 #pragma unroll
-    for (int i = 0; i < kPlanVals; ++i) v[i] = b < nblocks ? block_tot[kPlanVals * b + i] : 0;
-    block_scan_vals(v, tot);
-    if (b < nblocks) {
+    for (int i = 0; i < kPlanVals; ++i) v[i] += block_tot[kPlanVals * b + i];
+  }
+  block_scan_vals(v, tot);  // v: exclusive offset of this thread's run
+#pragma unroll 8
+  for (int64_t b = b0; b < b1; ++b) {
 #pragma unroll
-      for (int i = 0; i < kPlanVals; ++i) block_tot[kPlanVals * b + i] = carry[i] + v[i];
+    for (int i = 0; i < kPlanVals; ++i) {
+      const int64_t x = block_tot[kPlanVals * b + i];
+      block_tot[kPlanVals * b + i] = v[i];
+      v[i] += x;
     }
-#pragma unroll
-    for (int i = 0; i < kPlanVals; ++i) carry[i] += tot[i];
   }
   if (threadIdx.x == 0) {
-    counters[0] = (unsigned long long)carry[1];
-    counters[1] = (unsigned long long)carry[0];
+    counters[0] = (unsigned long long)tot[1];
+    counters[1] = (unsigned long long)tot[0];
     int64_t start = 0;
     for (int b = 0; b < kBins; ++b) {
       counters[2 + b] = (unsigned long long)start;
-      start += carry[2 + b];
+      start += tot[2 + b];
     }
   }
 }
@@ -167,16 +177,20 @@ __global__ void __launch_bounds__(kBlock)
   int64_t pos[kBins];
 #pragma unroll
   for (int b = 0; b < kBins; ++b) pos[b] = (int64_t)counters[2 + b] + off[2 + b] + v[2 + b];
+  int64_t first[kPlanRowsPerThread];
 #pragma unroll
   for (int q = 0; q < kPlanRowsPerThread; ++q) {
     const int64_t g = base + q;
+    first[q] = slot;
     if (cls[q] == -1) {
       hubs[3 * hi + 0] = g;
       hubs[3 * hi + 1] = slot;
       hubs[3 * hi + 2] = nc[q];
-      for (int64_t c = 0; c < nc[q]; ++c) {
-        items[2 * (slot + c) + 0] = g;
-        items[2 * (slot + c) + 1] = c;
+      if (nc[q] <= kOwnItems) {
+        for (int64_t c = 0; c < nc[q]; ++c) {
+          items[2 * (slot + c) + 0] = g;
+          items[2 * (slot + c) + 1] = c;
+        }
       }
       ++hi;
       slot += nc[q];
@@ -184,6 +198,23 @@ __global__ void __launch_bounds__(kBlock)
 #pragma unroll
       for (int b = 0; b < kBins; ++b)
         if (cls[q] == b) order[pos[b]++] = g;
+    }
+  }
+  // Hubs with many chunks: the whole wave writes their (row, chunk) items, 64 lanes strided
+  // (one thread looping over a 900-chunk hub held the Reddit-shaped plan at 38 us).
+#pragma unroll
+  for (int q = 0; q < kPlanRowsPerThread; ++q) {
+    unsigned long long big = __ballot(cls[q] == -1 && nc[q] > kOwnItems);
+    while (big) {
+      const int src = __ffsll((long long)big) - 1;
+      big &= big - 1;
+      const int64_t g = (int64_t)__shfl((long long)(base + q), src);
+      const int64_t s0 = (int64_t)__shfl((long long)first[q], src);
+      const int64_t ncs = (int64_t)__shfl((long long)nc[q], src);
+      for (int64_t c = threadIdx.x & 63; c < ncs; c += 64) {
+        items[2 * (s0 + c) + 0] = g;
+        items[2 * (s0 + c) + 1] = c;
+      }
     }
   }
 }
