@@ -103,6 +103,7 @@ def _worker(rank, world, port, m, k, n, local_csr, pipeline, density, q):
     (3, 500, 400, 8, True),
     (4, 603, 1001, 16, True),   # 4 ranks: K % 4 = 1, one long shard and three short ones
     (6, 700, 1003, 12, False),  # 6 ranks: grids 3x2, 2x3 and the 1x6 column split
+    (8, 1201, 1205, 32, True),  # the 8-GPU node's shape: grids 4x2, 2x4, 1x8 (and /s2 each)
 ])
 def test_row_split_gloo(world, m, k, n, local_csr):
     _run(world, m, k, n, local_csr, 1, 30)
