@@ -119,6 +119,17 @@ int ofx_spmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t 
                  int64_t row_end, void* workspace, size_t workspace_bytes,
                  const ofx_spmm_options* opts);
 
+/* ofx_spmm_csr with the values read through a permutation: nonzero j's value is
+ * values[values_perm[j]] (values_perm: idx_dtype[nnz], device).  The backward's
+ * d(b) = A^T @ d(out) runs on A^T's structure (ofx_csr_transpose) with A's values and the
+ * transpose's `perm`, so the gathered copy values[perm] (ofx_gather_values) is never written.
+ * Same bits as ofx_spmm_csr on the gathered values; same workspace.                        */
+int ofx_spmm_csr_gathered(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k,
+                          int64_t n, int64_t nnz, const void* row_ptr, const void* col_idx,
+                          const void* values, const void* values_perm, const void* b,
+                          int64_t ldb, void* c, int64_t ldc, int64_t row_begin, int64_t row_end,
+                          void* workspace, size_t workspace_bytes, const ofx_spmm_options* opts);
+
 /* Plans rows [row_begin, row_end) into `workspace` (the hub chunks and degree-binned work list
  * every ofx_spmm_csr launch otherwise builds first: three small kernels over row_ptr), so that
  * launches with opts->planned != 0 on the same row_ptr, range, shapes and options skip it.

@@ -121,6 +121,7 @@ __device__ __forceinline__ int64_t uniform64(int64_t v) {
 // Bc = B + cc.  All lanes of a group call this with the same j0/j1.
 template <typename T, typename I, typename K>
 __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* __restrict__ val,
+                                           const I* __restrict__ vperm,
                                            const T* __restrict__ Bc, int64_t ldb, int64_t j0,
                                            int64_t j1, int gl, int gbase, bool active,
                                            typename Num<T>::acc (&acc)[K::VEC]) {
@@ -138,7 +139,8 @@ __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* _
       for (int u = 0; u < kUnroll; ++u) {
         if (u < cnt) {
           const int64_t cu = (int64_t)ld_stream<K::NT>(col + j + u);
-          vv[u] = Num<T>::load(ld_stream<K::NT>(val + j + u));
+          const int64_t jv = vperm ? (int64_t)ld_stream<K::NT>(vperm + j + u) : j + u;
+          vv[u] = Num<T>::load(ld_stream<K::NT>(val + jv));
           if (active) bv[u] = *reinterpret_cast<const P*>(Bc + cu * ldb);
         }
       }
@@ -157,7 +159,8 @@ __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* _
       A myv = 0;
       if (gl < cnt) {
         myc = ld_stream<K::NT>(col + jb + gl);
-        myv = Num<T>::load(ld_stream<K::NT>(val + jb + gl));
+        const int64_t jv = vperm ? (int64_t)ld_stream<K::NT>(vperm + jb + gl) : jb + gl;
+        myv = Num<T>::load(ld_stream<K::NT>(val + jv));
       }
       for (int k = 0; k < cnt; k += kUnroll) {
         P bv[kUnroll];
@@ -211,7 +214,8 @@ __device__ __forceinline__ void store_partial(A* __restrict__ p, const A (&acc)[
 template <typename T, typename I, typename K>
 __global__ void __launch_bounds__(64 * K::WPB)
     spmm_main_kernel(const I* __restrict__ rp, const I* __restrict__ col,
-                     const T* __restrict__ val, const T* __restrict__ B, int64_t ldb,
+                     const T* __restrict__ val, const I* __restrict__ vperm,
+                     const T* __restrict__ B, int64_t ldb,
                      T* __restrict__ C, int64_t ldc, int64_t row_begin, int64_t nrows, int64_t n,
                      int64_t chunk, const unsigned long long* __restrict__ counters,
                      const int64_t* __restrict__ items, const int64_t* __restrict__ order,
@@ -259,7 +263,7 @@ __global__ void __launch_bounds__(64 * K::WPB)
     A acc[VEC];
 #pragma unroll
     for (int e = 0; e < VEC; ++e) acc[e] = A(0);
-    accumulate<T, I, K>(col, val, B + cc, ldb, j0, j1, gl, gbase, active, acc);
+    accumulate<T, I, K>(col, val, vperm, B + cc, ldb, j0, j1, gl, gbase, active, acc);
     if (active) {
       if (c >= 0)
         store_partial<A, VEC>(part + g * n + cc, acc);
@@ -410,6 +414,7 @@ struct Launch {
   const void* bias;  // fused epilogue (T[n] or NULL) and OFX_ACT_*
   int act;
   int64_t b_rows;  // k: rows of B (cache-footprint choice of load hints)
+  const void* vperm;  // NULL, or I[nnz]: nonzero j's value is val[vperm[j]] (A^T of a gradient)
 };
 
 int pick_vec(int elem_bytes, const Launch& L, int forced_vec) {
@@ -465,7 +470,8 @@ int launch_cfg(const Launch& L) {
   OFX_REQUIRE(grid < (int64_t)UINT32_MAX, OFX_EINVAL, "spmm_csr: too many rows (%lld)",
               (long long)L.nrows);
   hipLaunchKernelGGL((spmm_main_kernel<T, I, K>), dim3((unsigned)grid), dim3(64 * K::WPB), 0,
-                     L.stream, rp, col, val, B, L.ldb, C, L.ldc, L.row_begin, L.nrows, L.n,
+                     L.stream, rp, col, val, static_cast<const I*>(L.vperm), B, L.ldb, C, L.ldc,
+                     L.row_begin, L.nrows, L.n,
                      plan ? L.sched.chunk : INT64_MAX, counters, items, order, part,
                      static_cast<const T*>(L.bias), L.act);
   OFX_HIP_CHECK(hipGetLastError());
@@ -597,7 +603,7 @@ namespace ofx {
 namespace {
 int spmm_entry(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k, int64_t n,
                int64_t nnz, const void* row_ptr, const void* col_idx, const void* values,
-               const void* b, int64_t ldb, void* c, int64_t ldc, int64_t row_begin,
+               const void* values_perm, const void* b, int64_t ldb, void* c, int64_t ldc, int64_t row_begin,
                int64_t row_end, const void* bias, int act, void* workspace,
                size_t workspace_bytes, const ofx_spmm_options* opts) {
   int rc = check_common(idx_dtype, val_dtype, m, k, n, nnz);
@@ -616,7 +622,7 @@ int spmm_entry(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k,
               "spmm_csr: NULL col_idx/values/b with nnz=%lld", (long long)nnz);
   Launch L{static_cast<hipStream_t>(stream), row_ptr, col_idx, values, b, c, ldb, ldc,
            row_begin, nrows, n, nnz, resolve_schedule(n, opts), workspace, workspace_bytes,
-           bias, act, k};
+           bias, act, k, values_perm};
   if (idx_dtype == OFX_DT_INT32) return launch_idx<int32_t>(val_dtype, L);
   return launch_idx<int64_t>(val_dtype, L);
 }
@@ -628,9 +634,23 @@ extern "C" int ofx_spmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t 
                             const void* values, const void* b, int64_t ldb, void* c, int64_t ldc,
                             int64_t row_begin, int64_t row_end, void* workspace,
                             size_t workspace_bytes, const ofx_spmm_options* opts) {
-  return spmm_entry(stream, idx_dtype, val_dtype, m, k, n, nnz, row_ptr, col_idx, values, b, ldb,
-                    c, ldc, row_begin, row_end, nullptr, OFX_ACT_NONE, workspace, workspace_bytes,
-                    opts);
+  return spmm_entry(stream, idx_dtype, val_dtype, m, k, n, nnz, row_ptr, col_idx, values, nullptr,
+                    b, ldb, c, ldc, row_begin, row_end, nullptr, OFX_ACT_NONE, workspace,
+                    workspace_bytes, opts);
+}
+
+extern "C" int ofx_spmm_csr_gathered(void* stream, int idx_dtype, int val_dtype, int64_t m,
+                                     int64_t k, int64_t n, int64_t nnz, const void* row_ptr,
+                                     const void* col_idx, const void* values,
+                                     const void* values_perm, const void* b, int64_t ldb, void* c,
+                                     int64_t ldc, int64_t row_begin, int64_t row_end,
+                                     void* workspace, size_t workspace_bytes,
+                                     const ofx_spmm_options* opts) {
+  OFX_REQUIRE(nnz == 0 || values_perm != nullptr, OFX_EINVAL,
+              "spmm_csr_gathered: NULL values_perm with nnz=%lld", (long long)nnz);
+  return spmm_entry(stream, idx_dtype, val_dtype, m, k, n, nnz, row_ptr, col_idx, values,
+                    values_perm, b, ldb, c, ldc, row_begin, row_end, nullptr, OFX_ACT_NONE,
+                    workspace, workspace_bytes, opts);
 }
 
 extern "C" int ofx_spmm_csr_plan(void* stream, int idx_dtype, int val_dtype, int64_t m,
@@ -668,8 +688,9 @@ extern "C" int ofx_spmm_csr_fused(void* stream, int idx_dtype, int val_dtype, in
                                   int64_t row_end, const void* bias, int activation,
                                   void* workspace, size_t workspace_bytes,
                                   const ofx_spmm_options* opts) {
-  return spmm_entry(stream, idx_dtype, val_dtype, m, k, n, nnz, row_ptr, col_idx, values, b, ldb,
-                    c, ldc, row_begin, row_end, bias, activation, workspace, workspace_bytes, opts);
+  return spmm_entry(stream, idx_dtype, val_dtype, m, k, n, nnz, row_ptr, col_idx, values, nullptr,
+                    b, ldb, c, ldc, row_begin, row_end, bias, activation, workspace,
+                    workspace_bytes, opts);
 }
 
 extern "C" int ofx_csr_validate(void* stream, int idx_dtype, int64_t m, int64_t k, int64_t nnz,

@@ -58,6 +58,8 @@ def _load():
         "ofx_spmm_csr_workspace_size": ([i32, i32, i64, i64, i64, i64, popt, ctypes.POINTER(sz)], i32),
         "ofx_spmm_csr": ([p, i32, i32, i64, i64, i64, i64, p, p, p, p, i64, p, i64, i64, i64, p, sz,
                           popt], i32),
+        "ofx_spmm_csr_gathered": ([p, i32, i32, i64, i64, i64, i64, p, p, p, p, p, i64, p, i64, i64,
+                                   i64, p, sz, popt], i32),
         "ofx_spmm_csr_plan": ([p, i32, i32, i64, i64, i64, i64, p, i64, i64, p, sz, popt], i32),
         "ofx_spmm_csr_fused": ([p, i32, i32, i64, i64, i64, i64, p, p, p, p, i64, p, i64, i64, i64,
                                 p, i32, p, sz, popt], i32),

@@ -5,7 +5,9 @@ oneflow/core/autograd/gradient_funcs/matrix_vector_product.cpp:26-91: capture wh
 needs, then call the grad functors): for out = A @ b,
     d(values)[j] = <d(out)[row(j), :], b[col(j), :]>      ofx_sddmm_csr
     d(b)         = A^T @ d(out)                            ofx_csr_transpose (cached per graph)
-                                                           + ofx_gather_values + ofx_spmm_csr
+                                                           + ofx_spmm_csr_gathered (values read
+                                                           through perm), or ofx_gather_values
+                                                           once + ofx_spmm_csr for constant values
 The index inputs never get gradients (spmm_op.cpp ModifyInputArg).  All device work runs in the
 HIP kernels; CPU tensors run the kCPU kernels.  Both give the same bits (contracts in
 include/ofx_spmm.h).
@@ -52,6 +54,7 @@ class _TransposeCache:
         self.capacity = capacity
         self.entries: OrderedDict = OrderedDict()
         self.value_entries: OrderedDict = OrderedDict()
+        self.seen: OrderedDict = OrderedDict()  # value keys met once (not yet worth a copy)
 
     def get(self, row_ptr, col_idx, k):
         key = (row_ptr.data_ptr(), col_idx.data_ptr(), row_ptr._version, col_idx._version,
@@ -86,6 +89,24 @@ class _TransposeCache:
         return rp_t, ci_t, vals_t
 
 
+    def grad_b(self, row_ptr, col_idx, values, m, k, d_out):
+        """d(b) = A^T @ d(out).  Values met for the first time (e.g. learnable edge weights,
+        new every step) are read through the transpose's perm inside the SpMM
+        (ofx_spmm_csr_gathered: no values[perm] copy written); values met again unchanged
+        (constant GCN weights) are gathered once and cached, then the plain SpMM runs on them.
+        Every route gives the same bits."""
+        rp_t, ci_t, perm = self.get(row_ptr, col_idx, k)
+        key = (row_ptr.data_ptr(), col_idx.data_ptr(), row_ptr._version, col_idx._version, k,
+               values.data_ptr(), values._version, values.dtype, values.numel(), str(values.device))
+        if key not in self.value_entries and values.device.type == "cuda" and key not in self.seen:
+            self.seen[key] = values  # holds values: its storage cannot be reused under the key
+            while len(self.seen) > self.capacity:
+                self.seen.popitem(last=False)
+            return ops.spmm_csr_gathered(rp_t, ci_t, values, perm, d_out, k, m)
+        _, _, vals_t = self.values_t(row_ptr, col_idx, values, k)
+        return spmm_csr(rp_t, ci_t, vals_t, k, m, d_out)
+
+
 TRANSPOSE_CACHE = _TransposeCache()
 
 
@@ -105,8 +126,7 @@ class SpmmCsrFunction(torch.autograd.Function):
         if ctx.needs_input_grad[2]:
             d_values = sddmm(row_ptr, col_idx, d_out, b)
         if ctx.needs_input_grad[5]:
-            rp_t, ci_t, vals_t = TRANSPOSE_CACHE.values_t(row_ptr, col_idx, values.detach(), ctx.k)
-            d_b = spmm_csr(rp_t, ci_t, vals_t, ctx.k, ctx.m, d_out)
+            d_b = TRANSPOSE_CACHE.grad_b(row_ptr, col_idx, values.detach(), ctx.m, ctx.k, d_out)
         return None, None, d_values, None, None, d_b
 
 
@@ -145,8 +165,7 @@ class FusedSpmmCsrFunction(torch.autograd.Function):
         if ctx.needs_input_grad[2]:
             d_values = sddmm(row_ptr, col_idx, g, b)
         if ctx.needs_input_grad[5]:
-            rp_t, ci_t, vals_t = TRANSPOSE_CACHE.values_t(row_ptr, col_idx, values.detach(), ctx.k)
-            d_b = spmm_csr(rp_t, ci_t, vals_t, ctx.k, ctx.m, g)
+            d_b = TRANSPOSE_CACHE.grad_b(row_ptr, col_idx, values.detach(), ctx.m, ctx.k, g)
         return None, None, d_values, None, None, d_b, d_bias, None
 
 

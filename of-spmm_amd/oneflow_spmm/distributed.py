@@ -366,7 +366,9 @@ class RowSplitSpmm:
         self._comm = None
         self.comm_stream = None
         if self.device.type == "cuda":
-            self.comm_stream = torch.cuda.Stream(self.device)
+            # high priority: the exchange kernels of a pipelined step get CUs as soon as SpMM
+            # workgroups retire instead of queueing behind the whole SpMM grid
+            self.comm_stream = torch.cuda.Stream(self.device, priority=-1)
         self.gathered = None
         self.halo = None
         self.ns = None      # the column split (C = G grid), when bound

@@ -108,6 +108,31 @@ def spmm_csr_device(row_ptr, col_idx, values, b, m, k, *, out=None, row_begin=0,
     return kern(row_ptr, col_idx, values, b, out, row_begin, row_end)
 
 
+def spmm_csr_gathered(row_ptr, col_idx, values, values_perm, b, m, k, *, out=None,
+                      options: Options | None = None):
+    """out = A @ b where nonzero j's value is values[values_perm[j]] (ofx_spmm_csr_gathered):
+    the backward's A^T @ d(out) on A's values without writing values[perm].  Same bits as
+    spmm_csr on the gathered values."""
+    if b.device.type != "cuda":
+        return spmm_csr_cpu(row_ptr, col_idx, values[values_perm.long()], b, m, k, out=out,
+                            options=options)
+    if values_perm.dtype != row_ptr.dtype or values_perm.numel() != col_idx.numel():
+        raise RuntimeError("spmm_csr_gathered: values_perm must be [nnz] in the index dtype")
+    if out is None:
+        out = torch.empty((m, b.shape[1]), dtype=b.dtype, device=b.device)
+    n, nnz = b.shape[1], col_idx.numel()
+    ws = workspace_size(row_ptr.dtype, b.dtype, m, k, n, nnz, options)
+    wbuf = torch.empty(max(ws, 1), dtype=torch.uint8, device=b.device)
+    nz = lambda t: t.data_ptr() if t.numel() else None  # noqa: E731
+    check(LIB.ofx_spmm_csr_gathered(current_stream_handle(b), dtype_code(row_ptr.dtype),
+                                    dtype_code(b.dtype), m, k, n, nnz, row_ptr.data_ptr(),
+                                    nz(col_idx), nz(values), nz(values_perm), nz(b), b.stride(0),
+                                    out.data_ptr(), out.stride(0), 0, m, wbuf.data_ptr(), ws,
+                                    ctypes.byref(options) if options else None),
+          "spmm_csr_gathered")
+    return out
+
+
 def spmm_csr_cpu(row_ptr, col_idx, values, b, m, k, *, out=None, row_begin=0, row_end=None,
                  options: Options | None = None, num_threads: int = 0, bias=None, relu=False):
     """The DeviceType::kCPU kernel (C-ABI ofx_spmm_csr_fused_cpu), host tensors."""
@@ -151,4 +176,5 @@ def csr_row_slice(row_ptr, row_begin: int, row_end: int):
 
 
 __all__ = ["make_options", "default_split", "workspace_size", "SpmmCsrKernel", "spmm_csr_device",
+           "spmm_csr_gathered",
            "spmm_csr_cpu", "validate_csr", "csr_row_slice", "INT64_MAX", "_lib"]

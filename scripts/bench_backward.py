@@ -65,6 +65,13 @@ def main():
         db_bytes = 4 * (k + 1) + (4 + sv) * nnz + sv * nnz * n + sv * k * n
         res["db_spmm_ms"] = t
         res["db_spmm_gbs"] = db_bytes / (t * 1e-3) / 1e9
+        # the same product reading A's values through perm (no values[perm] copy): the
+        # learnable-edge-weight backward; its bytes add one 4-B perm read per nonzero
+        from oneflow_spmm import ops
+        out_g = torch.empty((k, n), dtype=dt, device=dev)
+        t = timed(lambda: ops.spmm_csr_gathered(rt, ct, v, perm, g, k, m, out=out_g))
+        res["db_gathered_ms"] = t
+        res["db_gathered_bitexact"] = bool(torch.equal(out_g, fs.spmm_csr(rt, ct, vt, k, m, g)))
     if "fwd" in only:
         res["forward_ms"] = timed(lambda: fs.spmm_csr(rp, ci, v, m, k, b))
     print(json.dumps({kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in res.items()}))
