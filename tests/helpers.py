@@ -77,6 +77,8 @@ def assert_bitwise(out: torch.Tensor, ref: np.ndarray, what=""):
 
 
 def power_law_degrees(m, nnz, k, rng, gamma=2.5):
+    if nnz > m * k:
+        raise ValueError(f"power_law_degrees: {nnz} nonzeros do not fit {m} x {k}")
     w = (np.arange(1, m + 1, dtype=np.float64)) ** (-1.0 / (gamma - 1.0))
     d = np.floor(nnz * w / w.sum()).astype(np.int64)
     d = np.minimum(d, k)

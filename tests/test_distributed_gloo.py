@@ -32,7 +32,7 @@ def _worker(rank, world, port, m, k, n, local_csr, pipeline, density, q):
         from tests.helpers import power_law_degrees, random_csr, random_dense
 
         rng = np.random.default_rng(1234)
-        rp, ci, v = random_csr(m, k, power_law_degrees(m, density * m, k, rng), rng)
+        rp, ci, v = random_csr(m, k, power_law_degrees(m, min(density * m, m * k // 2), k, rng), rng)
         b = random_dense(k, n, rng)
         full = oracle.spmm(rp.numpy(), ci.numpy(), v.numpy(), b.numpy())
         lo, hi = oracle.balanced_range(m, world, rank)
@@ -104,6 +104,7 @@ def _worker(rank, world, port, m, k, n, local_csr, pipeline, density, q):
     (4, 603, 1001, 16, True),   # 4 ranks: K % 4 = 1, one long shard and three short ones
     (6, 700, 1003, 12, False),  # 6 ranks: grids 3x2, 2x3 and the 1x6 column split
     (8, 1201, 1205, 32, True),  # the 8-GPU node's shape: grids 4x2, 2x4, 1x8 (and /s2 each)
+    (8, 5, 6, 8, False),        # fewer rows and B rows than ranks: empty shards, 1-wide blocks
 ])
 def test_row_split_gloo(world, m, k, n, local_csr):
     _run(world, m, k, n, local_csr, 1, 30)
