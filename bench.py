@@ -300,7 +300,9 @@ def main():
             "pipeline_blocks": rs.chunks,
             "halo_rows_received": rs.halo.halo_rows if rs.halo is not None else None,
             "remote_rows_total": (rs.k - (khi - klo)),
-            "allgather_tune_ms": {kk: round(vv, 4) for kk, vv in comm_times.items()},
+            "allgather_tune_ms": {kk: (round(vv, 4) if np.isfinite(vv) else None)
+                                  for kk, vv in comm_times.items()},
+            "tune_errors": getattr(rs, "tune_errors", {}) or None,
             "nnz_per_rank_max_over_mean": round(float(nz[0]) / (float(nz[1]) / world), 4)})
 
     # ---- CPU baseline: oracle restatement on the host cores (rank 0, N=1 only) ---------------

@@ -720,19 +720,27 @@ class RowSplitSpmm:
             return {}
 
         def measure():
-            self.step(out)
-            torch.cuda.synchronize(self.device)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(reps):
+            # A candidate that raises on any rank (a host-side error, deterministic across ranks)
+            # is timed as +inf everywhere by the max-reduce, so no rank keeps it.
+            ms = float("inf")
+            try:
                 self.step(out)
-            e1.record()
-            torch.cuda.synchronize(self.device)
-            t = torch.tensor([e0.elapsed_time(e1) / reps], dtype=torch.float64, device=self.device)
+                torch.cuda.synchronize(self.device)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(reps):
+                    self.step(out)
+                e1.record()
+                torch.cuda.synchronize(self.device)
+                ms = e0.elapsed_time(e1) / reps
+            except Exception as e:  # noqa: BLE001 -- reported, candidate dropped
+                self.tune_errors[f"{self.exchange}/{self.comm_kind}/p{self.chunks}"] = repr(e)
+            t = torch.tensor([ms], dtype=torch.float64, device=self.device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
             return float(t.item())
 
         times = {}
+        self.tune_errors = {}
         self.exchange = "allgather"
         for chunks in pipelines:
             if self.n % chunks:
@@ -748,6 +756,8 @@ class RowSplitSpmm:
             self.exchange, self.comm_kind = name, "rccl"
             times[name] = measure()
         best = min(times, key=times.get)
+        if not math.isfinite(times[best]):
+            raise RuntimeError(f"RowSplitSpmm.tune: every exchange failed: {self.tune_errors}")
         if best == "halo" or best in self.grids:
             self.exchange, self.comm_kind = best, "rccl"
             self.set_pipeline(1)
