@@ -19,3 +19,29 @@ def test_c_host_calls_the_abi(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("OK")
+
+
+CLANG = "/opt/rocm/lib/llvm/bin/clang++"
+
+
+@pytest.mark.skipif(not os.path.exists(CLANG), reason="ROCm clang++ not found")
+def test_cpu_kernels_under_sanitizers(tmp_path):
+    """the host kernels (spmm_cpu.cpp, synth.cpp, errors.cpp) built from source
+    with AddressSanitizer + UndefinedBehaviorSanitizer (host code only) and driven over the edge
+    cases by tests/native/cpu_sanitize.cpp, which also checks their results against naive loops."""
+    exe = tmp_path / "cpu_sanitize"
+    csrc = os.path.join(ROOT, "of-spmm_amd", "csrc")
+    subprocess.run([CLANG, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer",
+                    "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-fopenmp",
+                    "-ffp-contract=off", "-Wall", "-Werror", "-Wno-unknown-pragmas",
+                    "-Wno-duplicate-decl-specifier", "-I", os.path.join(ROOT, "include"), "-I", csrc,
+                    os.path.join(ROOT, "tests", "native", "cpu_sanitize.cpp"),
+                    os.path.join(csrc, "spmm_cpu.cpp"), os.path.join(csrc, "synth.cpp"),
+                    os.path.join(csrc, "errors.cpp"), "-o", str(exe)], check=True)
+    supp = tmp_path / "lsan.supp"
+    supp.write_text("leak:___kmp_allocate\n")  # the OpenMP runtime's own thread-pool state
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
+               LSAN_OPTIONS=f"suppressions={supp}", UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.strip().endswith("OK") and "runtime error" not in r.stderr, r.stdout + r.stderr
