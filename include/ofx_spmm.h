@@ -191,6 +191,9 @@ int ofx_csr_transpose_cpu(int idx_dtype, int64_t m, int64_t k, int64_t nnz, cons
 /* dst[t] = src[perm[t]] for t < nnz (any 2/4/8-byte value dtype). */
 int ofx_gather_values(void* stream, int idx_dtype, int val_dtype, int64_t nnz, const void* perm,
                       const void* src, void* dst);
+/* Host version (CPU kernel of spmm_csr_gathered). */
+int ofx_gather_values_host(int idx_dtype, int val_dtype, int64_t nnz, const void* perm,
+                           const void* src, void* dst);
 /* out[j] = sum_n a[r - row_begin, n] * b[col_idx[j], n] for the nonzeros j of rows
  * r in [row_begin, row_end).  Order: products rounded, 8-element leaves summed sequentially from
  * +0, leaves (zero-padded to a power of two) added pairwise; fp32 accumulation for 16-bit types.
@@ -375,6 +378,14 @@ int ofx_functional_csr_transpose(void* stream, const ofx_tensor_desc* row_ptr,
                                  int64_t a_num_cols, ofx_tensor_desc* out_row_ptr,
                                  ofx_tensor_desc* out_col_idx, ofx_tensor_desc* out_perm,
                                  void* tmp, size_t tmp_bytes, size_t* tmp_size_out);
+/* functional::SpmmCsrGathered: op "spmm_csr_gathered" (out = A @ b with values read through
+ * values_perm; the d(b) gradient with learnable values). */
+int ofx_functional_spmm_csr_gathered(void* stream, const ofx_tensor_desc* row_ptr,
+                                     const ofx_tensor_desc* col_idx,
+                                     const ofx_tensor_desc* values,
+                                     const ofx_tensor_desc* values_perm, const ofx_tensor_desc* b,
+                                     int64_t a_num_rows, int64_t a_num_cols, ofx_tensor_desc* out,
+                                     void* tmp, size_t tmp_bytes, size_t* tmp_size_out);
 /* The op's registered SBP signatures and no-grad inputs, as text (tests / introspection). */
 int ofx_op_spmm_csr_sbp_signatures(char* buf, size_t len);
 /* Same for any registered op; optional_inputs = comma-separated optional inputs present.   */

@@ -232,6 +232,27 @@ void cpu_sddmm(int nthreads, int64_t n, const I* rp, const I* col, const T* a, i
 }  // namespace
 }  // namespace ofx
 
+extern "C" int ofx_gather_values_host(int idx_dtype, int val_dtype, int64_t nnz, const void* perm,
+                                      const void* src, void* dst) {
+  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "gather_values: bad index dtype %d",
+              idx_dtype);
+  const int vs = dtype_size(val_dtype);
+  OFX_REQUIRE(vs == 2 || vs == 4 || vs == 8, OFX_EUNSUPPORTED, "gather_values: bad value dtype %d",
+              val_dtype);
+  OFX_REQUIRE(nnz >= 0 && (nnz == 0 || (perm && src && dst)), OFX_EINVAL,
+              "gather_values: NULL argument");
+  const char* s = static_cast<const char*>(src);
+  char* d = static_cast<char*>(dst);
+  for (int64_t t = 0; t < nnz; ++t) {
+    const int64_t j = idx_dtype == OFX_DT_INT32 ? (int64_t) static_cast<const int32_t*>(perm)[t]
+                                                : static_cast<const int64_t*>(perm)[t];
+    OFX_REQUIRE(j >= 0 && j < nnz, OFX_EINVAL, "gather_values: perm[%lld] = %lld outside [0, %lld)",
+                (long long)t, (long long)j, (long long)nnz);
+    memcpy(d + (size_t)t * vs, s + (size_t)j * vs, (size_t)vs);
+  }
+  return OFX_OK;
+}
+
 extern "C" int ofx_csr_transpose_cpu(int idx_dtype, int64_t m, int64_t k, int64_t nnz,
                                      const void* row_ptr, const void* col_idx, void* out_row_ptr,
                                      void* out_col_idx, void* out_perm) {

@@ -42,6 +42,16 @@ enum DataType : int {
 };
 const char* DataType_Name(DataType dt);
 inline bool IsIndexDataType(DataType dt) { return dt == kInt32 || dt == kInt64; }
+// oneflow/core/common/data_type.h GetSizeOfDataType
+inline size_t GetSizeOfDataType(DataType dt) {
+  switch (dt) {
+    case kChar: case kInt8: case kUInt8: case kBool: return 1;
+    case kFloat16: case kBFloat16: return 2;
+    case kFloat: case kInt32: return 4;
+    case kDouble: case kInt64: return 8;
+    default: return 0;
+  }
+}
 
 enum class DeviceType : int { kInvalidDevice = 0, kCPU = 1, kCUDA = 2, kMockDevice = 3, kHIP = 4 };
 const char* DeviceTypeName(DeviceType t);

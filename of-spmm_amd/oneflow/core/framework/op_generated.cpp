@@ -48,6 +48,21 @@ REGISTER_USER_OP("sddmm_csr")
     .SetGetSbpFn(SddmmCsrOp::GetSbp)
     .SetDataTypeInferFn(SddmmCsrOp::InferDataType);
 
+REGISTER_USER_OP("spmm_csr_gathered")
+    .Input("a_csr_row_ptr")
+    .Input("a_csr_col_idx")
+    .Input("a_csr_values")
+    .Input("values_perm")
+    .Input("b")
+    .Output("out")
+    .Attr<int64_t>("a_num_rows", 0)
+    .Attr<int64_t>("a_num_cols", 0)
+    .SetLogicalTensorDescInferFn(SpmmCsrGatheredOp::InferLogicalTensorDesc)
+    .SetPhysicalTensorDescInferFn(SpmmCsrGatheredOp::InferPhysicalTensorDesc)
+    .SetGetSbpFn(SpmmCsrGatheredOp::GetSbp)
+    .SetDataTypeInferFn(SpmmCsrGatheredOp::InferDataType)
+    .SetInputArgModifyFn(SpmmCsrGatheredOp::ModifyInputArg);
+
 REGISTER_USER_OP("csr_transpose")
     .Input("a_csr_row_ptr")
     .Input("a_csr_col_idx")

@@ -37,6 +37,17 @@ class SddmmCsrOp {
   static Maybe<void> InferDataType(user_op::InferContext* ctx);
 };
 
+// d(b) of spmm_csr with A's values read through A^T's perm (learnable edge weights).
+class SpmmCsrGatheredOp {
+ public:
+  static Maybe<void> InferLogicalTensorDesc(user_op::InferContext* ctx);
+  static Maybe<void> InferPhysicalTensorDesc(user_op::InferContext* ctx);
+  static Maybe<void> GetSbp(user_op::SbpContext* ctx);
+  static Maybe<void> InferDataType(user_op::InferContext* ctx);
+  static Maybe<void> ModifyInputArg(const user_op::GetInputArgModifier& GetInputArgModifierFn,
+                                    const user_op::UserOpConfWrapper& conf);
+};
+
 class CsrTransposeOp {
  public:
   static Maybe<void> InferLogicalTensorDesc(user_op::InferContext* ctx);

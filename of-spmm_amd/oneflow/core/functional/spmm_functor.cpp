@@ -358,6 +358,23 @@ extern "C" int ofx_functional_csr_transpose(void* stream, const ofx_tensor_desc*
                             tmp_bytes, tmp_size_out));
 }
 
+// functional::SpmmCsrGathered: the d(b) gradient of spmm_csr with learnable values, A^T's
+// structure with A's values read through A^T's perm.
+extern "C" int ofx_functional_spmm_csr_gathered(void* stream, const ofx_tensor_desc* row_ptr,
+                                                const ofx_tensor_desc* col_idx,
+                                                const ofx_tensor_desc* values,
+                                                const ofx_tensor_desc* values_perm,
+                                                const ofx_tensor_desc* b, int64_t a_num_rows,
+                                                int64_t a_num_cols, ofx_tensor_desc* out,
+                                                void* tmp, size_t tmp_bytes,
+                                                size_t* tmp_size_out) {
+  return ToStatus(RunUserOp("spmm_csr_gathered",
+                            {{"a_csr_row_ptr", row_ptr}, {"a_csr_col_idx", col_idx},
+                             {"a_csr_values", values}, {"values_perm", values_perm}, {"b", b}},
+                            {{"out", out}}, {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols}},
+                            stream, tmp, tmp_bytes, tmp_size_out));
+}
+
 // functional::FusedSpmmCsr: relu?(A @ b + bias?) through op
 // "fused_spmm_csr"; `bias` may be NULL (the optional input is then absent).
 extern "C" int ofx_functional_fused_spmm_csr(void* stream, const ofx_tensor_desc* row_ptr,

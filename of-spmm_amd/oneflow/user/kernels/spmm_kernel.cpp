@@ -138,6 +138,79 @@ class FusedSpmmCsrKernel final : public user_op::OpKernel, public user_op::CudaG
   }
 };
 
+// "spmm_csr_gathered": out = A @ b with nonzero j's value a_csr_values[values_perm[j]] (the
+// d(b) gradient with learnable values).  HIP reads the values through the permutation inside
+// the SpMM (ofx_spmm_csr_gathered); the CPU kernel gathers them into its tmp buffer first and
+// runs the kCPU SpMM on the copy (same bits).
+template <DeviceType device_type>
+class SpmmCsrGatheredKernel final : public user_op::OpKernel, public user_op::CudaGraphSupport {
+ public:
+  SpmmCsrGatheredKernel() = default;
+  ~SpmmCsrGatheredKernel() override = default;
+
+  std::shared_ptr<user_op::OpKernelCache> InitOpKernelCache(
+      user_op::KernelCacheContext* ctx) const override {
+    return CreateSpmmCsrOpKernelCache(ctx);
+  }
+
+  bool AlwaysComputeWhenAllOutputsEmpty() const override { return false; }
+
+ private:
+  using user_op::OpKernel::Compute;
+  void Compute(user_op::KernelComputeContext* ctx, user_op::OpKernelState*,
+               const user_op::OpKernelCache* cache) const override {
+    const user_op::Tensor* row_ptr = ctx->Tensor4ArgNameAndIndex("a_csr_row_ptr", 0);
+    const user_op::Tensor* col_idx = ctx->Tensor4ArgNameAndIndex("a_csr_col_idx", 0);
+    const user_op::Tensor* values = ctx->Tensor4ArgNameAndIndex("a_csr_values", 0);
+    const user_op::Tensor* perm = ctx->Tensor4ArgNameAndIndex("values_perm", 0);
+    const user_op::Tensor* b = ctx->Tensor4ArgNameAndIndex("b", 0);
+    user_op::Tensor* out = ctx->Tensor4ArgNameAndIndex("out", 0);
+    user_op::Tensor* tmp = ctx->Tensor4ArgNameAndIndex("tmp_buffer", 0);
+    const int64_t m = ctx->Attr<int64_t>("a_num_rows");
+    const int64_t k = ctx->Attr<int64_t>("a_num_cols");
+    const int64_t n = out->shape_view().At(1);
+    const int64_t nnz = col_idx->shape_view().elem_cnt();
+    int64_t row_begin = 0, row_end = m;
+    if (cache != nullptr) {
+      const auto* range = dynamic_cast<const SpmmCsrOpKernelCache*>(cache);
+      OFX_KERNEL_CHECK(range != nullptr, "unexpected kernel cache type");
+      row_begin = range->lower();
+      row_end = range->upper();
+    }
+    OFX_KERNEL_CHECK(out->shape_view().At(0) == row_end - row_begin,
+                     "out rows " << out->shape_view().At(0) << " != row range "
+                                 << row_end - row_begin);
+    const int idx_dt = DtCode(row_ptr->data_type());
+    const int val_dt = DtCode(values->data_type());
+    void* ws = tmp ? tmp->mut_dptr() : nullptr;
+    const size_t ws_bytes = tmp ? (size_t)tmp->shape_view().elem_cnt() : 0;
+    int rc;
+    if (device_type == DeviceType::kHIP) {
+      void* stream = ctx->stream()->As<ep::HipStream>()->hip_stream();
+      rc = ofx_spmm_csr_gathered(stream, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
+                                 col_idx->dptr(), values->dptr(), perm->dptr(), b->dptr(),
+                                 b->row_stride(), out->mut_dptr(), out->row_stride(), row_begin,
+                                 row_end, ws, ws_bytes, nullptr);
+    } else {
+      const size_t vbytes = (size_t)nnz * (size_t)GetSizeOfDataType(values->data_type());
+      OFX_KERNEL_CHECK(nnz == 0 || ws_bytes >= vbytes, "tmp buffer smaller than the values");
+      rc = ofx_gather_values_host(idx_dt, val_dt, nnz, perm->dptr(), values->dptr(), ws);
+      if (rc == OFX_OK)
+        rc = ofx_spmm_csr_cpu(ctx->stream()->As<ep::CpuStream>()->num_threads(), idx_dt, val_dt,
+                              m, k, n, nnz, row_ptr->dptr(), col_idx->dptr(), ws, b->dptr(),
+                              b->row_stride(), out->mut_dptr(), out->row_stride(), row_begin,
+                              row_end, nullptr);
+    }
+    OFX_KERNEL_CHECK(rc == OFX_OK,
+                     "spmm_csr_gathered kernel failed (" << rc << "): " << ofx_last_error());
+  }
+};
+
+size_t InferSpmmCsrGatheredCpuTmpSize(user_op::InferSizeContext* ctx) {
+  const user_op::TensorDesc& values = ctx->InputTensorDesc("a_csr_values", 0);
+  return (size_t)values.shape().elem_cnt() * (size_t)GetSizeOfDataType(values.data_type());
+}
+
 size_t InferSpmmCsrTmpSize(user_op::InferSizeContext* ctx) {
   const user_op::TensorDesc& row_ptr = ctx->InputTensorDesc("a_csr_row_ptr", 0);
   const user_op::TensorDesc& col_idx = ctx->InputTensorDesc("a_csr_col_idx", 0);
@@ -179,5 +252,27 @@ size_t InferSpmmCsrTmpSize(user_op::InferSizeContext* ctx) {
 
 REGISTER_SPMM_CSR_KERNEL_ALL(DeviceType::kCPU)
 REGISTER_SPMM_CSR_KERNEL_ALL(DeviceType::kHIP)
+
+#define REGISTER_SPMM_CSR_GATHERED_KERNEL(device, dtype, itype)                                \
+  REGISTER_USER_KERNEL("spmm_csr_gathered")                                                   \
+      .SetCreateFn<SpmmCsrGatheredKernel<device>>()                                           \
+      .SetIsMatchedHob((user_op::HobDeviceType() == device)                                   \
+                       && (user_op::HobDataType("out", 0) == dtype)                           \
+                       && (user_op::HobDataType("a_csr_row_ptr", 0) == itype))                \
+      .SetInferTmpSizeFn(device == DeviceType::kHIP ? InferSpmmCsrTmpSize                     \
+                                                    : InferSpmmCsrGatheredCpuTmpSize);
+
+#define REGISTER_SPMM_CSR_GATHERED_KERNEL_ALL(device)                 \
+  REGISTER_SPMM_CSR_GATHERED_KERNEL(device, kFloat, kInt32)           \
+  REGISTER_SPMM_CSR_GATHERED_KERNEL(device, kFloat, kInt64)           \
+  REGISTER_SPMM_CSR_GATHERED_KERNEL(device, kDouble, kInt32)          \
+  REGISTER_SPMM_CSR_GATHERED_KERNEL(device, kDouble, kInt64)          \
+  REGISTER_SPMM_CSR_GATHERED_KERNEL(device, kFloat16, kInt32)         \
+  REGISTER_SPMM_CSR_GATHERED_KERNEL(device, kFloat16, kInt64)         \
+  REGISTER_SPMM_CSR_GATHERED_KERNEL(device, kBFloat16, kInt32)        \
+  REGISTER_SPMM_CSR_GATHERED_KERNEL(device, kBFloat16, kInt64)
+
+REGISTER_SPMM_CSR_GATHERED_KERNEL_ALL(DeviceType::kCPU)
+REGISTER_SPMM_CSR_GATHERED_KERNEL_ALL(DeviceType::kHIP)
 
 }  // namespace oneflow

@@ -11,6 +11,10 @@
  *   A parts B, b B,    out S(0)   row split: each rank computes its BalancedSplitter row range
  *                                 (the framework all-gathers b from S(0) -> B first).
  *   A parts B, b S(1), out S(1)   column split of the dense operand, no communication.
+ *
+ * Op "spmm_csr_gathered" (the d(b) gradient with learnable values) takes one more input,
+ * values_perm [nnz] (A^T's perm from csr_transpose): nonzero j's value is
+ * a_csr_values[values_perm[j]].  Same shapes, dtypes and SBP signatures otherwise.
  */
 #include "oneflow/core/framework/framework.h"
 #include "oneflow/core/framework/op_generated.h"
@@ -70,6 +74,34 @@ Maybe<void> InferDataType4SpmmCsr(user_op::InferContext* ctx) {
   return Maybe<void>::Ok();
 }
 
+Maybe<void> CheckValuesPerm(user_op::InferContext* ctx) {
+  const user_op::TensorDesc& perm = ctx->InputTensorDesc("values_perm", 0);
+  const user_op::TensorDesc& col_idx = ctx->InputTensorDesc(kColIdx, 0);
+  CHECK_EQ_OR_RETURN(perm.shape().NumAxes(), 1)
+      << Error::RuntimeError() << "values_perm should be 1-D, got shape " << perm.shape().ToString();
+  CHECK_EQ_OR_RETURN(perm.shape().At(0), col_idx.shape().At(0))
+      << Error::RuntimeError() << "values_perm should have nnz elements. ";
+  return Maybe<void>::Ok();
+}
+
+Maybe<void> GetSbp4SpmmCsr(user_op::SbpContext* ctx, bool with_perm) {
+  // Row split: the CSR is broadcast, b is gathered to broadcast, out rows are split.
+  auto row = ctx->NewBuilder();
+  row.Broadcast(user_op::OpArg(kRowPtr, 0))
+      .Broadcast(user_op::OpArg(kColIdx, 0))
+      .Broadcast(user_op::OpArg(kValues, 0));
+  if (with_perm) row.Broadcast(user_op::OpArg("values_perm", 0));
+  row.Broadcast(user_op::OpArg("b", 0)).Split(user_op::OpArg("out", 0), 0).Build();
+  // Column split of the dense operand: no exchange at all.
+  auto col = ctx->NewBuilder();
+  col.Broadcast(user_op::OpArg(kRowPtr, 0))
+      .Broadcast(user_op::OpArg(kColIdx, 0))
+      .Broadcast(user_op::OpArg(kValues, 0));
+  if (with_perm) col.Broadcast(user_op::OpArg("values_perm", 0));
+  col.Split(user_op::OpArg("b", 0), 1).Split(user_op::OpArg("out", 0), 1).Build();
+  return Maybe<void>::Ok();
+}
+
 }  // namespace
 
 /* static */ Maybe<void> SpmmCsrOp::InferLogicalTensorDesc(user_op::InferContext* ctx) {
@@ -81,23 +113,7 @@ Maybe<void> InferDataType4SpmmCsr(user_op::InferContext* ctx) {
 }
 
 /* static */ Maybe<void> SpmmCsrOp::GetSbp(user_op::SbpContext* ctx) {
-  // Row split: the CSR is broadcast, b is gathered to broadcast, out rows are split.
-  ctx->NewBuilder()
-      .Broadcast(user_op::OpArg(kRowPtr, 0))
-      .Broadcast(user_op::OpArg(kColIdx, 0))
-      .Broadcast(user_op::OpArg(kValues, 0))
-      .Broadcast(user_op::OpArg("b", 0))
-      .Split(user_op::OpArg("out", 0), 0)
-      .Build();
-  // Column split of the dense operand: no exchange at all.
-  ctx->NewBuilder()
-      .Broadcast(user_op::OpArg(kRowPtr, 0))
-      .Broadcast(user_op::OpArg(kColIdx, 0))
-      .Broadcast(user_op::OpArg(kValues, 0))
-      .Split(user_op::OpArg("b", 0), 1)
-      .Split(user_op::OpArg("out", 0), 1)
-      .Build();
-  return Maybe<void>::Ok();
+  return GetSbp4SpmmCsr(ctx, false);
 }
 
 /* static */ Maybe<void> SpmmCsrOp::InferDataType(user_op::InferContext* ctx) {
@@ -112,6 +128,35 @@ Maybe<void> InferDataType4SpmmCsr(user_op::InferContext* ctx) {
   user_op::InputArgModifier* col_idx_modifier = GetInputArgModifierFn(kColIdx, 0);
   CHECK_NOTNULL_OR_RETURN(col_idx_modifier);
   col_idx_modifier->set_requires_grad(false);
+  return Maybe<void>::Ok();
+}
+
+// ---- spmm_csr_gathered ----------------------------------------------------------------------
+/* static */ Maybe<void> SpmmCsrGatheredOp::InferLogicalTensorDesc(user_op::InferContext* ctx) {
+  JUST(CheckValuesPerm(ctx));
+  return InferTensorDesc4SpmmCsr(ctx);
+}
+
+/* static */ Maybe<void> SpmmCsrGatheredOp::InferPhysicalTensorDesc(user_op::InferContext* ctx) {
+  return InferLogicalTensorDesc(ctx);
+}
+
+/* static */ Maybe<void> SpmmCsrGatheredOp::GetSbp(user_op::SbpContext* ctx) {
+  return GetSbp4SpmmCsr(ctx, true);
+}
+
+/* static */ Maybe<void> SpmmCsrGatheredOp::InferDataType(user_op::InferContext* ctx) {
+  CHECK_EQ_OR_RETURN(ctx->InputDType("values_perm", 0), ctx->InputDType(kRowPtr, 0))
+      << Error::TypeError() << "values_perm should have the dtype of a_csr_row_ptr. ";
+  return InferDataType4SpmmCsr(ctx);
+}
+
+/* static */ Maybe<void> SpmmCsrGatheredOp::ModifyInputArg(
+    const user_op::GetInputArgModifier& GetInputArgModifierFn, const user_op::UserOpConfWrapper& c) {
+  JUST(SpmmCsrOp::ModifyInputArg(GetInputArgModifierFn, c));
+  user_op::InputArgModifier* perm_modifier = GetInputArgModifierFn("values_perm", 0);
+  CHECK_NOTNULL_OR_RETURN(perm_modifier);
+  perm_modifier->set_requires_grad(false);
   return Maybe<void>::Ok();
 }
 

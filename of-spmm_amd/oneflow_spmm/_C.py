@@ -154,7 +154,7 @@ def _run_grad_op(fn, stream_of, ins, outs, extra):
     descs_out = [ctypes.byref(desc(t)) for t in outs]
     check(fn(None, *descs_in, *extra, *descs_out, None, 0, ctypes.byref(size)), fn.__name__)
     tmp = None
-    if size.value and stream_of.device.type != "cpu":
+    if size.value:  # the op's tmp_buffer, on the op's device (host memory for kCPU kernels)
         tmp = torch.empty(size.value, dtype=torch.uint8, device=stream_of.device)
     check(fn(current_stream_handle(stream_of), *descs_in, *extra, *descs_out,
              tmp.data_ptr() if tmp is not None else None, size.value if tmp is not None else 0,
@@ -173,6 +173,24 @@ def sddmm_csr(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor, a: torch
     if b.dim() == 2 and b.shape[1] == 0 and a.dim() == 2 and a.shape[1] == 0:
         return out
     _run_grad_op(LIB.ofx_functional_sddmm_csr, b, [rp, ci, a, b], [out],
+                 [int(a_num_rows), int(a_num_cols)])
+    return out
+
+
+def spmm_csr_gathered(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor,
+                      a_csr_values: torch.Tensor, values_perm: torch.Tensor, a_num_rows: int,
+                      a_num_cols: int, b: torch.Tensor, *, out: torch.Tensor | None = None):
+    """Op "spmm_csr_gathered": A @ b with nonzero j's value a_csr_values[values_perm[j]] (the
+    d(b) gradient of spmm_csr with learnable values: A^T's structure, A's values, A^T's perm)."""
+    rp, ci = _prep(a_csr_row_ptr, "a_csr_row_ptr"), _prep(a_csr_col_idx, "a_csr_col_idx")
+    vals, perm = _prep(a_csr_values, "a_csr_values"), _prep(values_perm, "values_perm")
+    bb = _prep(b, "b", matrix=True)
+    if out is None:
+        out = torch.empty((int(a_num_rows), bb.shape[1] if bb.dim() == 2 else 0), dtype=bb.dtype,
+                          device=bb.device)
+    if out.numel() == 0:
+        return out
+    _run_grad_op(LIB.ofx_functional_spmm_csr_gathered, bb, [rp, ci, vals, perm, bb], [out],
                  [int(a_num_rows), int(a_num_cols)])
     return out
 

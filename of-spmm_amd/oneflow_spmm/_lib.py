@@ -74,6 +74,7 @@ def _load():
         "ofx_csr_transpose": ([p, i32, i64, i64, i64, p, p, p, p, p, p, sz], i32),
         "ofx_csr_transpose_cpu": ([i32, i64, i64, i64, p, p, p, p, p], i32),
         "ofx_gather_values": ([p, i32, i32, i64, p, p, p], i32),
+        "ofx_gather_values_host": ([i32, i32, i64, p, p, p], i32),
         "ofx_sddmm_csr_workspace_size": ([i32, i32, i64, i64, i64, ctypes.POINTER(sz)], i32),
         "ofx_sddmm_csr": ([p, i32, i32, i64, i64, i64, i64, p, p, p, i64, p, i64, p, i64, i64, p, sz], i32),
         "ofx_sddmm_csr_cpu": ([i32, i32, i32, i64, i64, i64, i64, p, p, p, i64, p, i64, p, i64, i64], i32),
@@ -124,6 +125,8 @@ def _load():
                                         i64, i32, i32], i32),
         "ofx_functional_sddmm_csr": ([p, pdesc, pdesc, pdesc, pdesc, i64, i64, pdesc, p, sz,
                                       ctypes.POINTER(sz)], i32),
+        "ofx_functional_spmm_csr_gathered": ([p, pdesc, pdesc, pdesc, pdesc, pdesc, i64, i64, pdesc,
+                                              p, sz, ctypes.POINTER(sz)], i32),
         "ofx_functional_csr_transpose": ([p, pdesc, pdesc, i64, i64, pdesc, pdesc, pdesc, p, sz,
                                           ctypes.POINTER(sz)], i32),
         "ofx_op_spmm_csr_sbp_signatures": ([ctypes.c_char_p, sz], i32),

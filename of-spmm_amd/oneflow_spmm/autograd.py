@@ -102,7 +102,7 @@ class _TransposeCache:
             self.seen[key] = values  # holds values: its storage cannot be reused under the key
             while len(self.seen) > self.capacity:
                 self.seen.popitem(last=False)
-            return ops.spmm_csr_gathered(rp_t, ci_t, values, perm, d_out, k, m)
+            return _C.spmm_csr_gathered(rp_t, ci_t, values, perm, k, m, d_out)
         _, _, vals_t = self.values_t(row_ptr, col_idx, values, k)
         return spmm_csr(rp_t, ci_t, vals_t, k, m, d_out)
 

@@ -265,9 +265,12 @@ def test_gpu_spmm_gathered_values(device, idx, dtype, n):
     g = random_dense(m, n, rng, DTYPES[dtype])
     d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
     out = ops.spmm_csr_gathered(d(rt), d(ct), v.to(device), d(perm), g.to(device), k, m)
+    out_op = fs._C.spmm_csr_gathered(d(rt), d(ct), v.to(device), d(perm), k, m, g.to(device))
     torch.cuda.synchronize()
     vals = to_oracle(v)[perm]
-    assert_bitwise(out, oracle.spmm(rt, ct, vals, to_oracle(g), dtype=dtype), f"{dtype} n={n}")
+    ref = oracle.spmm(rt, ct, vals, to_oracle(g), dtype=dtype)
+    assert_bitwise(out, ref, f"{dtype} n={n}")
+    assert_bitwise(out_op, ref, f"op layer {dtype} n={n}")
 
 
 @pytest.mark.gpu
@@ -292,3 +295,27 @@ def test_gpu_learnable_values_backward(device):
         with torch.no_grad():
             vv.mul_(0.5).add_(0.25)
     assert len(TRANSPOSE_CACHE.seen) <= TRANSPOSE_CACHE.capacity
+
+
+@pytest.mark.parametrize("idx", [torch.int32, torch.int64])
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_cpu_spmm_csr_gathered_op(idx, dtype):
+    """Op "spmm_csr_gathered" through the op layer on CPU (its kCPU kernel gathers the values
+    into the tmp buffer and runs the CPU SpMM): bit-exact vs the oracle on values[perm]; shape
+    and dtype errors from the op's inference; SBP signatures with values_perm broadcast."""
+    rng = np.random.default_rng(12)
+    m, k, n = 120, 90, 9
+    rp, ci, v = random_csr(m, k, power_law_degrees(m, 3000, k, rng), rng, idx, DTYPES[dtype])
+    rt, ct, perm = fs.csr_transpose(rp, ci, k)
+    g = random_dense(m, n, rng, DTYPES[dtype])
+    out = fs._C.spmm_csr_gathered(rt, ct, v, perm, k, m, g)
+    ref = oracle.spmm(rt.numpy(), ct.numpy(), to_oracle(v)[perm.numpy()], to_oracle(g), dtype=dtype)
+    assert_bitwise(out, ref, f"gathered op {dtype}/{idx}")
+    with pytest.raises(RuntimeError, match="values_perm should have nnz"):
+        fs._C.spmm_csr_gathered(rt, ct, v, perm[:-1].contiguous(), k, m, g)
+    with pytest.raises(TypeError, match="values_perm should have the dtype"):
+        other = torch.int64 if idx == torch.int32 else torch.int32
+        fs._C.spmm_csr_gathered(rt, ct, v, perm.to(other), k, m, g)
+    sig = fs._C.sbp_signatures("spmm_csr_gathered")
+    assert "values_perm:B" in sig and "out:S(0)" in sig and "out:S(1)" in sig
+    assert "values_perm" in sig.split("|no_grad:")[1]
