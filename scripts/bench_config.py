@@ -9,6 +9,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -18,7 +19,28 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 
+def log(msg):
+    print(f"[bench_config {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def heartbeat(stop: threading.Event, period: float = 30.0):
+    """Papers-scale phases (host generation of 1.6B columns, the 57 GB B copy for the check)
+    run minutes without output; a line every 30 s keeps the run visibly alive."""
+    t0 = time.time()
+    while not stop.wait(period):
+        log(f"... {time.time() - t0:.0f} s")
+
+
 def main():
+    stop = threading.Event()
+    threading.Thread(target=heartbeat, args=(stop,), daemon=True).start()
+    try:
+        run()
+    finally:
+        stop.set()
+
+
+def run():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="papers")
     ap.add_argument("--reps", type=int, default=5)
@@ -44,6 +66,7 @@ def main():
     d_v = vals.to(dev)
     d_b = synth.dense(0, k, n, dt, device=dev)
     out = torch.empty((m, n), dtype=dt, device=dev)
+    log("inputs resident; timing")
     fs.spmm(d_rp, d_ci, d_v, m, k, d_b, out=out)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -55,6 +78,7 @@ def main():
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
     ms = float(np.median(ts))
+    log(f"median {ms:.3f} ms; checking sampled rows against the oracle")
     sv = d_b.element_size()
     nbytes = alg_bytes(m, nnz, n, sv)
     # sampled check (bit-exact vs oracle with the operator's schedule)
