@@ -45,6 +45,20 @@ def alg_bytes(rows: int, nnz: int, n: int, s_v: int, s_i: int = 4) -> int:
     return s_i * (rows + 1) + (s_i + s_v) * nnz + s_v * nnz * n + s_v * rows * n
 
 
+def host_cpu() -> dict:
+    """nproc and the CPU model of this host (recorded with every CPU number)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "model": model}
+
+
 def _claim_stdout():
     """Route fd 1 to stderr for the whole run (RCCL and the HIP runtime print banners on stdout)
     and return a writer on the real stdout for the one JSON line of the bench contract."""
@@ -330,7 +344,7 @@ def main():
             reps += 1
         cpu_gflops = flops_s * reps / t_cpu / 1e9
         result["cpu_baseline"] = {"value": round(cpu_gflops, 3), "unit": "GFLOP/s", "cores": threads,
-                                  "kind": "port",
+                                  "kind": "port", "host": host_cpu(),
                                   "sample": f"{what} x{reps} runs ({t_cpu:.1f} s), oracle/spmm_oracle.c "
                                             f"OpenMP {threads} threads, same inputs and schedule"}
         # single thread (OneFlow's default CPU_THREADING_RUNTIME=SEQ) on the first
