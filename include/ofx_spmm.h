@@ -225,6 +225,21 @@ int ofx_coo_to_csr_cpu(int idx_dtype, int val_dtype, int64_t m, int64_t k, int64
                        const void* row, const void* col, const void* values, int merge_duplicates,
                        void* out_row_ptr, void* out_col_idx, void* out_values, int64_t* out_nnz);
 
+/* ---- fused-epilogue backward ------------------------------------------
+ * For y = relu?(A @ b + bias?):  dx = relu ? (y > 0 ? dy : 0) : dy   (ReluGrad from the output,
+ * oneflow/core/autograd/gradient_funcs/activation.cpp:195-205) and d_bias[j] = sum_i dx[i, j]
+ * (bias_add grad, gradient_funcs/bias_add.cpp:62), in one pass.  dx may be NULL (only d_bias),
+ * d_bias may be NULL (only dx).  Column-sum order (identical on CPU and GPU): chunks of 2048 rows
+ * summed in row order from +0 in the accumulation type; chunk partials in 8 interleaved lanes
+ * (lane l: chunks l, l+8, ...), lanes combined ((l0+l4)+(l2+l6))+((l1+l5)+(l3+l7)); one rounding. */
+int ofx_relu_bias_grad_workspace_size(int val_dtype, int64_t m, int64_t n, size_t* bytes);
+int ofx_relu_bias_grad(void* stream, int val_dtype, int64_t m, int64_t n, const void* y,
+                       int64_t ldy, const void* dy, int64_t lddy, void* dx, int64_t lddx,
+                       void* d_bias, int relu, void* workspace, size_t workspace_bytes);
+int ofx_relu_bias_grad_cpu(int num_threads, int val_dtype, int64_t m, int64_t n, const void* y,
+                           int64_t ldy, const void* dy, int64_t lddy, void* dx, int64_t lddx,
+                           void* d_bias, int relu);
+
 /* ---- row partition (BalancedSplitter) ---------------------------------------------------- */
 int ofx_balanced_range(int64_t total, int64_t parts, int64_t idx, int64_t* begin, int64_t* end);
 /* Rebase a row slice of a CSR: out_row_ptr[i] = row_ptr[row_begin + i] - row_ptr[row_begin],

@@ -386,3 +386,72 @@ extern "C" int ofx_coo_to_csr_cpu(int idx_dtype, int val_dtype, int64_t m, int64
   if (idx_dtype == OFX_DT_INT32) return run((const int32_t*)nullptr);
   return run((const int64_t*)nullptr);
 }
+
+// ---- fused-epilogue backward on the host (csrc/epilogue_grad.hip states the order) -----------
+namespace {
+
+constexpr int64_t kGradRows = 2048;  // same chunking as the HIP kernel
+constexpr int kGradLanes = 8;
+
+template <typename T>
+int relu_bias_grad_cpu(int num_threads, int64_t m, int64_t n, const T* y, int64_t ldy,
+                       const T* dy, int64_t lddy, T* dx, int64_t lddx, T* d_bias, int relu) {
+#pragma clang fp contract(off)
+  using A = typename Num<T>::acc;
+  const int64_t nch = (m + kGradRows - 1) / kGradRows;
+  std::vector<A> part(d_bias ? (size_t)nch * (size_t)n : 0);
+  if (num_threads > 0) omp_set_num_threads(num_threads);
+#pragma omp parallel for schedule(static)
+  for (int64_t c = 0; c < nch; ++c) {
+    const int64_t r1 = (c + 1) * kGradRows < m ? (c + 1) * kGradRows : m;
+    for (int64_t j = 0; j < n; ++j) {
+      A acc = A(0);
+      for (int64_t r = c * kGradRows; r < r1; ++r) {
+        const A g = (relu && !(Num<T>::load(y[r * ldy + j]) > A(0))) ? A(0)
+                                                                       : Num<T>::load(dy[r * lddy + j]);
+        if (dx) dx[r * lddx + j] = Num<T>::store(g);
+        acc = acc + g;
+      }
+      if (d_bias) part[(size_t)c * n + j] = acc;
+    }
+  }
+  if (d_bias) {
+    for (int64_t j = 0; j < n; ++j) {
+      A lane[kGradLanes];
+      for (int l = 0; l < kGradLanes; ++l) {
+        A acc = A(0);
+        for (int64_t c = l; c < nch; c += kGradLanes) acc = acc + part[(size_t)c * n + j];
+        lane[l] = acc;
+      }
+      for (int s = kGradLanes / 2; s >= 1; s >>= 1)
+        for (int l = 0; l < s; ++l) lane[l] = lane[l] + lane[l + s];
+      d_bias[j] = Num<T>::store(lane[0]);
+    }
+  }
+  return OFX_OK;
+}
+
+}  // namespace
+
+extern "C" int ofx_relu_bias_grad_cpu(int num_threads, int val_dtype, int64_t m, int64_t n,
+                                      const void* y, int64_t ldy, const void* dy, int64_t lddy,
+                                      void* dx, int64_t lddx, void* d_bias, int relu) {
+  OFX_REQUIRE(is_value_dtype(val_dtype), OFX_EUNSUPPORTED, "relu_bias_grad: bad dtype %d",
+              val_dtype);
+  OFX_REQUIRE(m >= 0 && n >= 0, OFX_EINVAL, "relu_bias_grad: negative size");
+  if (n == 0) return OFX_OK;
+  OFX_REQUIRE(m == 0 || (dy && (!relu || y) && lddy >= n && (!relu || ldy >= n)), OFX_EINVAL,
+              "relu_bias_grad: NULL input or leading dimension < n");
+  OFX_REQUIRE(dx == nullptr || lddx >= n, OFX_EINVAL, "relu_bias_grad: lddx < n");
+#define OFX_RBG(T)                                                                               \
+  return relu_bias_grad_cpu<T>(num_threads, m, n, static_cast<const T*>(y), ldy,                 \
+                               static_cast<const T*>(dy), lddy, static_cast<T*>(dx), lddx,       \
+                               static_cast<T*>(d_bias), relu)
+  switch (val_dtype) {
+    case OFX_DT_FLOAT: OFX_RBG(float);
+    case OFX_DT_DOUBLE: OFX_RBG(double);
+    case OFX_DT_BFLOAT16: OFX_RBG(bf16);
+    default: OFX_RBG(f16);
+  }
+#undef OFX_RBG
+}

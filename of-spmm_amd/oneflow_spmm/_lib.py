@@ -60,6 +60,9 @@ def _load():
                           popt], i32),
         "ofx_spmm_csr_gathered": ([p, i32, i32, i64, i64, i64, i64, p, p, p, p, p, i64, p, i64, i64,
                                    i64, p, sz, popt], i32),
+        "ofx_relu_bias_grad_workspace_size": ([i32, i64, i64, ctypes.POINTER(sz)], i32),
+        "ofx_relu_bias_grad": ([p, i32, i64, i64, p, i64, p, i64, p, i64, p, i32, p, sz], i32),
+        "ofx_relu_bias_grad_cpu": ([i32, i32, i64, i64, p, i64, p, i64, p, i64, p, i32], i32),
         "ofx_spmm_csr_plan": ([p, i32, i32, i64, i64, i64, i64, p, i64, i64, p, sz, popt], i32),
         "ofx_spmm_csr_fused": ([p, i32, i32, i64, i64, i64, i64, p, p, p, p, i64, p, i64, i64, i64,
                                 p, i32, p, sz, popt], i32),

@@ -157,10 +157,9 @@ class FusedSpmmCsrFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, d_out):
         row_ptr, col_idx, values, b, out = ctx.saved_tensors
-        g = d_out.contiguous()
-        if ctx.relu:
-            g = torch.where(out > 0, g, torch.zeros_like(g))
-        d_bias = g.sum(0) if ctx.has_bias and ctx.needs_input_grad[6] else None
+        # relu_grad and the bias column sum in one HIP pass (ofx_relu_bias_grad)
+        g, d_bias = ops.relu_bias_grad(out, d_out.contiguous(), relu=ctx.relu,
+                                       bias_grad=ctx.has_bias and ctx.needs_input_grad[6])
         d_values = d_b = None
         if ctx.needs_input_grad[2]:
             d_values = sddmm(row_ptr, col_idx, g, b)

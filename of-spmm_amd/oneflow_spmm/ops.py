@@ -133,6 +133,31 @@ def spmm_csr_gathered(row_ptr, col_idx, values, values_perm, b, m, k, *, out=Non
     return out
 
 
+def relu_bias_grad(y, dy, *, relu: bool, bias_grad: bool, num_threads: int = 0):
+    """Backward of the fused epilogue (ofx_relu_bias_grad[_cpu]): returns (dx, d_bias).
+    dx = relu ? where(y > 0, dy, 0) : dy (dy itself when relu is off); d_bias = column sum of dx
+    in the contract's fixed order, or None."""
+    m, n = dy.shape
+    dt = dtype_code(dy.dtype)
+    dx = torch.empty_like(dy) if relu else dy
+    db = torch.empty(n, dtype=dy.dtype, device=dy.device) if bias_grad else None
+    if not relu and not bias_grad:
+        return dx, db
+    nz = lambda t: t.data_ptr() if t is not None and t.numel() else None  # noqa: E731
+    yy = y if relu else None
+    args = (m, n, nz(yy), yy.stride(0) if yy is not None else n, nz(dy), dy.stride(0),
+            nz(dx) if relu else None, dx.stride(0) if relu else n, nz(db), 1 if relu else 0)
+    if dy.device.type == "cpu":
+        check(LIB.ofx_relu_bias_grad_cpu(int(num_threads), dt, *args), "relu_bias_grad")
+        return dx, db
+    size = ctypes.c_size_t(0)
+    check(LIB.ofx_relu_bias_grad_workspace_size(dt, m, n, ctypes.byref(size)), "relu_bias_grad")
+    ws = torch.empty(max(size.value, 1), dtype=torch.uint8, device=dy.device)
+    check(LIB.ofx_relu_bias_grad(current_stream_handle(dy), dt, *args, ws.data_ptr(), size.value),
+          "relu_bias_grad")
+    return dx, db
+
+
 def spmm_csr_cpu(row_ptr, col_idx, values, b, m, k, *, out=None, row_begin=0, row_end=None,
                  options: Options | None = None, num_threads: int = 0, bias=None, relu=False):
     """The DeviceType::kCPU kernel (C-ABI ofx_spmm_csr_fused_cpu), host tensors."""

@@ -151,6 +151,48 @@ def bias_act(out, bias=None, activation="none", *, dtype="f32"):
     return y
 
 
+def relu_bias_grad(y, dy, *, relu: bool, dtype="f32"):
+    """Backward of the fused epilogue, restating csrc/epilogue_grad.hip (TEST INFRASTRUCTURE):
+    dx = relu ? (y > 0 ? dy : 0) : dy   (ReluGrad from the output,
+         oneflow/core/autograd/gradient_funcs/activation.cpp:195-205),
+    d_bias[j] = sum_i dx[i, j]           (bias_add grad, gradient_funcs/bias_add.cpp:62) in the
+    operator's stated order: chunks of 2048 rows summed in row order from +0 in the
+    accumulation type, chunk partials in 8 interleaved lanes, lanes combined
+    ((l0+l4)+(l2+l6))+((l1+l5)+(l3+l7)), one rounding.  The reference's reduce_sum order is
+    its device reduction's, so only this restatement pins the bits.  bf16 = uint16 bits."""
+    def to_acc(a):
+        if dtype == "bf16":
+            return bf16_bits_to_f32(np.asarray(a))
+        return np.asarray(a).astype(np.float64 if dtype == "f64" else np.float32)
+    acc_t = np.float64 if dtype == "f64" else np.float32
+    g = to_acc(dy)
+    if relu:
+        g = np.where(to_acc(y) > 0, g, acc_t(0)).astype(acc_t)
+    m, n = g.shape
+    rows, lanes = 2048, 8
+    nch = (m + rows - 1) // rows
+    part = np.zeros((nch, n), dtype=acc_t)
+    for c in range(nch):
+        blk = g[c * rows:(c + 1) * rows]
+        part[c] = np.cumsum(blk, axis=0, dtype=acc_t)[-1]  # sequential, rounded each step
+    lane = np.zeros((lanes, n), dtype=acc_t)
+    for l in range(lanes):
+        sel = part[l::lanes]
+        if len(sel):
+            lane[l] = np.cumsum(sel, axis=0, dtype=acc_t)[-1]
+    s = lanes // 2
+    while s >= 1:
+        lane[:s] = (lane[:s] + lane[s:2 * s]).astype(acc_t)
+        s //= 2
+    def store(a):
+        if dtype == "bf16":
+            return f32_to_bf16_bits(a.astype(np.float32))
+        if dtype == "f16":
+            return a.astype(np.float16)
+        return a.astype(acc_t)
+    return store(g), store(lane[0])
+
+
 def ref64(row_ptr, col_idx, values_f32, b_f32, *, row_begin=0, row_end=None, nthreads=None):
     """fp64 product C64 and |.|-sum bound of an fp32 (or upcast 16-bit) problem."""
     m = len(row_ptr) - 1

@@ -135,3 +135,46 @@ def test_gpu_fused_autograd_matches_cpu(device):
         grads.append([out.detach().cpu(), vv.grad.cpu(), bb.grad.cpu()])
     for a, c in zip(*grads):  # forward, d values (SDDMM) and dB are bit-identical CPU vs GPU
         assert torch.equal(a.view(torch.int32), c.view(torch.int32))
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f64"])
+@pytest.mark.parametrize("relu", [False, True])
+@pytest.mark.parametrize("m", [0, 5, 2048, 2049, 40000])
+def test_cpu_relu_bias_grad_bitexact(dtype, relu, m):
+    """The fused epilogue's backward on the host (ofx_relu_bias_grad_cpu): dx and the bias
+    column sum equal the oracle's restatement of the stated order bit for bit (chunk edges at
+    2048 rows, more than 8 chunks at 40000 rows, an empty batch)."""
+    from oneflow_spmm import ops
+    rng = np.random.default_rng(m + 3)
+    n = 13
+    y = random_dense(m, n, rng, DTYPES[dtype])
+    dy = random_dense(m, n, rng, DTYPES[dtype])
+    dx, db = ops.relu_bias_grad(y, dy, relu=relu, bias_grad=True)
+    ref_dx, ref_db = oracle.relu_bias_grad(to_oracle(y), to_oracle(dy), relu=relu, dtype=dtype)
+    assert_bitwise(dx, ref_dx, "dx")
+    assert_bitwise(db, ref_db, "d_bias")
+    if m:
+        exact = (torch.where(y > 0, dy, torch.zeros_like(dy)) if relu else dy).double().sum(0)
+        assert torch.allclose(db.double(), exact, rtol=1e-2 if dtype == "bf16" else 1e-5, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
+@pytest.mark.parametrize("m,n", [(0, 7), (3, 300), (2049, 64), (70001, 129)])
+def test_gpu_relu_bias_grad_bitexact(device, dtype, m, n):
+    """ofx_relu_bias_grad on the device: same bits as the oracle and as the CPU kernel."""
+    from oneflow_spmm import ops
+    rng = np.random.default_rng(m + n)
+    y = random_dense(m, n, rng, DTYPES[dtype])
+    dy = random_dense(m, n, rng, DTYPES[dtype])
+    dx, db = ops.relu_bias_grad(y.to(device), dy.to(device), relu=True, bias_grad=True)
+    _, db_only = ops.relu_bias_grad(y.to(device), dy.to(device), relu=False, bias_grad=True)
+    torch.cuda.synchronize()
+    ref_dx, ref_db = oracle.relu_bias_grad(to_oracle(y), to_oracle(dy), relu=True, dtype=dtype)
+    assert_bitwise(dx, ref_dx, "dx")
+    assert_bitwise(db, ref_db, "d_bias")
+    assert_bitwise(db_only, oracle.relu_bias_grad(to_oracle(y), to_oracle(dy), relu=False,
+                                                  dtype=dtype)[1], "d_bias without relu")
+    cdx, cdb = ops.relu_bias_grad(y, dy, relu=True, bias_grad=True)
+    assert torch.equal(cdx.view(torch.uint8), dx.cpu().view(torch.uint8))
+    assert torch.equal(cdb.view(torch.uint8), db.cpu().view(torch.uint8))
