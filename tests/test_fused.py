@@ -176,5 +176,5 @@ def test_gpu_relu_bias_grad_bitexact(device, dtype, m, n):
     assert_bitwise(db_only, oracle.relu_bias_grad(to_oracle(y), to_oracle(dy), relu=False,
                                                   dtype=dtype)[1], "d_bias without relu")
     cdx, cdb = ops.relu_bias_grad(y, dy, relu=True, bias_grad=True)
-    assert torch.equal(cdx.view(torch.uint8), dx.cpu().view(torch.uint8))
-    assert torch.equal(cdb.view(torch.uint8), db.cpu().view(torch.uint8))
+    assert_bitwise(dx, to_oracle(cdx), "dx vs the CPU kernel")
+    assert_bitwise(db, to_oracle(cdb), "d_bias vs the CPU kernel")
