@@ -54,10 +54,12 @@ struct alignas(sizeof(T) * VEC) Pack {
 // Compile-time kernel configuration: VEC elements per lane, LPR lanes per row-group, U B-row
 // loads in flight per lane, WPB waves per block, NT = non-temporal hints on the once-touched
 // streams (col_idx, values, C) so they do not displace B rows from L2 / Infinity Cache.
-template <int VEC_, int LPR_, int U_ = 8, int WPB_ = 4, bool NT_ = false>
+// PF: the next batch's (col, val) pairs are loaded before this batch's B rows, so a long row
+// pays one memory round trip per batch instead of two (the small-problem configurations).
+template <int VEC_, int LPR_, int U_ = 8, int WPB_ = 4, bool NT_ = false, bool PF_ = false>
 struct Cfg {
   static constexpr int VEC = VEC_, LPR = LPR_, U = U_, WPB = WPB_;
-  static constexpr bool NT = NT_;
+  static constexpr bool NT = NT_, PF = PF_;
 };
 
 template <typename X>
@@ -122,7 +124,8 @@ __device__ __forceinline__ int64_t uniform64(int64_t v) {
 template <typename T, typename I, typename K>
 __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* __restrict__ val,
                                            const I* __restrict__ vperm,
-                                           const T* __restrict__ Bc, int64_t ldb, int64_t j0,
+                                           const T* __restrict__ Bc, const T* __restrict__ B0,
+                                           int64_t ldb, int64_t j0,
                                            int64_t j1, int gl, int gbase, bool active,
                                            typename Num<T>::acc (&acc)[K::VEC]) {
 #pragma clang fp contract(off)
@@ -153,24 +156,74 @@ __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* _
       }
     }
   } else {
-    for (int64_t jb = j0; jb < j1; jb += LPR) {
-      const int cnt = (int)((j1 - jb) < LPR ? (j1 - jb) : LPR);
-      I myc = 0;
-      A myv = 0;
-      if (gl < cnt) {
-        myc = ld_stream<K::NT>(col + jb + gl);
-        const int64_t jv = vperm ? (int64_t)ld_stream<K::NT>(vperm + jb + gl) : jb + gl;
-        myv = Num<T>::load(ld_stream<K::NT>(val + jv));
+    // A batch is R * LPR nonzeros: each lane loads R (col, val) pairs coalesced, the group
+    // broadcasts them with ds_bpermute.  R > 1 only when more B-row loads are kept in flight
+    // than there are lanes in the group (kUnroll > LPR: the small-problem configurations).
+    constexpr int R = kUnroll > LPR ? kUnroll / LPR : 1;
+    constexpr int BATCH = LPR * R;
+    auto load_batch = [&](int64_t jb, I (&c)[R], A (&v)[R]) {
+      const int n_ = (int)((j1 - jb) < BATCH ? (j1 - jb) : BATCH);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        c[r] = 0;
+        v[r] = 0;
+        const int idx = r * LPR + gl;
+        if (idx < n_) {
+          c[r] = ld_stream<K::NT>(col + jb + idx);
+          const int64_t jv = vperm ? (int64_t)ld_stream<K::NT>(vperm + jb + idx) : jb + idx;
+          v[r] = Num<T>::load(ld_stream<K::NT>(val + jv));
+        }
+      }
+    };
+    I nxc[R];
+    A nxv[R];
+    if constexpr (K::PF) {
+      if (j0 < j1) load_batch(j0, nxc, nxv);
+    }
+    for (int64_t jb = j0; jb < j1; jb += BATCH) {
+      const int cnt = (int)((j1 - jb) < BATCH ? (j1 - jb) : BATCH);
+      I myc[R];
+      A myv[R];
+      if constexpr (K::PF) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          myc[r] = nxc[r];
+          myv[r] = nxv[r];
+        }
+        if (jb + BATCH < j1) load_batch(jb + BATCH, nxc, nxv);  // in flight during this batch
+      } else {
+        load_batch(jb, myc, myv);
       }
       for (int k = 0; k < cnt; k += kUnroll) {
         P bv[kUnroll];
         A vv[kUnroll];
+        if constexpr (K::PF) {
+          // Branch-free issue for the latency-bound small launches: every broadcast first, then
+          // every load (slots past the row end read B row 0, inactive lanes read from B's first
+          // columns; both discarded below), so the group pays one LDS wait and one memory round
+          // trip per batch instead of one ds_bpermute wait per load.
+          int64_t cuv[kUnroll];
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-          const int src = gbase + ((k + u) & (LPR - 1));
-          const int64_t cu = (int64_t)shfl(myc, src);
-          vv[u] = shfl(myv, src);
-          if (k + u < cnt && active) bv[u] = *reinterpret_cast<const P*>(Bc + cu * ldb);
+          for (int u = 0; u < kUnroll; ++u) {
+            const int src = gbase + ((k + u) & (LPR - 1));
+            const int r = R > 1 ? u / LPR : 0;
+            cuv[u] = (int64_t)shfl(myc[r], src);
+            vv[u] = shfl(myv[r], src);
+          }
+          const T* Bs = active ? Bc : B0;
+#pragma unroll
+          for (int u = 0; u < kUnroll; ++u)
+            bv[u] = *reinterpret_cast<const P*>(Bs + (k + u < cnt ? cuv[u] : 0) * ldb);
+        } else {
+#pragma unroll
+          for (int u = 0; u < kUnroll; ++u) {
+            // R > 1: the batch is exactly kUnroll long, so k == 0 and the register is static
+            const int src = gbase + ((k + u) & (LPR - 1));
+            const int r = R > 1 ? u / LPR : 0;
+            const int64_t cu = (int64_t)shfl(myc[r], src);
+            vv[u] = shfl(myv[r], src);
+            if (k + u < cnt && active) bv[u] = *reinterpret_cast<const P*>(Bc + cu * ldb);
+          }
         }
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
@@ -263,7 +316,7 @@ __global__ void __launch_bounds__(64 * K::WPB)
     A acc[VEC];
 #pragma unroll
     for (int e = 0; e < VEC; ++e) acc[e] = A(0);
-    accumulate<T, I, K>(col, val, vperm, B + cc, ldb, j0, j1, gl, gbase, active, acc);
+    accumulate<T, I, K>(col, val, vperm, B + cc, B, ldb, j0, j1, gl, gbase, active, acc);
     if (active) {
       if (c >= 0)
         store_partial<A, VEC>(part + g * n + cc, acc);
@@ -487,8 +540,31 @@ int launch_cfg(const Launch& L) {
 // (1M power-law, 256 MB) the same hint costs +8%, hence the threshold.
 constexpr int64_t kNtBytes = int64_t(1) << 30;
 
+// Small problems (<= kSmallRows rows: too few lane-groups to be bandwidth-bound) run as long as
+// their longest non-split row, a chain of len / U dependent B-row load rounds; these launches keep
+// 32 (16 for 8-16 B lanes) loads in flight per lane instead of 8.  A Cora-shaped layer (max row
+// 253 nonzeros, N=16) took 25 us with U=8.  Same bits: U only changes how many loads are issued
+// ahead of the in-order adds.
+constexpr int64_t kSmallRows = 32768;
+
+template <typename T, typename I, int VEC>
+int launch_vec_small(const Launch& L, int lpr) {
+  constexpr int U = VEC * sizeof(T) <= 4 ? 32 : 16;
+  switch (lpr) {
+    case 4: return launch_cfg<T, I, Cfg<VEC, 4, U, 4, false, true>>(L);
+    case 8: return launch_cfg<T, I, Cfg<VEC, 8, U, 4, false, true>>(L);
+    case 16: return launch_cfg<T, I, Cfg<VEC, 16, U, 4, false, true>>(L);
+    case 32: return launch_cfg<T, I, Cfg<VEC, 32, U, 4, false, true>>(L);
+    case 64: return launch_cfg<T, I, Cfg<VEC, 64, U>>(L);
+    default: return fail(OFX_EINVAL, "spmm_csr: unsupported lanes-per-row %d", lpr);
+  }
+}
+
 template <typename T, typename I, int VEC>
 int launch_vec(const Launch& L, int lpr, bool nt) {
+  // forced variants (tests, tuning) keep the U = 8 configurations at every size
+  if (L.nrows <= kSmallRows && !nt && L.sched.variant == 0)
+    return launch_vec_small<T, I, VEC>(L, lpr);
   switch (lpr) {
     case 4: return launch_cfg<T, I, Cfg<VEC, 4>>(L);
     case 8: return launch_cfg<T, I, Cfg<VEC, 8>>(L);

@@ -158,25 +158,20 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
-template <typename I>
-__global__ void __launch_bounds__(kBlock)
-    spmm_plan_write_kernel(const I* __restrict__ rp, int64_t row_begin, int64_t nrows,
-                           int64_t split, int64_t chunk, int64_t heavy,
-                           const int64_t* __restrict__ block_off,
-                           const unsigned long long* __restrict__ counters,
-                           int64_t* __restrict__ hubs, int64_t* __restrict__ items,
-                           int64_t* __restrict__ order) {
-  int cls[kPlanRowsPerThread];
-  int64_t nc[kPlanRowsPerThread], v[kPlanVals], tot[kPlanVals];
-  const int64_t base = (int64_t)blockIdx.x * kPlanRows + (int64_t)threadIdx.x * kPlanRowsPerThread;
-  plan_thread(rp, row_begin, nrows, base, split, chunk, heavy, cls, nc, v);
-  block_scan_vals(v, tot);
-  const int64_t* off = block_off + kPlanVals * blockIdx.x;
+// Writes one tile's hubs / chunk items / binned order, given this thread's exclusive offsets `v`
+// inside the tile, the tile's offsets `off` across tiles and the bins' start positions.
+__device__ __forceinline__ void plan_write_rows(const int (&cls)[kPlanRowsPerThread],
+                                                const int64_t (&nc)[kPlanRowsPerThread],
+                                                const int64_t (&v)[kPlanVals], const int64_t* off,
+                                                const unsigned long long* bin_start, int64_t base,
+                                                int64_t* __restrict__ hubs,
+                                                int64_t* __restrict__ items,
+                                                int64_t* __restrict__ order) {
   int64_t hi = off[0] + v[0];
   int64_t slot = off[1] + v[1];
   int64_t pos[kBins];
 #pragma unroll
-  for (int b = 0; b < kBins; ++b) pos[b] = (int64_t)counters[2 + b] + off[2 + b] + v[2 + b];
+  for (int b = 0; b < kBins; ++b) pos[b] = (int64_t)bin_start[b] + off[2 + b] + v[2 + b];
   int64_t first[kPlanRowsPerThread];
 #pragma unroll
   for (int q = 0; q < kPlanRowsPerThread; ++q) {
@@ -217,6 +212,23 @@ __global__ void __launch_bounds__(kBlock)
       }
     }
   }
+}
+
+template <typename I>
+__global__ void __launch_bounds__(kBlock)
+    spmm_plan_write_kernel(const I* __restrict__ rp, int64_t row_begin, int64_t nrows,
+                           int64_t split, int64_t chunk, int64_t heavy,
+                           const int64_t* __restrict__ block_off,
+                           const unsigned long long* __restrict__ counters,
+                           int64_t* __restrict__ hubs, int64_t* __restrict__ items,
+                           int64_t* __restrict__ order) {
+  int cls[kPlanRowsPerThread];
+  int64_t nc[kPlanRowsPerThread], v[kPlanVals], tot[kPlanVals];
+  const int64_t base = (int64_t)blockIdx.x * kPlanRows + (int64_t)threadIdx.x * kPlanRowsPerThread;
+  plan_thread(rp, row_begin, nrows, base, split, chunk, heavy, cls, nc, v);
+  block_scan_vals(v, tot);
+  plan_write_rows(cls, nc, v, block_off + kPlanVals * blockIdx.x, counters + 2, base, hubs, items,
+                  order);
 }
 
 struct WsLayout {

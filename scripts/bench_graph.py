@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Eager op-layer calls vs one hipGraph replay (oneflow_spmm.SpmmGraph) for a two-layer GCN
+forward: fused_spmm(+bias, relu) then spmm, on a BASELINE-shaped graph.  Small graphs (Cora) are
+launch- and host-bound in eager mode; the graph removes the per-op host work.
+
+    python scripts/bench_graph.py [--config cora] [--iters 200]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "of-spmm_amd"), ROOT]
+
+import torch  # noqa: E402
+
+
+def per_iter_ms(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e3 / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cora")
+    ap.add_argument("--iters", type=int, default=200)
+    args = ap.parse_args()
+    import oneflow_spmm as fs
+    from oneflow_spmm import synth
+
+    cfg = synth.CONFIGS[args.config]
+    m, k, nnz, n, dt = cfg["m"], cfg["k"], cfg["nnz"], cfg["n"], cfg["dtype"]
+    assert m == k, "a GCN layer stack needs a square adjacency"
+    dev = torch.device("cuda", 0)
+    rp, ci, v = synth.csr(m, k, nnz, val_dtype=dt, threads=16)
+    rp, ci, v = rp.to(dev), ci.to(dev), v.to(dev)
+    x = synth.dense(0, k, n, dt, device=dev)
+    bias = synth.dense(0, 1, n, dt, device=dev, seed=5)[0]
+
+    def gcn(h):
+        h1 = fs.fused_spmm(rp, ci, v, m, m, h, bias, relu=True)
+        return fs.spmm(rp, ci, v, m, m, h1)
+
+    with torch.no_grad():
+        eager = per_iter_ms(lambda: gcn(x), args.iters)
+        g = fs.SpmmGraph(gcn, x)
+        replay = per_iter_ms(lambda: g.graph.replay(), args.iters)
+        same = bool(torch.equal(g.run(x).view(torch.uint8), gcn(x).view(torch.uint8)))
+    print(json.dumps({"config": args.config, "m": m, "nnz": nnz, "n": n, "layers": 2,
+                      "eager_ms_per_forward": round(eager, 4),
+                      "graph_replay_ms_per_forward": round(replay, 4),
+                      "speedup": round(eager / replay, 2), "bitexact": same}))
+
+
+if __name__ == "__main__":
+    main()
