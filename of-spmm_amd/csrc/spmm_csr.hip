@@ -596,6 +596,11 @@ int launch_tuned(const Launch& L, int id) {
       case 8: return launch_cfg<T, I, Cfg<4, 32, 16, 4, true>>(L);
       case 9: return launch_cfg<T, I, Cfg<4, 16, 8, 4, false>>(L);
       case 10: return launch_cfg<T, I, Cfg<4, 16, 8, 4, true>>(L);
+      // prefetch + branch-free issue (the small-launch form) at products scale
+      case 11: return launch_cfg<T, I, Cfg<4, 32, 8, 4, true, true>>(L);
+      case 12: return launch_cfg<T, I, Cfg<4, 32, 16, 4, true, true>>(L);
+      case 13: return launch_cfg<T, I, Cfg<4, 32, 32, 4, true, true>>(L);
+      case 14: return launch_cfg<T, I, Cfg<4, 32, 8, 4, false, true>>(L);
       default: break;
     }
   }
