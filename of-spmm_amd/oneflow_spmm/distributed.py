@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import time
 
 import torch
 import torch.distributed as dist
@@ -713,11 +714,17 @@ class RowSplitSpmm:
         Keeps the fastest.  Timings are max-reduced over ranks, so all ranks choose the same; every
         candidate produces the same bytes.  Returns {"<comm>/p<C>" | "halo" | "nsplit[/s<S>]" |
         "grid<R>x<C>[/s<S>]": ms}.  One rank has nothing to exchange, so it keeps its setting unless
-        `force` (tests)."""
+        `force` (tests).  With torch.distributed as the transport (gloo on CPU, the tests) the
+        all-gather candidates are its collectives and the clock is the host's."""
         if self._bound is None:
             raise RuntimeError("tune: bind() the CSR first")
-        if not self.comm_kind.startswith("rccl") or (self.world == 1 and not force):
+        if self.world == 1 and not force:
             return {}
+        native = self.comm_kind.startswith("rccl")
+        kinds = ("rccl", "rccl-p2p") if native else ("torch",)
+        base = "rccl" if native else "torch"
+        on_gpu = self.device.type == "cuda"
+        red_dev = self.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
 
         def measure():
             # A candidate that raises on any rank (a host-side error, deterministic across ranks)
@@ -725,17 +732,24 @@ class RowSplitSpmm:
             ms = float("inf")
             try:
                 self.step(out)
-                torch.cuda.synchronize(self.device)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(reps):
-                    self.step(out)
-                e1.record()
-                torch.cuda.synchronize(self.device)
-                ms = e0.elapsed_time(e1) / reps
+                if on_gpu:
+                    torch.cuda.synchronize(self.device)
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(reps):
+                        self.step(out)
+                    e1.record()
+                    torch.cuda.synchronize(self.device)
+                    ms = e0.elapsed_time(e1) / reps
+                else:
+                    t0 = time.perf_counter()
+                    for _ in range(reps):
+                        self.step(out)
+                    ms = (time.perf_counter() - t0) * 1e3 / reps
             except Exception as e:  # noqa: BLE001 -- reported, candidate dropped
                 self.tune_errors[f"{self.exchange}/{self.comm_kind}/p{self.chunks}"] = repr(e)
-            t = torch.tensor([ms], dtype=torch.float64, device=self.device)
+            t = torch.tensor([ms], dtype=torch.float64, device=red_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
             return float(t.item())
 
@@ -746,20 +760,20 @@ class RowSplitSpmm:
             if self.n % chunks:
                 continue
             self.set_pipeline(chunks)
-            for kind in ("rccl", "rccl-p2p"):
+            for kind in kinds:
                 self.comm_kind = kind
                 times[f"{kind}/p{chunks}"] = measure()
         if self.halo is not None:
-            self.exchange, self.comm_kind = "halo", "rccl"
+            self.exchange, self.comm_kind = "halo", base
             times["halo"] = measure()
         for name in self.grids:
-            self.exchange, self.comm_kind = name, "rccl"
+            self.exchange, self.comm_kind = name, base
             times[name] = measure()
         best = min(times, key=times.get)
         if not math.isfinite(times[best]):
             raise RuntimeError(f"RowSplitSpmm.tune: every exchange failed: {self.tune_errors}")
         if best == "halo" or best in self.grids:
-            self.exchange, self.comm_kind = best, "rccl"
+            self.exchange, self.comm_kind = best, base
             self.set_pipeline(1)
         else:
             kind, p = best.split("/p")

@@ -183,3 +183,59 @@ def test_halo_exchange_moves_only_the_band_edges(world):
     res = [q.get(timeout=5) for _ in range(world)]
     assert all(p.exitcode == 0 for p in procs)
     assert all(ok for _, ok, _ in res), res
+
+
+def _tune_worker(rank, world, port, q):
+    """tune() over torch.distributed (gloo): every candidate (all-gather x pipeline depth, halo,
+    every grid with and without sub-blocks) runs the real step, the max-reduced timings make every
+    rank keep the same one, and the kept exchange still gives the oracle's bits."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    import sys
+    for p in (root, os.path.join(root, "of-spmm_amd")):
+        sys.path.insert(0, p)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oneflow_spmm import ops
+        from oneflow_spmm.distributed import RowSplitSpmm
+        from oracle import oracle
+        from tests.helpers import power_law_degrees, random_csr, random_dense
+
+        rng = np.random.default_rng(55)
+        m, k, n = 900, 850, 16
+        rp, ci, v = random_csr(m, k, power_law_degrees(m, 20000, k, rng), rng)
+        b = random_dense(k, n, rng)
+        full = oracle.spmm(rp.numpy(), ci.numpy(), v.numpy(), b.numpy())
+        lo, hi = oracle.balanced_range(m, world, rank)
+        lrp, n0, n1 = ops.csr_row_slice(rp, lo, hi)
+        rs = RowSplitSpmm(m, k, n, n1 - n0, torch.float32, torch.int32, "cpu")
+        klo, khi = rs.k_range
+        rs.load_shard(b[klo:khi])
+        rs.bind(lrp, ci[n0:n1], v[n0:n1], halo=True, full_csr=(rp, ci, v), grid_subs=(1, 2))
+        out = torch.empty((hi - lo, n))
+        times = rs.tune(out, reps=1)
+        want = {"torch/p1", "torch/p2", "torch/p4", "halo", "grid2x2", "grid2x2/s2", "nsplit",
+                "nsplit/s2"}
+        ok = set(times) == want and all(np.isfinite(t) for t in times.values())
+        out.fill_(float("nan"))
+        rs.step(out)
+        ok = ok and np.array_equal(out.numpy().view(np.uint32), full[lo:hi].view(np.uint32))
+        q.put((rank, (bool(ok), rs.exchange, rs.comm_kind, rs.chunks, sorted(times))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tune_over_gloo_keeps_one_choice_everywhere():
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tune_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    res = dict(q.get(timeout=5) for _ in range(world))
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert all(r[0] for r in res.values()), res
+    assert len({r[1:4] for r in res.values()}) == 1, res  # the same exchange on every rank
