@@ -170,6 +170,9 @@ def main():
             rs.set_pipeline(args.pipeline or 1)
         else:
             comm_times = rs.tune(out, force=args.force_rowsplit)
+            log("[bench] exchange candidates (ms, max over ranks): " +
+                ", ".join(f"{kk} {vv:.3f}" for kk, vv in sorted(comm_times.items(), key=lambda x: x[1])))
+        log(f"[bench] exchange kept: {rs.exchange} / {rs.comm_kind} / pipeline {rs.chunks}")
 
         def step():
             rs.step(out)
