@@ -310,6 +310,13 @@ int ofx_exchange_rows(void* stream, void* comm, int dtype, int64_t n, const void
 /* Row gather on the device: dst[i, :] = src[idx[i], :] for i < count, rows of row_bytes bytes,
  * strides in bytes (packs the halo rows a peer requested into one send buffer).  idx == NULL
  * is the identity: a strided 2-D copy (column-block packing of the N-split exchange).        */
+/* 3-level strided block copy on the device, strides in bytes: for o < nouter, i < ninner,
+ * r < rows, row_bytes from src + o*src_outer + i*src_inner + r*src_row to the same position in
+ * dst's strides.  One launch packs a B shard into the grid exchange's column blocks (and
+ * unpacks the returned C blocks); replaces per-block ofx_gather_rows calls.                  */
+int ofx_copy_blocks(void* stream, int64_t nouter, int64_t ninner, int64_t rows, int64_t row_bytes,
+                    const void* src, int64_t src_outer, int64_t src_inner, int64_t src_row,
+                    void* dst, int64_t dst_outer, int64_t dst_inner, int64_t dst_row);
 int ofx_gather_rows(void* stream, int idx_dtype, int64_t count, int64_t row_bytes,
                     const void* idx, const void* src, int64_t src_stride_bytes, void* dst,
                     int64_t dst_stride_bytes);

@@ -92,6 +92,84 @@ extern "C" int ofx_gather_rows(void* stream, int idx_dtype, int64_t count, int64
                   dst_stride_bytes);
 }
 
+// ---- 3-level strided block copy (grid exchange pack / unpack) ---------------
+// Row q = (o, i, r) of an nouter x ninner x rows set of rows, each row_bytes long:
+//   dst + o*dst_outer + i*dst_inner + r*dst_row  <-  src + o*src_outer + i*src_inner + r*src_row
+// One launch replaces the C x S per-block copies of a grid step (pack the shard into column
+// blocks, unpack the received blocks into the output rows).
+namespace ofx {
+namespace {
+template <typename W, int LPR>
+__global__ void __launch_bounds__(kBlock)
+    copy_blocks_kernel(int64_t count, int64_t ninner, int64_t rows, int64_t words,
+                       const char* __restrict__ src, int64_t so, int64_t si, int64_t sr,
+                       char* __restrict__ dst, int64_t dout, int64_t di, int64_t dr) {
+  constexpr int GPB = kBlock / LPR;
+  const int gl = threadIdx.x % LPR;
+  for (int64_t q = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR; q < count;
+       q += (int64_t)gridDim.x * GPB) {
+    const int64_t r = q % rows, oi = q / rows;
+    const int64_t i = oi % ninner, o = oi / ninner;
+    const W* s = reinterpret_cast<const W*>(src + o * so + i * si + r * sr);
+    W* d = reinterpret_cast<W*>(dst + o * dout + i * di + r * dr);
+    for (int64_t w = gl; w < words; w += LPR) d[w] = s[w];
+  }
+}
+
+template <typename W>
+int launch_blocks(hipStream_t s, int64_t nouter, int64_t ninner, int64_t rows, int64_t row_bytes,
+                  const void* src, int64_t so, int64_t si, int64_t sr, void* dst, int64_t dout,
+                  int64_t di, int64_t dr) {
+  const int64_t words = row_bytes / (int64_t)sizeof(W);
+  const int64_t count = nouter * ninner * rows;
+  int lpr = 1;
+  while (lpr < 64 && lpr < words) lpr *= 2;
+  const int64_t gpb = kBlock / lpr;
+  const unsigned grid = (unsigned)std::min<int64_t>((count + gpb - 1) / gpb, 65536);
+  auto go = [&](auto k) {
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, s, count, ninner, rows, words,
+                       static_cast<const char*>(src), so, si, sr, static_cast<char*>(dst), dout,
+                       di, dr);
+  };
+  switch (lpr) {
+    case 1: go(copy_blocks_kernel<W, 1>); break;
+    case 2: go(copy_blocks_kernel<W, 2>); break;
+    case 4: go(copy_blocks_kernel<W, 4>); break;
+    case 8: go(copy_blocks_kernel<W, 8>); break;
+    case 16: go(copy_blocks_kernel<W, 16>); break;
+    case 32: go(copy_blocks_kernel<W, 32>); break;
+    default: go(copy_blocks_kernel<W, 64>); break;
+  }
+  OFX_HIP_CHECK(hipGetLastError());
+  return OFX_OK;
+}
+}  // namespace
+}  // namespace ofx
+
+extern "C" int ofx_copy_blocks(void* stream, int64_t nouter, int64_t ninner, int64_t rows,
+                               int64_t row_bytes, const void* src, int64_t src_outer,
+                               int64_t src_inner, int64_t src_row, void* dst, int64_t dst_outer,
+                               int64_t dst_inner, int64_t dst_row) {
+  OFX_REQUIRE(nouter >= 0 && ninner >= 0 && rows >= 0 && row_bytes >= 0, OFX_EINVAL,
+              "copy_blocks: negative size");
+  if (nouter == 0 || ninner == 0 || rows == 0 || row_bytes == 0) return OFX_OK;
+  OFX_REQUIRE(src && dst, OFX_EINVAL, "copy_blocks: NULL pointer");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  auto aligned = [&](int64_t a) {
+    return row_bytes % a == 0 && src_outer % a == 0 && src_inner % a == 0 && src_row % a == 0 &&
+           dst_outer % a == 0 && dst_inner % a == 0 && dst_row % a == 0 &&
+           (uintptr_t)src % a == 0 && (uintptr_t)dst % a == 0;
+  };
+  if (aligned(16))
+    return launch_blocks<uint4>(s, nouter, ninner, rows, row_bytes, src, src_outer, src_inner,
+                                src_row, dst, dst_outer, dst_inner, dst_row);
+  if (aligned(4))
+    return launch_blocks<uint32_t>(s, nouter, ninner, rows, row_bytes, src, src_outer, src_inner,
+                                   src_row, dst, dst_outer, dst_inner, dst_row);
+  return launch_blocks<unsigned char>(s, nouter, ninner, rows, row_bytes, src, src_outer,
+                                      src_inner, src_row, dst, dst_outer, dst_inner, dst_row);
+}
+
 // ---- padded-owner column remap (row split) -----------------------------------
 // Column c of B lives in shard owner(c) = BalancedSplitter(k, world) and, in the padded gathered
 // buffer [world * P, n] (P = ceil(k / world)), at row c + max(owner(c) - extra, 0) where

@@ -77,6 +77,7 @@ def _load():
         "ofx_csr_transpose": ([p, i32, i64, i64, i64, p, p, p, p, p, p, sz], i32),
         "ofx_csr_transpose_cpu": ([i32, i64, i64, i64, p, p, p, p, p], i32),
         "ofx_gather_values": ([p, i32, i32, i64, p, p, p], i32),
+        "ofx_copy_blocks": ([p, i64, i64, i64, i64, p, i64, i64, i64, p, i64, i64, i64], i32),
         "ofx_gather_values_host": ([i32, i32, i64, p, p, p], i32),
         "ofx_sddmm_csr_workspace_size": ([i32, i32, i64, i64, i64, ctypes.POINTER(sz)], i32),
         "ofx_sddmm_csr": ([p, i32, i32, i64, i64, i64, i64, p, p, p, i64, p, i64, p, i64, i64, p, sz], i32),

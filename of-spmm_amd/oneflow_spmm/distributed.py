@@ -262,6 +262,25 @@ class GridPlan:
 
     def _pack(self, owner):
         lo, hi = self.k_rng[owner.rank]
+        if self.shard.device.type == "cuda":
+            # two launches: every (sub-block, block) of the shard into send_b, this rank's own
+            # block into its rows of b_cols (ofx_copy_blocks, strides in bytes)
+            e, w, nb, S, C = self.shard.element_size(), self.w, self.ng, self.sub, self.cn
+            k_r, st = self.k_r, current_stream_handle(self.shard)
+            if k_r:
+                sh, sb, bc = self.shard.data_ptr(), self.send_b.data_ptr(), self.b_cols.data_ptr()
+                # blocks some peer needs: all of them with other row groups, else all but c
+                ranges = [(0, C)] if self.rg > 1 else [(0, self.c), (self.c + 1, C)]
+                for b0, b1 in ranges:
+                    if b1 > b0:
+                        check(LIB.ofx_copy_blocks(st, S, b1 - b0, k_r, w * e, sh + b0 * nb * e,
+                                                  w * e, nb * e, self.shard.stride(0) * e,
+                                                  sb + b0 * k_r * w * e, C * k_r * w * e,
+                                                  k_r * w * e, w * e), "copy_blocks")
+                check(LIB.ofx_copy_blocks(st, S, 1, k_r, w * e, sh + self.c * nb * e, w * e, 0,
+                                          self.shard.stride(0) * e, bc + lo * w * e,
+                                          owner.k * w * e, 0, w * e), "copy_blocks")
+            return
         for s in range(self.sub):
             for b in self.packed:
                 _copy_rows(self.send_b[s, b], self.shard[:, self._cols(b, s)])
@@ -277,6 +296,27 @@ class GridPlan:
 
     def _unpack(self, owner, out):
         lo, hi = self.m_rng[owner.rank]
+        if out.device.type == "cuda":
+            # the received (sub-block, block)s into out's columns (at most two launches around
+            # block c), then this rank's own block from c_grp
+            e, w, nb, S, C, m_r = out.element_size(), self.w, self.ng, self.sub, self.cn, self.m_r
+            st = current_stream_handle(out)
+            if m_r:
+                ld = out.stride(0) * e
+                rc_, o_ = self.recv_c.data_ptr(), out.data_ptr()
+                for b0, b1 in ((0, self.c), (self.c + 1, C)):  # the received blocks
+                    if b1 > b0:
+                        check(LIB.ofx_copy_blocks(st, S, b1 - b0, m_r, w * e,
+                                                  rc_ + b0 * m_r * w * e, C * m_r * w * e,
+                                                  m_r * w * e, w * e, o_ + b0 * nb * e, w * e,
+                                                  nb * e, ld), "copy_blocks")
+                m_g = self.ghi - self.glo
+                check(LIB.ofx_copy_blocks(st, S, 1, m_r, w * e,
+                                          self.c_grp.data_ptr() + (lo - self.glo) * w * e,
+                                          m_g * w * e, 0, w * e,
+                                          out.data_ptr() + self.c * nb * e, w * e, 0, ld),
+                      "copy_blocks")
+            return
         for s in range(self.sub):
             for b in range(self.cn):
                 src = (self.c_grp[s, lo - self.glo:hi - self.glo] if b == self.c

@@ -113,12 +113,31 @@ def grid(args):
     recv_c = torch.empty((C * m0, nb), dtype=dt, device=dev)
     out = torch.empty((m0, n), dtype=dt, device=dev)
 
-    def copies():
+    def copies_per_block():  # the CPU-path form: one copy per block each way
         for b in range(C):
             _copy_rows(send_b[b * k0:(b + 1) * k0], shard[:, b * nb:(b + 1) * nb])
         for b in range(C):
             _copy_rows(out[:, b * nb:(b + 1) * nb], recv_c[b * m0:(b + 1) * m0])
+
+    from oneflow_spmm._C import current_stream_handle
+    from oneflow_spmm._lib import LIB, check
+    e = shard.element_size()
+    b_own = torch.empty((k, nb), dtype=dt, device=dev)
+
+    def copies():  # GridPlan's GPU form: ofx_copy_blocks, two launches each way
+        st = current_stream_handle(shard)
+        check(LIB.ofx_copy_blocks(st, 1, C, k0, nb * e, shard.data_ptr(), 0, nb * e, n * e,
+                                  send_b.data_ptr(), 0, k0 * nb * e, nb * e), "copy_blocks")
+        check(LIB.ofx_copy_blocks(st, 1, 1, k0, nb * e, shard.data_ptr(), 0, 0, n * e,
+                                  b_own.data_ptr(), 0, 0, nb * e), "copy_blocks")
+        if C > 1:  # rank 0 sits at column 0: the received blocks are 1..C-1
+            check(LIB.ofx_copy_blocks(st, 1, C - 1, m0, nb * e, recv_c.data_ptr() + m0 * nb * e, 0,
+                                      m0 * nb * e, nb * e, out.data_ptr() + nb * e, 0, nb * e,
+                                      n * e), "copy_blocks")
+        check(LIB.ofx_copy_blocks(st, 1, 1, m0, nb * e, recv_c.data_ptr(), 0, 0, nb * e,
+                                  out.data_ptr(), 0, 0, n * e), "copy_blocks")
     copy_ms = _median_ms(copies, args.reps)
+    copy_ms_per_block = _median_ms(copies_per_block, args.reps)
     res = []
     for g in range(R):
         lo = _C.balanced_range(m, G, g * C)[0]
@@ -131,6 +150,7 @@ def grid(args):
     s_v = torch.empty(0, dtype=dt).element_size()
     print(json.dumps({"config": args.config, "world": G, "grid": f"{R}x{C}", "block_n": nb,
                       "per_row_group": res, "max_spmm_ms": worst, "local_copies_ms": round(copy_ms, 4),
+                      "local_copies_ms_per_block_form": round(copy_ms_per_block, 4),
                       "b_bytes_received_per_rank": (k - k0) * nb * s_v,
                       "c_bytes_received_per_rank": (C - 1) * m0 * nb * s_v,
                       "spmm_phase_gflops_aggregate": round(2.0 * nnz * n / ((worst + copy_ms) * 1e-3) / 1e9, 1)}))

@@ -54,3 +54,32 @@ def test_device_padded_remap_matches_host(device, k, world, idx_dtype):
                                      d.data_ptr(), out.data_ptr()), "remap")
     torch.cuda.synchronize()
     assert torch.equal(out.cpu(), padded_owner_remap(col, k, world))
+
+
+@pytest.mark.parametrize("S,C,rows,w,dtype", [(1, 1, 7, 16, torch.float32), (2, 4, 33, 8, torch.float32),
+                                             (2, 2, 100, 3, torch.float32), (3, 2, 5, 5, torch.bfloat16),
+                                             (1, 8, 1000, 16, torch.float64), (2, 3, 0, 4, torch.float32)])
+def test_copy_blocks_pack_and_unpack(device, S, C, rows, w, dtype):
+    """ofx_copy_blocks as the grid exchange uses it: a shard [rows, S*C*w] packed into
+    [S][C][rows][w] (block b, sub-block s = columns b*S*w + s*w), then unpacked back into a
+    row-major [rows, N] output with a padded leading dimension; 16-B, 4-B and 1-B word paths."""
+    import ctypes
+    from oneflow_spmm._C import current_stream_handle
+    from oneflow_spmm._lib import LIB, check
+    n = S * C * w
+    e = torch.empty(0, dtype=dtype).element_size()
+    shard = torch.randn(rows, n + 3, device=device).to(dtype)[:, :n]  # leading dim n + 3
+    packed = torch.full((S, C, rows, w), 7, dtype=dtype, device=device)
+    st = current_stream_handle(shard)
+    check(LIB.ofx_copy_blocks(st, S, C, rows, w * e, shard.data_ptr(), w * e, S * w * e,
+                              shard.stride(0) * e, packed.data_ptr(), C * rows * w * e,
+                              rows * w * e, w * e), "copy_blocks")
+    ref = torch.stack([torch.stack([shard[:, b * S * w + s * w: b * S * w + (s + 1) * w]
+                                    for b in range(C)]) for s in range(S)])
+    assert torch.equal(packed, ref)
+    out = torch.zeros(rows, n + 5, dtype=dtype, device=device)
+    check(LIB.ofx_copy_blocks(st, S, C, rows, w * e, packed.data_ptr(), C * rows * w * e,
+                              rows * w * e, w * e, out.data_ptr(), w * e, S * w * e,
+                              out.stride(0) * e), "copy_blocks")
+    torch.cuda.synchronize()
+    assert torch.equal(out[:, :n], shard) and (out[:, n:] == 0).all()
