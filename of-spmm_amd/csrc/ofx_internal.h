@@ -18,9 +18,11 @@ void clear_error();
 #define OFX_HIP_CHECK(expr)                                                                 \
   do {                                                                                      \
     hipError_t ofx_e_ = (expr);                                                             \
-    if (ofx_e_ != hipSuccess)                                                               \
+    if (ofx_e_ != hipSuccess) {                                                             \
+      (void)hipGetLastError(); /* reported here: not again at the next launch check */      \
       return ::ofx::fail(OFX_EDEVICE, "%s failed: %s (%s:%d)", #expr,                       \
                          hipGetErrorString(ofx_e_), __FILE__, __LINE__);                    \
+    }                                                                                       \
   } while (0)
 
 #define OFX_REQUIRE(cond, code, ...)              \

@@ -469,8 +469,16 @@ class RowSplitSpmm:
         """Writes this rank's rows of B ([K_r, N]) into its slot of every column block."""
         lo, hi = self.k_range
         r0 = self.rank * self.pad
-        for c in range(self.chunks):
-            self.gathered[c, r0:r0 + (hi - lo)].copy_(b_shard[:, c * self.nc:(c + 1) * self.nc])
+        if b_shard.is_cuda and b_shard.dtype == self.dtype and hi > lo and b_shard.stride(-1) == 1:
+            # every column block's slot in one launch
+            e = b_shard.element_size()
+            check(LIB.ofx_copy_blocks(current_stream_handle(self.gathered), 1, self.chunks, hi - lo,
+                                      self.nc * e, b_shard.data_ptr(), 0, self.nc * e,
+                                      b_shard.stride(0) * e, self.gathered[0, r0].data_ptr(), 0,
+                                      self.k_padded * self.nc * e, self.nc * e), "copy_blocks")
+        else:
+            for c in range(self.chunks):
+                self.gathered[c, r0:r0 + (hi - lo)].copy_(b_shard[:, c * self.nc:(c + 1) * self.nc])
         if self.halo is not None:
             self.compact[: self.halo.k_own].copy_(b_shard)
         for gp in self.grids.values():

@@ -112,3 +112,13 @@ def test_shim_errors(device):
     assert LIB.ofx_malloc(None, 16) != OFX_OK
     assert LIB.ofx_memcpy_async(None, None, None, 16, 99) != OFX_OK
     assert len(LIB.ofx_last_error()) > 0
+    # a reported HIP failure does not resurface at the next launch's error check
+    from oneflow_spmm import _C
+    x = torch.ones(4, 8, device=device)
+    rp = torch.tensor([0, 1, 1, 2, 2], dtype=torch.int32, device=device)
+    ci = torch.tensor([0, 3], dtype=torch.int32, device=device)
+    v = torch.tensor([2.0, 3.0], device=device)
+    assert LIB.ofx_set_device(1 << 20) != OFX_OK
+    out = _C.spmm_csr(rp, ci, v, 4, 4, x)
+    torch.cuda.synchronize()
+    assert out[0].eq(2).all() and out[2].eq(3).all() and out[1].eq(0).all()

@@ -291,6 +291,13 @@ def test_row_split_rccl_single_rank(device):
                 rs(rp.to(device), rs.remap_columns(ci.to(device)), v.to(device), out=out2)
             torch.cuda.synchronize()
             assert_bitwise(out2, oracle_spmm(rp, ci, v, b), f"{kind} pipeline {chunks}")
+            # load_shard into the column-block layout (one copy_blocks launch) from a strided shard
+            b_new = random_dense(k, n + 3, rng)
+            rs.load_shard(b_new.to(device)[:, :n])
+            rs(rp.to(device), rs.remap_columns(ci.to(device)), v.to(device), out=out2)
+            torch.cuda.synchronize()
+            assert_bitwise(out2, oracle_spmm(rp, ci, v, b_new[:, :n].contiguous()), f"{kind} load_shard")
+            rs.load_shard(b.to(device))
         # the setup-time choice runs every candidate step and keeps one; output stays exact
         d = (rp.to(device), ci.to(device), v.to(device))
         rs.bind(*d, halo=True, full_csr=d, grid_subs=(1, 4))
