@@ -134,9 +134,21 @@ def _copy_rows(dst: torch.Tensor, src: torch.Tensor):
                               dst.stride(0) * esz), "copy_rows")
 
 
+def _host_staged(group, *tensors) -> bool:
+    """gloo moves host memory: device buffers on a gloo group go through host copies (the
+    multi-rank GPU tests run several ranks on one GPU, where RCCL refuses the layout)."""
+    return dist.get_backend(group) != "nccl" and any(t.is_cuda for t in tensors)
+
+
 def _torch_exchange(send, send_counts, send_offsets, recv, recv_counts, recv_offsets, group):
     """Grouped point-to-point rows exchange through torch.distributed (the CPU/gloo path of
     ofx_exchange_rows; same counts/offsets convention, rows of the buffers' width)."""
+    if _host_staged(group, send, recv):
+        host = recv.cpu()
+        _torch_exchange(send.cpu(), send_counts, send_offsets, host, recv_counts, recv_offsets,
+                        group)
+        recv.copy_(host)
+        return
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     reqs = []
     for p in range(world):
@@ -533,8 +545,11 @@ class RowSplitSpmm:
         slot = blk[self.rank * self.pad:(self.rank + 1) * self.pad]
         count = self.pad * self.nc
         if self.comm_kind == "torch":
-            parts = list(blk.view(self.world, self.pad, self.nc).unbind(0))
-            dist.all_gather(parts, slot.clone(), group=self.group)  # views: lands in place
+            host = blk.cpu() if _host_staged(self.group, blk) else blk
+            parts = list(host.view(self.world, self.pad, self.nc).unbind(0))
+            dist.all_gather(parts, parts[self.rank].clone(), group=self.group)  # views: in place
+            if host is not blk:
+                blk.copy_(host)
             return
         s = stream if stream is not None else current_stream_handle(blk)
         if self.comm_kind == "rccl":

@@ -18,7 +18,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, m, k, n, local_csr, pipeline, density, q):
+def _worker(rank, world, port, m, k, n, local_csr, pipeline, density, q, device="cpu"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     import sys
@@ -31,6 +31,13 @@ def _worker(rank, world, port, m, k, n, local_csr, pipeline, density, q):
         from oracle import oracle
         from tests.helpers import power_law_degrees, random_csr, random_dense
 
+        dev = torch.device(device)
+        if dev.type == "cuda":  # every rank on the one GPU; gloo moves the bytes (host-staged)
+            torch.cuda.set_device(0)
+            dev = torch.device("cuda", 0)
+        D = lambda t: t.to(dev)  # noqa: E731
+        same = lambda got, want: np.array_equal(got.cpu().numpy().view(np.uint32),  # noqa: E731
+                                                want.view(np.uint32))
         rng = np.random.default_rng(1234)
         rp, ci, v = random_csr(m, k, power_law_degrees(m, min(density * m, m * k // 2), k, rng), rng)
         b = random_dense(k, n, rng)
@@ -41,55 +48,56 @@ def _worker(rank, world, port, m, k, n, local_csr, pipeline, density, q):
             lci, lv = ci[n0:n1], v[n0:n1]
         else:
             lrp, lci, lv = rp, ci, v
-        rs = RowSplitSpmm(m, k, n, lci.numel(), torch.float32, torch.int32, "cpu",
-                          local_csr=local_csr, pipeline=pipeline)
+        rs = RowSplitSpmm(m, k, n, lci.numel(), torch.float32, torch.int32, dev,
+                          comm="torch", local_csr=local_csr, pipeline=pipeline)
         assert rs.row_range == (lo, hi)
         klo, khi = rs.k_range
         assert (klo, khi) == oracle.balanced_range(k, world, rank)
-        rs.load_shard(b[klo:khi])
-        out = rs(lrp, rs.remap_columns(lci), lv)
-        ok = np.array_equal(out.numpy().view(np.uint32), full[lo:hi].view(np.uint32))
+        drp, dci, dv = D(lrp), D(lci), D(lv)
+        rs.load_shard(D(b[klo:khi]))
+        out = rs(drp, rs.remap_columns(dci), dv)
+        ok = same(out, full[lo:hi])
         # the gathered buffer holds every shard at its padded slot, in every column block
         nc = n // pipeline
         for c in range(pipeline):
-            g = rs.block(c).view(world, rs.pad, nc)
+            g = rs.block(c).cpu().view(world, rs.pad, nc)
             for r in range(world):
                 a, e = oracle.balanced_range(k, world, r)
                 ok = ok and torch.equal(g[r, : e - a], b[a:e, c * nc:(c + 1) * nc])
         # a second step with a new dense operand passed as a separate shard tensor
         b2 = random_dense(k, n, np.random.default_rng(99))
-        out2 = rs(lrp, rs.remap_columns(lci), lv, b_shard=b2[klo:khi])
+        out2 = rs(drp, rs.remap_columns(dci), dv, b_shard=D(b2[klo:khi]))
         full2 = oracle.spmm(rp.numpy(), ci.numpy(), v.numpy(), b2.numpy())
-        ok = ok and np.array_equal(out2.numpy().view(np.uint32), full2[lo:hi].view(np.uint32))
+        ok = ok and same(out2, full2[lo:hi])
         # the bound form with the halo-only exchange: same bytes
-        rs.bind(lrp, lci, lv, halo=True)
+        rs.bind(drp, dci, dv, halo=True)
         h = rs.halo
         ok = ok and h.k_compact == (khi - klo) + h.halo_rows and h.halo_rows <= k - (khi - klo)
         rs.exchange = "halo"
         out3 = torch.full_like(out2, float("nan"))
-        rs.step(out3, b_shard=b[klo:khi])
-        ok = ok and np.array_equal(out3.numpy().view(np.uint32), full[lo:hi].view(np.uint32))
+        rs.step(out3, b_shard=D(b[klo:khi]))
+        ok = ok and same(out3, full[lo:hi])
         # every halo row holds the B row it stands for
         uniq = torch.unique((lci if local_csr else lci[int(lrp[lo]):int(lrp[hi])]).long())
-        ok = ok and torch.equal(rs.compact[: h.k_own], b[klo:khi])
+        ok = ok and torch.equal(rs.compact[: h.k_own].cpu(), b[klo:khi])
         remote = uniq[(uniq < klo) | (uniq >= khi)]
-        ok = ok and torch.equal(rs.compact[h.k_own:], b[remote])
+        ok = ok and torch.equal(rs.compact[h.k_own:].cpu(), b[remote])
         # the grids (B to column blocks, SpMM of the row group's rows, C back inside the group;
         # the column split is the 1 x G grid): same bytes
         # (and S = 2 sub-blocks, the pipelined form's layout)
-        rs.bind(lrp, lci, lv, halo=False, full_csr=(rp, ci, v), grid_subs=(1, 2))
+        rs.bind(drp, dci, dv, halo=False, full_csr=(D(rp), D(ci), D(v)), grid_subs=(1, 2))
         want = {("nsplit" if c == world else f"grid{world // c}x{c}") + ("" if s == 1 else f"/s{s}")
                 for c in range(2, world + 1) for s in (1, 2) if world % c == 0 and n % (c * s) == 0}
         ok = ok and set(rs.grids) == want and (rs.ns is not None) == (n % world == 0)
         for name, gp in rs.grids.items():
             rs.exchange = name
             out4 = torch.full_like(out2, float("nan"))
-            rs.step(out4, b_shard=b2[klo:khi])
-            ok = ok and np.array_equal(out4.numpy().view(np.uint32), full2[lo:hi].view(np.uint32))
+            rs.step(out4, b_shard=D(b2[klo:khi]))
+            ok = ok and same(out4, full2[lo:hi])
             nb = n // gp.cn
             for s in range(gp.sub):
                 c0 = gp.c * nb + s * gp.w
-                ok = ok and torch.equal(gp.b_cols[s], b2[:, c0:c0 + gp.w])
+                ok = ok and torch.equal(gp.b_cols[s].cpu(), b2[:, c0:c0 + gp.w])
             ok = ok and (gp.glo, gp.ghi) == (oracle.balanced_range(m, world, gp.g * gp.cn)[0],
                                              oracle.balanced_range(m, world, gp.g * gp.cn + gp.cn - 1)[1])
         q.put((rank, bool(ok)))
@@ -119,11 +127,12 @@ def test_row_split_pipelined_gloo(world, m, k, n, local_csr, pipeline):
     _run(world, m, k, n, local_csr, pipeline, 60)
 
 
-def _run(world, m, k, n, local_csr, pipeline, density):
+def _run(world, m, k, n, local_csr, pipeline, density, device="cpu"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, m, k, n, local_csr, pipeline, density, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, m, k, n, local_csr, pipeline,
+                                               density, q, device)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -185,7 +194,7 @@ def test_halo_exchange_moves_only_the_band_edges(world):
     assert all(ok for _, ok, _ in res), res
 
 
-def _tune_worker(rank, world, port, q):
+def _tune_worker(rank, world, port, q, device="cpu"):
     """tune() over torch.distributed (gloo): every candidate (all-gather x pipeline depth, halo,
     every grid with and without sub-blocks) runs the real step, the max-reduced timings make every
     rank keep the same one, and the kept exchange still gives the oracle's bits."""
@@ -201,6 +210,10 @@ def _tune_worker(rank, world, port, q):
         from oracle import oracle
         from tests.helpers import power_law_degrees, random_csr, random_dense
 
+        dev = torch.device(device)
+        if dev.type == "cuda":
+            torch.cuda.set_device(0)
+            dev = torch.device("cuda", 0)
         rng = np.random.default_rng(55)
         m, k, n = 900, 850, 16
         rp, ci, v = random_csr(m, k, power_law_degrees(m, 20000, k, rng), rng)
@@ -208,29 +221,31 @@ def _tune_worker(rank, world, port, q):
         full = oracle.spmm(rp.numpy(), ci.numpy(), v.numpy(), b.numpy())
         lo, hi = oracle.balanced_range(m, world, rank)
         lrp, n0, n1 = ops.csr_row_slice(rp, lo, hi)
-        rs = RowSplitSpmm(m, k, n, n1 - n0, torch.float32, torch.int32, "cpu")
+        rs = RowSplitSpmm(m, k, n, n1 - n0, torch.float32, torch.int32, dev, comm="torch")
         klo, khi = rs.k_range
-        rs.load_shard(b[klo:khi])
-        rs.bind(lrp, ci[n0:n1], v[n0:n1], halo=True, full_csr=(rp, ci, v), grid_subs=(1, 2))
-        out = torch.empty((hi - lo, n))
+        rs.load_shard(b[klo:khi].to(dev))
+        rs.bind(lrp.to(dev), ci[n0:n1].to(dev), v[n0:n1].to(dev), halo=True,
+                full_csr=(rp.to(dev), ci.to(dev), v.to(dev)), grid_subs=(1, 2))
+        out = torch.empty((hi - lo, n), device=dev)
         times = rs.tune(out, reps=1)
         want = {"torch/p1", "torch/p2", "torch/p4", "halo", "grid2x2", "grid2x2/s2", "nsplit",
                 "nsplit/s2"}
         ok = set(times) == want and all(np.isfinite(t) for t in times.values())
         out.fill_(float("nan"))
         rs.step(out)
-        ok = ok and np.array_equal(out.numpy().view(np.uint32), full[lo:hi].view(np.uint32))
+        ok = ok and np.array_equal(out.cpu().numpy().view(np.uint32), full[lo:hi].view(np.uint32))
         q.put((rank, (bool(ok), rs.exchange, rs.comm_kind, rs.chunks, sorted(times))))
     finally:
         dist.destroy_process_group()
 
 
-def test_tune_over_gloo_keeps_one_choice_everywhere():
+def _tune_run(device):
     world = 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_tune_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_tune_worker, args=(r, world, port, q, device))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -239,3 +254,38 @@ def test_tune_over_gloo_keeps_one_choice_everywhere():
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert all(r[0] for r in res.values()), res
     assert len({r[1:4] for r in res.values()}) == 1, res  # the same exchange on every rank
+
+
+def test_tune_over_gloo_keeps_one_choice_everywhere():
+    _tune_run("cpu")
+
+
+# ---- the same ranks on the GPU --------------------------------------------------------------
+# RCCL refuses two ranks on one GPU, so on a one-GPU box these tests put every rank on cuda:0 and
+# let gloo carry the exchanged bytes (host-staged).  Everything else is the device path the
+# RCCL runs take: the remap kernel, the halo row gather, the grid pack/unpack block copies
+# (ofx_copy_blocks) with this rank's offsets, the planned row-range SpMM launches of every row
+# group and column block — checked bit-exactly against the oracle at world sizes > 1.
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,m,k,n,local_csr,pipeline,density", [
+    (2, 301, 257, 16, True, 1, 30),     # K % G != 0 -> padded shards + remap on the device
+    (3, 500, 400, 8, False, 1, 30),     # full CSR, the kernel computes the row range
+    (4, 400, 3001, 128, True, 4, 60),   # hub rows that split, four column blocks
+    (8, 1201, 1205, 32, True, 2, 30),   # the 8-GPU node's grids 4x2, 2x4, 1x8 (and /s2 each)
+    (8, 5, 6, 8, False, 1, 30),         # fewer rows and B rows than ranks
+])
+def test_row_split_device_path_multirank(world, m, k, n, local_csr, pipeline, density):
+    _need_gpu()
+    _run(world, m, k, n, local_csr, pipeline, density, device="cuda")
+
+
+@pytest.mark.gpu
+def test_tune_device_path_multirank():
+    _need_gpu()
+    _tune_run("cuda")
