@@ -168,11 +168,15 @@ def main():
                 raise SystemExit(f"--exchange {rs.exchange}: not available (grids: {list(rs.grids)})")
             rs.comm_kind = args.comm or rs.comm_kind
             rs.set_pipeline(args.pipeline or 1)
+            if rs.exchange == "halo":  # column blocks of the halo exchange
+                rs.set_pipeline(1)
+                rs.set_halo_pipeline(args.pipeline or 1)
         else:
             comm_times = rs.tune(out, force=args.force_rowsplit)
             log("[bench] exchange candidates (ms, max over ranks): " +
                 ", ".join(f"{kk} {vv:.3f}" for kk, vv in sorted(comm_times.items(), key=lambda x: x[1])))
-        log(f"[bench] exchange kept: {rs.exchange} / {rs.comm_kind} / pipeline {rs.chunks}")
+        log(f"[bench] exchange kept: {rs.exchange} / {rs.comm_kind} / pipeline "
+            f"{rs.halo_chunks if rs.exchange == 'halo' else rs.chunks}")
 
         def step():
             rs.step(out)
@@ -314,7 +318,7 @@ def main():
             if phase["gather_ms_max"] > 0 else None,
             "rows_rank0": rows, "nnz_rank0": nnz_local,
             "exchange": rs.exchange, "allgather_schedule": rs.comm_kind,
-            "pipeline_blocks": rs.chunks,
+            "pipeline_blocks": rs.halo_chunks if rs.exchange == "halo" else rs.chunks,
             "halo_rows_received": rs.halo.halo_rows if rs.halo is not None else None,
             "remote_rows_total": (rs.k - (khi - klo)),
             "allgather_tune_ms": {kk: (round(vv, 4) if np.isfinite(vv) else None)

@@ -492,7 +492,7 @@ class RowSplitSpmm:
             for c in range(self.chunks):
                 self.gathered[c, r0:r0 + (hi - lo)].copy_(b_shard[:, c * self.nc:(c + 1) * self.nc])
         if self.halo is not None:
-            self.compact[: self.halo.k_own].copy_(b_shard)
+            self._load_halo_shard(b_shard)
         for gp in self.grids.values():
             gp.shard.copy_(b_shard)
 
@@ -670,57 +670,124 @@ class RowSplitSpmm:
                 full[j0:j1] = hc
                 hc = full
             cols["halo"] = hc
-            self.compact = torch.zeros((self.halo.k_compact, self.n), dtype=self.dtype,
-                                       device=self.device)
-            self.send_buf = torch.empty((self.halo.send_rows, self.n), dtype=self.dtype,
-                                        device=self.device)
-            rows_local = self.row_range[1] - self.row_range[0]
-            self.halo_kernel = None
-            if self.device.type == "cuda":
-                self.halo_kernel = ops.SpmmCsrKernel(rows_local if self.local_csr else self.m,
-                                                     self.halo.k_compact, self.n, col_idx.numel(),
-                                                     self.idx_dtype, self.dtype, self.device,
-                                                     self.options).plan(row_ptr, *self._rows())
-            self.compact[: self.halo.k_own].copy_(self.shard())
+            self.compact = None
+            self.set_halo_pipeline(1, row_ptr=row_ptr, nnz=col_idx.numel())
         self._bound = (row_ptr, cols, values)
         if self.kernel is not None:
             self.kernel.plan(row_ptr, *self._rows())
 
-    def halo_exchange(self, b_shard=None):
-        """Pack the rows each peer asked for, then grouped send/recv into the compact buffer."""
+    def set_halo_pipeline(self, chunks: int, row_ptr=None, nnz=None):
+        """(Re)lays out the halo buffers for `chunks` column blocks of N/C, block-major like the
+        all-gather's: compact B [C, K_own + halo rows, N/C] and the rows peers asked for
+        [C, send rows, N/C], so every block's exchange is one contiguous run per peer.  Block c+1
+        is packed and exchanged on the side stream while the SpMM of block c runs; every block
+        keeps the full-width hub schedule, so the bits are those of chunks = 1.  Keeps the shard."""
         h = self.halo
-        if b_shard is not None:
-            self.compact[: h.k_own].copy_(b_shard)
+        if h is None:
+            raise RuntimeError("set_halo_pipeline: bind(halo=True) first")
+        if chunks < 1 or self.n % chunks:
+            raise ValueError(f"RowSplitSpmm: halo pipeline {chunks} must divide n={self.n}")
+        row_ptr = row_ptr if row_ptr is not None else self._bound[0]
+        nnz = nnz if nnz is not None else self._bound[1]["halo"].numel()
+        shard = self._halo_shard() if self.compact is not None else self.shard()
+        nc = self.n // chunks
+        self.halo_chunks, self.halo_nc = chunks, nc
+        self.compact = torch.zeros((chunks, h.k_compact, nc), dtype=self.dtype, device=self.device)
+        self.send_buf = torch.empty((chunks, h.send_rows, nc), dtype=self.dtype, device=self.device)
+        self.halo_events = None
+        self.halo_kernel = None
+        if self.device.type == "cuda":
+            self.halo_events = [torch.cuda.Event() for _ in range(chunks)]
+            rows_local = self.row_range[1] - self.row_range[0]
+            self.halo_kernel = ops.SpmmCsrKernel(rows_local if self.local_csr else self.m,
+                                                 h.k_compact, nc, nnz, self.idx_dtype, self.dtype,
+                                                 self.device, self.options).plan(row_ptr, *self._rows())
+        self._load_halo_shard(shard)
+
+    def _load_halo_shard(self, b_shard: torch.Tensor):
+        k_own, nc = self.halo.k_own, self.halo_nc
+        for c in range(self.halo_chunks):
+            self.compact[c, :k_own].copy_(b_shard[:, c * nc:(c + 1) * nc])
+
+    def _halo_shard(self) -> torch.Tensor:
+        return torch.cat(list(self.compact[:, : self.halo.k_own].unbind(0)), dim=1)
+
+    def _halo_block(self, c: int, stream=None):
+        """Block c: pack the rows each peer asked for, then grouped send/recv into compact[c]."""
+        h = self.halo
+        comp, send = self.compact[c], self.send_buf[c]
         if self.comm_kind == "torch":
             if h.send_rows:
-                torch.index_select(self.compact, 0, h.send_idx, out=self.send_buf)
-            _torch_exchange(self.send_buf, h.send_counts, h.send_offsets, self.compact,
+                torch.index_select(comp, 0, h.send_idx, out=send)
+            _torch_exchange(send, h.send_counts, h.send_offsets, comp,
                             h.recv_counts, [h.k_own + o for o in h.recv_offsets], self.group)
             return
-        s = current_stream_handle(self.compact)
-        esz = self.compact.element_size()
+        s = stream if stream is not None else current_stream_handle(comp)
+        esz, nc = comp.element_size(), self.halo_nc
         if h.send_rows:
-            check(LIB.ofx_gather_rows(s, dtype_code(torch.int64), h.send_rows, self.n * esz,
-                                      h.send_idx.data_ptr(), self.compact.data_ptr(),
-                                      self.compact.stride(0) * esz, self.send_buf.data_ptr(),
-                                      self.send_buf.stride(0) * esz), "gather_rows")
+            check(LIB.ofx_gather_rows(s, dtype_code(torch.int64), h.send_rows, nc * esz,
+                                      h.send_idx.data_ptr(), comp.data_ptr(), nc * esz,
+                                      send.data_ptr(), nc * esz), "gather_rows")
         sc, so, rc, ro = h._c
-        check(LIB.ofx_exchange_rows(s, self._comm, dtype_code(self.dtype), self.n,
-                                    self.send_buf.data_ptr() if h.send_rows else None, sc, so,
-                                    self.compact.data_ptr() + h.k_own * self.n * esz, rc, ro),
+        check(LIB.ofx_exchange_rows(s, self._comm, dtype_code(self.dtype), nc,
+                                    send.data_ptr() if h.send_rows else None, sc, so,
+                                    comp.data_ptr() + h.k_own * nc * esz, rc, ro),
               "exchange_rows")
 
-    def halo_compute(self, out):
+    def halo_exchange(self, b_shard=None):
+        """Every block's pack + exchange on the current stream."""
+        if b_shard is not None:
+            self._load_halo_shard(b_shard)
+        for c in range(self.halo_chunks):
+            self._halo_block(c)
+
+    def _halo_compute_block(self, c: int, out):
         row_ptr, cols, values = self._bound
         lo, hi = self.row_range
         rb, re = (0, hi - lo) if self.local_csr else (lo, hi)
+        nc = self.halo_nc
+        o = out[:, c * nc:(c + 1) * nc]
         if self.halo_kernel is not None:
-            self.halo_kernel(row_ptr, cols["halo"], values, self.compact, out, rb, re, planned=True)
+            self.halo_kernel(row_ptr, cols["halo"], values, self.compact[c], o, rb, re, planned=True)
         else:
             m_kernel = hi - lo if self.local_csr else self.m
-            ops.spmm_csr_cpu(row_ptr, cols["halo"], values, self.compact, m_kernel,
-                             self.halo.k_compact, out=out, row_begin=rb, row_end=re,
+            ops.spmm_csr_cpu(row_ptr, cols["halo"], values, self.compact[c], m_kernel,
+                             self.halo.k_compact, out=o, row_begin=rb, row_end=re,
                              options=self.options)
+
+    def halo_compute(self, out):
+        for c in range(self.halo_chunks):
+            self._halo_compute_block(c, out)
+        return out
+
+    def _halo_step(self, out, b_shard=None, events=None):
+        pipelined = (self.halo_chunks > 1 and self.comm_stream is not None
+                     and self.comm_kind != "torch" and not events)
+        if not pipelined:
+            if events:
+                events[0].record()
+            self.halo_exchange(b_shard)
+            if events:
+                events[1].record()
+            self.halo_compute(out)
+            if events:
+                events[2].record()
+            return out
+        if b_shard is not None:
+            self._load_halo_shard(b_shard)
+        cur = torch.cuda.current_stream(self.device)
+        cs = self.comm_stream
+        cs.wait_stream(cur)  # shard written; the previous step's reads of the blocks are done
+        side = ctypes.c_void_p(cs.cuda_stream)
+        for c in range(self.halo_chunks):
+            self._halo_block(c, stream=side)
+            self.halo_events[c].record(cs)
+        for c in range(self.halo_chunks):
+            cur.wait_event(self.halo_events[c])
+            self._halo_compute_block(c, out)
+        cur.wait_stream(cs)
+        for t in (self.compact, self.send_buf):
+            t.record_stream(cs)
         return out
 
     def step(self, out, b_shard=None, events=None):
@@ -739,15 +806,7 @@ class RowSplitSpmm:
             events[2].record()
             return out
         if self.exchange == "halo":
-            if events:
-                events[0].record()
-            self.halo_exchange(b_shard)
-            if events:
-                events[1].record()
-            self.halo_compute(out)
-            if events:
-                events[2].record()
-            return out
+            return self._halo_step(out, b_shard, events)
         if b_shard is not None:
             self.load_shard(b_shard)
         return self(row_ptr, cols["allgather"], values, out=out, events=events)
@@ -827,15 +886,24 @@ class RowSplitSpmm:
                 self.comm_kind = kind
                 times[f"{kind}/p{chunks}"] = measure()
         if self.halo is not None:
-            self.exchange, self.comm_kind = "halo", base
-            times["halo"] = measure()
+            for chunks in pipelines:
+                if self.n % chunks:
+                    continue
+                self.set_halo_pipeline(chunks)
+                self.exchange, self.comm_kind = "halo", base
+                times["halo" if chunks == 1 else f"halo/p{chunks}"] = measure()
         for name in self.grids:
             self.exchange, self.comm_kind = name, base
             times[name] = measure()
         best = min(times, key=times.get)
         if not math.isfinite(times[best]):
             raise RuntimeError(f"RowSplitSpmm.tune: every exchange failed: {self.tune_errors}")
-        if best == "halo" or best in self.grids:
+        if self.halo is not None:
+            self.set_halo_pipeline(int(best.split("/p")[1]) if best.startswith("halo/p") else 1)
+        if best.startswith("halo"):
+            self.exchange, self.comm_kind = "halo", base
+            self.set_pipeline(1)
+        elif best in self.grids:
             self.exchange, self.comm_kind = best, base
             self.set_pipeline(1)
         else:

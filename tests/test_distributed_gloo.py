@@ -79,9 +79,20 @@ def _worker(rank, world, port, m, k, n, local_csr, pipeline, density, q, device=
         ok = ok and same(out3, full[lo:hi])
         # every halo row holds the B row it stands for
         uniq = torch.unique((lci if local_csr else lci[int(lrp[lo]):int(lrp[hi])]).long())
-        ok = ok and torch.equal(rs.compact[: h.k_own].cpu(), b[klo:khi])
+        ok = ok and torch.equal(rs.compact[0, : h.k_own].cpu(), b[klo:khi])
         remote = uniq[(uniq < klo) | (uniq >= khi)]
-        ok = ok and torch.equal(rs.compact[h.k_own:].cpu(), b[remote])
+        ok = ok and torch.equal(rs.compact[0, h.k_own:].cpu(), b[remote])
+        # the halo exchange in column blocks (block-major compact B): same bytes
+        for hp in (2, 4):
+            if n % hp == 0:
+                rs.set_halo_pipeline(hp)
+                out3.fill_(float("nan"))
+                rs.step(out3, b_shard=D(b2[klo:khi]))
+                ok = ok and same(out3, full2[lo:hi])
+                nc = n // hp
+                for c in range(hp):
+                    ok = ok and torch.equal(rs.compact[c, h.k_own:].cpu(), b2[remote, c * nc:(c + 1) * nc])
+        rs.set_halo_pipeline(1)
         # the grids (B to column blocks, SpMM of the row group's rows, C back inside the group;
         # the column split is the 1 x G grid): same bytes
         # (and S = 2 sub-blocks, the pipelined form's layout)
@@ -228,8 +239,8 @@ def _tune_worker(rank, world, port, q, device="cpu"):
                 full_csr=(rp.to(dev), ci.to(dev), v.to(dev)), grid_subs=(1, 2))
         out = torch.empty((hi - lo, n), device=dev)
         times = rs.tune(out, reps=1)
-        want = {"torch/p1", "torch/p2", "torch/p4", "halo", "grid2x2", "grid2x2/s2", "nsplit",
-                "nsplit/s2"}
+        want = {"torch/p1", "torch/p2", "torch/p4", "halo", "halo/p2", "halo/p4", "grid2x2",
+                "grid2x2/s2", "nsplit", "nsplit/s2"}
         ok = set(times) == want and all(np.isfinite(t) for t in times.values())
         out.fill_(float("nan"))
         rs.step(out)

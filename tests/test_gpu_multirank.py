@@ -37,7 +37,7 @@ def _worker(rank, world, port, kind, rp, ci, v, b, q):
         m, k, n = rp.numel() - 1, b.shape[0], b.shape[1]
         try:
             rs = RowSplitSpmm(m, k, n, ci.numel(), torch.float32, torch.int32, device,
-                              comm="rccl" if kind in ("tune", "halo", "nsplit", "nsplit/s2") else kind,
+                              comm="rccl" if kind in ("tune", "halo", "halo/p2", "nsplit", "nsplit/s2") else kind,
                               local_csr=False)
         except Exception as e:  # OfxError(OFX_ECOMM) when RCCL rejects the layout
             q.put((rank, "skip", str(e)))
@@ -47,9 +47,12 @@ def _worker(rank, world, port, kind, rp, ci, v, b, q):
         rs.load_shard(b[lo:hi].to(device))
         out = torch.empty((rs.row_range[1] - rs.row_range[0], n), device=device)
         d = (rp.to(device), ci.to(device), v.to(device))
-        rs.bind(*d, halo=kind in ("tune", "halo"),
+        rs.bind(*d, halo=kind in ("tune", "halo", "halo/p2"),
                 full_csr=d if kind in ("tune", "nsplit", "nsplit/s2") else None, grid_subs=(1, 2))
-        if kind in ("halo", "nsplit", "nsplit/s2"):
+        if kind == "halo/p2":
+            rs.exchange = "halo"
+            rs.set_halo_pipeline(2)
+        elif kind in ("halo", "nsplit", "nsplit/s2"):
             rs.exchange = kind
         times = rs.tune(out, reps=2) if kind == "tune" else {}
         # clear everything received, so the checked step must exchange it again
@@ -70,7 +73,8 @@ def _worker(rank, world, port, kind, rp, ci, v, b, q):
         q.put((rank, "err", traceback.format_exc()))
 
 
-@pytest.mark.parametrize("kind", ["rccl", "rccl-p2p", "halo", "nsplit", "nsplit/s2", "tune"])
+@pytest.mark.parametrize("kind", ["rccl", "rccl-p2p", "halo", "halo/p2", "nsplit", "nsplit/s2",
+                                  "tune"])
 def test_row_split_two_ranks(kind):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")

@@ -303,11 +303,15 @@ def test_row_split_rccl_single_rank(device):
         rs.bind(*d, halo=True, full_csr=d, grid_subs=(1, 4))
         assert rs.halo.halo_rows == 0 and rs.halo.k_compact == k  # one rank owns every row
         times = rs.tune(out2, reps=1, force=True)
-        assert len(times) == 9 and "halo" in times and "nsplit" in times and "nsplit/s4" in times
-        for exchange in ("allgather", "halo", "nsplit", "nsplit/s4"):
-            rs.exchange = exchange
+        assert len(times) == 11 and "halo" in times and "nsplit" in times and "nsplit/s4" in times
+        assert "halo/p2" in times and "halo/p4" in times
+        for exchange in ("allgather", "halo", "halo/p4", "nsplit", "nsplit/s4"):
+            rs.exchange = exchange.split("/p")[0]
+            if rs.exchange == "halo":  # column blocks of the halo exchange on the side stream
+                rs.set_halo_pipeline(int(exchange.split("/p")[1]) if "/p" in exchange else 1)
             out2.fill_(float("nan"))
-            rs.step(out2)
+            for _ in range(2):
+                rs.step(out2)
             torch.cuda.synchronize()
             assert_bitwise(out2, oracle_spmm(rp, ci, v, b), f"after tune, {exchange}")
         rs.close()
