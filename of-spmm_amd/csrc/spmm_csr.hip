@@ -601,6 +601,10 @@ int launch_tuned(const Launch& L, int id) {
       case 12: return launch_cfg<T, I, Cfg<4, 32, 16, 4, true, true>>(L);
       case 13: return launch_cfg<T, I, Cfg<4, 32, 32, 4, true, true>>(L);
       case 14: return launch_cfg<T, I, Cfg<4, 32, 8, 4, false, true>>(L);
+      // small launches at N = 16 (VEC 1, 16 lanes per row): loads in flight per lane
+      case 15: return launch_cfg<T, I, Cfg<1, 16, 32, 4, false, true>>(L);
+      case 16: return launch_cfg<T, I, Cfg<1, 16, 64, 4, false, true>>(L);
+      case 17: return launch_cfg<T, I, Cfg<1, 16, 128, 4, false, true>>(L);
       default: break;
     }
   }
