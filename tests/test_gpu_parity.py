@@ -52,6 +52,21 @@ def test_forced_variants_bitexact(device, variant):
     assert_bitwise(out, oracle_spmm(rp, ci, v, b), f"variant {variant}")
 
 
+@pytest.mark.parametrize("n", [16, 128])
+@pytest.mark.parametrize("tuned", list(range(1, 18)))
+def test_tuning_table_bitexact(device, tuned, n):
+    """Every entry of the tuning table (variant 10000 + id, spmm_csr.hip launch_tuned) computes
+    the contract's bits: only the launch shape and loads in flight differ."""
+    rng = np.random.default_rng(1000 + tuned)
+    m, k = 700, 600
+    rp, ci, v = random_csr(m, k, power_law_degrees(m, 20000, k, rng), rng)
+    b = random_dense(k, n, rng)
+    out = ops.spmm_csr_device(rp.to(device), ci.to(device), v.to(device), b.to(device), m, k,
+                              options=ops.make_options(variant=10000 + tuned))
+    torch.cuda.synchronize()
+    assert_bitwise(out, oracle_spmm(rp, ci, v, b), f"tuning variant {tuned} n={n}")
+
+
 @pytest.mark.parametrize("n", [16, 64, 128, 256])
 def test_hub_rows_split_bitexact_and_tolerance(device, n):
     rng = np.random.default_rng(7 + n)
