@@ -368,9 +368,26 @@ int ofx_functional_spmm_csr(void* stream, const ofx_tensor_desc* row_ptr,
                             const ofx_tensor_desc* col_idx, const ofx_tensor_desc* values,
                             int64_t a_num_rows, int64_t a_num_cols, const ofx_tensor_desc* b,
                             ofx_tensor_desc* out, void* tmp, size_t tmp_bytes);
-/* Global (multi-rank) form: the kernel's OpKernelCache derives this rank's row range from
- * (parallel_id, parallel_num) when out is split on axis 0 (out_split_axis 0; -1 = broadcast,
- * 1 = column split); `out` is then the physical (local) slice.  num_threads: CPU kernel only. */
+/* Global form on one rank of a placement: the op's physical inference gives this rank's out
+ * shape and the kernel's OpKernelCache its row range, both from the hierarchy and out's NdSbp
+ * (GetPhysicalShape, oneflow/core/operator/operator.cpp:1551-1626; GetTensorSliceView4ParallelId,
+ * oneflow/core/job/nd_sbp_util.cpp:58-104, as oneflow/user/kernels/unsorted_segment_sum_kernel.cpp:
+ * 59-78 uses it).  hierarchy: hierarchy_ndim dims (e.g. {8} or {2, 4}); out_split_axes: per
+ * hierarchy axis, out's split axis (0 = rows, 1 = columns, -1 = broadcast); b's NdSbp follows (B
+ * for a row split, S(1) for a column split).  `b` and `out` are this rank's physical tensors;
+ * b_logical_cols is the logical N (-1: b's own width).  The hub-row schedule is that of the
+ * logical N, so every rank's bits equal the matching slice of the single-device result.
+ * tmp_size_out != NULL: only the tmp size is computed.  num_threads: CPU kernel only.       */
+int ofx_functional_spmm_csr_global(void* stream, const ofx_tensor_desc* row_ptr,
+                                   const ofx_tensor_desc* col_idx, const ofx_tensor_desc* values,
+                                   int64_t a_num_rows, int64_t a_num_cols, const ofx_tensor_desc* b,
+                                   int64_t b_logical_cols, ofx_tensor_desc* out, void* tmp,
+                                   size_t tmp_bytes, int hierarchy_ndim, const int64_t* hierarchy,
+                                   const int32_t* out_split_axes, int64_t parallel_id,
+                                   int num_threads, size_t* tmp_size_out);
+/* 1-D shorthand of ofx_functional_spmm_csr_global: hierarchy {parallel_num}, out split on
+ * out_split_axis (0 or -1; a column split needs the logical width, so it takes the _global form).
+ * 2-D tensors must have unit column stride (refused with OFX_EINVAL otherwise).            */
 int ofx_functional_spmm_csr_ex(void* stream, const ofx_tensor_desc* row_ptr,
                                const ofx_tensor_desc* col_idx, const ofx_tensor_desc* values,
                                int64_t a_num_rows, int64_t a_num_cols, const ofx_tensor_desc* b,

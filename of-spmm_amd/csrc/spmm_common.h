@@ -45,7 +45,24 @@ OFX_HD uint16_t f32_to_bf16(float f) {
 OFX_HD float f16_to_f32(uint16_t h) { return float(__builtin_bit_cast(_Float16, h)); }
 OFX_HD uint16_t f32_to_f16(float f) { return __builtin_bit_cast(uint16_t, _Float16(f)); }
 
-// Accumulator type and load/store conversions per storage type.
+// bf16 rounding of an fp32 value, returned as fp32 (round-to-nearest-even, NaN quieted): the
+// same bits as bf16_to_f32(f32_to_bf16(f)) without the 16-bit round trip.
+OFX_HD float round_bf16(float f) {
+  const uint32_t u = f32_to_bits(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return bits_to_f32((u & 0xffff0000u) | 0x400000u);
+  return bits_to_f32((u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u);
+}
+
+// Accumulator type, load/store conversions and the multiply per storage type.
+//
+// mul(v, b) is the elementwise multiply of the reference composition, whose output tensor has
+// the storage type T: BinaryFunctor<kMul> is `static_cast<Dst>(src0 * src1)`
+// (oneflow/core/ep/common/primitive/binary_functor.h:46-51), i.e. the product is rounded to T
+// before unsorted_segment_sum adds it.  For bf16/f16 the fp32 product of two 16-bit values is
+// exact (8+8 / 11+11 significand bits), so rounding it once to T is the correctly rounded 16-bit
+// product (for bf16, except where the product falls below fp32's normal range, ~1e-38, where
+// the fp32 step can round first).  The fp32 sum of the rounded products is then
+// rounded once at the end (unsorted_segment_sum_kernel.cpp:146-205).
 template <typename T>
 struct Num;
 template <>
@@ -53,24 +70,28 @@ struct Num<float> {
   using acc = float;
   OFX_HD static float load(float v) { return v; }
   OFX_HD static float store(float a) { return a; }
+  OFX_HD static float mul(float v, float b) { return v * b; }
 };
 template <>
 struct Num<double> {
   using acc = double;
   OFX_HD static double load(double v) { return v; }
   OFX_HD static double store(double a) { return a; }
+  OFX_HD static double mul(double v, double b) { return v * b; }
 };
 template <>
 struct Num<bf16> {
   using acc = float;
   OFX_HD static float load(bf16 v) { return bf16_to_f32(v.x); }
   OFX_HD static bf16 store(float a) { return bf16{f32_to_bf16(a)}; }
+  OFX_HD static float mul(float v, float b) { return round_bf16(v * b); }
 };
 template <>
 struct Num<f16> {
   using acc = float;
   OFX_HD static float load(f16 v) { return f16_to_f32(v.x); }
   OFX_HD static f16 store(float a) { return f16{f32_to_f16(a)}; }
+  OFX_HD static float mul(float v, float b) { return float(_Float16(v * b)); }
 };
 
 // Epilogue of the fused op (include/ofx_spmm.h ofx_spmm_csr_fused): the composition

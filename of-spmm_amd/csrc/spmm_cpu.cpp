@@ -28,7 +28,7 @@ void row_sum(const I* col, const T* val, const T* B, int64_t ldb, int64_t n, int
   for (int64_t j = j0; j < j1; ++j) {
     const A v = Num<T>::load(val[j]);
     const T* brow = B + (int64_t)col[j] * ldb;
-    for (int64_t c = 0; c < n; ++c) acc[c] = acc[c] + v * Num<T>::load(brow[c]);
+    for (int64_t c = 0; c < n; ++c) acc[c] = acc[c] + Num<T>::mul(v, Num<T>::load(brow[c]));
   }
 }
 

@@ -151,7 +151,7 @@ __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* _
       for (int u = 0; u < kUnroll; ++u) {
         if (u < cnt && active) {
 #pragma unroll
-          for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + vv[u] * Num<T>::load(bv[u].v[e]);
+          for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + Num<T>::mul(vv[u], Num<T>::load(bv[u].v[e]));
         }
       }
     }
@@ -229,7 +229,7 @@ __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* _
         for (int u = 0; u < kUnroll; ++u) {
           if (k + u < cnt && active) {
 #pragma unroll
-            for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + vv[u] * Num<T>::load(bv[u].v[e]);
+            for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + Num<T>::mul(vv[u], Num<T>::load(bv[u].v[e]));
           }
         }
       }

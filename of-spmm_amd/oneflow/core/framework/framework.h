@@ -63,6 +63,7 @@ class Shape {
   explicit Shape(std::vector<int64_t> d) : dims_(std::move(d)) {}
   int64_t NumAxes() const { return (int64_t)dims_.size(); }
   int64_t At(int64_t i) const { return dims_.at(i); }
+  void Set(int64_t i, int64_t v) { dims_.at(i) = v; }
   int64_t elem_cnt() const {
     int64_t c = 1;
     for (int64_t d : dims_) c *= d;
@@ -206,6 +207,58 @@ class ParallelContext {
   int64_t id_, num_;
 };
 
+// Placement hierarchy (oneflow/core/job/parallel_desc.h: ParallelDesc::hierarchy()).  A 1-D
+// placement of G devices is {G}; a 2-D one (e.g. nodes x devices) is {R, C}.
+class ParallelDesc {
+ public:
+  explicit ParallelDesc(Shape hierarchy = Shape({1}))
+      : hierarchy_(std::make_shared<const Shape>(std::move(hierarchy))) {}
+  std::shared_ptr<const Shape> hierarchy() const { return hierarchy_; }
+  int64_t parallel_num() const { return hierarchy_->elem_cnt(); }
+
+ private:
+  std::shared_ptr<const Shape> hierarchy_;
+};
+
+// NdSbp: one SbpParallel per hierarchy axis ("S(axis)", "B" or "P"; sbp_parallel.proto).
+using NdSbp = std::vector<std::string>;
+// Split axis of one SbpParallel, -1 when it is B or P.
+int64_t SplitAxisOf(const std::string& sbp);
+
+// [begin, end) of one axis of a tensor slice (oneflow/core/common/range.h).
+class Range {
+ public:
+  Range(int64_t b = 0, int64_t e = 0) : b_(b), e_(e) {}
+  int64_t begin() const { return b_; }
+  int64_t end() const { return e_; }
+  int64_t size() const { return e_ - b_; }
+  int64_t& mut_begin() { return b_; }
+  int64_t& mut_end() { return e_; }
+
+ private:
+  int64_t b_, e_;
+};
+class TensorSliceView {
+ public:
+  explicit TensorSliceView(std::vector<Range> r) : r_(std::move(r)) {}
+  const Range& At(int64_t i) const { return r_.at(i); }
+  int64_t NumAxes() const { return (int64_t)r_.size(); }
+
+ private:
+  std::vector<Range> r_;
+};
+
+// The slice of a logical tensor that parallel_id holds (oneflow/core/job/nd_sbp_util.cpp:58-104):
+// 1-D hierarchy: BalancedSplitter over the split axis; N-D: each split hierarchy axis divides
+// the current range evenly (CHECK: divisible).  Failed CHECKs throw KernelCheckError.
+TensorSliceView GetTensorSliceView4ParallelId(const Shape& parallel_hierarchy, const NdSbp& nd_sbp,
+                                              const Shape& logical_shape, int64_t parallel_id);
+// Physical (per-rank) shape of a logical shape under nd_sbp (oneflow/core/operator/
+// operator.cpp:1551-1626, eager flavour: nested BalancedSplitter per split hierarchy axis).
+Maybe<void> GetPhysicalShape(const Shape& logical_shape, const NdSbp& nd_sbp,
+                             const ParallelDesc& parallel_desc, const ParallelContext& parallel_ctx,
+                             Shape* physical);
+
 // ---- device layer (ep) ------------------------------------------------------------------------
 namespace ep {
 class Stream {
@@ -309,9 +362,34 @@ class InferContext {
   }
   const TensorDesc& OutputTensorDesc(const std::string& n, int32_t i) const { return out_.at({n, i}); }
 
+  // Placement of a global op (physical inference; oneflow/core/framework/infer_util.h:50,84-93).
+  // Without SetParallel the op is local: one device, every argument B.
+  void SetParallel(ParallelContext pc, ParallelDesc pd, std::map<std::string, NdSbp> nd_sbp,
+                   std::map<std::string, TensorDesc> logical) {
+    pc_ = pc;
+    pd_ = std::move(pd);
+    nd_sbp_ = std::move(nd_sbp);
+    logical_ = std::move(logical);
+  }
+  const ParallelContext& parallel_ctx() const { return pc_; }
+  const ParallelDesc& parallel_desc() const { return pd_; }
+  const NdSbp& NdSbp4ArgNameAndIndex(const std::string& n, int32_t) const {
+    auto it = nd_sbp_.find(n);
+    return it == nd_sbp_.end() ? broadcast_ : it->second;
+  }
+  const TensorDesc* LogicalTensorDesc4ArgNameAndIndex(const std::string& n, int32_t) const {
+    auto it = logical_.find(n);
+    return it == logical_.end() ? nullptr : &it->second;
+  }
+
  private:
   std::map<std::pair<std::string, int32_t>, TensorDesc> in_, out_;
   AttrMap attrs_;
+  ParallelContext pc_;
+  ParallelDesc pd_;
+  std::map<std::string, NdSbp> nd_sbp_;
+  std::map<std::string, TensorDesc> logical_;
+  NdSbp broadcast_{"B"};
 };
 
 // One SBP signature: per argument "S(axis)", "B" or "P".
@@ -383,24 +461,31 @@ class OpKernelCache {
   virtual ~OpKernelCache() = default;
 };
 
+// oneflow/core/framework/op_kernel.h:40-60 (KernelCacheContext / KernelInitContext).
 class KernelCacheContext {
  public:
-  KernelCacheContext(ParallelContext pc, std::map<std::string, std::string> out_sbp,
+  KernelCacheContext(ParallelContext pc, ParallelDesc pd, std::map<std::string, NdSbp> nd_sbp,
                      std::map<std::string, TensorDesc> logical, DeviceType dev)
-      : pc_(pc), out_sbp_(std::move(out_sbp)), logical_(std::move(logical)), dev_(dev) {}
+      : pc_(pc), pd_(std::move(pd)), nd_sbp_(std::move(nd_sbp)), logical_(std::move(logical)),
+        dev_(dev) {}
   const ParallelContext& parallel_ctx() const { return pc_; }
+  const ParallelDesc& parallel_desc() const { return pd_; }
   DeviceType device_type() const { return dev_; }
-  // "S(0)", "B", ... of an argument (1-D hierarchy).
-  const std::string& Sbp4ArgName(const std::string& n) const { return out_sbp_.at(n); }
+  const NdSbp& NdSbp4ArgNameAndIndex(const std::string& n, int32_t) const {
+    auto it = nd_sbp_.find(n);
+    return it == nd_sbp_.end() ? broadcast_ : it->second;
+  }
   const TensorDesc* LogicalTensorDesc4ArgNameAndIndex(const std::string& n, int32_t) const {
     return &logical_.at(n);
   }
 
  private:
   ParallelContext pc_;
-  std::map<std::string, std::string> out_sbp_;
+  ParallelDesc pd_;
+  std::map<std::string, NdSbp> nd_sbp_;
   std::map<std::string, TensorDesc> logical_;
   DeviceType dev_;
+  NdSbp broadcast_{"B"};
 };
 
 class KernelComputeContext {
@@ -479,7 +564,12 @@ inline HobDataTypeProxy HobDataType(const std::string& n, int32_t i) { return {n
 struct InferSizeContext {
   std::map<std::pair<std::string, int32_t>, TensorDesc> descs;
   AttrMap attrs;
+  std::map<std::string, TensorDesc> logical;  // of a global op (empty for a local one)
   const TensorDesc& InputTensorDesc(const std::string& n, int32_t i) const { return descs.at({n, i}); }
+  const TensorDesc* LogicalTensorDesc4ArgNameAndIndex(const std::string& n, int32_t) const {
+    auto it = logical.find(n);
+    return it == logical.end() ? nullptr : &it->second;
+  }
   template <typename T>
   T Attr(const std::string& n) const {
     return static_cast<T>(attrs.at(n));

@@ -50,21 +50,81 @@ Maybe<void> CheckArgs(const ofx_tensor_desc* row_ptr, const ofx_tensor_desc* col
   return Maybe<void>::Ok();
 }
 
+// Stride contract of the kernels: a 2-D tensor is rows of unit-stride elements at row_stride
+// >= shape[1] (b may be a row-strided view; out too).  A column stride != 1 (e.g. out[:, ::2])
+// cannot be expressed to the kernel, which takes only the row stride, and is refused.
+Maybe<void> CheckUnitColumnStride(const ofx_tensor_desc* t, const char* name) {
+  if (t->ndim == 2 && t->shape[0] > 0 && t->shape[1] > 1) {
+    CHECK_OR_RETURN(t->stride[1] == 1 && t->stride[0] >= t->shape[1])
+        << Error::RuntimeError() << "spmm_csr: " << name << " must have unit column stride and "
+        << "row stride >= its columns, got strides (" << t->stride[0] << ", " << t->stride[1]
+        << ")";
+  }
+  return Maybe<void>::Ok();
+}
+
+// Placement of a (possibly global) call: the hierarchy, out's NdSbp and b's NdSbp (out S(0) ->
+// b B, out S(1) -> b S(1), out B -> b B), and this rank.  A local call is the 1-device placement.
+struct Placement {
+  Shape hierarchy{1};
+  NdSbp out_sbp{"B"}, b_sbp{"B"};
+  int64_t parallel_id = 0;
+  int64_t parallel_num() const { return hierarchy.elem_cnt(); }
+};
+
+Maybe<void> MakePlacement(int hierarchy_ndim, const int64_t* hierarchy, const int32_t* out_split,
+                          int64_t parallel_id, Placement* p) {
+  CHECK_OR_RETURN(hierarchy_ndim >= 1 && hierarchy_ndim <= 4 && hierarchy && out_split)
+      << Error::RuntimeError() << "spmm_csr: placement needs a 1-D..4-D hierarchy";
+  std::vector<int64_t> dims;
+  p->out_sbp.clear();
+  p->b_sbp.clear();
+  for (int i = 0; i < hierarchy_ndim; ++i) {
+    CHECK_GE_OR_RETURN(hierarchy[i], 1) << Error::RuntimeError() << "bad hierarchy dim";
+    CHECK_OR_RETURN(out_split[i] >= -1 && out_split[i] <= 1)
+        << Error::RuntimeError() << "out can be split on axis 0 or 1 only";
+    dims.push_back(hierarchy[i]);
+    p->out_sbp.push_back(out_split[i] < 0 ? "B" : "S(" + std::to_string(out_split[i]) + ")");
+    p->b_sbp.push_back(out_split[i] == 1 ? "S(1)" : "B");
+  }
+  p->hierarchy = Shape(dims);
+  CHECK_OR_RETURN(parallel_id >= 0 && parallel_id < p->parallel_num())
+      << Error::RuntimeError() << "spmm_csr: parallel_id " << parallel_id << " outside "
+      << p->hierarchy.ToString();
+  p->parallel_id = parallel_id;
+  return Maybe<void>::Ok();
+}
+
+// Logical inference (the op's logical rule on the logical b: K x b_logical_cols), then the
+// physical out of this rank (the op's physical rule on the physical inputs + placement).
 Maybe<void> Infer(const ofx_tensor_desc* row_ptr, const ofx_tensor_desc* col_idx,
                   const ofx_tensor_desc* values, int64_t m, int64_t k, const ofx_tensor_desc* b,
-                  user_op::TensorDesc* out) {
+                  int64_t b_logical_cols, const Placement& pl, user_op::TensorDesc* logical_out,
+                  user_op::TensorDesc* physical_out) {
   JUST(CheckArgs(row_ptr, col_idx, values, b));
+  JUST(CheckUnitColumnStride(b, "b"));
   const user_op::OpRegistryResult* op = user_op::UserOpRegistryMgr::Get().GetOpRegistryResult("spmm_csr");
   CHECK_OR_RETURN(op != nullptr) << Error::RuntimeError() << "op spmm_csr is not registered";
   DescMap in;
   in[{"a_csr_row_ptr", 0}] = user_op::TensorDesc(ShapeOf(row_ptr), (DataType)row_ptr->dtype);
   in[{"a_csr_col_idx", 0}] = user_op::TensorDesc(ShapeOf(col_idx), (DataType)col_idx->dtype);
   in[{"a_csr_values", 0}] = user_op::TensorDesc(ShapeOf(values), (DataType)values->dtype);
+  DescMap logical_in = in;
+  Shape b_logical = ShapeOf(b);
+  if (b_logical.NumAxes() == 2 && b_logical_cols >= 0) b_logical.Set(1, b_logical_cols);
+  logical_in[{"b", 0}] = user_op::TensorDesc(b_logical, (DataType)b->dtype);
+  const user_op::AttrMap attrs = {{"a_num_rows", m}, {"a_num_cols", k}};
+  user_op::InferContext lctx(logical_in, attrs);
+  JUST(op->logical_infer(&lctx));
+  JUST(op->dtype_infer(&lctx));
+  *logical_out = lctx.OutputTensorDesc("out", 0);
   in[{"b", 0}] = user_op::TensorDesc(ShapeOf(b), (DataType)b->dtype);
-  user_op::InferContext ctx(in, {{"a_num_rows", m}, {"a_num_cols", k}});
-  JUST(op->logical_infer(&ctx));
-  JUST(op->dtype_infer(&ctx));
-  *out = ctx.OutputTensorDesc("out", 0);
+  user_op::InferContext pctx(in, attrs);
+  pctx.SetParallel(ParallelContext(pl.parallel_id, pl.parallel_num()), ParallelDesc(pl.hierarchy),
+                   {{"out", pl.out_sbp}, {"b", pl.b_sbp}}, {{"out", *logical_out}});
+  JUST(op->physical_infer(&pctx));
+  JUST(op->dtype_infer(&pctx));
+  *physical_out = pctx.OutputTensorDesc("out", 0);
   return Maybe<void>::Ok();
 }
 
@@ -92,77 +152,36 @@ Maybe<void> Choose(const ofx_tensor_desc* row_ptr, const ofx_tensor_desc* b, int
   return user_op::UserOpRegistryMgr::Get().GetOpKernelRegistryResult("spmm_csr", rc, reg);
 }
 
-}  // namespace
-}  // namespace oneflow
-
-using namespace oneflow;
-
-extern "C" int ofx_functional_spmm_csr_infer(const ofx_tensor_desc* row_ptr,
-                                             const ofx_tensor_desc* col_idx,
-                                             const ofx_tensor_desc* values, int64_t a_num_rows,
-                                             int64_t a_num_cols, const ofx_tensor_desc* b,
-                                             ofx_tensor_desc* out) {
-  user_op::TensorDesc od;
-  int rc = ToStatus(Infer(row_ptr, col_idx, values, a_num_rows, a_num_cols, b, &od));
-  if (rc) return rc;
-  if (out) {
-    out->dtype = od.data_type();
-    out->ndim = (int32_t)od.shape().NumAxes();
-    for (int i = 0; i < out->ndim; ++i) out->shape[i] = od.shape().At(i);
-    out->device = b->device;
-  }
-  return OFX_OK;
-}
-
-extern "C" int ofx_functional_spmm_csr_tmp_size(const ofx_tensor_desc* row_ptr,
-                                                const ofx_tensor_desc* col_idx,
-                                                const ofx_tensor_desc* values, int64_t a_num_rows,
-                                                int64_t a_num_cols, const ofx_tensor_desc* b,
-                                                size_t* bytes) {
-  OFX_REQUIRE(bytes, OFX_EINVAL, "spmm_csr_tmp_size: bytes is NULL");
-  user_op::TensorDesc od;
-  int rc = ToStatus(Infer(row_ptr, col_idx, values, a_num_rows, a_num_cols, b, &od));
+// functional::SpmmCsr on a local or global tensor set: inference, kernel choice, then either the
+// tmp size (tmp_size_out != NULL) or the kernel's cache init + Compute on the stream.
+int RunSpmmCsr(void* stream, const ofx_tensor_desc* row_ptr, const ofx_tensor_desc* col_idx,
+               const ofx_tensor_desc* values, int64_t m, int64_t k, const ofx_tensor_desc* b,
+               int64_t b_logical_cols, ofx_tensor_desc* out, void* tmp, size_t tmp_bytes,
+               const Placement& pl, int num_threads, size_t* tmp_size_out) {
+  user_op::TensorDesc logical_od, od;
+  int rc = ToStatus(Infer(row_ptr, col_idx, values, m, k, b, b_logical_cols, pl, &logical_od, &od));
   if (rc) return rc;
   const user_op::OpKernelRegistryResult* reg = nullptr;
   rc = ToStatus(Choose(row_ptr, b, b->device, &reg));
   if (rc) return rc;
-  user_op::InferSizeContext sc;
-  sc.descs[{"a_csr_row_ptr", 0}] = user_op::TensorDesc(ShapeOf(row_ptr), (DataType)row_ptr->dtype);
-  sc.descs[{"a_csr_col_idx", 0}] = user_op::TensorDesc(ShapeOf(col_idx), (DataType)col_idx->dtype);
-  sc.descs[{"b", 0}] = user_op::TensorDesc(ShapeOf(b), (DataType)b->dtype);
-  sc.attrs = {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols}};
-  *bytes = reg->infer_tmp_size ? reg->infer_tmp_size(&sc) : 0;
-  return OFX_OK;
-}
-
-extern "C" int ofx_functional_spmm_csr_ex(void* stream, const ofx_tensor_desc* row_ptr,
-                                          const ofx_tensor_desc* col_idx,
-                                          const ofx_tensor_desc* values, int64_t a_num_rows,
-                                          int64_t a_num_cols, const ofx_tensor_desc* b,
-                                          ofx_tensor_desc* out, void* tmp, size_t tmp_bytes,
-                                          int64_t parallel_id, int64_t parallel_num,
-                                          int out_split_axis, int num_threads) {
-  OFX_REQUIRE(out, OFX_EINVAL, "spmm_csr: out is NULL");
-  OFX_REQUIRE(parallel_num >= 1 && parallel_id >= 0 && parallel_id < parallel_num, OFX_EINVAL,
-              "spmm_csr: bad parallel context %lld/%lld", (long long)parallel_id,
-              (long long)parallel_num);
-  user_op::TensorDesc od;
-  int rc = ToStatus(Infer(row_ptr, col_idx, values, a_num_rows, a_num_cols, b, &od));
-  if (rc) return rc;
-  // The physical out of a row split holds only this rank's rows (S(0) slice of the logical out).
-  int64_t phys_rows = od.shape().At(0);
-  int64_t lo = 0, hi = phys_rows;
-  if (parallel_num > 1 && out_split_axis == 0) {
-    ofx_balanced_range(phys_rows, parallel_num, parallel_id, &lo, &hi);
-    phys_rows = hi - lo;
+  if (tmp_size_out) {
+    user_op::InferSizeContext sc;
+    sc.descs[{"a_csr_row_ptr", 0}] = user_op::TensorDesc(ShapeOf(row_ptr), (DataType)row_ptr->dtype);
+    sc.descs[{"a_csr_col_idx", 0}] = user_op::TensorDesc(ShapeOf(col_idx), (DataType)col_idx->dtype);
+    sc.descs[{"b", 0}] = user_op::TensorDesc(ShapeOf(b), (DataType)b->dtype);
+    sc.attrs = {{"a_num_rows", m}, {"a_num_cols", k}};
+    sc.logical["out"] = logical_od;
+    *tmp_size_out = reg->infer_tmp_size ? reg->infer_tmp_size(&sc) : 0;
+    return OFX_OK;
   }
+  OFX_REQUIRE(out, OFX_EINVAL, "spmm_csr: out is NULL");
+  const int64_t phys_rows = od.shape().At(0);
   OFX_REQUIRE(out->ndim == 2 && out->shape[0] == phys_rows && out->shape[1] == od.shape().At(1) &&
                   out->dtype == (int32_t)od.data_type() && out->device == b->device,
               OFX_EINVAL,
               "spmm_csr: out must be a (%lld, %lld) tensor of dtype %d on device %d",
               (long long)phys_rows, (long long)od.shape().At(1), (int)od.data_type(), b->device);
-  const user_op::OpKernelRegistryResult* reg = nullptr;
-  rc = ToStatus(Choose(row_ptr, b, b->device, &reg));
+  rc = ToStatus(CheckUnitColumnStride(out, "out"));
   if (rc) return rc;
   const user_op::OpKernel* kernel = GetKernel(reg);
 
@@ -181,11 +200,11 @@ extern "C" int ofx_functional_spmm_csr_ex(void* stream, const ofx_tensor_desc* r
   ep::HipStream hip_stream(stream, b->device);
   ep::Stream* s = dev == DeviceType::kCPU ? static_cast<ep::Stream*>(&cpu_stream)
                                           : static_cast<ep::Stream*>(&hip_stream);
-  const user_op::AttrMap attrs = {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols}};
-  user_op::KernelCacheContext cache_ctx(
-      ParallelContext(parallel_id, parallel_num),
-      {{"out", out_split_axis == 0 ? "S(0)" : (out_split_axis == 1 ? "S(1)" : "B")}},
-      {{"out", od}}, dev);
+  const user_op::AttrMap attrs = {{"a_num_rows", m}, {"a_num_cols", k}};
+  user_op::KernelCacheContext cache_ctx(ParallelContext(pl.parallel_id, pl.parallel_num()),
+                                        ParallelDesc(pl.hierarchy),
+                                        {{"out", pl.out_sbp}, {"b", pl.b_sbp}},
+                                        {{"out", logical_od}}, dev);
   user_op::KernelComputeContext ctx(s, tensors, attrs, dev);
   try {
     std::shared_ptr<user_op::OpKernelCache> cache = kernel->InitOpKernelCache(&cache_ctx);
@@ -199,13 +218,76 @@ extern "C" int ofx_functional_spmm_csr_ex(void* stream, const ofx_tensor_desc* r
   return OFX_OK;
 }
 
+}  // namespace
+}  // namespace oneflow
+
+using namespace oneflow;
+
+extern "C" int ofx_functional_spmm_csr_infer(const ofx_tensor_desc* row_ptr,
+                                             const ofx_tensor_desc* col_idx,
+                                             const ofx_tensor_desc* values, int64_t a_num_rows,
+                                             int64_t a_num_cols, const ofx_tensor_desc* b,
+                                             ofx_tensor_desc* out) {
+  user_op::TensorDesc lod, od;
+  int rc = ToStatus(Infer(row_ptr, col_idx, values, a_num_rows, a_num_cols, b, -1, Placement(),
+                          &lod, &od));
+  if (rc) return rc;
+  if (out) {
+    out->dtype = od.data_type();
+    out->ndim = (int32_t)od.shape().NumAxes();
+    for (int i = 0; i < out->ndim; ++i) out->shape[i] = od.shape().At(i);
+    out->device = b->device;
+  }
+  return OFX_OK;
+}
+
+extern "C" int ofx_functional_spmm_csr_tmp_size(const ofx_tensor_desc* row_ptr,
+                                                const ofx_tensor_desc* col_idx,
+                                                const ofx_tensor_desc* values, int64_t a_num_rows,
+                                                int64_t a_num_cols, const ofx_tensor_desc* b,
+                                                size_t* bytes) {
+  OFX_REQUIRE(bytes, OFX_EINVAL, "spmm_csr_tmp_size: bytes is NULL");
+  return RunSpmmCsr(nullptr, row_ptr, col_idx, values, a_num_rows, a_num_cols, b, -1, nullptr,
+                    nullptr, 0, Placement(), 0, bytes);
+}
+
+extern "C" int ofx_functional_spmm_csr_global(
+    void* stream, const ofx_tensor_desc* row_ptr, const ofx_tensor_desc* col_idx,
+    const ofx_tensor_desc* values, int64_t a_num_rows, int64_t a_num_cols,
+    const ofx_tensor_desc* b, int64_t b_logical_cols, ofx_tensor_desc* out, void* tmp,
+    size_t tmp_bytes, int hierarchy_ndim, const int64_t* hierarchy, const int32_t* out_split_axes,
+    int64_t parallel_id, int num_threads, size_t* tmp_size_out) {
+  Placement pl;
+  int rc = ToStatus(MakePlacement(hierarchy_ndim, hierarchy, out_split_axes, parallel_id, &pl));
+  if (rc) return rc;
+  return RunSpmmCsr(stream, row_ptr, col_idx, values, a_num_rows, a_num_cols, b, b_logical_cols,
+                    out, tmp, tmp_bytes, pl, num_threads, tmp_size_out);
+}
+
+extern "C" int ofx_functional_spmm_csr_ex(void* stream, const ofx_tensor_desc* row_ptr,
+                                          const ofx_tensor_desc* col_idx,
+                                          const ofx_tensor_desc* values, int64_t a_num_rows,
+                                          int64_t a_num_cols, const ofx_tensor_desc* b,
+                                          ofx_tensor_desc* out, void* tmp, size_t tmp_bytes,
+                                          int64_t parallel_id, int64_t parallel_num,
+                                          int out_split_axis, int num_threads) {
+  OFX_REQUIRE(out_split_axis != 1 || parallel_num == 1, OFX_EINVAL,
+              "spmm_csr_ex: a column split needs the logical width: use "
+              "ofx_functional_spmm_csr_global");
+  const int64_t h = parallel_num;
+  const int32_t ax = out_split_axis;
+  return ofx_functional_spmm_csr_global(stream, row_ptr, col_idx, values, a_num_rows, a_num_cols,
+                                        b, -1, out, tmp, tmp_bytes, 1, &h, &ax, parallel_id,
+                                        num_threads, nullptr);
+}
+
 extern "C" int ofx_functional_spmm_csr(void* stream, const ofx_tensor_desc* row_ptr,
                                        const ofx_tensor_desc* col_idx,
                                        const ofx_tensor_desc* values, int64_t a_num_rows,
                                        int64_t a_num_cols, const ofx_tensor_desc* b,
                                        ofx_tensor_desc* out, void* tmp, size_t tmp_bytes) {
-  return ofx_functional_spmm_csr_ex(stream, row_ptr, col_idx, values, a_num_rows, a_num_cols, b,
-                                    out, tmp, tmp_bytes, 0, 1, -1, 0);
+  return RunSpmmCsr(stream, row_ptr, col_idx, values, a_num_rows, a_num_cols, b, -1, out, tmp,
+                    tmp_bytes, Placement(), 0, nullptr);
 }
 
 // SBP signatures of a registered op, for the tests: "arg:sbp,arg:sbp;...|no_grad:..." into buf.
@@ -283,6 +365,7 @@ Maybe<void> RunUserOp(const std::string& op_name, const std::vector<Arg>& ins,
         << Error::RuntimeError() << op_name << ": " << a.name << " must be 1-D or 2-D";
     CHECK_EQ_OR_RETURN(a.d->device, device)
         << Error::RuntimeError() << op_name << ": expected all tensors on the same device";
+    JUST(CheckUnitColumnStride(a.d, a.name));
     in[{a.name, 0}] = user_op::TensorDesc(ShapeOf(a.d), (DataType)a.d->dtype);
   }
   user_op::InferContext ictx(in, attrs);
@@ -316,6 +399,7 @@ Maybe<void> RunUserOp(const std::string& op_name, const std::vector<Arg>& ins,
                     o.d->device == device)
         << Error::RuntimeError() << op_name << ": output " << o.name << " must be "
         << want.shape().ToString() << " of dtype " << DataType_Name(want.data_type());
+    JUST(CheckUnitColumnStride(o.d, o.name));
     add(o);
   }
   user_op::Tensor t_tmp(Shape({(int64_t)tmp_bytes}), kChar, tmp);

@@ -16,26 +16,47 @@ namespace oneflow {
 
 namespace {
 
+// Row range [lower, upper) of this rank's physical out and the logical width N.  The range
+// follows unsorted_segment_sum_kernel.cpp:59-78: GetTensorSliceView4ParallelId over out's nd_sbp
+// and the placement hierarchy (1-D: BalancedSplitter; 2-D: e.g. (S(0), S(1)) rows x columns).
+// The logical N fixes the hub-row schedule: split = default_split(N) whatever slice of the
+// columns this rank computes, so a column-split rank's bits equal the single-device op's.
 class SpmmCsrOpKernelCache final : public user_op::OpKernelCache {
  public:
-  SpmmCsrOpKernelCache(int64_t lower, int64_t upper) : lower_(lower), upper_(upper) {}
+  SpmmCsrOpKernelCache(int64_t lower, int64_t upper, int64_t logical_n)
+      : lower_(lower), upper_(upper), logical_n_(logical_n) {}
   ~SpmmCsrOpKernelCache() override = default;
   int64_t lower() const { return lower_; }
   int64_t upper() const { return upper_; }
+  int64_t logical_n() const { return logical_n_; }
 
  private:
   const int64_t lower_;
   const int64_t upper_;
+  const int64_t logical_n_;
 };
 
 std::shared_ptr<user_op::OpKernelCache> CreateSpmmCsrOpKernelCache(user_op::KernelCacheContext* ctx) {
-  if (ctx->parallel_ctx().parallel_num() > 1 && ctx->Sbp4ArgName("out") == "S(0)") {
-    const user_op::TensorDesc* out_logical = ctx->LogicalTensorDesc4ArgNameAndIndex("out", 0);
-    const BalancedSplitter bs(out_logical->shape().At(0), ctx->parallel_ctx().parallel_num());
-    const auto range = bs.At(ctx->parallel_ctx().parallel_id());
-    return std::make_shared<SpmmCsrOpKernelCache>(range.first, range.second);
+  const user_op::TensorDesc* out_logical = ctx->LogicalTensorDesc4ArgNameAndIndex("out", 0);
+  const Shape& shape = out_logical->shape();
+  int64_t lower = 0, upper = shape.At(0);
+  if (ctx->parallel_ctx().parallel_num() > 1) {
+    const TensorSliceView view =
+        GetTensorSliceView4ParallelId(*ctx->parallel_desc().hierarchy(),
+                                      ctx->NdSbp4ArgNameAndIndex("out", 0), shape,
+                                      ctx->parallel_ctx().parallel_id());
+    lower = view.At(0).begin();
+    upper = view.At(0).end();
   }
-  return nullptr;
+  return std::make_shared<SpmmCsrOpKernelCache>(lower, upper, shape.At(1));
+}
+
+// Options of a launch: the contract's schedule for the logical width (no cache: local op, the
+// physical width is the logical one).
+ofx_spmm_options OptionsOf(const SpmmCsrOpKernelCache* cache) {
+  ofx_spmm_options o{};
+  if (cache != nullptr) o.split_threshold = ofx_spmm_default_split(cache->logical_n());
+  return o;
 }
 
 int DtCode(DataType dt) { return static_cast<int>(dt); }
@@ -59,12 +80,13 @@ void ComputeSpmmCsr(user_op::KernelComputeContext* ctx, const user_op::OpKernelC
   const int64_t nnz = col_idx->shape_view().elem_cnt();
   int64_t row_begin = 0;
   int64_t row_end = m;
-  if (cache != nullptr) {
-    const auto* range = dynamic_cast<const SpmmCsrOpKernelCache*>(cache);
-    OFX_KERNEL_CHECK(range != nullptr, "unexpected kernel cache type");
+  const auto* range = dynamic_cast<const SpmmCsrOpKernelCache*>(cache);
+  OFX_KERNEL_CHECK(cache == nullptr || range != nullptr, "unexpected kernel cache type");
+  if (range != nullptr) {
     row_begin = range->lower();
     row_end = range->upper();
   }
+  const ofx_spmm_options opts = OptionsOf(range);
   OFX_KERNEL_CHECK(out->shape_view().At(0) == row_end - row_begin,
                    "out rows " << out->shape_view().At(0) << " != row range "
                                << row_end - row_begin);
@@ -84,13 +106,13 @@ void ComputeSpmmCsr(user_op::KernelComputeContext* ctx, const user_op::OpKernelC
     rc = ofx_spmm_csr_fused(stream, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
                             col_idx->dptr(), values->dptr(), b->dptr(), b->row_stride(),
                             out->mut_dptr(), out->row_stride(), row_begin, row_end, bias_ptr, act,
-                            ws, ws_bytes, nullptr);
+                            ws, ws_bytes, &opts);
   } else {
     const int threads = ctx->stream()->As<ep::CpuStream>()->num_threads();
     rc = ofx_spmm_csr_fused_cpu(threads, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
                                 col_idx->dptr(), values->dptr(), b->dptr(), b->row_stride(),
                                 out->mut_dptr(), out->row_stride(), row_begin, row_end, bias_ptr,
-                                act, nullptr);
+                                act, &opts);
   }
   OFX_KERNEL_CHECK(rc == OFX_OK, op_name << " kernel failed (" << rc << "): " << ofx_last_error());
 }
@@ -171,12 +193,13 @@ class SpmmCsrGatheredKernel final : public user_op::OpKernel, public user_op::Cu
     const int64_t n = out->shape_view().At(1);
     const int64_t nnz = col_idx->shape_view().elem_cnt();
     int64_t row_begin = 0, row_end = m;
-    if (cache != nullptr) {
-      const auto* range = dynamic_cast<const SpmmCsrOpKernelCache*>(cache);
-      OFX_KERNEL_CHECK(range != nullptr, "unexpected kernel cache type");
+    const auto* range = dynamic_cast<const SpmmCsrOpKernelCache*>(cache);
+    OFX_KERNEL_CHECK(cache == nullptr || range != nullptr, "unexpected kernel cache type");
+    if (range != nullptr) {
       row_begin = range->lower();
       row_end = range->upper();
     }
+    const ofx_spmm_options opts = OptionsOf(range);
     OFX_KERNEL_CHECK(out->shape_view().At(0) == row_end - row_begin,
                      "out rows " << out->shape_view().At(0) << " != row range "
                                  << row_end - row_begin);
@@ -190,7 +213,7 @@ class SpmmCsrGatheredKernel final : public user_op::OpKernel, public user_op::Cu
       rc = ofx_spmm_csr_gathered(stream, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
                                  col_idx->dptr(), values->dptr(), perm->dptr(), b->dptr(),
                                  b->row_stride(), out->mut_dptr(), out->row_stride(), row_begin,
-                                 row_end, ws, ws_bytes, nullptr);
+                                 row_end, ws, ws_bytes, &opts);
     } else {
       const size_t vbytes = (size_t)nnz * (size_t)GetSizeOfDataType(values->data_type());
       OFX_KERNEL_CHECK(nnz == 0 || ws_bytes >= vbytes, "tmp buffer smaller than the values");
@@ -199,7 +222,7 @@ class SpmmCsrGatheredKernel final : public user_op::OpKernel, public user_op::Cu
         rc = ofx_spmm_csr_cpu(ctx->stream()->As<ep::CpuStream>()->num_threads(), idx_dt, val_dt,
                               m, k, n, nnz, row_ptr->dptr(), col_idx->dptr(), ws, b->dptr(),
                               b->row_stride(), out->mut_dptr(), out->row_stride(), row_begin,
-                              row_end, nullptr);
+                              row_end, &opts);
     }
     OFX_KERNEL_CHECK(rc == OFX_OK,
                      "spmm_csr_gathered kernel failed (" << rc << "): " << ofx_last_error());
@@ -211,14 +234,18 @@ size_t InferSpmmCsrGatheredCpuTmpSize(user_op::InferSizeContext* ctx) {
   return (size_t)values.shape().elem_cnt() * (size_t)GetSizeOfDataType(values.data_type());
 }
 
+// Workspace for the physical width with the logical width's schedule (as Compute launches it).
 size_t InferSpmmCsrTmpSize(user_op::InferSizeContext* ctx) {
   const user_op::TensorDesc& row_ptr = ctx->InputTensorDesc("a_csr_row_ptr", 0);
   const user_op::TensorDesc& col_idx = ctx->InputTensorDesc("a_csr_col_idx", 0);
   const user_op::TensorDesc& b = ctx->InputTensorDesc("b", 0);
+  const user_op::TensorDesc* out_logical = ctx->LogicalTensorDesc4ArgNameAndIndex("out", 0);
+  ofx_spmm_options o{};
+  if (out_logical != nullptr) o.split_threshold = ofx_spmm_default_split(out_logical->shape().At(1));
   size_t bytes = 0;
   const int rc = ofx_spmm_csr_workspace_size(
       DtCode(row_ptr.data_type()), DtCode(b.data_type()), ctx->Attr<int64_t>("a_num_rows"),
-      ctx->Attr<int64_t>("a_num_cols"), b.shape().At(1), col_idx.shape().At(0), nullptr, &bytes);
+      ctx->Attr<int64_t>("a_num_cols"), b.shape().At(1), col_idx.shape().At(0), &o, &bytes);
   return rc == OFX_OK ? bytes : 0;
 }
 

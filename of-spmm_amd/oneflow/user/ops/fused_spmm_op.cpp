@@ -14,6 +14,8 @@
 
 namespace oneflow {
 
+Maybe<void> SpmmCsrInferPhysicalOut(user_op::InferContext* ctx);  // spmm_op.cpp
+
 namespace {
 // The spmm_csr half of the checks reuses the spmm_csr schema functions (same input names).
 Maybe<void> InferBias(user_op::InferContext* ctx) {
@@ -35,7 +37,8 @@ Maybe<void> InferBias(user_op::InferContext* ctx) {
 }
 
 /* static */ Maybe<void> FusedSpmmCsrOp::InferPhysicalTensorDesc(user_op::InferContext* ctx) {
-  return InferLogicalTensorDesc(ctx);
+  JUST(InferLogicalTensorDesc(ctx));  // bias checked against the physical b (S(0) with S(1) b)
+  return SpmmCsrInferPhysicalOut(ctx);
 }
 
 /* static */ Maybe<void> FusedSpmmCsrOp::GetSbp(user_op::SbpContext* ctx) {

@@ -84,6 +84,27 @@ Maybe<void> CheckValuesPerm(user_op::InferContext* ctx) {
   return Maybe<void>::Ok();
 }
 
+// Physical out of a global spmm_csr.  Every signature keeps the CSR broadcast, so the logical
+// rule applied to the physical inputs gives [a_num_rows, N_phys]: right for a broadcast out and
+// for the column split (b is then its S(1) slice).  A row split (out S(0)) holds only this rank's
+// rows, which no input shows: they come from out's nd_sbp and the placement as GetPhysicalShape
+// computes them (oneflow/core/operator/operator.cpp:1551-1626; the same pattern as
+// oneflow/user/ops/affine_grid_op.cpp:113-120), so OneFlow's check of each physical blob against
+// GetPhysicalShape (oneflow/core/graph/exec_graph.cpp:84-123) holds under S(0) and (S(0), S(1)).
+Maybe<void> InferPhysicalOut4SpmmCsr(user_op::InferContext* ctx) {
+  if (ctx->parallel_ctx().parallel_num() == 1) return Maybe<void>::Ok();
+  const user_op::TensorDesc* logical_out = ctx->LogicalTensorDesc4ArgNameAndIndex("out", 0);
+  CHECK_NOTNULL_OR_RETURN(logical_out) << Error::RuntimeError() << "no logical desc for out";
+  Shape physical;
+  JUST(GetPhysicalShape(logical_out->shape(), ctx->NdSbp4ArgNameAndIndex("out", 0),
+                        ctx->parallel_desc(), ctx->parallel_ctx(), &physical));
+  CHECK_EQ_OR_RETURN(physical.At(1), ctx->InputTensorDesc("b", 0).shape().At(1))
+      << Error::RuntimeError() << "physical b has " << ctx->InputTensorDesc("b", 0).shape().At(1)
+      << " columns but out's slice has " << physical.At(1);
+  ctx->SetOutputShape("out", 0, physical);
+  return Maybe<void>::Ok();
+}
+
 Maybe<void> GetSbp4SpmmCsr(user_op::SbpContext* ctx, bool with_perm) {
   // Row split: the CSR is broadcast, b is gathered to broadcast, out rows are split.
   auto row = ctx->NewBuilder();
@@ -104,12 +125,18 @@ Maybe<void> GetSbp4SpmmCsr(user_op::SbpContext* ctx, bool with_perm) {
 
 }  // namespace
 
+// Shared with fused_spmm_csr (fused_spmm_op.cpp).
+Maybe<void> SpmmCsrInferPhysicalOut(user_op::InferContext* ctx) {
+  return InferPhysicalOut4SpmmCsr(ctx);
+}
+
 /* static */ Maybe<void> SpmmCsrOp::InferLogicalTensorDesc(user_op::InferContext* ctx) {
   return InferTensorDesc4SpmmCsr(ctx);
 }
 
 /* static */ Maybe<void> SpmmCsrOp::InferPhysicalTensorDesc(user_op::InferContext* ctx) {
-  return InferLogicalTensorDesc(ctx);
+  JUST(InferLogicalTensorDesc(ctx));
+  return InferPhysicalOut4SpmmCsr(ctx);
 }
 
 /* static */ Maybe<void> SpmmCsrOp::GetSbp(user_op::SbpContext* ctx) {
@@ -138,7 +165,8 @@ Maybe<void> GetSbp4SpmmCsr(user_op::SbpContext* ctx, bool with_perm) {
 }
 
 /* static */ Maybe<void> SpmmCsrGatheredOp::InferPhysicalTensorDesc(user_op::InferContext* ctx) {
-  return InferLogicalTensorDesc(ctx);
+  JUST(InferLogicalTensorDesc(ctx));
+  return InferPhysicalOut4SpmmCsr(ctx);
 }
 
 /* static */ Maybe<void> SpmmCsrGatheredOp::GetSbp(user_op::SbpContext* ctx) {

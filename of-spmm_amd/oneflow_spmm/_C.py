@@ -72,44 +72,73 @@ def current_stream_handle(t: torch.Tensor):
     return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
 
+def _placement(_parallel, _placement_nd):
+    """(hierarchy dims, out split axis per hierarchy axis, parallel_id, logical N or -1)."""
+    if _placement_nd is not None:
+        pl = dict(_placement_nd)
+        hier = tuple(int(x) for x in pl["hierarchy"])
+        axes = tuple(-1 if a in (None, "B") else (int(a[2:-1]) if isinstance(a, str) else int(a))
+                     for a in pl["nd_sbp"])
+        return hier, axes, int(pl["parallel_id"]), int(pl.get("logical_n", -1))
+    if _parallel is None:
+        return (1,), (-1,), 0, -1
+    pid, pnum, axis = _parallel[:3]
+    logical_n = _parallel[3] if len(_parallel) > 3 else -1
+    return (int(pnum),), (int(axis),), int(pid), int(logical_n)
+
+
 def spmm_csr(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor,
              a_csr_values: torch.Tensor, a_num_rows: int, a_num_cols: int, b: torch.Tensor, *,
-             out: torch.Tensor | None = None, _parallel=None, num_threads: int = 0) -> torch.Tensor:
+             out: torch.Tensor | None = None, _parallel=None, _placement_nd=None,
+             num_threads: int = 0) -> torch.Tensor:
     """out[M, N] = CSR(a_csr_row_ptr, a_csr_col_idx, a_csr_values; M x K) @ b[K, N].
 
-    `_parallel=(parallel_id, parallel_num, out_split_axis)` runs the global form: with
-    out_split_axis 0 this rank computes its BalancedSplitter row slice (the physical S(0) out).
+    Global form (one rank of a placement; `b` and `out` are this rank's physical tensors):
+      `_parallel=(parallel_id, parallel_num, out_split_axis[, logical_n])` for a 1-D placement
+      (out_split_axis 0: this rank's BalancedSplitter rows; 1: a column slice of width b.shape[1]
+      out of logical_n; -1: broadcast), or
+      `_placement_nd=dict(hierarchy=(R, C), nd_sbp=("S(0)", "S(1)"), parallel_id=p, logical_n=N)`
+      for an N-D one.  The op's physical inference shapes `out`; the kernel's cache takes the row
+      range from out's NdSbp (GetTensorSliceView4ParallelId) and the hub schedule from logical N.
     """
     rp = _prep(a_csr_row_ptr, "a_csr_row_ptr")
     ci = _prep(a_csr_col_idx, "a_csr_col_idx")
     vals = _prep(a_csr_values, "a_csr_values")
     bb = _prep(b, "b", matrix=True)
     d_rp, d_ci, d_v, d_b = desc(rp), desc(ci), desc(vals), desc(bb)
-    od = TensorDesc()
-    check(LIB.ofx_functional_spmm_csr_infer(ctypes.byref(d_rp), ctypes.byref(d_ci), ctypes.byref(d_v),
-                                            int(a_num_rows), int(a_num_cols), ctypes.byref(d_b),
-                                            ctypes.byref(od)), "spmm_csr")
-    pid, pnum, axis = _parallel if _parallel is not None else (0, 1, -1)
-    rows, n = od.shape[0], od.shape[1]
-    if pnum > 1 and axis == 0:
-        lo, hi = balanced_range(rows, pnum, pid)
-        rows = hi - lo
+    hier, axes, pid, logical_n = _placement(_parallel, _placement_nd)
+    c_hier = (ctypes.c_int64 * len(hier))(*hier)
+    c_axes = (ctypes.c_int32 * len(axes))(*axes)
+    common = (ctypes.byref(d_rp), ctypes.byref(d_ci), ctypes.byref(d_v), int(a_num_rows),
+              int(a_num_cols), ctypes.byref(d_b), logical_n)
+    tail = (len(hier), c_hier, c_axes, pid, int(num_threads))
     if out is None:
+        # the physical out of this rank: the op's physical inference, through a dry run on an
+        # empty descriptor (tmp size query) would not return the shape, so ask the infer entry
+        # for the logical shape and apply the placement like GetPhysicalShape
+        od = TensorDesc()
+        check(LIB.ofx_functional_spmm_csr_infer(ctypes.byref(d_rp), ctypes.byref(d_ci),
+                                                ctypes.byref(d_v), int(a_num_rows), int(a_num_cols),
+                                                ctypes.byref(d_b), ctypes.byref(od)), "spmm_csr")
+        rows, n = od.shape[0], od.shape[1]
+        for i, (h, a) in enumerate(zip(hier, axes)):
+            if a == 0 and h > 1 and rows > 0:
+                idx = pid
+                for hh in hier[i + 1:]:
+                    idx //= hh
+                lo, hi = balanced_range(rows, h, idx % h)
+                rows = hi - lo
         out = torch.empty((rows, n), dtype=_DT_TO_TORCH[od.dtype], device=bb.device)
     d_o = desc(out)
     tmp_bytes = ctypes.c_size_t(0)
-    check(LIB.ofx_functional_spmm_csr_tmp_size(ctypes.byref(d_rp), ctypes.byref(d_ci), ctypes.byref(d_v),
-                                               int(a_num_rows), int(a_num_cols), ctypes.byref(d_b),
-                                               ctypes.byref(tmp_bytes)), "spmm_csr")
+    check(LIB.ofx_functional_spmm_csr_global(None, *common, None, None, 0, *tail,
+                                             ctypes.byref(tmp_bytes)), "spmm_csr")
     tmp = None
     if tmp_bytes.value:
         tmp = torch.empty(tmp_bytes.value, dtype=torch.uint8, device=bb.device)
-    check(LIB.ofx_functional_spmm_csr_ex(current_stream_handle(bb), ctypes.byref(d_rp),
-                                         ctypes.byref(d_ci), ctypes.byref(d_v), int(a_num_rows),
-                                         int(a_num_cols), ctypes.byref(d_b), ctypes.byref(d_o),
-                                         tmp.data_ptr() if tmp is not None else None,
-                                         tmp_bytes.value, pid, pnum, axis, int(num_threads)),
-          "spmm_csr")
+    check(LIB.ofx_functional_spmm_csr_global(current_stream_handle(bb), *common, ctypes.byref(d_o),
+                                             tmp.data_ptr() if tmp is not None else None,
+                                             tmp_bytes.value, *tail, None), "spmm_csr")
     return out
 
 

@@ -127,6 +127,9 @@ def _load():
         "ofx_functional_spmm_csr": ([p, pdesc, pdesc, pdesc, i64, i64, pdesc, pdesc, p, sz], i32),
         "ofx_functional_spmm_csr_ex": ([p, pdesc, pdesc, pdesc, i64, i64, pdesc, pdesc, p, sz, i64,
                                         i64, i32, i32], i32),
+        "ofx_functional_spmm_csr_global": ([p, pdesc, pdesc, pdesc, i64, i64, pdesc, i64, pdesc, p,
+                                            sz, i32, ctypes.POINTER(i64), ctypes.POINTER(i32), i64,
+                                            i32, ctypes.POINTER(sz)], i32),
         "ofx_functional_sddmm_csr": ([p, pdesc, pdesc, pdesc, pdesc, i64, i64, pdesc, p, sz,
                                       ctypes.POINTER(sz)], i32),
         "ofx_functional_spmm_csr_gathered": ([p, pdesc, pdesc, pdesc, pdesc, pdesc, i64, i64, pdesc,

@@ -8,8 +8,11 @@ test pinning one); cross-validated against scipy.sparse and 
 
 Semantics (see spmm_oracle.c header for the reference file:line anchors):
   C[r, :] = sum_{j in row r, ascending} val[j] * B[col[j], :]   from +0, multiply then add.
-16-bit types are carried as numpy uint16 bit patterns (bf16) / float16 and computed in fp32,
-rounded once at the end (oneflow/user/kernels/unsorted_segment_sum_kernel.cpp:146-205).
+16-bit types are carried as numpy uint16 bit patterns (bf16) / float16.  Each product is rounded
+to the 16-bit type (the multiply's output tensor has that dtype: BinaryFunctor<kMul> is
+`static_cast<Dst>(src0 * src1)`, oneflow/core/ep/common/primitive/binary_functor.h:46-51), the
+products are summed in fp32 and the sum is rounded once at the end
+(oneflow/user/kernels/unsorted_segment_sum_kernel.cpp:146-205).
 """
 from __future__ import annotations
 
@@ -37,8 +40,9 @@ def lib():
     if _LIB is None:
         _LIB = ctypes.CDLL(build())
         i64, p, c_int = ctypes.c_int64, ctypes.c_void_p, ctypes.c_int
-        _LIB.orc_spmm_f32.argtypes = [i64, i64, i64, p, p, p, p, i64, p, i64, i64, i64, i64, i64, c_int]
-        _LIB.orc_spmm_f64.argtypes = _LIB.orc_spmm_f32.argtypes
+        _LIB.orc_spmm_f64.argtypes = [i64, i64, i64, p, p, p, p, i64, p, i64, i64, i64, i64, i64, c_int]
+        _LIB.orc_spmm_f32.argtypes = _LIB.orc_spmm_f64.argtypes + [c_int]
+        _LIB.orc_round16.argtypes = [p, i64, c_int]
         _LIB.orc_spmm_f32_ref64.argtypes = [i64, p, p, p, p, i64, p, p, i64, i64, c_int]
         _LIB.orc_balanced_range.argtypes = [i64, i64, i64, ctypes.POINTER(i64), ctypes.POINTER(i64)]
     return _LIB
@@ -73,6 +77,16 @@ def f32_to_bf16_bits(x: np.ndarray) -> np.ndarray:
     nan = (u & 0x7FFFFFFF) > 0x7F800000
     r[nan] = ((u[nan] >> 16) | 0x40).astype(np.uint16)
     return r
+
+
+_ROUND16 = {"f32": 0, "bf16": 1, "f16": 2}
+
+
+def round16(x: np.ndarray, dtype: str) -> np.ndarray:
+    """fp32 values rounded to bf16/f16 as the multiply rounds its products (returned as fp32)."""
+    y = np.array(x, dtype=np.float32, copy=True, order="C")
+    lib().orc_round16(_p(y), y.size, _ROUND16[dtype])
+    return y
 
 
 def _schedule(n, split, chunk, ordered):
@@ -115,7 +129,7 @@ def spmm(row_ptr, col_idx, values, b, *, dtype="f32", row_begin=0, row_end=None,
         v, bb = np.ascontiguousarray(v), np.ascontiguousarray(bb)
         out = np.zeros((rows, n), dtype=np.float32)
         rc = lib().orc_spmm_f32(m, k, n, _p(rp), _p(ci), _p(v), _p(bb), n, _p(out), n,
-                                row_begin, row_end, s, c, nt)
+                                row_begin, row_end, s, c, nt, _ROUND16.get(dtype, 0))
     if rc != 0:
         raise ValueError("oracle: column index out of range")
     if dtype == "bf16":

@@ -42,15 +42,63 @@ void orc_balanced_range(int64_t total, int64_t parts, int64_t idx, int64_t* lo, 
   }
 }
 
+/* Rounding of an fp32 value to the 16-bit storage types, returned as fp32 (round to nearest
+ * even).  The multiply of the reference composition stores its product in the tensor's dtype:
+ * BinaryFunctor<kMul> is `static_cast<Dst>(src0 * src1)`
+ * (oneflow/core/ep/common/primitive/binary_functor.h:46-51), so for bf16/f16 inputs each
+ * product is rounded to 16 bits before the fp32 segment sum (unsorted_segment_sum_kernel.cpp:
+ * 146-205) adds it.  The fp32 product of two 16-bit values is exact, so one rounding here is
+ * the 16-bit product. */
+enum { ORC_R_NONE = 0, ORC_R_BF16 = 1, ORC_R_F16 = 2 };
+
+static float orc_round_bf16(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u)
+    u = (u & 0xffff0000u) | 0x400000u; /* NaN: quiet, payload truncated */
+  else
+    u = (u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+static float orc_round_f16(float f) {
+  if (isnan(f)) return f;
+  const float a = fabsf(f);
+  float r;
+  if (a < 0x1p-14f) {
+    r = nearbyintf(a * 0x1p24f) * 0x1p-24f; /* subnormal f16: multiples of 2^-24 */
+  } else {
+    uint32_t u;
+    memcpy(&u, &a, 4);
+    u = (u + 0xfffu + ((u >> 13) & 1u)) & ~0x1fffu; /* 11 significant bits */
+    memcpy(&r, &u, 4);
+    if (r > 65504.0f) r = INFINITY;
+  }
+  return copysignf(r, f);
+}
+
+static inline float orc_mul(float v, float b, int round16) {
+  const float p = v * b;
+  if (round16 == ORC_R_BF16) return orc_round_bf16(p);
+  if (round16 == ORC_R_F16) return orc_round_f16(p);
+  return p;
+}
+
+/* exported for the tests: rounding of n fp32 values (in place) as the multiply does */
+void orc_round16(float* x, int64_t n, int round16) {
+  for (int64_t i = 0; i < n; ++i) x[i] = orc_mul(x[i], 1.0f, round16);
+}
+
 /* One segment [j0, j1) of row sums, f32 mul-then-add, from +0 (gather -> mul -> segsum). */
 static void seg_f32(const int64_t* col, const float* val, const float* b, int64_t ldb, int64_t n,
-                    int64_t j0, int64_t j1, float* acc) {
+                    int64_t j0, int64_t j1, float* acc, int round16) {
   for (int64_t c = 0; c < n; ++c) acc[c] = 0.0f;
   for (int64_t j = j0; j < j1; ++j) {
     const float* from = b + col[j] * ldb; /* gather */
     for (int64_t c = 0; c < n; ++c) {
-      const float prod = val[j] * from[c]; /* multiply (rounded; built -ffp-contract=off) */
-      acc[c] = acc[c] + prod;              /* segment-sum */
+      const float prod = orc_mul(val[j], from[c], round16); /* multiply, stored in T */
+      acc[c] = acc[c] + prod;                                /* segment-sum */
     }
   }
 }
@@ -72,7 +120,7 @@ static void seg_f64(const int64_t* col, const double* val, const double* b, int6
 int orc_spmm_f32(int64_t m, int64_t k, int64_t n, const int64_t* rp, const int64_t* col,
                  const float* val, const float* b, int64_t ldb, float* c, int64_t ldc,
                  int64_t row_begin, int64_t row_end, int64_t split, int64_t chunk,
-                 int nthreads) {
+                 int nthreads, int round16) {
   int bad = 0;
   (void)m;
   for (int64_t j = rp[row_begin]; j < rp[row_end]; ++j)
@@ -86,14 +134,14 @@ int orc_spmm_f32(int64_t m, int64_t k, int64_t n, const int64_t* rp, const int64
       float* out = c + (r - row_begin) * ldc;
       const int64_t j0 = rp[r], j1 = rp[r + 1], len = j1 - j0;
       if (len <= split) {
-        seg_f32(col, val, b, ldb, n, j0, j1, out);
+        seg_f32(col, val, b, ldb, n, j0, j1, out, round16);
       } else {
         const int64_t nc = len / chunk;
         for (int64_t x = 0; x < n; ++x) out[x] = 0.0f;
         for (int64_t q = 0; q < nc; ++q) {
           const int64_t a = j0 + q * chunk;
           const int64_t e = (q == nc - 1) ? j1 : a + chunk;
-          seg_f32(col, val, b, ldb, n, a, e, part);
+          seg_f32(col, val, b, ldb, n, a, e, part, round16);
           for (int64_t x = 0; x < n; ++x) out[x] = out[x] + part[x];
         }
       }

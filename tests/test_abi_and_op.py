@@ -97,9 +97,117 @@ def test_op_cpu_global_form_rows():
     for parts in (2, 5):
         chunks = [fs._C.spmm_csr(rp, ci, v, m, k, b, _parallel=(r, parts, 0)) for r in range(parts)]
         assert torch.equal(torch.cat(chunks), full)
-    # column split (S(1)): local b columns -> local out columns
-    left = fs._C.spmm_csr(rp, ci, v, m, k, b[:, :3].contiguous(), _parallel=(0, 2, 1))
-    assert torch.equal(left, full[:, :3])
+    # column split (S(1)): this rank's b columns (BalancedSplitter of the logical N) -> its out
+    # columns; the logical width is passed, as a global tensor knows it
+    for r in range(2):
+        lo, hi = fs._C.balanced_range(n, 2, r)
+        part = fs._C.spmm_csr(rp, ci, v, m, k, b[:, lo:hi].contiguous(), _parallel=(r, 2, 1, n))
+        assert torch.equal(part, full[:, lo:hi])
+    with pytest.raises(fs.OfxError, match="physical b"):  # b slice inconsistent with logical N
+        fs._C.spmm_csr(rp, ci, v, m, k, b[:, :3].contiguous(), _parallel=(0, 2, 1, n))
+
+
+def _hub_problem(n=128, seed=3):
+    """Rows between default_split(N) and default_split(N/4) nonzeros: chunked under the logical
+    width's schedule, not under the physical slice's, so a rank that used its own width would
+    compute other bits."""
+    rng = np.random.default_rng(seed)
+    m, k = 24, 4000
+    deg = rng.integers(0, 40, size=m)
+    deg[[2, 9, 17]] = [fs.ops.default_split(n) + 300, 3 * fs.ops.default_split(n) + 5, 1900]
+    rp, ci, v = random_csr(m, k, deg, rng)
+    return m, k, rp, ci, v, random_dense(k, n, rng)
+
+
+def test_op_column_split_keeps_logical_schedule():
+    """under S(1) every rank runs the hub schedule of the logical N (split =
+    default_split(128) = 512, not default_split(32) = 2048): each slice is bit-identical to the
+    single-device op's columns."""
+    n = 128
+    m, k, rp, ci, v, b = _hub_problem(n)
+    full = fs.spmm(rp, ci, v, m, k, b)
+    assert fs.ops.default_split(n // 4) != fs.ops.default_split(n)
+    for r in range(4):
+        lo, hi = fs._C.balanced_range(n, 4, r)
+        part = fs._C.spmm_csr(rp, ci, v, m, k, b[:, lo:hi].contiguous(), _parallel=(r, 4, 1, n))
+        assert torch.equal(part.view(torch.int32), full[:, lo:hi].contiguous().view(torch.int32))
+    # a rank that planned with its own width differs somewhere (the schedule is visible)
+    own = fs.spmm(rp, ci, v, m, k, b[:, :32].contiguous())
+    assert not torch.equal(own.view(torch.int32), full[:, :32].contiguous().view(torch.int32))
+
+
+@pytest.mark.parametrize("hier", [(2, 2), (2, 4), (4, 2)])
+def test_op_2d_placement_rows_x_columns(hier):
+    """(S(0), S(1)) over a 2-D hierarchy: physical inference gives each rank (M/R) x (N/C) and the
+    kernel cache the row range of GetTensorSliceView4ParallelId (nd_sbp_util.cpp:58-104); the
+    tiles reassemble the single-device result bit for bit."""
+    n = 128
+    m, k, rp, ci, v, b = _hub_problem(n, seed=7)
+    full = fs.spmm(rp, ci, v, m, k, b)
+    R, C = hier
+    got = torch.empty_like(full)
+    for pid in range(R * C):
+        r, c = divmod(pid, C)
+        rlo, rhi = r * m // R, (r + 1) * m // R
+        clo, chi = c * n // C, (c + 1) * n // C
+        tile = fs._C.spmm_csr(rp, ci, v, m, k, b[:, clo:chi].contiguous(),
+                              _placement_nd=dict(hierarchy=hier, nd_sbp=("S(0)", "S(1)"),
+                                                 parallel_id=pid, logical_n=n))
+        assert tile.shape == (rhi - rlo, chi - clo)
+        got[rlo:rhi, clo:chi] = tile
+    assert torch.equal(got.view(torch.int32), full.view(torch.int32))
+    # the transposed placement (S(1), S(0)) splits columns first, rows second
+    pid = R * C - 1
+    c, r = divmod(pid, R)
+    tile = fs._C.spmm_csr(rp, ci, v, m, k, b[:, c * n // C:(c + 1) * n // C].contiguous(),
+                          _placement_nd=dict(hierarchy=(C, R), nd_sbp=("S(1)", "S(0)"),
+                                             parallel_id=pid, logical_n=n))
+    assert torch.equal(tile, full[r * m // R:(r + 1) * m // R, c * n // C:(c + 1) * n // C])
+
+
+def test_op_physical_out_under_row_split_and_refusals():
+    """the physical out under S(0) is the rank's BalancedSplitter slice (an out of
+    the logical shape is refused); rows not divisible by a 2-D hierarchy axis are refused by the
+    slice view's CHECK, as in the reference."""
+    rng = np.random.default_rng(2)
+    m, k, n = 10, 12, 4
+    rp, ci, v = random_csr(m, k, rng.integers(0, 6, size=m), rng)
+    b = random_dense(k, n, rng)
+    with pytest.raises(RuntimeError, match="out must be"):
+        fs._C.spmm_csr(rp, ci, v, m, k, b, out=torch.empty(m, n), _parallel=(1, 3, 0))
+    o = fs._C.spmm_csr(rp, ci, v, m, k, b, out=torch.empty(3, n), _parallel=(2, 3, 0))
+    assert torch.equal(o, fs.spmm(rp, ci, v, m, k, b)[7:])
+    with pytest.raises(fs.OfxError, match="divisible"):
+        fs._C.spmm_csr(rp, ci, v, m, k, b[:, :2].contiguous(),
+                       _placement_nd=dict(hierarchy=(4, 2), nd_sbp=("S(0)", "S(1)"),
+                                          parallel_id=1, logical_n=n))
+
+
+def test_strided_out_and_b_column_stride_refused():
+    """a 2-D out/b whose column stride is not 1 cannot be expressed to the kernel
+    (it takes the row stride only) and is refused instead of written to the wrong elements;
+    row-strided views stay accepted."""
+    rp, ci, v, b = _small()
+    buf = torch.zeros(6, 10)
+    with pytest.raises(RuntimeError, match="unit column stride"):
+        fs.spmm(rp, ci, v, 6, 9, b, out=buf[:, ::2])
+    assert torch.count_nonzero(buf) == 0
+    wide = torch.zeros(6, 8)
+    r = fs.spmm(rp, ci, v, 6, 9, b, out=wide[:, 1:6])
+    assert torch.equal(r, fs.spmm(rp, ci, v, 6, 9, b)) and torch.count_nonzero(wide[:, 6:]) == 0
+    desc_b = fs._C.desc(b.t().contiguous().t())  # column-major b, passed raw to the C-ABI
+    from oneflow_spmm._lib import LIB, TensorDesc
+    import ctypes
+    d = [fs._C.desc(x) for x in (rp, ci, v)]
+    o = torch.empty(6, 5)
+    d_o = fs._C.desc(o)
+    rc = LIB.ofx_functional_spmm_csr(None, *[ctypes.byref(x) for x in d], 6, 9,
+                                     ctypes.byref(desc_b), ctypes.byref(d_o), None, 0)
+    assert rc != 0 and "unit column stride" in fs._lib.last_error()
+    # fused op path: the same refusal
+    with pytest.raises(RuntimeError, match="unit column stride"):
+        fs._C.fused_spmm_csr(rp, ci, v, 6, 9, b, torch.zeros(5), out=buf[:, ::2])
+    assert TensorDesc is not None
 
 
 def test_out_argument_validation():

@@ -111,3 +111,33 @@ def test_oracle_bias_act_matches_fused_fixture(path):
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
     op = _C.fused_spmm_csr(t(rp), t(c), t(v), int(z["m"]), int(z["k"]), t(b), t(bias), relu=True)
     np.testing.assert_array_equal(op.numpy().view(np.uint32), got.view(np.uint32))
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_oracle_16bit_products_rounded_like_torch_mul(dtype):
+    """16-bit dtypes: each product is the tensor-dtype multiply (BinaryFunctor<kMul>,
+    oneflow/core/ep/common/primitive/binary_functor.h:46-51: static_cast<Dst>(src0 * src1)),
+    summed in fp32 in ascending j and rounded once (unsorted_segment_sum_kernel.cpp:146-205).
+    Restated independently with torch's own CPU 16-bit multiply; the unrounded-product variant
+    must differ somewhere, so the test sees the rounding."""
+    import torch
+
+    from tests.helpers import DTYPES, random_csr, random_dense, to_oracle
+    tdt = DTYPES[dtype]
+    rng = np.random.default_rng(5)
+    m, k, n = 40, 30, 9
+    rp, ci, v, b = *random_csr(m, k, rng.integers(0, 25, size=m), rng, val_dtype=tdt), None
+    b = random_dense(k, n, rng, tdt)
+    got = oracle.spmm(to_oracle(rp), to_oracle(ci), to_oracle(v), to_oracle(b), dtype=dtype,
+                      ordered=True, nthreads=1)
+    want = torch.zeros((m, n), dtype=torch.float32)
+    plain = torch.zeros((m, n), dtype=torch.float32)
+    for r in range(m):
+        for j in range(int(rp[r]), int(rp[r + 1])):
+            want[r] = want[r] + (v[j] * b[ci[j]]).float()  # 16-bit multiply, fp32 add
+            plain[r] = plain[r] + v[j].float() * b[ci[j]].float()
+    np.testing.assert_array_equal(got, to_oracle(want.to(tdt)))
+    assert not np.array_equal(got, to_oracle(plain.to(tdt)))
+    x = rng.standard_normal(10000).astype(np.float32) * 3
+    ref = to_oracle(torch.from_numpy(x).to(tdt).float())
+    np.testing.assert_array_equal(oracle.round16(x, dtype).view(np.uint32), ref.view(np.uint32))
