@@ -280,6 +280,8 @@ int ofx_stream_wait_event(void* stream, void* event);
 int ofx_comm_get_unique_id(void* uid_out /* OFX_UNIQUE_ID_BYTES */);
 int ofx_comm_init_rank(void** comm, int nranks, const void* uid, int rank);
 int ofx_comm_destroy(void* comm);
+/* ncclCommCount / ncclCommUserRank of a communicator. */
+int ofx_comm_count(void* comm, int* nranks, int* rank);
 /* out[r*count .. (r+1)*count) = in of rank r; count in elements of dtype. */
 int ofx_allgather(void* stream, const void* in, void* out, size_t count, int dtype, void* comm);
 /* The same all-gather as grouped point-to-point send/recv with every peer (in place: this

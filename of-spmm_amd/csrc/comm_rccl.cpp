@@ -64,6 +64,14 @@ extern "C" int ofx_comm_destroy(void* comm) {
   return OFX_OK;
 }
 
+// Ranks and this rank's index in a communicator (what bench.py reports as the RCCL comm size).
+extern "C" int ofx_comm_count(void* comm, int* nranks, int* rank) {
+  OFX_REQUIRE(comm && nranks && rank, OFX_EINVAL, "comm_count: NULL argument");
+  OFX_NCCL_CHECK(ncclCommCount(static_cast<ncclComm_t>(comm), nranks));
+  OFX_NCCL_CHECK(ncclCommUserRank(static_cast<ncclComm_t>(comm), rank));
+  return OFX_OK;
+}
+
 extern "C" int ofx_allgather(void* stream, const void* in, void* out, size_t count, int dtype,
                              void* comm) {
   ncclDataType_t t;

@@ -110,6 +110,7 @@ def _load():
         "ofx_comm_get_unique_id": ([p], i32),
         "ofx_comm_init_rank": ([ctypes.POINTER(p), i32, p, i32], i32),
         "ofx_comm_destroy": ([p], i32),
+        "ofx_comm_count": ([p, ctypes.POINTER(i32), ctypes.POINTER(i32)], i32),
         "ofx_allgather": ([p, p, p, sz, i32, p], i32),
         "ofx_allgather_p2p": ([p, p, sz, i32, p], i32),
         "ofx_exchange_rows": ([p, p, i32, i64, p, p, p, p, p, p], i32),

@@ -527,6 +527,14 @@ class RowSplitSpmm:
         check(LIB.ofx_comm_init_rank(ctypes.byref(comm), self.world, uid, self.rank), "comm_init_rank")
         self._comm = comm
 
+    def comm_size(self):
+        """(ranks, this rank) of the native RCCL communicator, None without one."""
+        if self._comm is None:
+            return None
+        nr, rk = ctypes.c_int(), ctypes.c_int()
+        check(LIB.ofx_comm_count(self._comm, ctypes.byref(nr), ctypes.byref(rk)), "comm_count")
+        return nr.value, rk.value
+
     def close(self):
         if self._comm is not None:
             check(LIB.ofx_comm_destroy(self._comm), "comm_destroy")

@@ -94,6 +94,35 @@ void orc_round16(float* x, int64_t n, int round16) {
 static void seg_f32(const int64_t* col, const float* val, const float* b, int64_t ldb, int64_t n,
                     int64_t j0, int64_t j1, float* acc, int round16) {
   for (int64_t c = 0; c < n; ++c) acc[c] = 0.0f;
+  if (round16 == ORC_R_NONE) { /* fp32: a branch-free loop the compiler vectorises over c */
+    for (int64_t j = j0; j < j1; ++j) {
+      const float* from = b + col[j] * ldb; /* gather */
+      const float v = val[j];
+      for (int64_t c = 0; c < n; ++c) {
+        const float prod = v * from[c]; /* multiply (rounded; built -ffp-contract=off) */
+        acc[c] = acc[c] + prod;         /* segment-sum */
+      }
+    }
+    return;
+  }
+  if (round16 == ORC_R_BF16) { /* the same rounding as orc_round_bf16, written as a select */
+    for (int64_t j = j0; j < j1; ++j) {
+      const float* from = b + col[j] * ldb;
+      const float v = val[j];
+      for (int64_t c = 0; c < n; ++c) {
+        const float p = v * from[c];
+        uint32_t u;
+        memcpy(&u, &p, 4);
+        const uint32_t rne = (u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u;
+        const uint32_t qnan = (u & 0xffff0000u) | 0x400000u;
+        u = ((u & 0x7fffffffu) > 0x7f800000u) ? qnan : rne;
+        float prod;
+        memcpy(&prod, &u, 4);
+        acc[c] = acc[c] + prod;
+      }
+    }
+    return;
+  }
   for (int64_t j = j0; j < j1; ++j) {
     const float* from = b + col[j] * ldb; /* gather */
     for (int64_t c = 0; c < n; ++c) {

@@ -91,3 +91,42 @@ def power_law_degrees(m, nnz, k, rng, gamma=2.5):
         i += 1
     rng.shuffle(d)
     return d
+
+
+def sub_problem(rp: np.ndarray, cols: np.ndarray, vals: np.ndarray, rows):
+    """The rows `rows` of a CSR as a standalone problem over only the B rows they reference:
+    (sub_row_ptr, sub_cols into `uniq`, sub_vals, uniq).  Row lengths are unchanged, so the
+    operator's hub schedule (a function of the row length and N) is the same as in the full
+    problem, and the oracle on the sub-problem gives those rows' bits."""
+    rows = np.asarray(rows, dtype=np.int64)
+    deg = rp[rows + 1] - rp[rows]
+    sub_rp = np.zeros(len(rows) + 1, dtype=np.int64)
+    sub_rp[1:] = np.cumsum(deg)
+    idx = np.concatenate([np.arange(rp[r], rp[r + 1]) for r in rows]) if len(rows) else \
+        np.zeros(0, dtype=np.int64)
+    uniq, inv = np.unique(cols[idx], return_inverse=True)
+    return sub_rp, inv.astype(np.int64), vals[idx], uniq
+
+
+def check_sampled_rows(rp, cols, vals_t, d_b, out, rows, rtol, what, nthreads=16):
+    """Rows `rows` of a device result `out` (= A @ d_b) against the oracle: bit-exact with the
+    operator's schedule, and both the result and the pure reference order (ascending j, no
+    split) within rtol * |.|-sum of the fp64 product C64.  Only the B rows the
+    sample references leave the device."""
+    dev = d_b.device
+    vals_np = to_oracle(vals_t)
+    sub_rp, sub_c, sub_v, uniq = sub_problem(rp, cols, vals_np, rows)
+    b_sub = to_oracle(d_b.index_select(0, torch.from_numpy(uniq).to(dev)))
+    got = out.index_select(0, torch.from_numpy(np.asarray(rows, dtype=np.int64)).to(dev))
+    dname = dtype_name(d_b.dtype)
+    ref = oracle.spmm(sub_rp, sub_c, sub_v, b_sub, dtype=dname, nthreads=nthreads)
+    assert_bitwise(got, ref, f"{what}: sampled rows vs the oracle's schedule")
+    f32 = (lambda x: oracle.bf16_bits_to_f32(x)) if dname == "bf16" else \
+        (lambda x: np.asarray(x, dtype=np.float32))
+    c64, absum = oracle.ref64(sub_rp, sub_c, f32(sub_v), f32(b_sub), nthreads=nthreads)
+    ok, worst = oracle.within_tolerance(f32(to_oracle(got)), c64, absum, rtol)
+    assert ok, f"{what}: device result vs C64, worst {worst:.3e} > {rtol:.3e}"
+    ordered = oracle.spmm(sub_rp, sub_c, sub_v, b_sub, dtype=dname, ordered=True, nthreads=nthreads)
+    ok, worst = oracle.within_tolerance(f32(ordered), c64, absum, rtol)
+    assert ok, f"{what}: reference order vs C64, worst {worst:.3e} > {rtol:.3e}"
+    return len(uniq)

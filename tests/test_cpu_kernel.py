@@ -9,7 +9,8 @@ import torch
 import oneflow_spmm as fs
 from oneflow_spmm import ops, synth
 from oracle import oracle
-from tests.helpers import DTYPES, assert_bitwise, oracle_spmm, power_law_degrees, random_csr, random_dense
+from tests.helpers import (DTYPES, assert_bitwise, oracle_spmm, power_law_degrees, random_csr,
+                           random_dense, to_oracle)
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -117,3 +118,26 @@ def test_power_law_helper_sums():
     rng = np.random.default_rng(0)
     d = power_law_degrees(1000, 20000, 500, rng)
     assert d.sum() == 20000 and d.max() <= 500
+
+
+@pytest.mark.parametrize("dtype,rtol", [("f32", 1e-5), ("bf16", 2.0 ** -8)])
+def test_sampled_rows_check_on_cpu(dtype, rtol):
+    """The sampled-row checker the full-size GPU tests use (tests/helpers.check_sampled_rows):
+    a sub-problem of the sampled rows over only the B rows they reference gives those rows'
+    bits, with hub rows that split."""
+    from tests.helpers import check_sampled_rows, sub_problem
+    rng = np.random.default_rng(8)
+    m, k, n = 300, 5000, 64
+    deg = rng.integers(0, 40, size=m)
+    deg[[4, 77]] = [4500, ops.default_split(n) + 3]
+    rp, ci, v = random_csr(m, k, deg, rng, torch.int32, DTYPES[dtype])
+    b = random_dense(k, n, rng, DTYPES[dtype])
+    out = fs.spmm(rp, ci, v, m, k, b)
+    rows = np.array([0, 4, 5, 77, 299])
+    sub_rp, sub_c, _, uniq = sub_problem(rp.numpy().astype(np.int64), ci.numpy(), to_oracle(v), rows)
+    assert sub_rp[-1] == sum(deg[r] for r in rows) and np.all(uniq[sub_c] >= 0)
+    check_sampled_rows(rp.numpy().astype(np.int64), ci.numpy(), v, b, out, rows, rtol, dtype, 4)
+    bad = out.clone()
+    bad[77, 3] += 1
+    with pytest.raises(AssertionError):
+        check_sampled_rows(rp.numpy().astype(np.int64), ci.numpy(), v, b, bad, rows, rtol, dtype, 4)

@@ -1,0 +1,82 @@
+"""The single-node launcher (oneflow_spmm/launch.py, the environment contract of the reference's
+python/oneflow/distributed/launch.py:103-140) and bench.py's use of it: `--gpus N` without a
+launcher spawns N ranks, and a rank count that differs from --gpus is an error.  CPU only
+(gloo)."""
+import os
+import subprocess
+import sys
+import textwrap
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "of-spmm_amd"))
+
+from oneflow_spmm import launch  # noqa: E402
+
+RANK_SCRIPT = textwrap.dedent("""
+    import os, sys
+    import torch, torch.distributed as dist
+    dist.init_process_group("gloo")   # env:// rendezvous from the launcher's variables
+    r, w = dist.get_rank(), dist.get_world_size()
+    assert r == int(os.environ["RANK"]) == int(os.environ["LOCAL_RANK"])
+    t = torch.tensor([r + 1])
+    dist.all_reduce(t)
+    with open(os.path.join(sys.argv[1], f"rank{r}"), "w") as f:
+        f.write(f"{w} {int(t)} {sys.argv[2]}")
+    dist.destroy_process_group()
+""")
+
+
+def test_spawn_runs_every_rank_with_the_env_contract(tmp_path):
+    script = tmp_path / "rank.py"
+    script.write_text(RANK_SCRIPT)
+    rc = launch.spawn_local_ranks(3, [str(script), str(tmp_path), "arg"], timeout=120)
+    assert rc == 0
+    for r in range(3):
+        assert (tmp_path / f"rank{r}").read_text() == "3 6 arg"  # world 3, sum of 1+2+3
+
+
+def test_spawn_reports_the_failing_rank_and_stops_the_rest(tmp_path):
+    script = tmp_path / "fail.py"
+    script.write_text(textwrap.dedent("""
+        import os, sys, time
+        if os.environ["RANK"] == "1":
+            sys.exit(3)
+        time.sleep(120)
+    """))
+    import time
+    t0 = time.monotonic()
+    rc = launch.spawn_local_ranks(2, [str(script)], timeout=200)
+    assert rc == 3
+    assert time.monotonic() - t0 < 60  # rank 0 was terminated, not waited for
+
+
+def test_rank_env():
+    env = launch.rank_env({"X": "1"}, 4, 2, "127.0.0.1", 1234)
+    assert env["X"] == "1" and env["WORLD_SIZE"] == "4" and env["RANK"] == "2"
+    assert env["LOCAL_RANK"] == "2" and env["MASTER_ADDR"] == "127.0.0.1"
+    assert env["MASTER_PORT"] == "1234"
+
+
+def _bench(args, env_extra, drop=()):
+    env = {k: v for k, v in os.environ.items() if k not in drop}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env,
+                          capture_output=True, text=True, timeout=300)
+
+
+def test_bench_refuses_a_rank_count_other_than_gpus():
+    p = _bench(["--gpus", "2"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode == 2, p.stderr[-2000:]
+    assert "WORLD_SIZE=1" in p.stderr
+    assert p.stdout == ""  # no JSON line for a run that did not happen
+
+
+def test_bench_spawns_its_ranks_without_a_launcher():
+    """No WORLD_SIZE: the parent starts --gpus ranks (before any GPU call) and exits with their
+    status; on this CPU-only container every rank then fails at the GPU, so the status is
+    non-zero and comes from the ranks, not from a silent one-rank run."""
+    p = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0"], {},
+               drop=("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"))
+    assert "spawning 2 local ranks" in p.stderr
+    assert p.returncode != 0
+    assert '"n_gpus": 1' not in p.stdout
