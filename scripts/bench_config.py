@@ -45,6 +45,8 @@ def run():
     ap.add_argument("--config", default="papers")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--n", type=int, default=0, help="override the dense width")
+    ap.add_argument("--no-check", action="store_true", help="skip the sampled oracle check")
     args = ap.parse_args()
     import oneflow_spmm as fs
     from oneflow_spmm import synth
@@ -53,6 +55,7 @@ def run():
 
     cfg = {**synth.CONFIGS, **synth.EXTRA_CONFIGS}[args.config]
     m, k, nnz, n, dt = cfg["m"], cfg["k"], cfg["nnz"], cfg["n"], cfg["dtype"]
+    n = args.n or n
     dev = torch.device("cuda", 0)
     t0 = time.time()
     rp_full = synth.row_ptr(m, k, nnz)
@@ -79,8 +82,13 @@ def run():
         ts.append(e0.elapsed_time(e1))
     ms = float(np.median(ts))
     log(f"median {ms:.3f} ms; checking sampled rows against the oracle")
+    if args.no_check:
+        print(json.dumps({"config": args.config, "n": n, "ms": round(ms, 3),
+                          "gather_model_gbs": round(alg_bytes(m, nnz, n, d_b.element_size(), 8 if wide else 4) /
+                                                    (ms * 1e-3) / 1e9, 1)}), flush=True)
+        return
     sv = d_b.element_size()
-    nbytes = alg_bytes(m, nnz, n, sv)
+    nbytes = alg_bytes(m, nnz, n, sv, 8 if wide else 4)
     # sampled check (bit-exact vs oracle with the operator's schedule)
     deg = np.diff(rp_full)
     heavy = np.argsort(deg)[-20:]

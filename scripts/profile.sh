@@ -6,13 +6,14 @@
 set -u
 TAG=${1:-r01}; shift || true
 ARGS=${@:---steps 10 --warmup 3 --no-cpu-baseline}
+PROG=${PROG:-bench.py}  # or e.g. PROG=scripts/bench_config.py for the non-bench configurations
 export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
 run() {  # name, rocprofv3 options...
   local name=$1; shift
-  timeout -k 10 300 rocprofv3 "$@" --output-format csv -d $OUT/$name -o run -- python3 bench.py $ARGS \
+  timeout -k 10 300 rocprofv3 "$@" --output-format csv -d $OUT/$name -o run -- python3 $PROG $ARGS \
     > $OUT/${name}_bench.json 2> $OUT/${name}.err
 }
 run trace --kernel-trace --stats || exit $?
