@@ -432,6 +432,69 @@ int ofx_op_spmm_csr_sbp_signatures(char* buf, size_t len);
 /* Same for any registered op; optional_inputs = comma-separated optional inputs present.   */
 int ofx_op_sbp_signatures(const char* op_name, const char* optional_inputs, char* buf, size_t len);
 
+/* ---- collectives of the OneFlow mirror and the lazy path ------------------------------------
+ * The control plane a host passes in (OneFlow's CtrlClient KV store and ring transport, which
+ * this library does not reimplement): push/pull of the RCCL unique id under a key
+ * (EagerNcclCommMgr, oneflow/core/job/eager_nccl_comm_manager.cpp:57-131) and one ring step of
+ * the kCPU all-gather (collective_communication/cpu/cpu_all_gather.cpp:27-80).  Callbacks return
+ * 0 on success; pull blocks until the key exists and stores the value's length in *len.        */
+typedef int (*ofx_kv_push_fn)(void* user, const char* key, const void* val, size_t len);
+typedef int (*ofx_kv_pull_fn)(void* user, const char* key, void* val, size_t cap, size_t* len);
+typedef int (*ofx_sendrecv_fn)(void* user, const void* send, size_t send_bytes, int64_t to,
+                               void* recv, size_t recv_bytes, int64_t from);
+int ofx_process_ctx_init(int64_t rank, int64_t world, ofx_kv_push_fn push, ofx_kv_pull_fn pull,
+                         ofx_sendrecv_fn sendrecv, void* user);
+
+/* A placement (oneflow/core/job/parallel_desc.h): device type (OFX_DEV_*), parallel_num devices,
+ * this process's parallel_id, and per parallel id its machine (= process rank) and local device
+ * (NULL arrays: parallel id p is machine p, device p).                                          */
+#define OFX_DEV_CPU 1
+#define OFX_DEV_HIP 4
+typedef struct ofx_placement {
+  int32_t device_type;
+  int32_t reserved;
+  int64_t parallel_num;
+  int64_t parallel_id;
+  const int64_t* machine_ids;
+  const int64_t* device_ids;
+} ofx_placement;
+/* Whether ccl::AllGather and a ccl::CommunicationContext are registered for a device type
+ * (REGISTER_COLLECTIVE_COMMUNICATION, collective_communication/include/all_gather.h:24-38). */
+int ofx_ccl_registered(int device_type, int* all_gather, int* communication_context);
+/* Eager boxing "ccl-s-to-b" (oneflow/core/boxing/ccl_boxing_function.cpp:104-122,185-215): the
+ * check alone (OFX_OK or OFX_EINVAL with the failed condition; e.g. logical dim 0 % ranks != 0),
+ * and the boxing of this rank's S(0) slice `in` into the full B tensor `out` through op
+ * eager_ccl_all_gather and its registered kernel (RCCL on kHIP, host ring on kCPU).           */
+int ofx_boxing_check_ccl_s2b(const ofx_placement* pl, int ndim, const int64_t* logical_shape,
+                             const char* in_sbp, const char* out_sbp);
+int ofx_boxing_ccl_s2b(void* stream, const ofx_placement* pl, const ofx_tensor_desc* in,
+                       ofx_tensor_desc* out, int64_t logical_dim0);
+/* Op "_nccl_logical_all_gather" (the lazy compiler's S(0) -> B) through its kHIP kernel
+ * (reference kernel: oneflow/user/kernels/nccl_logical_kernels.cpp:175-205, kCUDA only).      */
+int ofx_nccl_logical_all_gather(void* stream, const ofx_placement* pl, const ofx_tensor_desc* in,
+                                ofx_tensor_desc* out, const char* stream_name);
+/* InsertNcclLogicalOpPass's choice for one edge of a 1-D placement
+ * (insert_nccl_logical_op_pass.cpp:150-240): the op type, or "" when none applies.            */
+int ofx_insert_nccl_logical_op(const char* src_sbp, const char* dst_sbp, int ndim,
+                               const int64_t* logical_shape, int64_t parallel_num, char* op_type,
+                               size_t len);
+/* The key EagerRcclCommMgr publishes a placement's unique id under, and the RCCL rank of
+ * (machine, device) in it (-1 if absent).                                                      */
+int ofx_rccl_comm_key(const ofx_placement* pl, const char* stream_name, int64_t machine,
+                      int64_t device, char* key, size_t len, int* rank);
+/* A compiled row-split spmm_csr job (the nn.Graph form of the layer): b (S(0), this rank's K/P
+ * rows) -> _nccl_logical_all_gather -> b (B) -> spmm_csr (a_csr_*: B) -> out (S(0), this rank's
+ * BalancedSplitter rows).  Create compiles once (every rank of the placement must call it: the
+ * logical collective's RCCL communicator is created collectively on the first run); run is
+ * stream-ordered launches only (hipGraph-capturable) with a caller tmp of the described size. */
+int ofx_spmm_job_create(const ofx_placement* pl, int idx_dtype, int val_dtype, int64_t m, int64_t k,
+                        int64_t n, int64_t nnz, const char* stream_name, void** job);
+int ofx_spmm_job_describe(void* job, char* buf, size_t len, size_t* tmp_bytes);
+int ofx_spmm_job_run(void* job, void* stream, const void* row_ptr, const void* col_idx,
+                     const void* values, const void* b_shard, void* out, void* tmp,
+                     size_t tmp_bytes);
+int ofx_spmm_job_destroy(void* job);
+
 #ifdef __cplusplus
 }
 #endif

@@ -162,7 +162,7 @@ Maybe<void> UserOpRegistryMgr::GetOpKernelRegistryResult(const std::string& op,
   if (matched == 0)
     return Maybe<void>("OpKernelNotFoundError",
                        "cannot find the kernel matching the current context: op " + op +
-                           " on device " + DeviceTypeName(ctx.device_type) +
+                           " on device " + DeviceTypeName(ctx.device_type()) +
                            " with dtype " + DataType_Name(ctx.dtype("out", 0)) +
                            "; registered kernels:" + tried);
   if (matched > 1)

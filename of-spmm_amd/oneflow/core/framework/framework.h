@@ -21,6 +21,7 @@
 #include <memory>
 #include <sstream>
 #include <string>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -207,17 +208,38 @@ class ParallelContext {
   int64_t id_, num_;
 };
 
-// Placement hierarchy (oneflow/core/job/parallel_desc.h: ParallelDesc::hierarchy()).  A 1-D
-// placement of G devices is {G}; a 2-D one (e.g. nodes x devices) is {R, C}.
+// Placement (oneflow/core/job/parallel_desc.h): device type, hierarchy and, per parallel id, the
+// (machine, device) it runs on (MachineId4ParallelId / DeviceId4ParallelId).  A 1-D placement of
+// G devices is {G}; a 2-D one (e.g. nodes x devices) is {R, C}.  "Machine" is the process rank,
+// as in OneFlow's multi-client mode; without explicit ids parallel id p is (p, p).
 class ParallelDesc {
  public:
   explicit ParallelDesc(Shape hierarchy = Shape({1}))
       : hierarchy_(std::make_shared<const Shape>(std::move(hierarchy))) {}
+  ParallelDesc(DeviceType device_type, std::vector<std::pair<int64_t, int64_t>> machine_device,
+               Shape hierarchy = Shape())
+      : hierarchy_(std::make_shared<const Shape>(
+            hierarchy.NumAxes() ? std::move(hierarchy) : Shape({(int64_t)machine_device.size()}))),
+        device_type_(device_type),
+        machine_device_(std::move(machine_device)) {}
   std::shared_ptr<const Shape> hierarchy() const { return hierarchy_; }
   int64_t parallel_num() const { return hierarchy_->elem_cnt(); }
+  DeviceType device_type() const { return device_type_; }
+  int64_t MachineId4ParallelId(int64_t parallel_id) const {
+    return machine_device_.empty() ? parallel_id : machine_device_.at(parallel_id).first;
+  }
+  int64_t DeviceId4ParallelId(int64_t parallel_id) const {
+    return machine_device_.empty() ? parallel_id : machine_device_.at(parallel_id).second;
+  }
+  bool operator==(const ParallelDesc& o) const {
+    return *hierarchy_ == *o.hierarchy_ && device_type_ == o.device_type_ &&
+           machine_device_ == o.machine_device_;
+  }
 
  private:
   std::shared_ptr<const Shape> hierarchy_;
+  DeviceType device_type_ = DeviceType::kInvalidDevice;
+  std::vector<std::pair<int64_t, int64_t>> machine_device_;
 };
 
 // NdSbp: one SbpParallel per hierarchy axis ("S(axis)", "B" or "P"; sbp_parallel.proto).
@@ -392,6 +414,34 @@ class InferContext {
   NdSbp broadcast_{"B"};
 };
 
+// oneflow/core/framework/infer_nd_sbp_fn_context.h: an op's NdSbp inference (the eager S(0)->B
+// boxing ops and the logical collectives fix their in/out NdSbp here).  String-list attributes
+// (e.g. "src_reduced_nd_sbp") live next to the integer ones.
+class InferNdSbpFnContext {
+ public:
+  InferNdSbpFnContext(Shape hierarchy, std::map<std::string, NdSbp> hints,
+                      std::map<std::string, std::vector<std::string>> str_attrs = {})
+      : hierarchy_(std::move(hierarchy)), hints_(std::move(hints)), str_attrs_(std::move(str_attrs)) {}
+  const Shape& parallel_hierarchy() const { return hierarchy_; }
+  const NdSbp& NdSbpHint4InputArgNameAndIndex(const std::string& n, int32_t) const {
+    auto it = hints_.find(n);
+    return it == hints_.end() ? empty_ : it->second;
+  }
+  NdSbp* NdSbp4ArgNameAndIndex(const std::string& n, int32_t) { return &nd_sbp_[n]; }
+  const NdSbp& NdSbp4ArgName(const std::string& n) const { return nd_sbp_.at(n); }
+  template <typename T>
+  T Attr(const std::string& n) const {
+    static_assert(std::is_same<T, std::vector<std::string>>::value, "string-list attrs only");
+    return str_attrs_.at(n);
+  }
+
+ private:
+  Shape hierarchy_;
+  std::map<std::string, NdSbp> hints_, nd_sbp_;
+  std::map<std::string, std::vector<std::string>> str_attrs_;
+  NdSbp empty_;
+};
+
 // One SBP signature: per argument "S(axis)", "B" or "P".
 using SbpSignature = std::vector<std::pair<std::string, std::string>>;
 
@@ -503,17 +553,42 @@ class KernelComputeContext {
   T Attr(const std::string& n) const {
     return static_cast<T>(attrs_.at(n));
   }
+  const ParallelContext& parallel_ctx() const { return pc_; }
+  void set_parallel_ctx(ParallelContext pc) { pc_ = pc; }
 
  private:
+  ParallelContext pc_;
   ep::Stream* s_;
   std::map<std::pair<std::string, int32_t>, Tensor*> t_;
   AttrMap attrs_;
   DeviceType dev_;
 };
 
+// oneflow/core/framework/op_kernel.h:62-88 (KernelInitContext): what CreateOpKernelState sees.
+class KernelInitContext {
+ public:
+  KernelInitContext(ParallelContext pc, ParallelDesc pd, DeviceType dev,
+                    std::string stream_name_hint = "")
+      : pc_(pc), pd_(std::move(pd)), dev_(dev), stream_name_hint_(std::move(stream_name_hint)) {}
+  const ParallelContext& parallel_ctx() const { return pc_; }
+  const ParallelDesc& parallel_desc() const { return pd_; }
+  DeviceType device_type() const { return dev_; }
+  bool has_stream_name_hint() const { return !stream_name_hint_.empty(); }
+  const std::string& stream_name_hint() const { return stream_name_hint_; }
+
+ private:
+  ParallelContext pc_;
+  ParallelDesc pd_;
+  DeviceType dev_;
+  std::string stream_name_hint_;
+};
+
 class OpKernel {
  public:
   virtual ~OpKernel() = default;
+  virtual std::shared_ptr<OpKernelState> CreateOpKernelState(KernelInitContext*) const {
+    return nullptr;
+  }
   virtual std::shared_ptr<OpKernelCache> InitOpKernelCache(KernelCacheContext*) const {
     return nullptr;
   }
@@ -527,8 +602,9 @@ class CudaGraphSupport {};  // marker, as user_op::CudaGraphSupport (captures fi
 
 // ---- kernel registry + HOB predicates ----------------------------------------------------------
 struct KernelRegContext {
-  DeviceType device_type;
+  DeviceType device_type_ = DeviceType::kInvalidDevice;
   std::map<std::pair<std::string, int32_t>, DataType> dtypes;
+  DeviceType device_type() const { return device_type_; }
   DataType dtype(const std::string& n, int32_t i) const {
     auto it = dtypes.find({n, i});
     return it == dtypes.end() ? kInvalidDataType : it->second;
@@ -544,7 +620,7 @@ inline Hob operator&&(const Hob& a, const Hob& b) {
 }
 struct HobDeviceTypeProxy {
   Hob operator==(DeviceType t) const {
-    return Hob{[t](const KernelRegContext& c) { return c.device_type == t; },
+    return Hob{[t](const KernelRegContext& c) { return c.device_type() == t; },
                std::string("device_type == ") + DeviceTypeName(t)};
   }
 };
@@ -560,6 +636,10 @@ struct HobDataTypeProxy {
   }
 };
 inline HobDataTypeProxy HobDataType(const std::string& n, int32_t i) { return {n, i}; }
+// hob::make_custom (oneflow/core/framework/user_op_hob.h): a named predicate on the context.
+inline Hob make_custom(const std::string& name, std::function<bool(const KernelRegContext&)> f) {
+  return Hob{std::move(f), name};
+}
 
 struct InferSizeContext {
   std::map<std::pair<std::string, int32_t>, TensorDesc> descs;
@@ -613,6 +693,7 @@ struct OpRegistryResult {
   std::function<Maybe<void>(InferContext*)> logical_infer, physical_infer, dtype_infer;
   std::function<Maybe<void>(SbpContext*)> get_sbp;
   std::function<Maybe<void>(const GetInputArgModifier&, const UserOpConfWrapper&)> input_modify;
+  std::function<Maybe<void>(InferNdSbpFnContext*)> nd_sbp_infer;
 };
 class OpRegistry {
  public:
@@ -644,6 +725,10 @@ class OpRegistry {
   }
   OpRegistry& SetDataTypeInferFn(std::function<Maybe<void>(InferContext*)> f) {
     r_.dtype_infer = std::move(f);
+    return *this;
+  }
+  OpRegistry& SetNdSbpInferFn(std::function<Maybe<void>(InferNdSbpFnContext*)> f) {
+    r_.nd_sbp_infer = std::move(f);
     return *this;
   }
   OpRegistry& SetGetSbpFn(std::function<Maybe<void>(SbpContext*)> f) {

@@ -76,4 +76,21 @@ REGISTER_USER_OP("csr_transpose")
     .SetGetSbpFn(CsrTransposeOp::GetSbp)
     .SetDataTypeInferFn(CsrTransposeOp::InferDataType);
 
+REGISTER_USER_OP("eager_ccl_all_gather")
+    .Input("in")
+    .Output("out")
+    .SetLogicalTensorDescInferFn(EagerCclAllGatherOp::InferLogicalTensorDesc)
+    .SetPhysicalTensorDescInferFn(EagerCclAllGatherOp::InferPhysicalTensorDesc)
+    .SetGetSbpFn(EagerCclAllGatherOp::GetSbp)
+    .SetNdSbpInferFn(EagerCclAllGatherOp::InferNdSbp)
+    .SetDataTypeInferFn(EagerCclAllGatherOp::InferDataType);
+
+REGISTER_USER_OP("_nccl_logical_all_gather")
+    .Input("in")
+    .Output("out")
+    .SetLogicalTensorDescInferFn(_ncclLogicalAllGatherOp::InferLogicalTensorDesc)
+    .SetGetSbpFn(_ncclLogicalAllGatherOp::GetSbp)
+    .SetNdSbpInferFn(_ncclLogicalAllGatherOp::InferNdSbp)
+    .SetDataTypeInferFn(_ncclLogicalAllGatherOp::InferDataType);
+
 }  // namespace oneflow

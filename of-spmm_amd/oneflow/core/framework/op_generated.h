@@ -56,6 +56,26 @@ class CsrTransposeOp {
   static Maybe<void> InferDataType(user_op::InferContext* ctx);
 };
 
+// The S(0) -> B collectives the row-split op's B operand goes through: eager boxing
+// (oneflow/user/ops/eager_nccl_ops.cpp:188-233) and the lazy graph's logical collective
+// (oneflow/user/ops/nccl_logical_ops.cpp:104-142, ODS OneFlowUserOps.td:5341-5357).
+class EagerCclAllGatherOp {
+ public:
+  static Maybe<void> InferLogicalTensorDesc(user_op::InferContext* ctx);
+  static Maybe<void> InferPhysicalTensorDesc(user_op::InferContext* ctx);
+  static Maybe<void> GetSbp(user_op::SbpContext* ctx);
+  static Maybe<void> InferNdSbp(user_op::InferNdSbpFnContext* ctx);
+  static Maybe<void> InferDataType(user_op::InferContext* ctx);
+};
+
+class _ncclLogicalAllGatherOp {
+ public:
+  static Maybe<void> InferLogicalTensorDesc(user_op::InferContext* ctx);
+  static Maybe<void> GetSbp(user_op::SbpContext* ctx);
+  static Maybe<void> InferNdSbp(user_op::InferNdSbpFnContext* ctx);
+  static Maybe<void> InferDataType(user_op::InferContext* ctx);
+};
+
 }  // namespace oneflow
 
 #endif  // OFX_ONEFLOW_SHIM_OP_GENERATED_H_

@@ -146,7 +146,7 @@ const user_op::OpKernel* GetKernel(const user_op::OpKernelRegistryResult* reg) {
 Maybe<void> Choose(const ofx_tensor_desc* row_ptr, const ofx_tensor_desc* b, int device,
                    const user_op::OpKernelRegistryResult** reg) {
   user_op::KernelRegContext rc;
-  rc.device_type = device < 0 ? DeviceType::kCPU : DeviceType::kHIP;
+  rc.device_type_ = device < 0 ? DeviceType::kCPU : DeviceType::kHIP;
   rc.dtypes[{"out", 0}] = (DataType)b->dtype;
   rc.dtypes[{"a_csr_row_ptr", 0}] = (DataType)row_ptr->dtype;
   return user_op::UserOpRegistryMgr::Get().GetOpKernelRegistryResult("spmm_csr", rc, reg);
@@ -372,7 +372,7 @@ Maybe<void> RunUserOp(const std::string& op_name, const std::vector<Arg>& ins,
   JUST(op->logical_infer(&ictx));
   JUST(op->dtype_infer(&ictx));
   user_op::KernelRegContext rc;
-  rc.device_type = device < 0 ? DeviceType::kCPU : DeviceType::kHIP;
+  rc.device_type_ = device < 0 ? DeviceType::kCPU : DeviceType::kHIP;
   for (const Arg& a : ins) rc.dtypes[{a.name, 0}] = (DataType)a.d->dtype;
   for (const std::string& o : op->outputs) rc.dtypes[{o, 0}] = ictx.OutputTensorDesc(o, 0).data_type();
   const user_op::OpKernelRegistryResult* reg = nullptr;
@@ -407,7 +407,7 @@ Maybe<void> RunUserOp(const std::string& op_name, const std::vector<Arg>& ins,
   ep::CpuStream cpu_stream(0);
   ep::HipStream hip_stream(stream, device);
   ep::Stream* s = device < 0 ? static_cast<ep::Stream*>(&cpu_stream) : static_cast<ep::Stream*>(&hip_stream);
-  user_op::KernelComputeContext ctx(s, tensors, attrs, rc.device_type);
+  user_op::KernelComputeContext ctx(s, tensors, attrs, rc.device_type());
   const user_op::OpKernel* kernel = GetKernel(reg);
   try {
     kernel->Compute(&ctx, nullptr, nullptr);

@@ -35,6 +35,23 @@ class Options(ctypes.Structure):
                 ("reserved", ctypes.c_int32)]
 
 
+class Placement(ctypes.Structure):
+    _fields_ = [("device_type", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("parallel_num", ctypes.c_int64), ("parallel_id", ctypes.c_int64),
+                ("machine_ids", ctypes.POINTER(ctypes.c_int64)),
+                ("device_ids", ctypes.POINTER(ctypes.c_int64))]
+
+
+# control-plane callbacks of ofx_process_ctx_init (include/ofx_spmm.h)
+KV_PUSH_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p,
+                              ctypes.c_size_t)
+KV_PULL_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p,
+                              ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t))
+SENDRECV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                               ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int64)
+DEV_CPU, DEV_HIP = 1, 4
+
+
 class TensorDesc(ctypes.Structure):
     _fields_ = [("dtype", ctypes.c_int32), ("device", ctypes.c_int32), ("ndim", ctypes.c_int32),
                 ("reserved", ctypes.c_int32), ("shape", ctypes.c_int64 * 2),
@@ -51,6 +68,7 @@ def _load():
     i32, i64, u64, p, sz = ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t
     popt = ctypes.POINTER(Options)
     pdesc = ctypes.POINTER(TensorDesc)
+    ppl = ctypes.POINTER(Placement)
     sigs = {
         "ofx_last_error": ([], ctypes.c_char_p),
         "ofx_version": ([], ctypes.c_char_p),
@@ -138,6 +156,20 @@ def _load():
         "ofx_functional_csr_transpose": ([p, pdesc, pdesc, i64, i64, pdesc, pdesc, pdesc, p, sz,
                                           ctypes.POINTER(sz)], i32),
         "ofx_op_spmm_csr_sbp_signatures": ([ctypes.c_char_p, sz], i32),
+        "ofx_process_ctx_init": ([i64, i64, KV_PUSH_FN, KV_PULL_FN, SENDRECV_FN, p], i32),
+        "ofx_ccl_registered": ([i32, ctypes.POINTER(i32), ctypes.POINTER(i32)], i32),
+        "ofx_boxing_check_ccl_s2b": ([ppl, i32, ctypes.POINTER(i64), ctypes.c_char_p,
+                                      ctypes.c_char_p], i32),
+        "ofx_boxing_ccl_s2b": ([p, ppl, pdesc, pdesc, i64], i32),
+        "ofx_nccl_logical_all_gather": ([p, ppl, pdesc, pdesc, ctypes.c_char_p], i32),
+        "ofx_insert_nccl_logical_op": ([ctypes.c_char_p, ctypes.c_char_p, i32, ctypes.POINTER(i64),
+                                        i64, p, sz], i32),
+        "ofx_rccl_comm_key": ([ppl, ctypes.c_char_p, i64, i64, p, sz, ctypes.POINTER(i32)], i32),
+        "ofx_spmm_job_create": ([ppl, i32, i32, i64, i64, i64, i64, ctypes.c_char_p,
+                                 ctypes.POINTER(p)], i32),
+        "ofx_spmm_job_describe": ([p, p, sz, ctypes.POINTER(sz)], i32),
+        "ofx_spmm_job_run": ([p, p, p, p, p, p, p, p, sz], i32),
+        "ofx_spmm_job_destroy": ([p], i32),
         "ofx_op_sbp_signatures": ([ctypes.c_char_p, ctypes.c_char_p, p, sz], i32),
     }
     for name, (args, res) in sigs.items():
