@@ -197,7 +197,8 @@ int ofx_gather_values_host(int idx_dtype, int val_dtype, int64_t nnz, const void
 /* out[j] = sum_n a[r - row_begin, n] * b[col_idx[j], n] for the nonzeros j of rows
  * r in [row_begin, row_end).  Order: products rounded, 8-element leaves summed sequentially from
  * +0, leaves (zero-padded to a power of two) added pairwise; fp32 accumulation for 16-bit types.
- * n <= 2048.  Asynchronous, workspace from ofx_sddmm_csr_workspace_size.                    */
+ * n <= 131072 (beyond 2048 the leaves are processed in 256-leaf tiles whose pairwise trees are
+ * added pairwise: the same order).  Asynchronous, workspace from ofx_sddmm_csr_workspace_size. */
 int ofx_sddmm_csr_workspace_size(int idx_dtype, int val_dtype, int64_t m, int64_t n, int64_t nnz,
                                  size_t* bytes);
 int ofx_sddmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k, int64_t n,

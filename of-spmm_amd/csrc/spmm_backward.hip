@@ -166,6 +166,42 @@ __device__ __forceinline__ void load_leaf(const T* __restrict__ p, int64_t base,
   }
 }
 
+// Work item of lane-group g: (local row, nonzero range) of a row or hub chunk; false if none.
+template <typename I>
+__device__ __forceinline__ bool sddmm_item(const I* __restrict__ rp, int64_t g, int64_t row_begin,
+                                           int64_t nrows, int64_t chunk,
+                                           const unsigned long long* __restrict__ counters,
+                                           const int64_t* __restrict__ items,
+                                           const int64_t* __restrict__ order, int64_t* lr_out,
+                                           int64_t* j0_out, int64_t* j1_out) {
+  int64_t lr, c = -1;
+  if (order == nullptr) {
+    if (g >= nrows) return false;
+    lr = g;
+  } else {
+    const int64_t nchunks = (int64_t)counters[0];
+    if (g < nchunks) {
+      lr = items[2 * g];
+      c = items[2 * g + 1];
+    } else {
+      const int64_t q = g - nchunks;
+      if (q >= nrows - (int64_t)counters[1]) return false;
+      lr = order[q];
+    }
+  }
+  const int64_t r = row_begin + lr;
+  const int64_t rs = (int64_t)rp[r], re = (int64_t)rp[r + 1];
+  int64_t j0 = rs, j1 = re;
+  if (c >= 0) {  // chunk c of len / chunk; the last takes the remainder
+    j0 = rs + c * chunk;
+    j1 = (re - j0 - chunk < chunk) ? re : j0 + chunk;
+  }
+  *lr_out = lr;
+  *j0_out = j0;
+  *j1_out = j1;
+  return j0 < j1;
+}
+
 template <typename T, typename I, int LG, int L, int U, bool ALIGNED>
 __global__ void __launch_bounds__(kBlock)
     sddmm_kernel(const I* __restrict__ rp, const I* __restrict__ col, const T* __restrict__ dC,
@@ -180,30 +216,8 @@ __global__ void __launch_bounds__(kBlock)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int gl = lane & (LG - 1);
   const int64_t g = ((int64_t)blockIdx.x * (kBlock / 64) + wave) * GPW + lane / LG;
-  int64_t lr, c = -1;
-  if (order == nullptr) {
-    if (g >= nrows) return;
-    lr = g;
-  } else {
-    const int64_t nchunks = (int64_t)counters[0];
-    if (g < nchunks) {
-      lr = items[2 * g];
-      c = items[2 * g + 1];
-    } else {
-      const int64_t q = g - nchunks;
-      if (q >= nrows - (int64_t)counters[1]) return;
-      lr = order[q];
-    }
-  }
-  const int64_t r = row_begin + lr;
-  const int64_t rs = (int64_t)rp[r], re = (int64_t)rp[r + 1];
-  int64_t j0 = rs, j1 = re;
-  if (c >= 0) {
-    const int64_t nc = num_chunks(re - rs, chunk);
-    j0 = rs + c * chunk;
-    j1 = (c == nc - 1) ? re : j0 + chunk;
-  }
-  if (j0 >= j1) return;
+  int64_t lr, j0, j1;
+  if (!sddmm_item<I>(rp, g, row_begin, nrows, chunk, counters, items, order, &lr, &j0, &j1)) return;
   // dC row, this lane's leaves
   A a[L][kLeaf];
   const T* arow = dC + lr * ldc;
@@ -251,6 +265,98 @@ __global__ void __launch_bounds__(kBlock)
       }
     }
     if (gl < cnt) out[jb + gl] = Num<T>::store(res);
+  }
+}
+
+// n > 2048: the padded leaves are cut into tiles of kWideLeaves (one wave, 4 leaves per lane);
+// each tile's value is its 256-leaf pairwise tree (the butterfly of the narrow kernel) and the
+// tile values are added pairwise in tile order through a binary-counter stack.  The pairwise tree
+// over all padded leaves is exactly the tree over its 256-leaf subtrees, so the contract's order
+// (8-element leaves, zero-padded to a power of two, pairwise) is unchanged.  One wave per row or
+// hub chunk; the dC tile is reloaded per batch of 64 nonzeros (only for these wide rows).
+constexpr int kWideLeaves = 256;
+constexpr int kMaxTilesLog = 6;  // n <= 2048 * 64 = 131072
+
+template <typename T, typename I, bool ALIGNED>
+__global__ void __launch_bounds__(kBlock)
+    sddmm_wide_kernel(const I* __restrict__ rp, const I* __restrict__ col, const T* __restrict__ dC,
+                      int64_t ldc, const T* __restrict__ B, int64_t ldb, T* __restrict__ out,
+                      int64_t row_begin, int64_t nrows, int64_t n, int64_t chunk, int tiles,
+                      const unsigned long long* __restrict__ counters,
+                      const int64_t* __restrict__ items, const int64_t* __restrict__ order) {
+#pragma clang fp contract(off)
+  using A = typename Num<T>::acc;
+  constexpr int L = kWideLeaves / 64, U = 2;
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int64_t lr, j0, j1;
+  if (!sddmm_item<I>(rp, g, row_begin, nrows, chunk, counters, items, order, &lr, &j0, &j1)) return;
+  const T* arow = dC + lr * ldc;
+  for (int64_t jb = j0; jb < j1; jb += 64) {
+    const int cnt = (int)((j1 - jb) < 64 ? (j1 - jb) : 64);
+    const I myc = lane < cnt ? col[jb + lane] : I(0);
+    A stk[kMaxTilesLog + 1];
+#pragma unroll
+    for (int l = 0; l <= kMaxTilesLog; ++l) stk[l] = A(0);
+    for (int t = 0; t < tiles; ++t) {
+      const int64_t leaf0 = (int64_t)t * kWideLeaves + (int64_t)lane * L;
+      A a[L][kLeaf];
+#pragma unroll
+      for (int l = 0; l < L; ++l) load_leaf<T, ALIGNED>(arow, (leaf0 + l) * kLeaf, n, a[l]);
+      A tv = A(0);
+      for (int k = 0; k < cnt; k += U) {
+        A bv[U][L][kLeaf];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t cu = (int64_t)__shfl((int64_t)myc, (k + u) & 63, 64);
+          if (k + u < cnt) {
+            const T* brow = B + cu * ldb;
+#pragma unroll
+            for (int l = 0; l < L; ++l) load_leaf<T, ALIGNED>(brow, (leaf0 + l) * kLeaf, n, bv[u][l]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (k + u < cnt) {
+            A leaf[L];
+#pragma unroll
+            for (int l = 0; l < L; ++l) {
+              A sl = A(0);
+#pragma unroll
+              for (int e = 0; e < kLeaf; ++e) sl = sl + a[l][e] * bv[u][l][e];
+              leaf[l] = sl;
+            }
+#pragma unroll
+            for (int w = 1; w < L; w <<= 1)
+#pragma unroll
+              for (int l = 0; l < L; l += 2 * w) leaf[l] = leaf[l] + leaf[l + w];
+            A x = leaf[0];
+#pragma unroll
+            for (int w = 1; w < 64; w <<= 1) x = x + __shfl_xor(x, w, 64);
+            if (lane == k + u) tv = x;
+          }
+        }
+      }
+      // pairwise merge of tile t into the stack: left operands are the earlier subtrees
+      A v = tv;
+      bool done = false;
+#pragma unroll
+      for (int l = 0; l <= kMaxTilesLog; ++l) {
+        if (!done) {
+          if ((t >> l) & 1) {
+            v = stk[l] + v;
+          } else {
+            stk[l] = v;
+            done = true;
+          }
+        }
+      }
+    }
+    A res = A(0);
+#pragma unroll
+    for (int l = 0; l <= kMaxTilesLog; ++l)
+      if ((1 << l) == tiles) res = stk[l];
+    if (lane < cnt) out[jb + lane] = Num<T>::store(res);
   }
 }
 
@@ -314,7 +420,31 @@ int sddmm_aligned(const SddmmArgs& a) {
   if (leaves <= 64) return sddmm_cfg<T, I, 64, 1, ALIGNED>(a);
   if (leaves <= 128) return sddmm_cfg<T, I, 64, 2, ALIGNED>(a);
   if (leaves <= 256) return sddmm_cfg<T, I, 64, 4, ALIGNED>(a);
-  return fail(OFX_EUNSUPPORTED, "sddmm_csr: n=%lld > 2048 is not supported", (long long)a.n);
+  int64_t tiles = 1;
+  while (tiles * kWideLeaves < leaves) tiles *= 2;
+  OFX_REQUIRE(tiles <= (1 << kMaxTilesLog), OFX_EUNSUPPORTED,
+              "sddmm_csr: n=%lld > %d is not supported", (long long)a.n,
+              kWideLeaves * kLeaf << kMaxTilesLog);
+  const Schedule sched = sddmm_schedule(a.n);
+  const plan::WsLayout w = plan::ws_layout(a.nrows, a.nnz, 0, 0, sched);
+  plan::WorkList wl{};
+  if (w.total > 0) {
+    OFX_REQUIRE(a.ws && a.ws_bytes >= w.total, OFX_EWORKSPACE,
+                "sddmm_csr: workspace of %zu bytes < %zu required", a.ws_bytes, w.total);
+    const int rc = plan::launch_plan<I>(a.s, static_cast<const I*>(a.rp), a.row_begin, a.nrows,
+                                        a.nnz, sched, w, static_cast<char*>(a.ws), &wl);
+    if (rc) return rc;
+  }
+  const int64_t work = a.nrows + (w.total > 0 ? w.max_chunks : 0);
+  const int64_t grid = (work + kBlock / 64 - 1) / (kBlock / 64);
+  hipLaunchKernelGGL((sddmm_wide_kernel<T, I, ALIGNED>), dim3((unsigned)grid), dim3(kBlock), 0, a.s,
+                     static_cast<const I*>(a.rp), static_cast<const I*>(a.col),
+                     static_cast<const T*>(a.dC), a.ldc, static_cast<const T*>(a.B), a.ldb,
+                     static_cast<T*>(a.out), a.row_begin, a.nrows, a.n,
+                     w.total > 0 ? sched.chunk : INT64_MAX, (int)tiles, wl.counters, wl.items,
+                     wl.order);
+  OFX_HIP_CHECK(hipGetLastError());
+  return OFX_OK;
 }
 
 template <typename T, typename I>

@@ -162,6 +162,27 @@ def test_gpu_sddmm_bitexact(device, dtype, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dtype,n", [("f32", 2049), ("f32", 4096), ("bf16", 5000), ("f64", 3000),
+                                     ("f32", 20003), ("f16", 8192)])
+def test_gpu_sddmm_wide_rows_bitexact(device, dtype, n):
+    """n > 2048: 256-leaf tiles whose pairwise trees are added pairwise (the same order as one
+    tree over all padded leaves), including a hub row split by the planner and unaligned n."""
+    rng = np.random.default_rng(200 + n)
+    m, k = 60, 900
+    deg = rng.integers(0, 30, size=m)
+    deg[5] = 850
+    rp, ci, v = random_csr(m, k, deg, rng)
+    a = random_dense(m, n, rng, DTYPES[dtype])
+    b = random_dense(k, n, rng, DTYPES[dtype])
+    got = fs.sddmm(rp.to(device), ci.to(device), a.to(device), b.to(device))
+    torch.cuda.synchronize()
+    ref = oracle.sddmm(rp.numpy(), ci.numpy(), to_oracle(a), to_oracle(b), dtype=dtype)
+    assert_bitwise(got, ref, f"gpu wide sddmm {dtype} n={n}")
+    cpu = fs.sddmm(rp, ci, a, b)  # the CPU kernel: same bits
+    assert_bitwise(cpu, ref, f"cpu wide sddmm {dtype} n={n}")
+
+
+@pytest.mark.gpu
 def test_gpu_sddmm_hub_rows_and_unaligned(device):
     rng = np.random.default_rng(7)
     m, k, n = 30, 70000, 128
