@@ -20,6 +20,8 @@
 //                (LPR < 64: coalesced, broadcast by ds_bpermute) or as wave-uniform scalar loads
 //                (LPR == 64); U B-row loads are in flight per lane before the in-order
 //                multiply-adds.  Hub chunks -> fp32/fp64 partial rows; rows -> C directly.
+//                Small launches: hub chunks and heavy rows take a whole wave each, its groups
+//                interleaving the nonzeros and adding the products in order (accumulate_wave).
 //   spmm_reduce  per hub row: sums its chunk partials in chunk order -> C row.
 // Every output element is produced by exactly one lane in a fixed order: results are
 // bitwise deterministic and equal to the CPU kernel / oracle with the same schedule.
@@ -57,11 +59,18 @@ struct alignas(sizeof(T) * VEC) Pack {
 // PF: the next batch's (col, val) pairs are loaded before this batch's B rows, so a long row
 // pays one memory round trip per batch instead of two (the small-problem configurations).
 // BNT: the B-row loads themselves carry the non-temporal hint (tuning variants only).
+// WH: small launches: hub chunks and heavy rows take a whole wave each (the wave's 64/LPR groups
+// interleave the nonzeros of one item), the light rows one group each (accumulate_wave).
 template <int VEC_, int LPR_, int U_ = 8, int WPB_ = 4, bool NT_ = false, bool PF_ = false,
-          bool BNT_ = false>
+          bool BNT_ = false, bool WH_ = false>
 struct Cfg {
   static constexpr int VEC = VEC_, LPR = LPR_, U = U_, WPB = WPB_;
-  static constexpr bool NT = NT_, PF = PF_, BNT = BNT_;
+  static constexpr bool NT = NT_, PF = PF_, BNT = BNT_, WH = WH_;
+  // loads in flight per lane of the wave-item form: G * UW * VEC cross-lane moves per batch are
+  // unrolled, so UW keeps that at <= 256 (4..32)
+  static constexpr int G = LPR < 64 ? 64 / LPR : 1;
+  static constexpr int UW_RAW = 256 / (G * VEC);
+  static constexpr int UW = UW_RAW > 32 ? 32 : (UW_RAW < 4 ? 4 : UW_RAW);
 };
 
 template <typename X>
@@ -250,6 +259,90 @@ __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* _
   }
 }
 
+// One work item for the whole wave (LPR < 64): group q = lane / LPR of the G = 64 / LPR groups
+// loads the B rows of nonzeros jb + G*u + q of each batch of G*U, forms their products in
+// parallel (U loads in flight per lane, the batch's (col, val) prefetched during the previous
+// one), then every group adds all G*U products in nonzero order, taking the other groups'
+// products through ds_bpermute.  The order (and each product's rounding) is the contract's, so
+// the bits equal the one-group traversal; a long row needs G times fewer dependent load rounds.
+template <typename T, typename I, typename K>
+__device__ __forceinline__ void accumulate_wave(const I* __restrict__ col, const T* __restrict__ val,
+                                                const I* __restrict__ vperm,
+                                                const T* __restrict__ Bc, const T* __restrict__ B0,
+                                                int64_t ldb, int64_t j0, int64_t j1, int lane,
+                                                int gl, bool active,
+                                                typename Num<T>::acc (&acc)[K::VEC]) {
+#pragma clang fp contract(off)
+  constexpr int VEC = K::VEC, LPR = K::LPR, U = K::UW, G = 64 / LPR;
+  constexpr int BATCH = G * U;
+  constexpr int R = (BATCH + 63) / 64;  // (col, val) registers per lane for one batch
+  static_assert(LPR < 64, "accumulate_wave needs several groups per wave");
+  using A = typename Num<T>::acc;
+  using P = Pack<T, VEC>;
+  const int q = lane / LPR;
+  auto load_batch = [&](int64_t jb, I (&c)[R], A (&v)[R]) {
+    const int n_ = (int)((j1 - jb) < BATCH ? (j1 - jb) : BATCH);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      c[r] = 0;
+      v[r] = 0;
+      const int idx = r * 64 + lane;
+      if (idx < n_) {
+        c[r] = col[jb + idx];
+        const int64_t jv = vperm ? (int64_t)vperm[jb + idx] : jb + idx;
+        v[r] = Num<T>::load(val[jv]);
+      }
+    }
+  };
+  I nxc[R];
+  A nxv[R];
+  if (j0 < j1) load_batch(j0, nxc, nxv);
+  const T* Bs = active ? Bc : B0;
+  for (int64_t jb = j0; jb < j1; jb += BATCH) {
+    const int cnt = (int)((j1 - jb) < BATCH ? (j1 - jb) : BATCH);
+    I myc[R];
+    A myv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      myc[r] = nxc[r];
+      myv[r] = nxv[r];
+    }
+    if (jb + BATCH < j1) load_batch(jb + BATCH, nxc, nxv);  // in flight during this batch
+    // this group's nonzeros of the batch: i = G*u + q, held by lane i % 64 in register i / 64
+    // G divides 64, so nonzero G*u + q sits in register (G*u) / 64 for every group q
+    I cuv[U];
+    A vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = G * u + q;
+      cuv[u] = shfl(myc[(G * u) >> 6], i & 63);
+      vv[u] = shfl(myv[(G * u) >> 6], i & 63);
+    }
+    P bv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      bv[u] = ld_brow<K::BNT, P>(Bs + (G * u + q < cnt ? (int64_t)cuv[u] : 0) * ldb);
+    // per u: this group's product, the G groups' products fetched with ds_bpermute (all issued
+    // before the first add, so their latency overlaps), then added in nonzero order
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      A pr[VEC];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) pr[e] = Num<T>::mul(vv[u], Num<T>::load(bv[u].v[e]));
+      A x[G][VEC];
+#pragma unroll
+      for (int g2 = 0; g2 < G; ++g2)
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) x[g2][e] = shfl(pr[e], g2 * LPR + gl);
+#pragma unroll
+      for (int g2 = 0; g2 < G; ++g2)
+        if (G * u + g2 < cnt)
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + x[g2][e];
+    }
+  }
+}
+
 template <typename T, int VEC, bool NT>
 __device__ __forceinline__ void store_row(T* __restrict__ p, const typename Num<T>::acc (&acc)[VEC],
                                           const T* __restrict__ bias, int act) {
@@ -286,7 +379,7 @@ __global__ void __launch_bounds__(64 * K::WPB)
                      int64_t chunk, const unsigned long long* __restrict__ counters,
                      const int64_t* __restrict__ items, const int64_t* __restrict__ order,
                      typename Num<T>::acc* __restrict__ part, const T* __restrict__ bias,
-                     int act) {
+                     int act, int64_t wave_blocks) {
   using A = typename Num<T>::acc;
   constexpr int VEC = K::VEC, LPR = K::LPR, kWaves = K::WPB;
   constexpr int GPW = 64 / LPR;
@@ -295,7 +388,51 @@ __global__ void __launch_bounds__(64 * K::WPB)
   const int gl = lane & (LPR - 1);
   const int gbase = lane & ~(LPR - 1);
   const int gsub = LPR == 64 ? 0 : lane / LPR;
-  const int64_t g = ((int64_t)blockIdx.x * kWaves + wave) * GPW + gsub;
+  if constexpr (K::WH && LPR < 64) {
+    // blocks [0, wave_blocks): one wave per hub chunk / heavy row (the plan's first items)
+    if ((int64_t)blockIdx.x < wave_blocks) {
+      const int64_t w = (int64_t)blockIdx.x * kWaves + wave;
+      const int64_t nchunks = (int64_t)counters[0];
+      const int64_t nheavy = (int64_t)counters[3] - (int64_t)counters[2];  // bin 0
+      if (w >= nchunks + nheavy) return;
+      int64_t wr, wc = -1;
+      if (w < nchunks) {
+        wr = items[2 * w + 0];
+        wc = items[2 * w + 1];
+      } else {
+        wr = order[w - nchunks];
+      }
+      wr = uniform64(wr);
+      wc = uniform64(wc);
+      const int64_t rs = (int64_t)rp[row_begin + wr];
+      const int64_t re = (int64_t)rp[row_begin + wr + 1];
+      int64_t j0 = rs, j1 = re;
+      if (wc >= 0) {
+        j0 = rs + wc * chunk;
+        j1 = (re - j0 - chunk < chunk) ? re : j0 + chunk;
+      }
+      for (int64_t c0 = 0; c0 < n; c0 += (int64_t)LPR * VEC) {
+        const int64_t cc = c0 + (int64_t)gl * VEC;
+        const bool active = cc < n;
+        A acc[VEC];
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[e] = A(0);
+        accumulate_wave<T, I, K>(col, val, vperm, B + cc, B, ldb, j0, j1, lane, gl, active, acc);
+        if (active && gsub == 0) {
+          if (wc >= 0)
+            store_partial<A, VEC>(part + w * n + cc, acc);
+          else
+            store_row<T, VEC, K::NT>(C + wr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
+        }
+      }
+      return;
+    }
+  }
+  // one lane-group per work item; in the WH form these are the light rows after the wave items
+  int64_t g = ((int64_t)(blockIdx.x - (K::WH ? wave_blocks : 0)) * kWaves + wave) * GPW + gsub;
+  if constexpr (K::WH && LPR < 64) {
+    if (order != nullptr) g += (int64_t)counters[0] + (int64_t)counters[3] - (int64_t)counters[2];
+  }
   int64_t lr, c = -1;  // local row; chunk index or -1 for a whole row
   if (order == nullptr) {
     if (g >= nrows) return;
@@ -531,16 +668,19 @@ int launch_cfg(const Launch& L) {
   unsigned long long* counters = wl.counters;
   int64_t *hub = wl.hubs, *items = wl.items, *order = wl.order;
   A* part = reinterpret_cast<A*>(wl.part);
-  // Work list length <= hub chunks + rows; surplus groups exit at once.
+  // Work list length <= hub chunks + rows; surplus groups exit at once.  The WH form puts one
+  // wave per hub chunk / heavy row first (upper bound: every chunk and row), then the groups.
   const int64_t work = L.nrows + (plan ? w.max_chunks : 0);
-  const int64_t grid = (work + GPB - 1) / GPB;
+  const int64_t wave_blocks =
+      (K::WH && K::LPR < 64 && plan) ? (work + K::WPB - 1) / K::WPB : 0;
+  const int64_t grid = wave_blocks + (work + GPB - 1) / GPB;
   OFX_REQUIRE(grid < (int64_t)UINT32_MAX, OFX_EINVAL, "spmm_csr: too many rows (%lld)",
               (long long)L.nrows);
   hipLaunchKernelGGL((spmm_main_kernel<T, I, K>), dim3((unsigned)grid), dim3(64 * K::WPB), 0,
                      L.stream, rp, col, val, static_cast<const I*>(L.vperm), B, L.ldb, C, L.ldc,
                      L.row_begin, L.nrows, L.n,
                      plan ? L.sched.chunk : INT64_MAX, counters, items, order, part,
-                     static_cast<const T*>(L.bias), L.act);
+                     static_cast<const T*>(L.bias), L.act, wave_blocks);
   OFX_HIP_CHECK(hipGetLastError());
   if (plan && w.max_hubs > 0)
     return launch_reduce<T>(L.stream, w.max_hubs, L.n, counters, hub, part, C, L.ldc,
@@ -565,10 +705,10 @@ template <typename T, typename I, int VEC>
 int launch_vec_small(const Launch& L, int lpr) {
   constexpr int U = VEC * sizeof(T) <= 4 ? 32 : 16;
   switch (lpr) {
-    case 4: return launch_cfg<T, I, Cfg<VEC, 4, U, 4, false, true>>(L);
-    case 8: return launch_cfg<T, I, Cfg<VEC, 8, U, 4, false, true>>(L);
-    case 16: return launch_cfg<T, I, Cfg<VEC, 16, U, 4, false, true>>(L);
-    case 32: return launch_cfg<T, I, Cfg<VEC, 32, U, 4, false, true>>(L);
+    case 4: return launch_cfg<T, I, Cfg<VEC, 4, U, 4, false, true, false, true>>(L);
+    case 8: return launch_cfg<T, I, Cfg<VEC, 8, U, 4, false, true, false, true>>(L);
+    case 16: return launch_cfg<T, I, Cfg<VEC, 16, U, 4, false, true, false, true>>(L);
+    case 32: return launch_cfg<T, I, Cfg<VEC, 32, U, 4, false, true, false, true>>(L);
     case 64: return launch_cfg<T, I, Cfg<VEC, 64, U>>(L);
     default: return fail(OFX_EINVAL, "spmm_csr: unsupported lanes-per-row %d", lpr);
   }
@@ -628,6 +768,11 @@ int launch_tuned(const Launch& L, int id) {
       case 19: return launch_cfg<T, I, Cfg<1, 16, 8, 4, true, false, true>>(L);
       case 20: return launch_cfg<T, I, Cfg<4, 32, 8, 4, false, false, true>>(L);
       case 21: return launch_cfg<T, I, Cfg<1, 16, 16, 4, false, false>>(L);
+      // small launches without / with the wave-item form (N = 16: VEC 1, N = 64: VEC 4)
+      case 22: return launch_cfg<T, I, Cfg<1, 16, 32, 4, false, true>>(L);
+      case 23: return launch_cfg<T, I, Cfg<1, 16, 32, 4, false, true, false, true>>(L);
+      case 24: return launch_cfg<T, I, Cfg<4, 16, 16, 4, false, true>>(L);
+      case 25: return launch_cfg<T, I, Cfg<4, 16, 16, 4, false, true, false, true>>(L);
       default: break;
     }
   }

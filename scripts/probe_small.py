@@ -18,7 +18,10 @@ for name, (m, nnz, n) in {"cora": (2708, 10556, 16), "cora64": (2708, 10556, 64)
     rp, ci, v = rp.to(dev), ci.to(dev), v.to(dev)
     b = synth.dense(0, m, n, device=dev); out = torch.empty((m, n), device=dev)
     for label, opts in {"default": None, "u8_forced": ops.make_options(variant=100 + (16 if n == 16 else 16)) if n == 16 else ops.make_options(variant=416),
-                        "ordered": ops.make_options(ordered=True), "noheavy": ops.make_options(heavy=-1)}.items():
+                        "ordered": ops.make_options(ordered=True), "noheavy": ops.make_options(heavy=-1),
+                        # small-launch form without / with wave items (tuning variants 10022-10025)
+                        "group_items": ops.make_options(variant=10022 if n == 16 else 10024),
+                        "wave_items": ops.make_options(variant=10023 if n == 16 else 10025)}.items():
         k = ops.SpmmCsrKernel(m, m, n, ci.numel(), torch.int32, torch.float32, dev, opts)
         res[f"{name}_{label}_us"] = round(t(lambda: k(rp, ci, v, b, out)), 2)
     # uniform-degree matrix, same nnz

@@ -462,3 +462,37 @@ def test_row_split_step_hipgraph_capture(device):
         rs.close()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dtype,idx", [("f32", torch.int32), ("bf16", torch.int64),
+                                       ("f64", torch.int32), ("f16", torch.int32)])
+@pytest.mark.parametrize("n", [1, 4, 16, 17, 64, 128])
+def test_small_launch_wave_items(device, dtype, idx, n):
+    """Small launches (<= 32768 rows): hub chunks and heavy rows (> 5x the mean degree) are taken
+    by a whole wave whose groups interleave the nonzeros and add the products in nonzero order
+    through cross-lane moves; light rows by one group.  Same bits as the oracle, with and without
+    the fused epilogue, and through the gathered-values form."""
+    rng = np.random.default_rng(500 + n)
+    m, k = 3000, 12000
+    deg = rng.integers(0, 12, size=m)
+    deg[[7, 70, 700, 2999]] = [300, 2500, 9000, 65]   # heavy rows, a hub at every n here
+    deg[100:110] = rng.integers(100, 600, size=10)
+    rp, ci, v = random_csr(m, k, deg, rng, idx, DTYPES[dtype])
+    b = random_dense(k, n, rng, DTYPES[dtype])
+    d = (rp.to(device), ci.to(device), v.to(device), b.to(device))
+    out = fs.spmm(d[0], d[1], d[2], m, k, d[3])
+    torch.cuda.synchronize()
+    ref = oracle_spmm(rp, ci, v, b)
+    assert_bitwise(out, ref, f"{dtype} n={n}")
+    bias = random_dense(1, n, rng, DTYPES[dtype])[0]
+    kern = ops.SpmmCsrKernel(m, k, n, ci.numel(), idx, DTYPES[dtype], device)
+    out2 = torch.full((m, n), float("nan"), dtype=DTYPES[dtype], device=device)
+    kern(*d, out2, bias=bias.to(device), relu=True)
+    torch.cuda.synchronize()
+    assert_bitwise(out2, oracle.bias_act(ref, to_oracle(bias), "relu", dtype=dtype), "epilogue")
+    perm = torch.from_numpy(rng.permutation(ci.numel()).astype(np.int64)).to(idx)
+    vals_src = torch.empty_like(v)
+    vals_src[perm.long()] = v  # values[perm[j]] == v[j]
+    out3 = ops.spmm_csr_gathered(d[0], d[1], vals_src.to(device), perm.to(device), d[3], m, k)
+    torch.cuda.synchronize()
+    assert_bitwise(out3, ref, "gathered values")
