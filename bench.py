@@ -394,18 +394,30 @@ def main():
                 reps_ += 1
             return flops_s * reps_ / t_ / 1e9, reps_, t_
 
-        # headline: every host core, OpenMP threads = nproc
+        # headline: every host core, and the cores this process may
+        # actually use (a cgroup CPU quota throttles an all-core run on the GPU box: 16 CPUs of a
+        # 256-core host); the faster of the two is the baseline, both are reported
+        hc = host_cpu()
+        usable = min(x for x in (hc["nproc"] or 1, hc["affinity"],
+                                 int(np.ceil(hc["cgroup_cpu_quota"])) if hc["cgroup_cpu_quota"]
+                                 else None) if x)
         nt_all = args.cpu_baseline_threads
-        cpu_gflops, reps, t_cpu = time_oracle(nt_all, 10.0, 5)
-        result["cpu_baseline"] = {"value": round(cpu_gflops, 3), "unit": "GFLOP/s", "cores": nt_all,
-                                  "kind": "port", "host": host_cpu(),
-                                  "sample": f"{what} x{reps} runs ({t_cpu:.1f} s), oracle/spmm_oracle.c "
-                                            f"OpenMP {nt_all} threads, same inputs and schedule"}
-        if threads != nt_all:
-            g16, reps16, t16 = time_oracle(threads, 5.0, 3)
-            result["extra"][f"cpu_{threads}threads"] = {
-                "value": round(g16, 3), "unit": "GFLOP/s", "cores": threads,
-                "sample": f"{what} x{reps16} runs ({t16:.1f} s), same oracle"}
+        runs = {nt_all: time_oracle(nt_all, 10.0, 5)}
+        if usable != nt_all:
+            runs[usable] = time_oracle(usable, 10.0, 5)
+        if threads not in runs:
+            runs[threads] = time_oracle(threads, 5.0, 3)
+        best = max(runs, key=lambda t_: runs[t_][0])
+        cpu_gflops, reps, t_cpu = runs[best]
+        result["cpu_baseline"] = {
+            "value": round(cpu_gflops, 3), "unit": "GFLOP/s", "cores": best, "kind": "port",
+            "host": hc,
+            "sample": f"{what} x{reps} runs ({t_cpu:.1f} s), oracle/spmm_oracle.c OpenMP {best} "
+                      f"threads (the fastest of {sorted(runs)} threads; the process may use "
+                      f"{usable} of {hc['nproc']} cores), same inputs and schedule"}
+        result["extra"]["cpu_by_threads"] = {
+            str(t_): {"value": round(g_, 3), "unit": "GFLOP/s", "runs": r_, "seconds": round(s_, 1)}
+            for t_, (g_, r_, s_) in sorted(runs.items())}
         # single thread (OneFlow's default CPU_THREADING_RUNTIME=SEQ) on the first
         # rows holding ~1/16 of the sample's nonzeros
         r1 = int(np.searchsorted(rp_np, rp_np[-1] // 16))
