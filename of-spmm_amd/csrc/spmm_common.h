@@ -37,20 +37,34 @@ OFX_HD uint32_t f32_to_bits(float f) { return __builtin_bit_cast(uint32_t, f); }
 
 OFX_HD float bf16_to_f32(uint16_t h) { return bits_to_f32(uint32_t(h) << 16); }
 // Round-to-nearest-even; NaN stays NaN (quiet bit forced).
+// On the device this is gfx950's v_cvt_pk_bf16_f32 (emitted for the conversion to __bf16), which
+// gives the same bits as the software rounding for all 2^32 f32 inputs, NaNs included
+// (scripts/bf16_cvt_probe.hip, profiles/r02_bf16_cvt_probe.json); the host (CPU kernel) keeps
+// the software form.
 OFX_HD uint16_t f32_to_bf16(float f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
+#else
   const uint32_t u = f32_to_bits(f);
   if ((u & 0x7fffffffu) > 0x7f800000u) return uint16_t((u >> 16) | 0x40u);
   return uint16_t((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+#endif
 }
 OFX_HD float f16_to_f32(uint16_t h) { return float(__builtin_bit_cast(_Float16, h)); }
 OFX_HD uint16_t f32_to_f16(float f) { return __builtin_bit_cast(uint16_t, _Float16(f)); }
 
 // bf16 rounding of an fp32 value, returned as fp32 (round-to-nearest-even, NaN quieted): the
 // same bits as bf16_to_f32(f32_to_bf16(f)) without the 16-bit round trip.
+// Device: one v_cvt_pk_bf16_f32 (per two values) and a shift instead of ~7 integer ops; the
+// software form made the bf16 N=256 Reddit-shaped SpMM ALU-bound (7.2 -> 12.5 ms).
 OFX_HD float round_bf16(float f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (float)(__bf16)f;
+#else
   const uint32_t u = f32_to_bits(f);
   if ((u & 0x7fffffffu) > 0x7f800000u) return bits_to_f32((u & 0xffff0000u) | 0x400000u);
   return bits_to_f32((u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u);
+#endif
 }
 
 // Accumulator type, load/store conversions and the multiply per storage type.
