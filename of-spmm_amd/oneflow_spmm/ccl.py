@@ -22,8 +22,7 @@ import torch
 import torch.distributed as dist
 
 from ._C import current_stream_handle, desc, dtype_code
-from ._lib import (DEV_CPU, DEV_HIP, KV_PULL_FN, KV_PUSH_FN, LIB, SENDRECV_FN, OfxError, Placement,
-                   check)
+from ._lib import DEV_CPU, DEV_HIP, KV_PULL_FN, KV_PUSH_FN, LIB, SENDRECV_FN, Placement, check
 
 __all__ = ["PlacementSpec", "install_control_plane", "ccl_registered", "check_ccl_s2b", "ccl_s2b",
            "nccl_logical_all_gather", "insert_nccl_logical_op", "rccl_comm_key", "SpmmJob"]
@@ -229,5 +228,3 @@ def _balanced(total, parts, idx):
     check(LIB.ofx_balanced_range(total, parts, idx, ctypes.byref(lo), ctypes.byref(hi)), "balanced")
     return lo.value, hi.value
 
-
-del OfxError  # re-exported by the package
