@@ -260,6 +260,8 @@ def test_products_scale_sampled_rows(device):
     torch.cuda.synchronize()
     b_h = b.cpu()
     rp_n, ci_n, v_n, b_n = to_oracle(rp), to_oracle(ci), to_oracle(v), to_oracle(b_h)
+    # the oracle takes int64 indices: convert once, not per call
+    rp_n, ci_n = rp_n.astype(np.int64), ci_n.astype(np.int64)
     deg = np.diff(rp_n)
     hubs = np.nonzero(deg > ops.default_split(n))[0]
     assert len(hubs) > 100
@@ -273,7 +275,7 @@ def test_products_scale_sampled_rows(device):
     # rows), relative to the |.|-sum: the 200 first hubs, the 20 heaviest (max degree 306k), the last
     heavy = np.argsort(deg)[-20:]
     rows = np.unique(np.concatenate([hubs[:200], heavy, hubs[-1:]]))
-    check_sampled_rows(rp_n.astype(np.int64), ci_n, v, b, out, rows, 1e-5, "products hubs")
+    check_sampled_rows(rp_n, ci_n, v, b, out, rows, 1e-5, "products hubs")
     # a checksum of checksums over all rows (size-independent): row sums vs oracle's
     assert torch.isfinite(out_h).all()
 
