@@ -184,7 +184,7 @@ class SpmmJob:
     def __init__(self, placement: PlacementSpec, m: int, k: int, n: int, nnz: int,
                  idx_dtype: torch.dtype, dtype: torch.dtype, device, stream_name: str = ""):
         self.placement, self.m, self.k, self.n, self.nnz = placement, m, k, n, nnz
-        self.dtype, self.device = dtype, torch.device(device)
+        self.dtype, self.idx_dtype, self.device = dtype, idx_dtype, torch.device(device)
         self._job = ctypes.c_void_p()
         check(LIB.ofx_spmm_job_create(ctypes.byref(placement.c()), dtype_code(idx_dtype),
                                       dtype_code(dtype), m, k, n, nnz, stream_name.encode(),
@@ -201,8 +201,18 @@ class SpmmJob:
         if out is None:
             out = torch.empty((self.row_range[1] - self.row_range[0], self.n), dtype=self.dtype,
                               device=self.device)
+        # the compiled job trusts these shapes (raw pointers cross the C-ABI): check them here
+        p = self.placement.parallel_num
+        want = {"row_ptr": ((self.m + 1,), self.idx_dtype), "col_idx": ((self.nnz,), self.idx_dtype),
+                "values": ((self.nnz,), self.dtype),
+                "b_shard": ((self.k // p if p > 1 else self.k, self.n), self.dtype),
+                "out": ((self.row_range[1] - self.row_range[0], self.n), self.dtype)}
         for t, name in ((row_ptr, "row_ptr"), (col_idx, "col_idx"), (values, "values"),
                         (b_shard, "b_shard"), (out, "out")):
+            shape, dt = want[name]
+            if tuple(t.shape) != shape or t.dtype != dt:
+                raise ValueError(f"SpmmJob: {name} must be {shape} {dt}, got {tuple(t.shape)} "
+                                 f"{t.dtype}")
             if not t.is_contiguous() or t.device != self.device:
                 raise ValueError(f"SpmmJob: {name} must be contiguous on {self.device}")
         ptr = lambda t: t.data_ptr() if t.numel() else None  # noqa: E731

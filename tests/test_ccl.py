@@ -141,6 +141,10 @@ def test_spmm_job_plan_and_one_device_cpu_run():
     out = job(rp, ci, v, b)
     ref = oracle.spmm(rp.numpy(), ci.numpy(), v.numpy(), b.numpy())
     assert np.array_equal(out.numpy().view(np.uint32), ref.view(np.uint32))
+    with pytest.raises(ValueError, match="b_shard must be"):
+        job(rp, ci, v, b[:-1])
+    with pytest.raises(ValueError, match="col_idx must be"):
+        job(rp, ci.long(), v, b)
     # a HIP placement of 4 ranks compiles the logical collective into the plan (the RCCL
     # communicator is created on the first run, on the GPU)
     job4 = ccl.SpmmJob(PlacementSpec("hip", 4, 2), m, 4 * 65, n, ci.numel(), torch.int32,
