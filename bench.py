@@ -113,6 +113,10 @@ def main():
     ap.add_argument("--exchange", default="auto",
                     help="B exchange for N>1: auto | allgather | halo | nsplit | grid<R>x<C> "
                          "(default: measured at setup)")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process-group backend at N>1; gloo is a rehearsal of the multi-rank code "
+                         "path on fewer GPUs (ranks share devices, bytes are host-staged: not a "
+                         "performance number)")
     ap.add_argument("--force-rowsplit", action="store_true",
                     help="run the N>1 code path (RCCL all-gather + local SpMM) even with one rank")
     args = ap.parse_args()
@@ -125,15 +129,21 @@ def main():
     if world != args.gpus:
         log(f"[bench] error: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
         sys.exit(2)
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    rehearsal = args.backend == "gloo"
+    dev_index = local_rank % torch.cuda.device_count() if rehearsal else local_rank
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
+    red_dev = "cpu" if rehearsal else device  # where the timing reductions run
     rowsplit = world > 1 or args.force_rowsplit
     if rowsplit:
         if world == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29571")
             os.environ.setdefault("RANK", "0")
-        dist.init_process_group("nccl", device_id=device, world_size=world, rank=rank)
+        if rehearsal:
+            dist.init_process_group("gloo", world_size=world, rank=rank)
+        else:
+            dist.init_process_group("nccl", device_id=device, world_size=world, rank=rank)
         if dist.get_world_size() != args.gpus and not (args.force_rowsplit and args.gpus == 1):
             log(f"[bench] error: {dist.get_world_size()} ranks joined, --gpus {args.gpus}")
             sys.exit(2)
@@ -177,7 +187,8 @@ def main():
                 kern(d_rp, d_ci, d_v, d_b, out)
     else:
         try:
-            rs = RowSplitSpmm(m, k, n, nnz_local, dt, torch.int32, device)
+            rs = RowSplitSpmm(m, k, n, nnz_local, dt, torch.int32, device,
+                              comm="torch" if rehearsal else "auto")
         except fs.OfxError as e:  # own RCCL communicator refused: torch.distributed's (also RCCL)
             log(f"[bench] native RCCL communicator unavailable ({e}); using torch.distributed")
             rs = RowSplitSpmm(m, k, n, nnz_local, dt, torch.int32, device, comm="torch")
@@ -234,7 +245,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     if rowsplit:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed * 1e3 / args.steps
@@ -270,7 +281,7 @@ def main():
     gather_mean = float(np.mean(gather_ms)) if gather_ms else 0.0
     phase = {"spmm_ms_max": kern_ms, "gather_ms_max": gather_mean}
     if rowsplit and world > 1:
-        t = torch.tensor([kern_ms, gather_mean], dtype=torch.float64, device=device)
+        t = torch.tensor([kern_ms, gather_mean], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         phase = {"spmm_ms_max": float(t[0]), "gather_ms_max": float(t[1])}
     # cold-cache SpMM: a 512 MB scratch write evicts the 256 MB Infinity Cache
@@ -326,6 +337,8 @@ def main():
         "config": {"workload": f"{args.config}: CSR {m}x{k}, {nnz} nnz x dense N={n}",
                    "m": m, "k": k, "nnz": nnz, "n": n, "index": "int32",
                    "parallelism": "single GPU" if not rowsplit else
+                   (f"REHEARSAL: row-split x{world} with gloo on {torch.cuda.device_count()} GPU(s), "
+                    "host-staged bytes; not a performance number") if rehearsal else
                    f"row-split x{world} + RCCL all-gather of B (padded shards)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -343,7 +356,7 @@ def main():
                        "kernel_ms_cold_median": round(cold_ms, 4),
                        "gbs_cold": round(bytes_launch / (cold_ms * 1e-3) / 1e9, 1)}
     if rowsplit:
-        nz = torch.tensor([nnz_local, nnz_local], dtype=torch.float64, device=device)
+        nz = torch.tensor([nnz_local, nnz_local], dtype=torch.float64, device=red_dev)
         if world > 1:
             dist.all_reduce(nz[:1], op=dist.ReduceOp.MAX)
             dist.all_reduce(nz[1:], op=dist.ReduceOp.SUM)

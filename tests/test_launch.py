@@ -1,11 +1,13 @@
 """The single-node launcher (oneflow_spmm/launch.py, the environment contract of the reference's
 python/oneflow/distributed/launch.py:103-140) and bench.py's use of it: `--gpus N` without a
 launcher spawns N ranks, and a rank count that differs from --gpus is an error.  CPU only
-(gloo)."""
+(gloo), plus one GPU rehearsal of the multi-rank bench path."""
 import os
 import subprocess
 import sys
 import textwrap
+
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "of-spmm_amd"))
@@ -80,3 +82,24 @@ def test_bench_spawns_its_ranks_without_a_launcher():
     assert "spawning 2 local ranks" in p.stderr
     assert p.returncode != 0
     assert '"n_gpus": 1' not in p.stdout
+
+
+@pytest.mark.gpu
+def test_bench_multi_rank_rehearsal_on_one_gpu():
+    """The whole N>1 bench path (self-spawn, process group, RowSplitSpmm bind + tune over every
+    exchange candidate, barrier-bracketed timing, max-over-ranks reduction, one JSON line from
+    rank 0) on the GPUs this box has, with gloo moving the bytes: a rehearsal of the driver's
+    multi-GPU run, flagged as such in the line."""
+    import json
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    p = _bench(["--gpus", "2", "--backend", "gloo", "--config", "plaw1m", "--steps", "2",
+                "--warmup", "1"], {},
+               drop=("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"))
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["extra"]["ranks_seen"] == 2 and line["value"] > 0
+    assert line["config"]["parallelism"].startswith("REHEARSAL")
+    assert len(line["extra"]["allgather_tune_ms"]) >= 5
+
