@@ -477,6 +477,200 @@ __global__ void __launch_bounds__(64 * K::WPB)
   }
 }
 
+// ---- small form: one launch, no plan, no workspace -------------------------------------------
+// Launches with few rows and little B-row traffic (use_small_form) run as ONE kernel.  Block b
+// owns rows [b*RPB, (b+1)*RPB), one lane-group per row.  A group takes its row when the row has at
+// most `light` nonzeros and is not split (accumulate, the group form).  The block's longer rows
+// are then taken one at a time by the whole block: each of its GB lane-groups loads the B rows of
+// a strided share of a batch of NB nonzeros, the products go to LDS, and the first lane-group of
+// wave 0 adds them in nonzero order while the next batch's loads are in flight.  A row longer
+// than `split` runs chunk by chunk and its chunk sums are added in chunk order from +0: the bits
+// of the planned form's partials + spmm_reduce (and of the CPU kernel).
+template <typename T, typename K>
+struct SmallForm {
+  using A = typename Num<T>::acc;
+  static constexpr int W = K::LPR * K::VEC;               // columns per pass
+  static constexpr int G = 64 / K::LPR;                   // lane-groups per wave
+  static constexpr int GB = G * K::WPB;                   // lane-groups per block
+  static constexpr int RPB = GB;                          // rows per block
+  static constexpr int kLdsElems = 32768 / (int)sizeof(A);  // 32 KB of products per batch
+  static constexpr int NB_RAW = kLdsElems / W < 512 ? kLdsElems / W : 512;
+  static constexpr int UW_RAW = NB_RAW / GB;
+  // loads in flight per lane: 16 or 32 ran these kernels out of registers (512 VGPRs + spills)
+  static constexpr int UW = UW_RAW > 8 ? 8 : (UW_RAW < 1 ? 1 : UW_RAW);
+  static constexpr int NB = UW * GB;                      // nonzeros per batch
+  static_assert(NB * W * (int)sizeof(A) <= 32768, "small form: LDS batch too large");
+};
+
+// acc[e] (valid in wave 0, group 0) = sum over j in [j0, j1) of val[j] * B[col[j], cc + e], in
+// ascending j from +0, computed by the whole block (see above).  Every thread of the block calls
+// this with the same j0/j1.
+template <typename T, typename I, typename K>
+__device__ __forceinline__ void block_accumulate(const I* __restrict__ col,
+                                                 const T* __restrict__ val,
+                                                 const I* __restrict__ vperm,
+                                                 const T* __restrict__ Bs, int64_t ldb,
+                                                 int64_t j0, int64_t j1, int gb, int gl,
+                                                 bool chain, typename Num<T>::acc* lds,
+                                                 typename Num<T>::acc (&acc)[K::VEC]) {
+#pragma clang fp contract(off)
+  using SF = SmallForm<T, K>;
+  using A = typename Num<T>::acc;
+  using P = Pack<T, K::VEC>;
+  constexpr int VEC = K::VEC, W = SF::W, GB = SF::GB, UW = SF::UW, NB = SF::NB;
+  // nonzero i of a batch is loaded by lane-group i % GB, in its slot i / GB
+  auto load_cv = [&](int64_t jb, I (&c)[UW], A (&v)[UW]) {
+#pragma unroll
+    for (int u = 0; u < UW; ++u) {
+      const int64_t j = jb + (int64_t)GB * u + gb;
+      c[u] = 0;
+      v[u] = A(0);
+      if (j < j1) {
+        c[u] = col[j];
+        v[u] = Num<T>::load(val[vperm ? (int64_t)vperm[j] : j]);
+      }
+    }
+  };
+  I cn[UW];
+  A vn[UW], vc[UW];
+  P bv[UW];
+  load_cv(j0, cn, vn);
+#pragma unroll
+  for (int u = 0; u < UW; ++u) {
+    bv[u] = ld_brow<K::BNT, P>(Bs + (int64_t)cn[u] * ldb);
+    vc[u] = vn[u];
+  }
+  if (j0 + NB < j1) load_cv(j0 + NB, cn, vn);
+  for (int64_t jb = j0; jb < j1; jb += NB) {
+    const int cnt = (int)((j1 - jb) < NB ? (j1 - jb) : NB);
+    A pr[UW][VEC];
+#pragma unroll
+    for (int u = 0; u < UW; ++u)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) pr[u][e] = Num<T>::mul(vc[u], Num<T>::load(bv[u].v[e]));
+    __syncthreads();  // the previous batch's adds have read the LDS products
+#pragma unroll
+    for (int u = 0; u < UW; ++u) {
+      const int i = GB * u + gb;
+      if (i < cnt) {
+        if constexpr (VEC * sizeof(A) == 16 || VEC * sizeof(A) == 8) {
+          Pack<A, VEC> o;
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) o.v[e] = pr[u][e];
+          *reinterpret_cast<Pack<A, VEC>*>(lds + i * W + gl * VEC) = o;
+        } else {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) lds[i * W + gl * VEC + e] = pr[u][e];
+        }
+      }
+    }
+    __syncthreads();
+    if (jb + NB < j1) {  // the next batch's B rows are in flight during this batch's adds
+#pragma unroll
+      for (int u = 0; u < UW; ++u) {
+        bv[u] = ld_brow<K::BNT, P>(Bs + (int64_t)cn[u] * ldb);
+        vc[u] = vn[u];
+      }
+      if (jb + 2 * NB < j1) load_cv(jb + 2 * NB, cn, vn);
+    }
+    if (chain) {
+      int i = 0;
+      for (; i + 8 <= cnt; i += 8) {
+        Pack<A, VEC> x[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) x[t] = *reinterpret_cast<const Pack<A, VEC>*>(lds + (i + t) * W + gl * VEC);
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + x[t].v[e];
+      }
+      for (; i < cnt; ++i) {
+        const Pack<A, VEC> x = *reinterpret_cast<const Pack<A, VEC>*>(lds + i * W + gl * VEC);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + x.v[e];
+      }
+    }
+  }
+}
+
+template <typename T, typename I, typename K>
+__global__ void __launch_bounds__(64 * K::WPB)
+    spmm_small_kernel(const I* __restrict__ rp, const I* __restrict__ col,
+                      const T* __restrict__ val, const I* __restrict__ vperm,
+                      const T* __restrict__ B, int64_t ldb, T* __restrict__ C, int64_t ldc,
+                      int64_t row_begin, int64_t nrows, int64_t n, int64_t split, int64_t chunk,
+                      int64_t light, const T* __restrict__ bias, int act) {
+  using SF = SmallForm<T, K>;
+  using A = typename Num<T>::acc;
+  constexpr int VEC = K::VEC, LPR = K::LPR, W = SF::W, RPB = SF::RPB;
+  __shared__ __attribute__((aligned(16))) A lds[SF::NB * W];
+  __shared__ int heavy_rows[RPB];
+  __shared__ int nheavy;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int gl = lane & (LPR - 1);
+  const int gbase = lane & ~(LPR - 1);
+  const int q = LPR == 64 ? 0 : lane / LPR;
+  const int gb = wave * SF::G + q;  // lane-group of the block
+  const int64_t row0 = (int64_t)blockIdx.x * RPB;
+  if (threadIdx.x == 0) nheavy = 0;
+  __syncthreads();
+  const int64_t lr = row0 + gb;
+  if (lr < nrows) {
+    const int64_t rs = (int64_t)rp[row_begin + lr];
+    const int64_t re = (int64_t)rp[row_begin + lr + 1];
+    const int64_t len = re - rs;
+    if (len > light || len > split) {
+      if (gl == 0) heavy_rows[atomicAdd(&nheavy, 1)] = gb;
+    } else {
+      for (int64_t c0 = 0; c0 < n; c0 += W) {
+        const int64_t cc = c0 + (int64_t)gl * VEC;
+        const bool active = cc < n;
+        A acc[VEC];
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[e] = A(0);
+        accumulate<T, I, K>(col, val, vperm, B + cc, B, ldb, rs, re, gl, gbase, active, acc);
+        if (active) store_row<T, VEC, K::NT>(C + lr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
+      }
+    }
+  }
+  __syncthreads();
+  const int nh = nheavy;
+  const bool chain = wave == 0 && q == 0;
+  for (int h = 0; h < nh; ++h) {
+    const int64_t hr = row0 + heavy_rows[h];
+    const int64_t rs = (int64_t)rp[row_begin + hr];
+    const int64_t re = (int64_t)rp[row_begin + hr + 1];
+    const bool split_row = re - rs > split;
+    const int64_t nc = split_row ? num_chunks(re - rs, chunk) : 1;
+    for (int64_t c0 = 0; c0 < n; c0 += W) {
+      const int64_t cc = c0 + (int64_t)gl * VEC;
+      const bool active = cc < n;
+      const T* Bs = active ? B + cc : B;
+      A total[VEC], acc[VEC];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) total[e] = A(0);
+      for (int64_t ci = 0; ci < nc; ++ci) {
+        int64_t j0 = rs, j1 = re;
+        if (split_row) {
+          j0 = rs + ci * chunk;
+          j1 = (re - j0 - chunk < chunk) ? re : j0 + chunk;
+        }
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[e] = A(0);
+        block_accumulate<T, I, K>(col, val, vperm, Bs, ldb, j0, j1, gb, gl, chain, lds, acc);
+        if (split_row) {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) total[e] = total[e] + acc[e];
+        }
+      }
+      if (chain && active)
+        store_row<T, VEC, K::NT>(C + hr * ldc + cc, split_row ? total : acc,
+                                 bias ? bias + cc : nullptr, act);
+    }
+  }
+}
+
 // ---- hub reduce: C[hub row] = ((0 + part[chunk 0]) + part[chunk 1]) + ... (chunk order) ---------
 // One group of L lanes per hub (64/L hubs per wave); each lane owns VEC consecutive columns and
 // reads them as one 16-B vector per partial row, kPre partial rows in flight before the in-order
@@ -688,6 +882,43 @@ int launch_cfg(const Launch& L) {
   return OFX_OK;
 }
 
+// Small form (spmm_small_kernel): one launch when the launch has at most kSmallRows rows and at
+// most kSmallFormElems products (nnz * n).  Its longest row then costs at most that many products
+// of one block's in-order adds, against the planned form's three planning launches + reduce.
+// A fixed function of (rows, nnz, n, variant): the workspace query and the launch agree.
+constexpr int64_t kSmallRows = 32768;
+constexpr int64_t kSmallFormElems = int64_t(1) << 20;
+constexpr int kSmallLight = 2;  // rows of more than kSmallLight * U nonzeros take the whole block
+
+bool use_small_form(int64_t nrows, int64_t nnz, int64_t n, const Schedule& s) {
+  return s.variant == 0 && nrows <= kSmallRows && nnz <= kSmallFormElems / (n > 0 ? n : 1);
+}
+
+template <typename T, typename I, typename K>
+int launch_small(const Launch& L) {
+  using SF = SmallForm<T, K>;
+  // options.heavy_threshold > 0 overrides the light/whole-block cut (tuning; no numeric effect)
+  const int64_t light =
+      (L.sched.heavy > 0 && L.sched.heavy != INT64_MAX) ? L.sched.heavy : (int64_t)kSmallLight * K::U;
+  const int64_t grid = (L.nrows + SF::RPB - 1) / SF::RPB;
+  OFX_REQUIRE(grid < (int64_t)UINT32_MAX, OFX_EINVAL, "spmm_csr: too many rows (%lld)",
+              (long long)L.nrows);
+  hipLaunchKernelGGL((spmm_small_kernel<T, I, K>), dim3((unsigned)grid), dim3(64 * K::WPB), 0,
+                     L.stream, static_cast<const I*>(L.rp), static_cast<const I*>(L.col),
+                     static_cast<const T*>(L.val), static_cast<const I*>(L.vperm),
+                     static_cast<const T*>(L.b), L.ldb, static_cast<T*>(L.c), L.ldc, L.row_begin,
+                     L.nrows, L.n, L.sched.split, L.sched.chunk, light,
+                     static_cast<const T*>(L.bias), L.act);
+  OFX_HIP_CHECK(hipGetLastError());
+  return OFX_OK;
+}
+
+template <typename T, typename I, typename K>
+int launch_small_or_planned(const Launch& L) {
+  if (use_small_form(L.nrows, L.nnz, L.n, L.sched)) return launch_small<T, I, K>(L);
+  return launch_cfg<T, I, K>(L);
+}
+
 // B far larger than the Infinity Cache (> 1 GiB): the col/val/C streams are loaded and stored
 // non-temporally so they do not evict the hot (hub) B rows that still hit on-die.  Measured
 // (scripts/ab.py, bit-identical): papers-scale -1.8%, products -0.3%; with B at cache size
@@ -698,18 +929,16 @@ constexpr int64_t kNtBytes = int64_t(1) << 30;
 // their longest non-split row, a chain of len / U dependent B-row load rounds; these launches keep
 // 32 (16 for 8-16 B lanes) loads in flight per lane instead of 8.  A Cora-shaped layer (max row
 // 253 nonzeros, N=16) took 25 us with U=8.  Same bits: U only changes how many loads are issued
-// ahead of the in-order adds.
-constexpr int64_t kSmallRows = 32768;
-
+// ahead of the in-order adds.  Below kSmallFormElems products the launch is the small form.
 template <typename T, typename I, int VEC>
 int launch_vec_small(const Launch& L, int lpr) {
   constexpr int U = VEC * sizeof(T) <= 4 ? 32 : 16;
   switch (lpr) {
-    case 4: return launch_cfg<T, I, Cfg<VEC, 4, U, 4, false, true, false, true>>(L);
-    case 8: return launch_cfg<T, I, Cfg<VEC, 8, U, 4, false, true, false, true>>(L);
-    case 16: return launch_cfg<T, I, Cfg<VEC, 16, U, 4, false, true, false, true>>(L);
-    case 32: return launch_cfg<T, I, Cfg<VEC, 32, U, 4, false, true, false, true>>(L);
-    case 64: return launch_cfg<T, I, Cfg<VEC, 64, U>>(L);
+    case 4: return launch_small_or_planned<T, I, Cfg<VEC, 4, U, 4, false, true, false, true>>(L);
+    case 8: return launch_small_or_planned<T, I, Cfg<VEC, 8, U, 4, false, true, false, true>>(L);
+    case 16: return launch_small_or_planned<T, I, Cfg<VEC, 16, U, 4, false, true, false, true>>(L);
+    case 32: return launch_small_or_planned<T, I, Cfg<VEC, 32, U, 4, false, true, false, true>>(L);
+    case 64: return launch_small_or_planned<T, I, Cfg<VEC, 64, U>>(L);
     default: return fail(OFX_EINVAL, "spmm_csr: unsupported lanes-per-row %d", lpr);
   }
 }
@@ -717,7 +946,8 @@ int launch_vec_small(const Launch& L, int lpr) {
 template <typename T, typename I, int VEC>
 int launch_vec(const Launch& L, int lpr, bool nt) {
   // forced variants (tests, tuning) keep the U = 8 configurations at every size
-  if (L.nrows <= kSmallRows && !nt && L.sched.variant == 0)
+  if (L.nrows <= kSmallRows && L.sched.variant == 0 &&
+      (!nt || use_small_form(L.nrows, L.nnz, L.n, L.sched)))
     return launch_vec_small<T, I, VEC>(L, lpr);
   switch (lpr) {
     case 4: return launch_cfg<T, I, Cfg<VEC, 4>>(L);
@@ -848,7 +1078,7 @@ extern "C" int ofx_spmm_csr_workspace_size(int idx_dtype, int val_dtype, int64_t
   int rc = check_common(idx_dtype, val_dtype, m, k, n, nnz);
   if (rc) return rc;
   const Schedule s = resolve_schedule(n, opts);
-  *bytes = ws_layout(m, nnz, n, acc_bytes_of(val_dtype), s).total;
+  *bytes = use_small_form(m, nnz, n, s) ? 0 : ws_layout(m, nnz, n, acc_bytes_of(val_dtype), s).total;
   return OFX_OK;
 }
 
@@ -918,6 +1148,7 @@ extern "C" int ofx_spmm_csr_plan(void* stream, int idx_dtype, int val_dtype, int
   const int64_t nrows = row_end - row_begin;
   if (nrows == 0 || n == 0) return OFX_OK;  // the launch writes nothing either
   const Schedule s = resolve_schedule(n, opts);
+  if (use_small_form(nrows, nnz, n, s)) return OFX_OK;  // the small form needs no plan
   const plan::WsLayout w = plan::ws_layout(nrows, nnz, n, acc_bytes_of(val_dtype), s);
   if (w.total == 0) return OFX_OK;  // identity work list: nothing to plan
   OFX_REQUIRE(row_ptr != nullptr, OFX_EINVAL, "spmm_csr_plan: NULL row_ptr");

@@ -228,6 +228,13 @@ def test_direct_abi_argument_checks():
     assert sz.value == 0  # every row is in the lightest degree bin: no plan, no workspace
     assert L.ofx_spmm_csr_workspace_size(5, 2, 10, 10, 128, 100000, None, ctypes.byref(sz)) == 0
     assert sz.value > 0
+    # the small form (one launch, no plan): <= 32768 rows and <= 2^20 products nnz * n
+    for m, n, nnz, small in [(32768, 16, 65536, True), (32769, 16, 65536, False),
+                             (2708, 16, 10556, True), (2708, 64, 10556, True),
+                             (2708, 128, 10556, False), (1000, 300, 3495, True),
+                             (1000, 300, 3496, False)]:
+        assert L.ofx_spmm_csr_workspace_size(5, 2, m, m, n, nnz, None, ctypes.byref(sz)) == 0
+        assert (sz.value == 0) == small, (m, n, nnz)
     rc = L.ofx_spmm_csr(None, 5, 2, 4, 4, 4, 0, None, None, None, None, 4, None, 4, 3, 2, None, 0, None)
     assert rc == _lib.OFX_EINVAL and "row range" in _lib.last_error()
     rc = L.ofx_spmm_csr_cpu(0, 5, 2, 4, 4, 4, 0, None, None, None, None, 2, None, 4, 0, 4, None)

@@ -498,3 +498,62 @@ def test_small_launch_wave_items(device, dtype, idx, n):
     out3 = ops.spmm_csr_gathered(d[0], d[1], vals_src.to(device), perm.to(device), d[3], m, k)
     torch.cuda.synchronize()
     assert_bitwise(out3, ref, "gathered values")
+
+
+@pytest.mark.parametrize("dtype,idx", [("f32", torch.int32), ("f32", torch.int64), ("bf16", torch.int32),
+                                       ("f16", torch.int64), ("f64", torch.int32)])
+@pytest.mark.parametrize("n", [1, 4, 16, 17, 33, 64, 300])
+def test_small_form_single_launch(device, dtype, idx, n):
+    """Launches of <= 32768 rows and <= 2^20 products (nnz * n) run as one kernel with no plan and
+    no workspace: light rows by one lane-group, rows above the light cut by the whole block (LDS
+    products added in nonzero order), split rows chunk by chunk with the chunk sums added in chunk
+    order.  Same bits as the oracle for every row class, the light-cut boundary, several column
+    passes (n = 300), the ordered option, row ranges, the epilogue and gathered values."""
+    rng = np.random.default_rng(900 + n)
+    budget = (1 << 20) // n
+    split = ops.default_split(n)
+    m, k = 1500, 9000
+    deg = rng.integers(0, 5, size=m)
+    light = 32  # the default cut is 2 x the group's loads in flight: 32 or 64 here
+    special = [31, 32, 33, 63, 64, 65, 128, 300, split, split + 1, 2 * split + 7, 3 * split]
+    for i, d in enumerate(special):
+        deg[17 + 97 * i] = min(d, k)
+    while deg.sum() > budget:  # keep the launch inside the small form
+        big = int(np.argmax(deg))
+        deg[big] = max(deg[big] // 2, light + 1)
+        if deg.sum() > budget:
+            deg[deg < light] = deg[deg < light] // 2
+    rp, ci, v = random_csr(m, k, deg, rng, idx, DTYPES[dtype])
+    b = random_dense(k, n, rng, DTYPES[dtype])
+    nnz = ci.numel()
+    assert nnz * n <= (1 << 20)
+    assert ops.workspace_size(idx, DTYPES[dtype], m, k, n, nnz) == 0  # the small form
+    d = (rp.to(device), ci.to(device), v.to(device), b.to(device))
+    out = fs.spmm(d[0], d[1], d[2], m, k, d[3])
+    torch.cuda.synchronize()
+    ref = oracle_spmm(rp, ci, v, b)
+    assert_bitwise(out, ref, f"{dtype} n={n}")
+    kern = ops.SpmmCsrKernel(m, k, n, nnz, idx, DTYPES[dtype], device)
+    sub = torch.full((700, n), float("nan"), dtype=DTYPES[dtype], device=device)
+    kern(*d, sub, row_begin=400, row_end=1100)
+    torch.cuda.synchronize()
+    assert_bitwise(sub, ref[400:1100], "row range")
+    bias = random_dense(1, n, rng, DTYPES[dtype])[0]
+    out2 = torch.full((m, n), float("nan"), dtype=DTYPES[dtype], device=device)
+    kern(*d, out2, bias=bias.to(device), relu=True)
+    torch.cuda.synchronize()
+    assert_bitwise(out2, oracle.bias_act(ref, to_oracle(bias), "relu", dtype=dtype), "epilogue")
+    opts = ops.make_options(ordered=True)
+    out3 = ops.spmm_csr_device(*d, m, k, options=opts)
+    torch.cuda.synchronize()
+    assert_bitwise(out3, oracle_spmm(rp, ci, v, b, ordered=True), "ordered")
+    perm = torch.from_numpy(rng.permutation(nnz).astype(np.int64)).to(idx)
+    vals_src = torch.empty_like(v)
+    vals_src[perm.long()] = v
+    out4 = ops.spmm_csr_gathered(d[0], d[1], vals_src.to(device), perm.to(device), d[3], m, k)
+    torch.cuda.synchronize()
+    assert_bitwise(out4, ref, "gathered values")
+    for cut in (1, 7, 1000):  # the light/whole-block cut moves work, never bits
+        out5 = ops.spmm_csr_device(*d, m, k, options=ops.make_options(heavy=cut))
+        torch.cuda.synchronize()
+        assert_bitwise(out5, ref, f"light cut {cut}")
