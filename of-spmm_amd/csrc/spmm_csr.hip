@@ -486,111 +486,205 @@ __global__ void __launch_bounds__(64 * K::WPB)
 // wave 0 adds them in nonzero order while the next batch's loads are in flight.  A row longer
 // than `split` runs chunk by chunk and its chunk sums are added in chunk order from +0: the bits
 // of the planned form's partials + spmm_reduce (and of the CPU kernel).
-template <typename T, typename K>
+template <typename T, typename I, typename K>
 struct SmallForm {
   using A = typename Num<T>::acc;
+  static constexpr int kThreads = 64 * K::WPB;
   static constexpr int W = K::LPR * K::VEC;               // columns per pass
   static constexpr int G = 64 / K::LPR;                   // lane-groups per wave
   static constexpr int GB = G * K::WPB;                   // lane-groups per block
   static constexpr int RPB = GB;                          // rows per block
-  static constexpr int kLdsElems = 32768 / (int)sizeof(A);  // 32 KB of products per batch
-  static constexpr int NB_RAW = kLdsElems / W < 512 ? kLdsElems / W : 512;
-  static constexpr int UW_RAW = NB_RAW / GB;
-  // loads in flight per lane: 16 or 32 ran these kernels out of registers (512 VGPRs + spills)
-  static constexpr int UW = UW_RAW > 8 ? 8 : (UW_RAW < 1 ? 1 : UW_RAW);
+  static constexpr int D = 4;                             // batches of B-row loads in flight
+  static constexpr int S = 8;                             // batches per (col, val) span
+  static constexpr int kLdsElems = 16384 / (int)sizeof(A);  // 16 KB of products per buffer
+  static constexpr int NB_RAW0 = kLdsElems / W < 128 ? kLdsElems / W : 128;
+  static constexpr int UW_RAW = NB_RAW0 / GB;
+  static constexpr int UW = UW_RAW > 8 ? 8 : (UW_RAW < 1 ? 1 : UW_RAW);  // loads per lane per batch
   static constexpr int NB = UW * GB;                      // nonzeros per batch
-  static_assert(NB * W * (int)sizeof(A) <= 32768, "small form: LDS batch too large");
+  static constexpr int SPAN = S * NB;                     // nonzeros per (col, val) span
+  static constexpr int PT = (SPAN + kThreads - 1) / kThreads;  // span entries per thread
+  // one element per lane: products column-major ([column][nonzero], rows padded by 4), so the
+  // in-order adds read 4 consecutive nonzeros per 16-B LDS read; wider lanes: row-major
+  static constexpr bool kColMajor = K::VEC == 1 && sizeof(A) == 4 && NB % 4 == 0;
+  static constexpr int NBP = NB + 4;
+  static constexpr int kBufElems = kColMajor ? W * NBP : NB * W;
+  static_assert(S % D == 0 && S > D, "small form: span must hold whole rounds of the load ring");
+  static_assert(kBufElems * (int)sizeof(A) <= 16384 + 4 * W * (int)sizeof(A),
+                "small form: LDS batch too large");
+};
+
+// Shared memory of the small form: two product buffers and two (col, val) span buffers.
+template <typename T, typename I, typename K>
+struct SmallLds {
+  using SF = SmallForm<T, I, K>;
+  using A = typename Num<T>::acc;
+  A prod[2 * SF::kBufElems];
+  A sval[2 * SF::SPAN];
+  I scol[2 * SF::SPAN];
 };
 
 // acc[e] (valid in wave 0, group 0) = sum over j in [j0, j1) of val[j] * B[col[j], cc + e], in
 // ascending j from +0, computed by the whole block (see above).  Every thread of the block calls
 // this with the same j0/j1.
+//   (col, val) of S batches (a span) are loaded coalesced by the whole block into LDS, one span
+//   ahead; every other load has a fixed place in the schedule (rows past j1 read B row 0 and
+//   are dropped), so a wait for one batch's B rows never waits for a younger batch's.
+//   B rows: a ring of D batches in flight per lane; batch k + D is issued right after batch k's
+//   products are in LDS.
+//   Products of consecutive batches alternate between two LDS buffers, so one barrier per batch
+//   orders the writes of batch k against the adds of batch k (after it) and of batch k - 1.
 template <typename T, typename I, typename K>
 __device__ __forceinline__ void block_accumulate(const I* __restrict__ col,
                                                  const T* __restrict__ val,
                                                  const I* __restrict__ vperm,
                                                  const T* __restrict__ Bs, int64_t ldb,
                                                  int64_t j0, int64_t j1, int gb, int gl,
-                                                 bool chain, typename Num<T>::acc* lds,
+                                                 bool chain, SmallLds<T, I, K>& sh,
                                                  typename Num<T>::acc (&acc)[K::VEC]) {
 #pragma clang fp contract(off)
-  using SF = SmallForm<T, K>;
+  using SF = SmallForm<T, I, K>;
   using A = typename Num<T>::acc;
   using P = Pack<T, K::VEC>;
-  constexpr int VEC = K::VEC, W = SF::W, GB = SF::GB, UW = SF::UW, NB = SF::NB;
-  // nonzero i of a batch is loaded by lane-group i % GB, in its slot i / GB
-  auto load_cv = [&](int64_t jb, I (&c)[UW], A (&v)[UW]) {
+  using PA = Pack<A, K::VEC>;
+  constexpr int VEC = K::VEC, W = SF::W, GB = SF::GB, UW = SF::UW, NB = SF::NB, NBP = SF::NBP;
+  constexpr int D = SF::D, S = SF::S, SPAN = SF::SPAN, PT = SF::PT, NT = SF::kThreads;
+  const int tid = threadIdx.x;
+  const int64_t nb = (j1 - j0 + NB - 1) / NB;  // batches
+  // span s: nonzeros [j0 + s*SPAN, j0 + (s+1)*SPAN)
+  auto span_load = [&](int64_t s, I (&c)[PT], A (&v)[PT]) {
 #pragma unroll
-    for (int u = 0; u < UW; ++u) {
-      const int64_t j = jb + (int64_t)GB * u + gb;
-      c[u] = 0;
-      v[u] = A(0);
-      if (j < j1) {
-        c[u] = col[j];
-        v[u] = Num<T>::load(val[vperm ? (int64_t)vperm[j] : j]);
+    for (int p = 0; p < PT; ++p) {
+      const int e = p * NT + tid < SPAN ? p * NT + tid : SPAN - 1;
+      const int64_t j = j0 + s * SPAN + e;
+      // past j1: nonzero j1 - 1 again (a valid row; its products are never added)
+      const int64_t jc = j < j1 ? j : j1 - 1;
+      c[p] = col[jc];
+      v[p] = Num<T>::load(val[vperm ? (int64_t)vperm[jc] : jc]);
+    }
+  };
+  auto span_store = [&](int64_t s, const I (&c)[PT], const A (&v)[PT]) {
+    const int off = (int)(s & 1) * SPAN;
+#pragma unroll
+    for (int p = 0; p < PT; ++p) {
+      if (p * NT + tid < SPAN) {
+        sh.scol[off + p * NT + tid] = c[p];
+        sh.sval[off + p * NT + tid] = v[p];
       }
     }
   };
-  I cn[UW];
-  A vn[UW], vc[UW];
-  P bv[UW];
-  load_cv(j0, cn, vn);
+  I rc[PT];  // the next span's (col, val), in flight until staged
+  A rv[PT];
+  // B rows of batch kb (B row 0 for a batch past the end: its span buffer may hold anything)
+  auto issue = [&](int64_t kb, P (&b)[UW]) {
+    const int off = (int)((kb / S) & 1) * SPAN + (int)(kb % S) * NB;
+    const int64_t live = -(int64_t)(kb < nb);
 #pragma unroll
-  for (int u = 0; u < UW; ++u) {
-    bv[u] = ld_brow<K::BNT, P>(Bs + (int64_t)cn[u] * ldb);
-    vc[u] = vn[u];
-  }
-  if (j0 + NB < j1) load_cv(j0 + NB, cn, vn);
-  for (int64_t jb = j0; jb < j1; jb += NB) {
-    const int cnt = (int)((j1 - jb) < NB ? (j1 - jb) : NB);
-    A pr[UW][VEC];
+    for (int u = 0; u < UW; ++u) {
+      const int64_t c = (int64_t)sh.scol[off + GB * u + gb] & live;
+      b[u] = ld_brow<K::BNT, P>(Bs + c * ldb);
+    }
+  };
+  // batch k: products of the B rows in `b` -> LDS; (span staging); barrier; B rows of batch
+  // k + D -> `b`; the in-order adds of batch k (wave 0, group 0)
+  auto step = [&](int64_t k, P (&b)[UW], bool stage) {
+    const int cnt = (int)((j1 - j0 - k * NB) < NB ? (j1 - j0 - k * NB) : NB);
+    A* buf = sh.prod + (int)(k & 1) * SF::kBufElems;
+    const int voff = (int)((k / S) & 1) * SPAN + (int)(k % S) * NB;
+    A vv[UW];
 #pragma unroll
-    for (int u = 0; u < UW; ++u)
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) pr[u][e] = Num<T>::mul(vc[u], Num<T>::load(bv[u].v[e]));
-    __syncthreads();  // the previous batch's adds have read the LDS products
+    for (int u = 0; u < UW; ++u) vv[u] = sh.sval[voff + GB * u + gb];
 #pragma unroll
     for (int u = 0; u < UW; ++u) {
       const int i = GB * u + gb;
-      if (i < cnt) {
-        if constexpr (VEC * sizeof(A) == 16 || VEC * sizeof(A) == 8) {
-          Pack<A, VEC> o;
+      A pr[VEC];
 #pragma unroll
-          for (int e = 0; e < VEC; ++e) o.v[e] = pr[u][e];
-          *reinterpret_cast<Pack<A, VEC>*>(lds + i * W + gl * VEC) = o;
-        } else {
+      for (int e = 0; e < VEC; ++e) pr[e] = Num<T>::mul(vv[u], Num<T>::load(b[u].v[e]));
+      if constexpr (SF::kColMajor) {
+        buf[gl * NBP + i] = pr[0];
+      } else if constexpr (VEC * sizeof(A) == 16 || VEC * sizeof(A) == 8) {
+        PA o;
 #pragma unroll
-          for (int e = 0; e < VEC; ++e) lds[i * W + gl * VEC + e] = pr[u][e];
+        for (int e = 0; e < VEC; ++e) o.v[e] = pr[e];
+        *reinterpret_cast<PA*>(buf + i * W + gl * VEC) = o;
+      } else {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) buf[i * W + gl * VEC + e] = pr[e];
+      }
+    }
+    // stage (k % S == S - D): batch k + D opens the next span, which goes to LDS now (its loads
+    // were issued a span earlier), and the span after it starts loading
+    if (stage) span_store((k + D) / S, rc, rv);
+    __syncthreads();
+    if (stage) span_load((k + D) / S + 1, rc, rv);
+    issue(k + D, b);
+    if (chain) {
+      int i = 0;
+      if constexpr (SF::kColMajor) {
+        // column gl: 4 consecutive nonzeros per 16-B read, 8 reads in flight
+        const A* cp = buf + gl * NBP;
+        for (; i + 32 <= cnt; i += 32) {
+          Pack<A, 4> x[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) x[q] = *reinterpret_cast<const Pack<A, 4>*>(cp + i + 4 * q);
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[0] = acc[0] + x[q].v[e];
+        }
+        for (; i < cnt; ++i) acc[0] = acc[0] + cp[i];
+      } else {
+        for (; i + 16 <= cnt; i += 16) {
+          PA x[16];
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+            x[q] = *reinterpret_cast<const PA*>(buf + (i + q) * W + gl * VEC);
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + x[q].v[e];
+        }
+        for (; i < cnt; ++i) {
+          const PA x = *reinterpret_cast<const PA*>(buf + i * W + gl * VEC);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + x.v[e];
         }
       }
     }
-    __syncthreads();
-    if (jb + NB < j1) {  // the next batch's B rows are in flight during this batch's adds
-#pragma unroll
-      for (int u = 0; u < UW; ++u) {
-        bv[u] = ld_brow<K::BNT, P>(Bs + (int64_t)cn[u] * ldb);
-        vc[u] = vn[u];
-      }
-      if (jb + 2 * NB < j1) load_cv(jb + 2 * NB, cn, vn);
-    }
-    if (chain) {
-      int i = 0;
-      for (; i + 8 <= cnt; i += 8) {
-        Pack<A, VEC> x[8];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) x[t] = *reinterpret_cast<const Pack<A, VEC>*>(lds + (i + t) * W + gl * VEC);
-#pragma unroll
-        for (int t = 0; t < 8; ++t)
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + x[t].v[e];
-      }
-      for (; i < cnt; ++i) {
-        const Pack<A, VEC> x = *reinterpret_cast<const Pack<A, VEC>*>(lds + i * W + gl * VEC);
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + x.v[e];
-      }
-    }
+  };
+  span_load(0, rc, rv);
+  span_store(0, rc, rv);
+  __syncthreads();
+  span_load(1, rc, rv);  // stored when batch S is first issued
+  // the ring: four named register sets, so batch k's rows stay in flight until step k
+  static_assert(D == 4, "small form: the load ring below is written out for D = 4");
+  P b0[UW], b1[UW], b2[UW], b3[UW];
+  issue(0, b0);
+  issue(1, b1);
+  issue(2, b2);
+  issue(3, b3);
+  // whole spans: no guards, the same loads outstanding at every step of every span (and at the
+  // loop entry), so each step's wait covers exactly its own batch
+  static_assert(S == 2 * D, "small form: a span is two turns of the ring");
+  int64_t k0 = 0;
+  for (; k0 + S <= nb; k0 += S) {
+    step(k0 + 0, b0, false);
+    step(k0 + 1, b1, false);
+    step(k0 + 2, b2, false);
+    step(k0 + 3, b3, false);
+    step(k0 + 4, b0, true);
+    step(k0 + 5, b1, false);
+    step(k0 + 6, b2, false);
+    step(k0 + 7, b3, false);
   }
+  // the last, partial span (its batches were staged by the loop or the prologue)
+  if (k0 + 0 < nb) step(k0 + 0, b0, false);
+  if (k0 + 1 < nb) step(k0 + 1, b1, false);
+  if (k0 + 2 < nb) step(k0 + 2, b2, false);
+  if (k0 + 3 < nb) step(k0 + 3, b3, false);
+  if (k0 + 4 < nb) step(k0 + 4, b0, false);
+  if (k0 + 5 < nb) step(k0 + 5, b1, false);
+  if (k0 + 6 < nb) step(k0 + 6, b2, false);
+  __syncthreads();  // the next call's first batch writes buffer 0, which the adds may still read
 }
 
 template <typename T, typename I, typename K>
@@ -600,10 +694,10 @@ __global__ void __launch_bounds__(64 * K::WPB)
                       const T* __restrict__ B, int64_t ldb, T* __restrict__ C, int64_t ldc,
                       int64_t row_begin, int64_t nrows, int64_t n, int64_t split, int64_t chunk,
                       int64_t light, const T* __restrict__ bias, int act) {
-  using SF = SmallForm<T, K>;
+  using SF = SmallForm<T, I, K>;
   using A = typename Num<T>::acc;
   constexpr int VEC = K::VEC, LPR = K::LPR, W = SF::W, RPB = SF::RPB;
-  __shared__ __attribute__((aligned(16))) A lds[SF::NB * W];
+  __shared__ __attribute__((aligned(16))) SmallLds<T, I, K> lds;
   __shared__ int heavy_rows[RPB];
   __shared__ int nheavy;
   const int lane = threadIdx.x & 63;
@@ -896,7 +990,7 @@ bool use_small_form(int64_t nrows, int64_t nnz, int64_t n, const Schedule& s) {
 
 template <typename T, typename I, typename K>
 int launch_small(const Launch& L) {
-  using SF = SmallForm<T, K>;
+  using SF = SmallForm<T, I, K>;
   // options.heavy_threshold > 0 overrides the light/whole-block cut (tuning; no numeric effect)
   const int64_t light =
       (L.sched.heavy > 0 && L.sched.heavy != INT64_MAX) ? L.sched.heavy : (int64_t)kSmallLight * K::U;
