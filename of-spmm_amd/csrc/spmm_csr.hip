@@ -1,30 +1,12 @@
-// spmm_csr.hip — CSR x dense SpMM for CDNA4 (gfx950), the hot path behind op "spmm_csr".
+// spmm_csr.hip — the C-ABI of the CSR x dense SpMM forward (op "spmm_csr") and its small helper
+// kernels (CSR validation, row slices, synthetic dense inputs).  The forward kernels themselves
+// (plan / main / small form / reduce) are in spmm_csr_impl.h, compiled once per
+// (value, index) type pair in spmm_inst_*.hip and dispatched from here through launch_typed.
 //
 // Reference semantics (OneFlow has no SpMM): the composition
 //   gather rows B[col[j]]      oneflow/user/kernels/gather_kernel_util.cpp:72-92
 //   multiply by val[j]
 //   unsorted_segment_sum       oneflow/user/kernels/unsorted_segment_sum_kernel_util.cpp:29-45
-// without materialising the nnz x N intermediate and without the CUDA path's atomics
-// (unsorted_segment_sum_kernel_util.cu:67), which are non-deterministic.  Width dispatch and
-// 64-bit addressing follow the intent of gather_kernel_util.cu:29-107.
-//
-// Layout on the device: row_ptr I[m+1], col_idx I[nnz], values T[nnz],
-// B T[k][ldb] row-major, C T[rows][ldc] row-major.
-//
-// Kernels:
-//   spmm_plan_*  count / scan / write: classify rows (hub = longer than the split threshold,
-//                else one of 4 degree bins), lay out the work list: hub chunks first, then the
-//                other rows heaviest bin first (stable counting sort; deterministic layout).
-//   spmm_main    the dominant launch.  One lane-group (LPR lanes) per work item; each lane owns
-//                VEC consecutive columns (16-B loads of B rows); col/val are loaded cooperatively
-//                (LPR < 64: coalesced, broadcast by ds_bpermute) or as wave-uniform scalar loads
-//                (LPR == 64); U B-row loads are in flight per lane before the in-order
-//                multiply-adds.  Hub chunks -> fp32/fp64 partial rows; rows -> C directly.
-//                Small launches: hub chunks and heavy rows take a whole wave each, its groups
-//                interleaving the nonzeros and adding the products in order (accumulate_wave).
-//   spmm_reduce  per hub row: sums its chunk partials in chunk order -> C row.
-// Every output element is produced by exactly one lane in a fixed order: results are
-// bitwise deterministic and equal to the CPU kernel / oracle with the same schedule.
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
@@ -36,825 +18,12 @@
 #include "ofx_internal.h"
 #include "spmm_common.h"
 #include "spmm_plan.h"
+#include "spmm_launch.h"
 
 namespace ofx {
 namespace {
 
-using plan::WorkList;
-using plan::WsLayout;
-using plan::launch_plan;
 using plan::ws_layout;
-
-constexpr int kBlock = 256;        // 4 waves
-constexpr int64_t kMaxReduceBlocks = 16384;
-
-template <typename T, int VEC>
-struct alignas(sizeof(T) * VEC) Pack {
-  T v[VEC];
-};
-
-// Compile-time kernel configuration: VEC elements per lane, LPR lanes per row-group, U B-row
-// loads in flight per lane, WPB waves per block, NT = non-temporal hints on the once-touched
-// streams (col_idx, values, C) so they do not displace B rows from L2 / Infinity Cache.
-// PF: the next batch's (col, val) pairs are loaded before this batch's B rows, so a long row
-// pays one memory round trip per batch instead of two (the small-problem configurations).
-// BNT: the B-row loads themselves carry the non-temporal hint (tuning variants only).
-// WH: small launches: hub chunks and heavy rows take a whole wave each (the wave's 64/LPR groups
-// interleave the nonzeros of one item), the light rows one group each (accumulate_wave).
-template <int VEC_, int LPR_, int U_ = 8, int WPB_ = 4, bool NT_ = false, bool PF_ = false,
-          bool BNT_ = false, bool WH_ = false>
-struct Cfg {
-  static constexpr int VEC = VEC_, LPR = LPR_, U = U_, WPB = WPB_;
-  static constexpr bool NT = NT_, PF = PF_, BNT = BNT_, WH = WH_;
-  // loads in flight per lane of the wave-item form: G * UW * VEC cross-lane moves per batch are
-  // unrolled, so UW keeps that at <= 256 (4..32)
-  static constexpr int G = LPR < 64 ? 64 / LPR : 1;
-  static constexpr int UW_RAW = 256 / (G * VEC);
-  static constexpr int UW = UW_RAW > 32 ? 32 : (UW_RAW < 4 ? 4 : UW_RAW);
-};
-
-template <typename X>
-struct RawOf {
-  using type = X;
-};
-template <>
-struct RawOf<bf16> {
-  using type = uint16_t;
-};
-template <>
-struct RawOf<f16> {
-  using type = uint16_t;
-};
-
-template <bool NT, typename X>
-__device__ __forceinline__ X ld_stream(const X* p) {
-  if constexpr (NT) {
-    using R = typename RawOf<X>::type;
-    const R r = __builtin_nontemporal_load(reinterpret_cast<const R*>(p));
-    return __builtin_bit_cast(X, r);
-  } else {
-    return *p;
-  }
-}
-
-template <int BYTES>
-struct RawVec;
-template <>
-struct RawVec<16> {
-  typedef uint32_t type __attribute__((ext_vector_type(4)));
-};
-template <>
-struct RawVec<8> {
-  typedef uint32_t type __attribute__((ext_vector_type(2)));
-};
-template <>
-struct RawVec<4> {
-  typedef uint32_t type;
-};
-template <>
-struct RawVec<2> {
-  typedef uint16_t type;
-};
-
-// One B-row slice of a lane (a Pack of VEC elements), optionally with the non-temporal hint.
-template <bool BNT, typename P>
-__device__ __forceinline__ P ld_brow(const void* p) {
-  if constexpr (BNT && (sizeof(P) == 16 || sizeof(P) == 8 || sizeof(P) == 4 || sizeof(P) == 2)) {
-    using R = typename RawVec<sizeof(P)>::type;
-    return __builtin_bit_cast(P, __builtin_nontemporal_load(reinterpret_cast<const R*>(p)));
-  } else {
-    return *reinterpret_cast<const P*>(p);
-  }
-}
-
-__device__ __forceinline__ int32_t shfl(int32_t v, int src) { return __shfl(v, src); }
-__device__ __forceinline__ int64_t shfl(int64_t v, int src) {
-  return (int64_t)__shfl((long long)v, src);
-}
-__device__ __forceinline__ float shfl(float v, int src) { return __shfl(v, src); }
-__device__ __forceinline__ double shfl(double v, int src) { return __shfl(v, src); }
-
-__device__ __forceinline__ int64_t uniform64(int64_t v) {
-  const uint64_t u = (uint64_t)v;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-
-// acc[e] += val[j] * B[col[j], cc + e] for j in [j0, j1), in ascending j, mul then add.
-// Bc = B + cc.  All lanes of a group call this with the same j0/j1.
-template <typename T, typename I, typename K>
-__device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* __restrict__ val,
-                                           const I* __restrict__ vperm,
-                                           const T* __restrict__ Bc, const T* __restrict__ B0,
-                                           int64_t ldb, int64_t j0,
-                                           int64_t j1, int gl, int gbase, bool active,
-                                           typename Num<T>::acc (&acc)[K::VEC]) {
-#pragma clang fp contract(off)
-  constexpr int VEC = K::VEC, LPR = K::LPR, kUnroll = K::U;
-  using A = typename Num<T>::acc;
-  using P = Pack<T, VEC>;
-  if constexpr (LPR == 64) {
-    // j0/j1 are wave-uniform: col/val come through the scalar cache.
-    for (int64_t j = j0; j < j1; j += kUnroll) {
-      const int cnt = (int)((j1 - j) < kUnroll ? (j1 - j) : kUnroll);
-      P bv[kUnroll];
-      A vv[kUnroll];
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        if (u < cnt) {
-          const int64_t cu = (int64_t)ld_stream<K::NT>(col + j + u);
-          const int64_t jv = vperm ? (int64_t)ld_stream<K::NT>(vperm + j + u) : j + u;
-          vv[u] = Num<T>::load(ld_stream<K::NT>(val + jv));
-          if (active) bv[u] = ld_brow<K::BNT, P>(Bc + cu * ldb);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        if (u < cnt && active) {
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + Num<T>::mul(vv[u], Num<T>::load(bv[u].v[e]));
-        }
-      }
-    }
-  } else {
-    // A batch is R * LPR nonzeros: each lane loads R (col, val) pairs coalesced, the group
-    // broadcasts them with ds_bpermute.  R > 1 only when more B-row loads are kept in flight
-    // than there are lanes in the group (kUnroll > LPR: the small-problem configurations).
-    constexpr int R = kUnroll > LPR ? kUnroll / LPR : 1;
-    constexpr int BATCH = LPR * R;
-    auto load_batch = [&](int64_t jb, I (&c)[R], A (&v)[R]) {
-      const int n_ = (int)((j1 - jb) < BATCH ? (j1 - jb) : BATCH);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        c[r] = 0;
-        v[r] = 0;
-        const int idx = r * LPR + gl;
-        if (idx < n_) {
-          c[r] = ld_stream<K::NT>(col + jb + idx);
-          const int64_t jv = vperm ? (int64_t)ld_stream<K::NT>(vperm + jb + idx) : jb + idx;
-          v[r] = Num<T>::load(ld_stream<K::NT>(val + jv));
-        }
-      }
-    };
-    I nxc[R];
-    A nxv[R];
-    if constexpr (K::PF) {
-      if (j0 < j1) load_batch(j0, nxc, nxv);
-    }
-    for (int64_t jb = j0; jb < j1; jb += BATCH) {
-      const int cnt = (int)((j1 - jb) < BATCH ? (j1 - jb) : BATCH);
-      I myc[R];
-      A myv[R];
-      if constexpr (K::PF) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          myc[r] = nxc[r];
-          myv[r] = nxv[r];
-        }
-        if (jb + BATCH < j1) load_batch(jb + BATCH, nxc, nxv);  // in flight during this batch
-      } else {
-        load_batch(jb, myc, myv);
-      }
-      for (int k = 0; k < cnt; k += kUnroll) {
-        P bv[kUnroll];
-        A vv[kUnroll];
-        if constexpr (K::PF) {
-          // Branch-free issue for the latency-bound small launches: every broadcast first, then
-          // every load (slots past the row end read B row 0, inactive lanes read from B's first
-          // columns; both discarded below), so the group pays one LDS wait and one memory round
-          // trip per batch instead of one ds_bpermute wait per load.
-          int64_t cuv[kUnroll];
-#pragma unroll
-          for (int u = 0; u < kUnroll; ++u) {
-            const int src = gbase + ((k + u) & (LPR - 1));
-            const int r = R > 1 ? u / LPR : 0;
-            cuv[u] = (int64_t)shfl(myc[r], src);
-            vv[u] = shfl(myv[r], src);
-          }
-          const T* Bs = active ? Bc : B0;
-#pragma unroll
-          for (int u = 0; u < kUnroll; ++u)
-            bv[u] = ld_brow<K::BNT, P>(Bs + (k + u < cnt ? cuv[u] : 0) * ldb);
-        } else {
-#pragma unroll
-          for (int u = 0; u < kUnroll; ++u) {
-            // R > 1: the batch is exactly kUnroll long, so k == 0 and the register is static
-            const int src = gbase + ((k + u) & (LPR - 1));
-            const int r = R > 1 ? u / LPR : 0;
-            const int64_t cu = (int64_t)shfl(myc[r], src);
-            vv[u] = shfl(myv[r], src);
-            if (k + u < cnt && active) bv[u] = ld_brow<K::BNT, P>(Bc + cu * ldb);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-          if (k + u < cnt && active) {
-#pragma unroll
-            for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + Num<T>::mul(vv[u], Num<T>::load(bv[u].v[e]));
-          }
-        }
-      }
-    }
-  }
-}
-
-// One work item for the whole wave (LPR < 64): group q = lane / LPR of the G = 64 / LPR groups
-// loads the B rows of nonzeros jb + G*u + q of each batch of G*U, forms their products in
-// parallel (U loads in flight per lane, the batch's (col, val) prefetched during the previous
-// one), then every group adds all G*U products in nonzero order, taking the other groups'
-// products through ds_bpermute.  The order (and each product's rounding) is the contract's, so
-// the bits equal the one-group traversal; a long row needs G times fewer dependent load rounds.
-template <typename T, typename I, typename K>
-__device__ __forceinline__ void accumulate_wave(const I* __restrict__ col, const T* __restrict__ val,
-                                                const I* __restrict__ vperm,
-                                                const T* __restrict__ Bc, const T* __restrict__ B0,
-                                                int64_t ldb, int64_t j0, int64_t j1, int lane,
-                                                int gl, bool active,
-                                                typename Num<T>::acc (&acc)[K::VEC]) {
-#pragma clang fp contract(off)
-  constexpr int VEC = K::VEC, LPR = K::LPR, U = K::UW, G = 64 / LPR;
-  constexpr int BATCH = G * U;
-  constexpr int R = (BATCH + 63) / 64;  // (col, val) registers per lane for one batch
-  static_assert(LPR < 64, "accumulate_wave needs several groups per wave");
-  using A = typename Num<T>::acc;
-  using P = Pack<T, VEC>;
-  const int q = lane / LPR;
-  auto load_batch = [&](int64_t jb, I (&c)[R], A (&v)[R]) {
-    const int n_ = (int)((j1 - jb) < BATCH ? (j1 - jb) : BATCH);
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      c[r] = 0;
-      v[r] = 0;
-      const int idx = r * 64 + lane;
-      if (idx < n_) {
-        c[r] = col[jb + idx];
-        const int64_t jv = vperm ? (int64_t)vperm[jb + idx] : jb + idx;
-        v[r] = Num<T>::load(val[jv]);
-      }
-    }
-  };
-  I nxc[R];
-  A nxv[R];
-  if (j0 < j1) load_batch(j0, nxc, nxv);
-  const T* Bs = active ? Bc : B0;
-  for (int64_t jb = j0; jb < j1; jb += BATCH) {
-    const int cnt = (int)((j1 - jb) < BATCH ? (j1 - jb) : BATCH);
-    I myc[R];
-    A myv[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      myc[r] = nxc[r];
-      myv[r] = nxv[r];
-    }
-    if (jb + BATCH < j1) load_batch(jb + BATCH, nxc, nxv);  // in flight during this batch
-    // this group's nonzeros of the batch: i = G*u + q, held by lane i % 64 in register i / 64
-    // G divides 64, so nonzero G*u + q sits in register (G*u) / 64 for every group q
-    I cuv[U];
-    A vv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = G * u + q;
-      cuv[u] = shfl(myc[(G * u) >> 6], i & 63);
-      vv[u] = shfl(myv[(G * u) >> 6], i & 63);
-    }
-    P bv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      bv[u] = ld_brow<K::BNT, P>(Bs + (G * u + q < cnt ? (int64_t)cuv[u] : 0) * ldb);
-    // per u: this group's product, the G groups' products fetched with ds_bpermute (all issued
-    // before the first add, so their latency overlaps), then added in nonzero order
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      A pr[VEC];
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) pr[e] = Num<T>::mul(vv[u], Num<T>::load(bv[u].v[e]));
-      A x[G][VEC];
-#pragma unroll
-      for (int g2 = 0; g2 < G; ++g2)
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) x[g2][e] = shfl(pr[e], g2 * LPR + gl);
-#pragma unroll
-      for (int g2 = 0; g2 < G; ++g2)
-        if (G * u + g2 < cnt)
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + x[g2][e];
-    }
-  }
-}
-
-template <typename T, int VEC, bool NT>
-__device__ __forceinline__ void store_row(T* __restrict__ p, const typename Num<T>::acc (&acc)[VEC],
-                                          const T* __restrict__ bias, int act) {
-  Pack<T, VEC> o;
-  if (bias == nullptr && act == OFX_ACT_NONE) {  // uniform: the plain op pays one branch
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) o.v[e] = Num<T>::store(acc[e]);
-  } else {
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) o.v[e] = epilogue<T>(acc[e], bias, e, act);
-  }
-  if constexpr (NT && (sizeof(o) == 16 || sizeof(o) == 8 || sizeof(o) == 4 || sizeof(o) == 2)) {
-    using R = typename RawVec<sizeof(o)>::type;
-    __builtin_nontemporal_store(__builtin_bit_cast(R, o), reinterpret_cast<R*>(p));
-  } else {
-    *reinterpret_cast<Pack<T, VEC>*>(p) = o;
-  }
-}
-
-template <typename A, int VEC>
-__device__ __forceinline__ void store_partial(A* __restrict__ p, const A (&acc)[VEC]) {
-#pragma unroll
-  for (int e = 0; e < VEC; ++e) p[e] = acc[e];
-}
-
-// ---- main kernel: one work list = hub chunks, then rows in bin order ------------------------
-// Without a plan (`order` == nullptr) the list is simply the rows in index order.
-template <typename T, typename I, typename K>
-__global__ void __launch_bounds__(64 * K::WPB)
-    spmm_main_kernel(const I* __restrict__ rp, const I* __restrict__ col,
-                     const T* __restrict__ val, const I* __restrict__ vperm,
-                     const T* __restrict__ B, int64_t ldb,
-                     T* __restrict__ C, int64_t ldc, int64_t row_begin, int64_t nrows, int64_t n,
-                     int64_t chunk, const unsigned long long* __restrict__ counters,
-                     const int64_t* __restrict__ items, const int64_t* __restrict__ order,
-                     typename Num<T>::acc* __restrict__ part, const T* __restrict__ bias,
-                     int act, int64_t wave_blocks) {
-  using A = typename Num<T>::acc;
-  constexpr int VEC = K::VEC, LPR = K::LPR, kWaves = K::WPB;
-  constexpr int GPW = 64 / LPR;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int gl = lane & (LPR - 1);
-  const int gbase = lane & ~(LPR - 1);
-  const int gsub = LPR == 64 ? 0 : lane / LPR;
-  if constexpr (K::WH && LPR < 64) {
-    // blocks [0, wave_blocks): one wave per hub chunk / heavy row (the plan's first items)
-    if ((int64_t)blockIdx.x < wave_blocks) {
-      const int64_t w = (int64_t)blockIdx.x * kWaves + wave;
-      const int64_t nchunks = (int64_t)counters[0];
-      const int64_t nheavy = (int64_t)counters[3] - (int64_t)counters[2];  // bin 0
-      if (w >= nchunks + nheavy) return;
-      int64_t wr, wc = -1;
-      if (w < nchunks) {
-        wr = items[2 * w + 0];
-        wc = items[2 * w + 1];
-      } else {
-        wr = order[w - nchunks];
-      }
-      wr = uniform64(wr);
-      wc = uniform64(wc);
-      const int64_t rs = (int64_t)rp[row_begin + wr];
-      const int64_t re = (int64_t)rp[row_begin + wr + 1];
-      int64_t j0 = rs, j1 = re;
-      if (wc >= 0) {
-        j0 = rs + wc * chunk;
-        j1 = (re - j0 - chunk < chunk) ? re : j0 + chunk;
-      }
-      for (int64_t c0 = 0; c0 < n; c0 += (int64_t)LPR * VEC) {
-        const int64_t cc = c0 + (int64_t)gl * VEC;
-        const bool active = cc < n;
-        A acc[VEC];
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) acc[e] = A(0);
-        accumulate_wave<T, I, K>(col, val, vperm, B + cc, B, ldb, j0, j1, lane, gl, active, acc);
-        if (active && gsub == 0) {
-          if (wc >= 0)
-            store_partial<A, VEC>(part + w * n + cc, acc);
-          else
-            store_row<T, VEC, K::NT>(C + wr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
-        }
-      }
-      return;
-    }
-  }
-  // one lane-group per work item; in the WH form these are the light rows after the wave items
-  int64_t g = ((int64_t)(blockIdx.x - (K::WH ? wave_blocks : 0)) * kWaves + wave) * GPW + gsub;
-  if constexpr (K::WH && LPR < 64) {
-    if (order != nullptr) g += (int64_t)counters[0] + (int64_t)counters[3] - (int64_t)counters[2];
-  }
-  int64_t lr, c = -1;  // local row; chunk index or -1 for a whole row
-  if (order == nullptr) {
-    if (g >= nrows) return;
-    lr = g;
-  } else {
-    const int64_t nchunks = (int64_t)counters[0];
-    if (g < nchunks) {
-      lr = items[2 * g + 0];
-      c = items[2 * g + 1];
-    } else {
-      const int64_t q = g - nchunks;
-      if (q >= nrows - (int64_t)counters[1]) return;
-      lr = order[q];
-    }
-  }
-  if constexpr (LPR == 64) {
-    lr = uniform64(lr);
-    c = uniform64(c);
-  }
-  const int64_t rs = (int64_t)rp[row_begin + lr];
-  const int64_t re = (int64_t)rp[row_begin + lr + 1];
-  int64_t j0 = rs, j1 = re;
-  if (c >= 0) {
-    // chunk c of num_chunks(len, chunk) = len / chunk; the last one (fewer than 2 * chunk
-    // nonzeros left from its start) takes the remainder.  No 64-bit division per work item.
-    j0 = rs + c * chunk;
-    j1 = (re - j0 - chunk < chunk) ? re : j0 + chunk;
-  }
-  for (int64_t c0 = 0; c0 < n; c0 += (int64_t)LPR * VEC) {
-    const int64_t cc = c0 + (int64_t)gl * VEC;
-    const bool active = cc < n;
-    A acc[VEC];
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) acc[e] = A(0);
-    accumulate<T, I, K>(col, val, vperm, B + cc, B, ldb, j0, j1, gl, gbase, active, acc);
-    if (active) {
-      if (c >= 0)
-        store_partial<A, VEC>(part + g * n + cc, acc);
-      else
-        store_row<T, VEC, K::NT>(C + lr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
-    }
-  }
-}
-
-// ---- small form: one launch, no plan, no workspace -------------------------------------------
-// Launches with few rows and little B-row traffic (use_small_form) run as ONE kernel.  Block b
-// owns rows [b*RPB, (b+1)*RPB), one lane-group per row.  A group takes its row when the row has at
-// most `light` nonzeros and is not split (accumulate, the group form).  The block's longer rows
-// are then taken one at a time by the whole block: each of its GB lane-groups loads the B rows of
-// a strided share of a batch of NB nonzeros, the products go to LDS, and the first lane-group of
-// wave 0 adds them in nonzero order while the next batch's loads are in flight.  A row longer
-// than `split` runs chunk by chunk and its chunk sums are added in chunk order from +0: the bits
-// of the planned form's partials + spmm_reduce (and of the CPU kernel).
-template <typename T, typename I, typename K>
-struct SmallForm {
-  using A = typename Num<T>::acc;
-  static constexpr int kThreads = 64 * K::WPB;
-  static constexpr int W = K::LPR * K::VEC;               // columns per pass
-  static constexpr int G = 64 / K::LPR;                   // lane-groups per wave
-  static constexpr int GB = G * K::WPB;                   // lane-groups per block
-  static constexpr int RPB = GB;                          // rows per block
-  static constexpr int D = 4;                             // batches of B-row loads in flight
-  static constexpr int S = 8;                             // batches per (col, val) span
-  static constexpr int kLdsElems = 16384 / (int)sizeof(A);  // 16 KB of products per buffer
-  static constexpr int NB_RAW0 = kLdsElems / W < 128 ? kLdsElems / W : 128;
-  static constexpr int UW_RAW = NB_RAW0 / GB;
-  static constexpr int UW = UW_RAW > 8 ? 8 : (UW_RAW < 1 ? 1 : UW_RAW);  // loads per lane per batch
-  static constexpr int NB = UW * GB;                      // nonzeros per batch
-  static constexpr int SPAN = S * NB;                     // nonzeros per (col, val) span
-  static constexpr int PT = (SPAN + kThreads - 1) / kThreads;  // span entries per thread
-  // one element per lane: products column-major ([column][nonzero], rows padded by 4), so the
-  // in-order adds read 4 consecutive nonzeros per 16-B LDS read; wider lanes: row-major
-  static constexpr bool kColMajor = K::VEC == 1 && sizeof(A) == 4 && NB % 4 == 0;
-  static constexpr int NBP = NB + 4;
-  static constexpr int kBufElems = kColMajor ? W * NBP : NB * W;
-  static_assert(S % D == 0 && S > D, "small form: span must hold whole rounds of the load ring");
-  static_assert(kBufElems * (int)sizeof(A) <= 16384 + 4 * W * (int)sizeof(A),
-                "small form: LDS batch too large");
-};
-
-// Shared memory of the small form: two product buffers and two (col, val) span buffers.
-template <typename T, typename I, typename K>
-struct SmallLds {
-  using SF = SmallForm<T, I, K>;
-  using A = typename Num<T>::acc;
-  A prod[2 * SF::kBufElems];
-  A sval[2 * SF::SPAN];
-  I scol[2 * SF::SPAN];
-};
-
-// acc[e] (valid in wave 0, group 0) = sum over j in [j0, j1) of val[j] * B[col[j], cc + e], in
-// ascending j from +0, computed by the whole block (see above).  Every thread of the block calls
-// this with the same j0/j1.
-//   (col, val) of S batches (a span) are loaded coalesced by the whole block into LDS, one span
-//   ahead; every other load has a fixed place in the schedule (rows past j1 read B row 0 and
-//   are dropped), so a wait for one batch's B rows never waits for a younger batch's.
-//   B rows: a ring of D batches in flight per lane; batch k + D is issued right after batch k's
-//   products are in LDS.
-//   Products of consecutive batches alternate between two LDS buffers, so one barrier per batch
-//   orders the writes of batch k against the adds of batch k (after it) and of batch k - 1.
-template <typename T, typename I, typename K>
-__device__ __forceinline__ void block_accumulate(const I* __restrict__ col,
-                                                 const T* __restrict__ val,
-                                                 const I* __restrict__ vperm,
-                                                 const T* __restrict__ Bs, int64_t ldb,
-                                                 int64_t j0, int64_t j1, int gb, int gl,
-                                                 bool chain, SmallLds<T, I, K>& sh,
-                                                 typename Num<T>::acc (&acc)[K::VEC]) {
-#pragma clang fp contract(off)
-  using SF = SmallForm<T, I, K>;
-  using A = typename Num<T>::acc;
-  using P = Pack<T, K::VEC>;
-  using PA = Pack<A, K::VEC>;
-  constexpr int VEC = K::VEC, W = SF::W, GB = SF::GB, UW = SF::UW, NB = SF::NB, NBP = SF::NBP;
-  constexpr int D = SF::D, S = SF::S, SPAN = SF::SPAN, PT = SF::PT, NT = SF::kThreads;
-  const int tid = threadIdx.x;
-  const int64_t nb = (j1 - j0 + NB - 1) / NB;  // batches
-  // span s: nonzeros [j0 + s*SPAN, j0 + (s+1)*SPAN)
-  auto span_load = [&](int64_t s, I (&c)[PT], A (&v)[PT]) {
-#pragma unroll
-    for (int p = 0; p < PT; ++p) {
-      const int e = p * NT + tid < SPAN ? p * NT + tid : SPAN - 1;
-      const int64_t j = j0 + s * SPAN + e;
-      // past j1: nonzero j1 - 1 again (a valid row; its products are never added)
-      const int64_t jc = j < j1 ? j : j1 - 1;
-      c[p] = col[jc];
-      v[p] = Num<T>::load(val[vperm ? (int64_t)vperm[jc] : jc]);
-    }
-  };
-  auto span_store = [&](int64_t s, const I (&c)[PT], const A (&v)[PT]) {
-    const int off = (int)(s & 1) * SPAN;
-#pragma unroll
-    for (int p = 0; p < PT; ++p) {
-      if (p * NT + tid < SPAN) {
-        sh.scol[off + p * NT + tid] = c[p];
-        sh.sval[off + p * NT + tid] = v[p];
-      }
-    }
-  };
-  I rc[PT];  // the next span's (col, val), in flight until staged
-  A rv[PT];
-  // B rows of batch kb (B row 0 for a batch past the end: its span buffer may hold anything)
-  auto issue = [&](int64_t kb, P (&b)[UW]) {
-    const int off = (int)((kb / S) & 1) * SPAN + (int)(kb % S) * NB;
-    const int64_t live = -(int64_t)(kb < nb);
-#pragma unroll
-    for (int u = 0; u < UW; ++u) {
-      const int64_t c = (int64_t)sh.scol[off + GB * u + gb] & live;
-      b[u] = ld_brow<K::BNT, P>(Bs + c * ldb);
-    }
-  };
-  // batch k: products of the B rows in `b` -> LDS; (span staging); barrier; B rows of batch
-  // k + D -> `b`; the in-order adds of batch k (wave 0, group 0)
-  auto step = [&](int64_t k, P (&b)[UW], bool stage) {
-    const int cnt = (int)((j1 - j0 - k * NB) < NB ? (j1 - j0 - k * NB) : NB);
-    A* buf = sh.prod + (int)(k & 1) * SF::kBufElems;
-    const int voff = (int)((k / S) & 1) * SPAN + (int)(k % S) * NB;
-    A vv[UW];
-#pragma unroll
-    for (int u = 0; u < UW; ++u) vv[u] = sh.sval[voff + GB * u + gb];
-#pragma unroll
-    for (int u = 0; u < UW; ++u) {
-      const int i = GB * u + gb;
-      A pr[VEC];
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) pr[e] = Num<T>::mul(vv[u], Num<T>::load(b[u].v[e]));
-      if constexpr (SF::kColMajor) {
-        buf[gl * NBP + i] = pr[0];
-      } else if constexpr (VEC * sizeof(A) == 16 || VEC * sizeof(A) == 8) {
-        PA o;
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) o.v[e] = pr[e];
-        *reinterpret_cast<PA*>(buf + i * W + gl * VEC) = o;
-      } else {
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) buf[i * W + gl * VEC + e] = pr[e];
-      }
-    }
-    // stage (k % S == S - D): batch k + D opens the next span, which goes to LDS now (its loads
-    // were issued a span earlier), and the span after it starts loading
-    if (stage) span_store((k + D) / S, rc, rv);
-    __syncthreads();
-    if (stage) span_load((k + D) / S + 1, rc, rv);
-    issue(k + D, b);
-    if (chain) {
-      int i = 0;
-      if constexpr (SF::kColMajor) {
-        // column gl: 4 consecutive nonzeros per 16-B read, 8 reads in flight
-        const A* cp = buf + gl * NBP;
-        for (; i + 32 <= cnt; i += 32) {
-          Pack<A, 4> x[8];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) x[q] = *reinterpret_cast<const Pack<A, 4>*>(cp + i + 4 * q);
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[0] = acc[0] + x[q].v[e];
-        }
-        for (; i < cnt; ++i) acc[0] = acc[0] + cp[i];
-      } else {
-        for (; i + 16 <= cnt; i += 16) {
-          PA x[16];
-#pragma unroll
-          for (int q = 0; q < 16; ++q)
-            x[q] = *reinterpret_cast<const PA*>(buf + (i + q) * W + gl * VEC);
-#pragma unroll
-          for (int q = 0; q < 16; ++q)
-#pragma unroll
-            for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + x[q].v[e];
-        }
-        for (; i < cnt; ++i) {
-          const PA x = *reinterpret_cast<const PA*>(buf + i * W + gl * VEC);
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + x.v[e];
-        }
-      }
-    }
-  };
-  span_load(0, rc, rv);
-  span_store(0, rc, rv);
-  __syncthreads();
-  span_load(1, rc, rv);  // stored when batch S is first issued
-  // the ring: four named register sets, so batch k's rows stay in flight until step k
-  static_assert(D == 4, "small form: the load ring below is written out for D = 4");
-  P b0[UW], b1[UW], b2[UW], b3[UW];
-  issue(0, b0);
-  issue(1, b1);
-  issue(2, b2);
-  issue(3, b3);
-  // whole spans: no guards, the same loads outstanding at every step of every span (and at the
-  // loop entry), so each step's wait covers exactly its own batch
-  static_assert(S == 2 * D, "small form: a span is two turns of the ring");
-  int64_t k0 = 0;
-  for (; k0 + S <= nb; k0 += S) {
-    step(k0 + 0, b0, false);
-    step(k0 + 1, b1, false);
-    step(k0 + 2, b2, false);
-    step(k0 + 3, b3, false);
-    step(k0 + 4, b0, true);
-    step(k0 + 5, b1, false);
-    step(k0 + 6, b2, false);
-    step(k0 + 7, b3, false);
-  }
-  // the last, partial span (its batches were staged by the loop or the prologue)
-  if (k0 + 0 < nb) step(k0 + 0, b0, false);
-  if (k0 + 1 < nb) step(k0 + 1, b1, false);
-  if (k0 + 2 < nb) step(k0 + 2, b2, false);
-  if (k0 + 3 < nb) step(k0 + 3, b3, false);
-  if (k0 + 4 < nb) step(k0 + 4, b0, false);
-  if (k0 + 5 < nb) step(k0 + 5, b1, false);
-  if (k0 + 6 < nb) step(k0 + 6, b2, false);
-  __syncthreads();  // the next call's first batch writes buffer 0, which the adds may still read
-}
-
-template <typename T, typename I, typename K>
-__global__ void __launch_bounds__(64 * K::WPB)
-    spmm_small_kernel(const I* __restrict__ rp, const I* __restrict__ col,
-                      const T* __restrict__ val, const I* __restrict__ vperm,
-                      const T* __restrict__ B, int64_t ldb, T* __restrict__ C, int64_t ldc,
-                      int64_t row_begin, int64_t nrows, int64_t n, int64_t split, int64_t chunk,
-                      int64_t light, const T* __restrict__ bias, int act) {
-  using SF = SmallForm<T, I, K>;
-  using A = typename Num<T>::acc;
-  constexpr int VEC = K::VEC, LPR = K::LPR, W = SF::W, RPB = SF::RPB;
-  __shared__ __attribute__((aligned(16))) SmallLds<T, I, K> lds;
-  __shared__ int heavy_rows[RPB];
-  __shared__ int nheavy;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int gl = lane & (LPR - 1);
-  const int gbase = lane & ~(LPR - 1);
-  const int q = LPR == 64 ? 0 : lane / LPR;
-  const int gb = wave * SF::G + q;  // lane-group of the block
-  const int64_t row0 = (int64_t)blockIdx.x * RPB;
-  if (threadIdx.x == 0) nheavy = 0;
-  __syncthreads();
-  const int64_t lr = row0 + gb;
-  if (lr < nrows) {
-    const int64_t rs = (int64_t)rp[row_begin + lr];
-    const int64_t re = (int64_t)rp[row_begin + lr + 1];
-    const int64_t len = re - rs;
-    if (len > light || len > split) {
-      if (gl == 0) heavy_rows[atomicAdd(&nheavy, 1)] = gb;
-    } else {
-      for (int64_t c0 = 0; c0 < n; c0 += W) {
-        const int64_t cc = c0 + (int64_t)gl * VEC;
-        const bool active = cc < n;
-        A acc[VEC];
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) acc[e] = A(0);
-        accumulate<T, I, K>(col, val, vperm, B + cc, B, ldb, rs, re, gl, gbase, active, acc);
-        if (active) store_row<T, VEC, K::NT>(C + lr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
-      }
-    }
-  }
-  __syncthreads();
-  const int nh = nheavy;
-  const bool chain = wave == 0 && q == 0;
-  for (int h = 0; h < nh; ++h) {
-    const int64_t hr = row0 + heavy_rows[h];
-    const int64_t rs = (int64_t)rp[row_begin + hr];
-    const int64_t re = (int64_t)rp[row_begin + hr + 1];
-    const bool split_row = re - rs > split;
-    const int64_t nc = split_row ? num_chunks(re - rs, chunk) : 1;
-    for (int64_t c0 = 0; c0 < n; c0 += W) {
-      const int64_t cc = c0 + (int64_t)gl * VEC;
-      const bool active = cc < n;
-      const T* Bs = active ? B + cc : B;
-      A total[VEC], acc[VEC];
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) total[e] = A(0);
-      for (int64_t ci = 0; ci < nc; ++ci) {
-        int64_t j0 = rs, j1 = re;
-        if (split_row) {
-          j0 = rs + ci * chunk;
-          j1 = (re - j0 - chunk < chunk) ? re : j0 + chunk;
-        }
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) acc[e] = A(0);
-        block_accumulate<T, I, K>(col, val, vperm, Bs, ldb, j0, j1, gb, gl, chain, lds, acc);
-        if (split_row) {
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) total[e] = total[e] + acc[e];
-        }
-      }
-      if (chain && active)
-        store_row<T, VEC, K::NT>(C + hr * ldc + cc, split_row ? total : acc,
-                                 bias ? bias + cc : nullptr, act);
-    }
-  }
-}
-
-// ---- hub reduce: C[hub row] = ((0 + part[chunk 0]) + part[chunk 1]) + ... (chunk order) ---------
-// One group of L lanes per hub (64/L hubs per wave); each lane owns VEC consecutive columns and
-// reads them as one 16-B vector per partial row, kPre partial rows in flight before the in-order
-// adds.  Memory-level parallelism is what bounds this pass (Reddit: ~450k chunk partials of 1 KB):
-// a 256-thread block per hub with 4-B loads ran at 3.1 TB/s; 16-B loads over 64/L hubs per wave
-// keep 4x the bytes in flight (Reddit 148 -> 125 us, products unchanged at 33 us; a separate
-// one-lane-per-column kernel with 64 partials in flight for hubs of > 64 chunks measured slower
-// for both, 45 / 147 us, and was dropped).
-
-template <typename T, int VEC, int L>
-__global__ void __launch_bounds__(kBlock)
-    spmm_reduce_kernel(const unsigned long long* __restrict__ counters,
-                       const int64_t* __restrict__ hubs,
-                       const typename Num<T>::acc* __restrict__ part, T* __restrict__ C,
-                       int64_t ldc, int64_t n, const T* __restrict__ bias, int act) {
-#pragma clang fp contract(off)
-  using A = typename Num<T>::acc;
-  using P = Pack<A, VEC>;
-  constexpr int kPre = 16;  // partial rows in flight per lane (the adds stay in chunk order)
-  const int64_t nhubs = (int64_t)counters[1];
-  const int gl = threadIdx.x % L;
-  const int64_t groups = (int64_t)gridDim.x * (kBlock / L);
-  for (int64_t h = (int64_t)blockIdx.x * (kBlock / L) + threadIdx.x / L; h < nhubs; h += groups) {
-    const int64_t lr = hubs[3 * h + 0];
-    const int64_t slot = hubs[3 * h + 1];
-    const int64_t nc = hubs[3 * h + 2];
-    for (int64_t c = (int64_t)gl * VEC; c < n; c += (int64_t)L * VEC) {
-      const A* p = part + slot * n + c;
-      A acc[VEC];
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) acc[e] = A(0);
-      int64_t q = 0;
-      for (; q + kPre <= nc; q += kPre) {
-        P v[kPre];
-#pragma unroll
-        for (int u = 0; u < kPre; ++u) v[u] = *reinterpret_cast<const P*>(p + (q + u) * n);
-#pragma unroll
-        for (int u = 0; u < kPre; ++u) {
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + v[u].v[e];
-        }
-      }
-      for (; q < nc; ++q) {
-        const P v = *reinterpret_cast<const P*>(p + q * n);
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + v.v[e];
-      }
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) C[lr * ldc + c + e] = epilogue<T>(acc[e], bias, c + e, act);
-    }
-  }
-}
-
-template <typename T, int VEC>
-int launch_reduce_vec(hipStream_t s, int64_t max_hubs, int64_t n,
-                      const unsigned long long* counters, const int64_t* hubs,
-                      const typename Num<T>::acc* part, T* C, int64_t ldc, const T* bias, int act) {
-  const int64_t lanes = (n + VEC - 1) / VEC;
-  int l = 4;
-  while (l < 64 && l < lanes) l *= 2;
-  const int64_t per_block = kBlock / l;
-  int64_t grid = (max_hubs + per_block - 1) / per_block;
-  if (grid > kMaxReduceBlocks) grid = kMaxReduceBlocks;
-#define OFX_REDUCE(LL)                                                                        \
-  hipLaunchKernelGGL((spmm_reduce_kernel<T, VEC, LL>), dim3((unsigned)grid), dim3(kBlock), 0, s, \
-                     counters, hubs, part, C, ldc, n, bias, act)
-  switch (l) {
-    case 4: OFX_REDUCE(4); break;
-    case 8: OFX_REDUCE(8); break;
-    case 16: OFX_REDUCE(16); break;
-    case 32: OFX_REDUCE(32); break;
-    default: OFX_REDUCE(64); break;
-  }
-#undef OFX_REDUCE
-  OFX_HIP_CHECK(hipGetLastError());
-  return OFX_OK;
-}
-
-// 16-B partial loads when every partial row starts 16-B aligned (the workspace base is 256-B
-// aligned and rows are n accumulators apart), else one accumulator per lane.
-template <typename T>
-int launch_reduce(hipStream_t s, int64_t max_hubs, int64_t n, const unsigned long long* counters,
-                  const int64_t* hubs, const typename Num<T>::acc* part, T* C, int64_t ldc,
-                  const T* bias, int act) {
-  using A = typename Num<T>::acc;
-  constexpr int kVec = 16 / (int)sizeof(A);
-  if ((n * (int64_t)sizeof(A)) % 16 == 0)
-    return launch_reduce_vec<T, kVec>(s, max_hubs, n, counters, hubs, part, C, ldc, bias, act);
-  return launch_reduce_vec<T, 1>(s, max_hubs, n, counters, hubs, part, C, ldc, bias, act);
-}
 
 // ---- validation / slicing / synthetic dense ------------------------------------------------
 template <typename I>
@@ -892,243 +61,6 @@ __global__ void synth_dense_kernel(int64_t r_begin, int64_t rows, int64_t n, int
     const float f = exact ? exact_dense(h) : u_pm1(h);
     out[rr * ld + cc] = Num<T>::store((typename Num<T>::acc)f);
   }
-}
-
-// ---- host-side dispatch ---------------------------------------------------------------------
-struct Launch {
-  hipStream_t stream;
-  const void *rp, *col, *val, *b;
-  void* c;
-  int64_t ldb, ldc, row_begin, nrows, n, nnz;
-  Schedule sched;
-  void* ws;
-  size_t ws_bytes;
-  const void* bias;  // fused epilogue (T[n] or NULL) and OFX_ACT_*
-  int act;
-  int64_t b_rows;  // k: rows of B (cache-footprint choice of load hints)
-  const void* vperm;  // NULL, or I[nnz]: nonzero j's value is val[vperm[j]] (A^T of a gradient)
-};
-
-int pick_vec(int elem_bytes, const Launch& L, int forced_vec) {
-  const int maxvec = 16 / elem_bytes;
-  for (int v = maxvec; v >= 1; v /= 2) {
-    if (forced_vec && v != forced_vec) continue;
-    const size_t vb = (size_t)v * elem_bytes;
-    if (L.n % v == 0 && L.ldb % v == 0 && L.ldc % v == 0 &&
-        ((uintptr_t)L.b % vb) == 0 && ((uintptr_t)L.c % vb) == 0)
-      return v;
-  }
-  return 0;
-}
-
-int pick_lpr(int64_t n, int vec) {
-  const int64_t lanes = (n + vec - 1) / vec;
-  int l = 4;
-  while (l < 64 && l < lanes) l *= 2;
-  return l;
-}
-
-template <typename T, typename I, typename K>
-int launch_cfg(const Launch& L) {
-  using A = typename Num<T>::acc;
-  constexpr int GPW = 64 / K::LPR;
-  constexpr int64_t GPB = (int64_t)K::WPB * GPW;  // lane-groups per block
-  const I* rp = static_cast<const I*>(L.rp);
-  const I* col = static_cast<const I*>(L.col);
-  const T* val = static_cast<const T*>(L.val);
-  const T* B = static_cast<const T*>(L.b);
-  T* C = static_cast<T*>(L.c);
-  const WsLayout w = ws_layout(L.nrows, L.nnz, L.n, sizeof(A), L.sched);
-  const bool plan = w.total > 0;
-  WorkList wl{};
-  if (plan) {
-    OFX_REQUIRE(L.ws != nullptr && L.ws_bytes >= w.total, OFX_EWORKSPACE,
-                "spmm_csr: workspace of %zu bytes is smaller than the %zu bytes required",
-                L.ws_bytes, w.total);
-    if (L.sched.planned) {
-      plan::worklist_of(w, static_cast<char*>(L.ws), &wl);
-    } else {
-      const int rc = launch_plan<I>(L.stream, rp, L.row_begin, L.nrows, L.nnz, L.sched, w,
-                                    static_cast<char*>(L.ws), &wl);
-      if (rc) return rc;
-    }
-  }
-  unsigned long long* counters = wl.counters;
-  int64_t *hub = wl.hubs, *items = wl.items, *order = wl.order;
-  A* part = reinterpret_cast<A*>(wl.part);
-  // Work list length <= hub chunks + rows; surplus groups exit at once.  The WH form puts one
-  // wave per hub chunk / heavy row first (upper bound: every chunk and row), then the groups.
-  const int64_t work = L.nrows + (plan ? w.max_chunks : 0);
-  const int64_t wave_blocks =
-      (K::WH && K::LPR < 64 && plan) ? (work + K::WPB - 1) / K::WPB : 0;
-  const int64_t grid = wave_blocks + (work + GPB - 1) / GPB;
-  OFX_REQUIRE(grid < (int64_t)UINT32_MAX, OFX_EINVAL, "spmm_csr: too many rows (%lld)",
-              (long long)L.nrows);
-  hipLaunchKernelGGL((spmm_main_kernel<T, I, K>), dim3((unsigned)grid), dim3(64 * K::WPB), 0,
-                     L.stream, rp, col, val, static_cast<const I*>(L.vperm), B, L.ldb, C, L.ldc,
-                     L.row_begin, L.nrows, L.n,
-                     plan ? L.sched.chunk : INT64_MAX, counters, items, order, part,
-                     static_cast<const T*>(L.bias), L.act, wave_blocks);
-  OFX_HIP_CHECK(hipGetLastError());
-  if (plan && w.max_hubs > 0)
-    return launch_reduce<T>(L.stream, w.max_hubs, L.n, counters, hub, part, C, L.ldc,
-                            static_cast<const T*>(L.bias), L.act);
-  return OFX_OK;
-}
-
-// Small form (spmm_small_kernel): one launch when the launch has at most kSmallRows rows and at
-// most kSmallFormElems products (nnz * n).  Its longest row then costs at most that many products
-// of one block's in-order adds, against the planned form's three planning launches + reduce.
-// A fixed function of (rows, nnz, n, variant): the workspace query and the launch agree.
-constexpr int64_t kSmallRows = 32768;
-constexpr int64_t kSmallFormElems = int64_t(1) << 20;
-constexpr int kSmallLight = 2;  // rows of more than kSmallLight * U nonzeros take the whole block
-
-bool use_small_form(int64_t nrows, int64_t nnz, int64_t n, const Schedule& s) {
-  return s.variant == 0 && nrows <= kSmallRows && nnz <= kSmallFormElems / (n > 0 ? n : 1);
-}
-
-template <typename T, typename I, typename K>
-int launch_small(const Launch& L) {
-  using SF = SmallForm<T, I, K>;
-  // options.heavy_threshold > 0 overrides the light/whole-block cut (tuning; no numeric effect)
-  const int64_t light =
-      (L.sched.heavy > 0 && L.sched.heavy != INT64_MAX) ? L.sched.heavy : (int64_t)kSmallLight * K::U;
-  const int64_t grid = (L.nrows + SF::RPB - 1) / SF::RPB;
-  OFX_REQUIRE(grid < (int64_t)UINT32_MAX, OFX_EINVAL, "spmm_csr: too many rows (%lld)",
-              (long long)L.nrows);
-  hipLaunchKernelGGL((spmm_small_kernel<T, I, K>), dim3((unsigned)grid), dim3(64 * K::WPB), 0,
-                     L.stream, static_cast<const I*>(L.rp), static_cast<const I*>(L.col),
-                     static_cast<const T*>(L.val), static_cast<const I*>(L.vperm),
-                     static_cast<const T*>(L.b), L.ldb, static_cast<T*>(L.c), L.ldc, L.row_begin,
-                     L.nrows, L.n, L.sched.split, L.sched.chunk, light,
-                     static_cast<const T*>(L.bias), L.act);
-  OFX_HIP_CHECK(hipGetLastError());
-  return OFX_OK;
-}
-
-template <typename T, typename I, typename K>
-int launch_small_or_planned(const Launch& L) {
-  if (use_small_form(L.nrows, L.nnz, L.n, L.sched)) return launch_small<T, I, K>(L);
-  return launch_cfg<T, I, K>(L);
-}
-
-// B far larger than the Infinity Cache (> 1 GiB): the col/val/C streams are loaded and stored
-// non-temporally so they do not evict the hot (hub) B rows that still hit on-die.  Measured
-// (scripts/ab.py, bit-identical): papers-scale -1.8%, products -0.3%; with B at cache size
-// (1M power-law, 256 MB) the same hint costs +8%, hence the threshold.
-constexpr int64_t kNtBytes = int64_t(1) << 30;
-
-// Small problems (<= kSmallRows rows: too few lane-groups to be bandwidth-bound) run as long as
-// their longest non-split row, a chain of len / U dependent B-row load rounds; these launches keep
-// 32 (16 for 8-16 B lanes) loads in flight per lane instead of 8.  A Cora-shaped layer (max row
-// 253 nonzeros, N=16) took 25 us with U=8.  Same bits: U only changes how many loads are issued
-// ahead of the in-order adds.  Below kSmallFormElems products the launch is the small form.
-template <typename T, typename I, int VEC>
-int launch_vec_small(const Launch& L, int lpr) {
-  constexpr int U = VEC * sizeof(T) <= 4 ? 32 : 16;
-  switch (lpr) {
-    case 4: return launch_small_or_planned<T, I, Cfg<VEC, 4, U, 4, false, true, false, true>>(L);
-    case 8: return launch_small_or_planned<T, I, Cfg<VEC, 8, U, 4, false, true, false, true>>(L);
-    case 16: return launch_small_or_planned<T, I, Cfg<VEC, 16, U, 4, false, true, false, true>>(L);
-    case 32: return launch_small_or_planned<T, I, Cfg<VEC, 32, U, 4, false, true, false, true>>(L);
-    case 64: return launch_small_or_planned<T, I, Cfg<VEC, 64, U>>(L);
-    default: return fail(OFX_EINVAL, "spmm_csr: unsupported lanes-per-row %d", lpr);
-  }
-}
-
-template <typename T, typename I, int VEC>
-int launch_vec(const Launch& L, int lpr, bool nt) {
-  // forced variants (tests, tuning) keep the U = 8 configurations at every size
-  if (L.nrows <= kSmallRows && L.sched.variant == 0 &&
-      (!nt || use_small_form(L.nrows, L.nnz, L.n, L.sched)))
-    return launch_vec_small<T, I, VEC>(L, lpr);
-  switch (lpr) {
-    case 4: return launch_cfg<T, I, Cfg<VEC, 4>>(L);
-    case 8: return launch_cfg<T, I, Cfg<VEC, 8>>(L);
-    case 16:
-      // fp32 rows of <= 64 B (one element per lane): 16 loads in flight instead of 8, -1.2% on
-      // products-shaped N = 16 (tuning variant 10021, profiles/r02_ab_n16_bnt.log), same bits
-      if constexpr (VEC == 1 && sizeof(T) == 4) return launch_cfg<T, I, Cfg<1, 16, 16>>(L);
-      return launch_cfg<T, I, Cfg<VEC, 16>>(L);
-    case 32:
-      return nt ? launch_cfg<T, I, Cfg<VEC, 32, 8, 4, true>>(L) : launch_cfg<T, I, Cfg<VEC, 32>>(L);
-    case 64:
-      return nt ? launch_cfg<T, I, Cfg<VEC, 64, 8, 4, true>>(L) : launch_cfg<T, I, Cfg<VEC, 64>>(L);
-    default: return fail(OFX_EINVAL, "spmm_csr: unsupported lanes-per-row %d", lpr);
-  }
-}
-
-// Tuning table (variant = 10000 + id), float values / int32 indices only; every entry computes the
-// same bits (the accumulation order does not depend on the launch shape).
-template <typename T, typename I>
-int launch_tuned(const Launch& L, int id) {
-  if constexpr (std::is_same<T, float>::value && std::is_same<I, int32_t>::value) {
-    OFX_REQUIRE(L.n % 4 == 0 && L.ldb % 4 == 0 && L.ldc % 4 == 0 && ((uintptr_t)L.b % 16) == 0 &&
-                    ((uintptr_t)L.c % 16) == 0,
-                OFX_EINVAL, "spmm_csr: tuning variant %d needs 16-B aligned rows", L.sched.variant);
-    switch (id) {
-      case 1: return launch_cfg<T, I, Cfg<4, 32, 8, 4, false>>(L);
-      case 2: return launch_cfg<T, I, Cfg<4, 32, 8, 4, true>>(L);
-      case 3: return launch_cfg<T, I, Cfg<4, 32, 8, 1, false>>(L);
-      case 4: return launch_cfg<T, I, Cfg<4, 32, 16, 4, false>>(L);
-      case 5: return launch_cfg<T, I, Cfg<4, 32, 4, 4, false>>(L);
-      case 6: return launch_cfg<T, I, Cfg<4, 32, 8, 2, true>>(L);
-      case 7: return launch_cfg<T, I, Cfg<4, 32, 8, 8, false>>(L);
-      case 8: return launch_cfg<T, I, Cfg<4, 32, 16, 4, true>>(L);
-      case 9: return launch_cfg<T, I, Cfg<4, 16, 8, 4, false>>(L);
-      case 10: return launch_cfg<T, I, Cfg<4, 16, 8, 4, true>>(L);
-      // prefetch + branch-free issue (the small-launch form) at products scale
-      case 11: return launch_cfg<T, I, Cfg<4, 32, 8, 4, true, true>>(L);
-      case 12: return launch_cfg<T, I, Cfg<4, 32, 16, 4, true, true>>(L);
-      case 13: return launch_cfg<T, I, Cfg<4, 32, 32, 4, true, true>>(L);
-      case 14: return launch_cfg<T, I, Cfg<4, 32, 8, 4, false, true>>(L);
-      // small launches at N = 16 (VEC 1, 16 lanes per row): loads in flight per lane
-      case 15: return launch_cfg<T, I, Cfg<1, 16, 32, 4, false, true>>(L);
-      case 16: return launch_cfg<T, I, Cfg<1, 16, 64, 4, false, true>>(L);
-      case 17: return launch_cfg<T, I, Cfg<1, 16, 128, 4, false, true>>(L);
-      // B-row loads non-temporal (request size / cache-policy probe at N = 16 and N = 128)
-      case 18: return launch_cfg<T, I, Cfg<1, 16, 8, 4, false, false, true>>(L);
-      case 19: return launch_cfg<T, I, Cfg<1, 16, 8, 4, true, false, true>>(L);
-      case 20: return launch_cfg<T, I, Cfg<4, 32, 8, 4, false, false, true>>(L);
-      case 21: return launch_cfg<T, I, Cfg<1, 16, 16, 4, false, false>>(L);
-      // small launches without / with the wave-item form (N = 16: VEC 1, N = 64: VEC 4)
-      case 22: return launch_cfg<T, I, Cfg<1, 16, 32, 4, false, true>>(L);
-      case 23: return launch_cfg<T, I, Cfg<1, 16, 32, 4, false, true, false, true>>(L);
-      case 24: return launch_cfg<T, I, Cfg<4, 16, 16, 4, false, true>>(L);
-      case 25: return launch_cfg<T, I, Cfg<4, 16, 16, 4, false, true, false, true>>(L);
-      default: break;
-    }
-  }
-  return fail(OFX_EINVAL, "spmm_csr: unknown tuning variant %d for this dtype", L.sched.variant);
-}
-
-template <typename T, typename I>
-int launch_typed(const Launch& L) {
-  if (L.sched.variant >= 10000) return launch_tuned<T, I>(L, L.sched.variant - 10000);
-  // variant = VEC * 100 + LPR forces a configuration (tuning / tests); 0 = auto.
-  const int forced_vec = L.sched.variant > 0 ? L.sched.variant / 100 : 0;
-  const int forced_lpr = L.sched.variant > 0 ? L.sched.variant % 100 : 0;
-  // fp32 rows of <= 64 B: one element per lane over 16 lanes beats 4 lanes of float4 (+9% on
-  // products-shaped N=16, scripts/ab.py); wider rows keep the widest vector
-  const int vec = (!forced_vec && sizeof(T) == 4 && L.n <= 16) ? 1
-                                                                 : pick_vec((int)sizeof(T), L, forced_vec);
-  OFX_REQUIRE(vec > 0, OFX_EINVAL,
-              "spmm_csr: variant %d not applicable (n=%lld ldb=%lld ldc=%lld or pointer alignment)",
-              L.sched.variant, (long long)L.n, (long long)L.ldb, (long long)L.ldc);
-  const int lpr = forced_lpr ? forced_lpr : pick_lpr(L.n, vec);
-  const bool nt = (L.b_rows * L.ldb * (int64_t)sizeof(T)) > kNtBytes;
-  switch (vec) {
-    case 1: return launch_vec<T, I, 1>(L, lpr, nt);
-    case 2: return launch_vec<T, I, 2>(L, lpr, nt);
-    case 4:
-      if constexpr (sizeof(T) <= 4) return launch_vec<T, I, 4>(L, lpr, nt);
-      break;
-    case 8:
-      if constexpr (sizeof(T) == 2) return launch_vec<T, I, 8>(L, lpr, nt);
-      break;
-  }
-  return fail(OFX_EINVAL, "spmm_csr: unsupported vector width %d", vec);
 }
 
 template <typename I>

@@ -1,0 +1,64 @@
+// spmm_csr_tuned.hip — the tuning table of the SpMM forward (variant = 10000 + id): forced
+// configurations for A/B runs (scripts/ab.py) and the tuning-table parity tests.
+#pragma clang fp contract(off)
+
+#include "spmm_csr_impl.h"
+
+namespace ofx {
+
+// Tuning table (variant = 10000 + id), float values / int32 indices only; every entry computes the
+// same bits (the accumulation order does not depend on the launch shape).
+template <typename T, typename I>
+int launch_tuned(const Launch& L, int id) {
+  if constexpr (std::is_same<T, float>::value && std::is_same<I, int32_t>::value) {
+    OFX_REQUIRE(L.n % 4 == 0 && L.ldb % 4 == 0 && L.ldc % 4 == 0 && ((uintptr_t)L.b % 16) == 0 &&
+                    ((uintptr_t)L.c % 16) == 0,
+                OFX_EINVAL, "spmm_csr: tuning variant %d needs 16-B aligned rows", L.sched.variant);
+    switch (id) {
+      case 1: return launch_cfg<T, I, Cfg<4, 32, 8, 4, false>>(L);
+      case 2: return launch_cfg<T, I, Cfg<4, 32, 8, 4, true>>(L);
+      case 3: return launch_cfg<T, I, Cfg<4, 32, 8, 1, false>>(L);
+      case 4: return launch_cfg<T, I, Cfg<4, 32, 16, 4, false>>(L);
+      case 5: return launch_cfg<T, I, Cfg<4, 32, 4, 4, false>>(L);
+      case 6: return launch_cfg<T, I, Cfg<4, 32, 8, 2, true>>(L);
+      case 7: return launch_cfg<T, I, Cfg<4, 32, 8, 8, false>>(L);
+      case 8: return launch_cfg<T, I, Cfg<4, 32, 16, 4, true>>(L);
+      case 9: return launch_cfg<T, I, Cfg<4, 16, 8, 4, false>>(L);
+      case 10: return launch_cfg<T, I, Cfg<4, 16, 8, 4, true>>(L);
+      // prefetch + branch-free issue (the small-launch form) at products scale
+      case 11: return launch_cfg<T, I, Cfg<4, 32, 8, 4, true, true>>(L);
+      case 12: return launch_cfg<T, I, Cfg<4, 32, 16, 4, true, true>>(L);
+      case 13: return launch_cfg<T, I, Cfg<4, 32, 32, 4, true, true>>(L);
+      case 14: return launch_cfg<T, I, Cfg<4, 32, 8, 4, false, true>>(L);
+      // small launches at N = 16 (VEC 1, 16 lanes per row): loads in flight per lane
+      case 15: return launch_cfg<T, I, Cfg<1, 16, 32, 4, false, true>>(L);
+      case 16: return launch_cfg<T, I, Cfg<1, 16, 64, 4, false, true>>(L);
+      case 17: return launch_cfg<T, I, Cfg<1, 16, 128, 4, false, true>>(L);
+      // B-row loads non-temporal (request size / cache-policy probe at N = 16 and N = 128)
+      case 18: return launch_cfg<T, I, Cfg<1, 16, 8, 4, false, false, true>>(L);
+      case 19: return launch_cfg<T, I, Cfg<1, 16, 8, 4, true, false, true>>(L);
+      case 20: return launch_cfg<T, I, Cfg<4, 32, 8, 4, false, false, true>>(L);
+      case 21: return launch_cfg<T, I, Cfg<1, 16, 16, 4, false, false>>(L);
+      // small launches without / with the wave-item form (N = 16: VEC 1, N = 64: VEC 4)
+      case 22: return launch_cfg<T, I, Cfg<1, 16, 32, 4, false, true>>(L);
+      case 23: return launch_cfg<T, I, Cfg<1, 16, 32, 4, false, true, false, true>>(L);
+      case 24: return launch_cfg<T, I, Cfg<4, 16, 16, 4, false, true>>(L);
+      case 25: return launch_cfg<T, I, Cfg<4, 16, 16, 4, false, true, false, true>>(L);
+      default: break;
+    }
+  }
+  return fail(OFX_EINVAL, "spmm_csr: unknown tuning variant %d for this dtype", L.sched.variant);
+}
+
+#define OFX_TUNED(T, I) template int launch_tuned<T, I>(const Launch& L, int id);
+OFX_TUNED(float, int32_t)
+OFX_TUNED(float, int64_t)
+OFX_TUNED(double, int32_t)
+OFX_TUNED(double, int64_t)
+OFX_TUNED(bf16, int32_t)
+OFX_TUNED(bf16, int64_t)
+OFX_TUNED(f16, int32_t)
+OFX_TUNED(f16, int64_t)
+#undef OFX_TUNED
+
+}  // namespace ofx
