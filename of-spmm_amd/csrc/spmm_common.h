@@ -158,12 +158,14 @@ struct Schedule {
                   // 0 = auto, INT64_MAX = off
   int32_t variant;
   int32_t planned;  // the workspace holds this launch's plan (ofx_spmm_csr_plan): skip planning
+  int32_t force_bin;  // plan a binned work list even for few rows (the mid form's block items)
 };
 
 static inline Schedule resolve_schedule(int64_t n, const ofx_spmm_options* o) {
   Schedule s;
   s.variant = o ? o->variant : 0;
   s.planned = o ? o->planned : 0;
+  s.force_bin = 0;
   const int64_t h = o ? o->heavy_threshold : 0;
   s.heavy = h > 0 ? h : (h < 0 ? INT64_MAX : 0);  // 0 = auto (device launch: 5x mean degree)
   if (o && o->ordered) {
@@ -175,6 +177,14 @@ static inline Schedule resolve_schedule(int64_t n, const ofx_spmm_options* o) {
   s.chunk = (o && o->chunk > 0) ? o->chunk : s.split;
   if (s.chunk > s.split) s.chunk = s.split;  // every split row then has >= 1 full chunk
   return s;
+}
+
+// The automatic heavy-bin threshold of the device work order (no numeric effect): 5x the mean
+// degree of the launch's rows, at least 16 (products and the 1M power-law config both peak at
+// 4-6x the mean).
+OFX_HD int64_t auto_heavy(int64_t nrows, int64_t nnz) {
+  const int64_t mean = nrows > 0 ? (nnz + nrows - 1) / nrows : 1;
+  return 5 * mean < 16 ? 16 : 5 * mean;
 }
 
 // Number of chunks of a split row of length len (> split): floor(len / chunk) — the last

@@ -103,7 +103,7 @@ extern "C" int ofx_spmm_csr_workspace_size(int idx_dtype, int val_dtype, int64_t
   OFX_REQUIRE(bytes != nullptr, OFX_EINVAL, "spmm_csr_workspace_size: bytes is NULL");
   int rc = check_common(idx_dtype, val_dtype, m, k, n, nnz);
   if (rc) return rc;
-  const Schedule s = resolve_schedule(n, opts);
+  const Schedule s = launch_schedule(m, nnz, n, resolve_schedule(n, opts));
   *bytes = use_small_form(m, nnz, n, s) ? 0 : ws_layout(m, nnz, n, acc_bytes_of(val_dtype), s).total;
   return OFX_OK;
 }
@@ -130,7 +130,8 @@ int spmm_entry(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k,
   OFX_REQUIRE(nnz == 0 || (col_idx && values && b), OFX_EINVAL,
               "spmm_csr: NULL col_idx/values/b with nnz=%lld", (long long)nnz);
   Launch L{static_cast<hipStream_t>(stream), row_ptr, col_idx, values, b, c, ldb, ldc,
-           row_begin, nrows, n, nnz, resolve_schedule(n, opts), workspace, workspace_bytes,
+           row_begin, nrows, n, nnz, launch_schedule(nrows, nnz, n, resolve_schedule(n, opts)),
+           workspace, workspace_bytes,
            bias, act, k, values_perm};
   if (idx_dtype == OFX_DT_INT32) return launch_idx<int32_t>(val_dtype, L);
   return launch_idx<int64_t>(val_dtype, L);
@@ -173,7 +174,7 @@ extern "C" int ofx_spmm_csr_plan(void* stream, int idx_dtype, int val_dtype, int
               (long long)row_end, (long long)m);
   const int64_t nrows = row_end - row_begin;
   if (nrows == 0 || n == 0) return OFX_OK;  // the launch writes nothing either
-  const Schedule s = resolve_schedule(n, opts);
+  const Schedule s = launch_schedule(nrows, nnz, n, resolve_schedule(n, opts));
   if (use_small_form(nrows, nnz, n, s)) return OFX_OK;  // the small form needs no plan
   const plan::WsLayout w = plan::ws_layout(nrows, nnz, n, acc_bytes_of(val_dtype), s);
   if (w.total == 0) return OFX_OK;  // identity work list: nothing to plan

@@ -68,11 +68,12 @@ struct alignas(sizeof(T) * VEC) Pack {
 // BNT: the B-row loads themselves carry the non-temporal hint (tuning variants only).
 // WH: small launches: hub chunks and heavy rows take a whole wave each (the wave's 64/LPR groups
 // interleave the nonzeros of one item), the light rows one group each (accumulate_wave).
+// BI: the mid form: hub chunks and heavy rows take a whole block each (block_accumulate).
 template <int VEC_, int LPR_, int U_ = 8, int WPB_ = 4, bool NT_ = false, bool PF_ = false,
-          bool BNT_ = false, bool WH_ = false>
+          bool BNT_ = false, bool WH_ = false, bool BI_ = false>
 struct Cfg {
   static constexpr int VEC = VEC_, LPR = LPR_, U = U_, WPB = WPB_;
-  static constexpr bool NT = NT_, PF = PF_, BNT = BNT_, WH = WH_;
+  static constexpr bool NT = NT_, PF = PF_, BNT = BNT_, WH = WH_, BI = BI_;
   // loads in flight per lane of the wave-item form: G * UW * VEC cross-lane moves per batch are
   // unrolled, so UW keeps that at <= 256 (4..32)
   static constexpr int G = LPR < 64 ? 64 / LPR : 1;
@@ -375,115 +376,6 @@ __device__ __forceinline__ void store_partial(A* __restrict__ p, const A (&acc)[
   for (int e = 0; e < VEC; ++e) p[e] = acc[e];
 }
 
-// ---- main kernel: one work list = hub chunks, then rows in bin order ------------------------
-// Without a plan (`order` == nullptr) the list is simply the rows in index order.
-template <typename T, typename I, typename K>
-__global__ void __launch_bounds__(64 * K::WPB)
-    spmm_main_kernel(const I* __restrict__ rp, const I* __restrict__ col,
-                     const T* __restrict__ val, const I* __restrict__ vperm,
-                     const T* __restrict__ B, int64_t ldb,
-                     T* __restrict__ C, int64_t ldc, int64_t row_begin, int64_t nrows, int64_t n,
-                     int64_t chunk, const unsigned long long* __restrict__ counters,
-                     const int64_t* __restrict__ items, const int64_t* __restrict__ order,
-                     typename Num<T>::acc* __restrict__ part, const T* __restrict__ bias,
-                     int act, int64_t wave_blocks) {
-  using A = typename Num<T>::acc;
-  constexpr int VEC = K::VEC, LPR = K::LPR, kWaves = K::WPB;
-  constexpr int GPW = 64 / LPR;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int gl = lane & (LPR - 1);
-  const int gbase = lane & ~(LPR - 1);
-  const int gsub = LPR == 64 ? 0 : lane / LPR;
-  if constexpr (K::WH && LPR < 64) {
-    // blocks [0, wave_blocks): one wave per hub chunk / heavy row (the plan's first items)
-    if ((int64_t)blockIdx.x < wave_blocks) {
-      const int64_t w = (int64_t)blockIdx.x * kWaves + wave;
-      const int64_t nchunks = (int64_t)counters[0];
-      const int64_t nheavy = (int64_t)counters[3] - (int64_t)counters[2];  // bin 0
-      if (w >= nchunks + nheavy) return;
-      int64_t wr, wc = -1;
-      if (w < nchunks) {
-        wr = items[2 * w + 0];
-        wc = items[2 * w + 1];
-      } else {
-        wr = order[w - nchunks];
-      }
-      wr = uniform64(wr);
-      wc = uniform64(wc);
-      const int64_t rs = (int64_t)rp[row_begin + wr];
-      const int64_t re = (int64_t)rp[row_begin + wr + 1];
-      int64_t j0 = rs, j1 = re;
-      if (wc >= 0) {
-        j0 = rs + wc * chunk;
-        j1 = (re - j0 - chunk < chunk) ? re : j0 + chunk;
-      }
-      for (int64_t c0 = 0; c0 < n; c0 += (int64_t)LPR * VEC) {
-        const int64_t cc = c0 + (int64_t)gl * VEC;
-        const bool active = cc < n;
-        A acc[VEC];
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) acc[e] = A(0);
-        accumulate_wave<T, I, K>(col, val, vperm, B + cc, B, ldb, j0, j1, lane, gl, active, acc);
-        if (active && gsub == 0) {
-          if (wc >= 0)
-            store_partial<A, VEC>(part + w * n + cc, acc);
-          else
-            store_row<T, VEC, K::NT>(C + wr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
-        }
-      }
-      return;
-    }
-  }
-  // one lane-group per work item; in the WH form these are the light rows after the wave items
-  int64_t g = ((int64_t)(blockIdx.x - (K::WH ? wave_blocks : 0)) * kWaves + wave) * GPW + gsub;
-  if constexpr (K::WH && LPR < 64) {
-    if (order != nullptr) g += (int64_t)counters[0] + (int64_t)counters[3] - (int64_t)counters[2];
-  }
-  int64_t lr, c = -1;  // local row; chunk index or -1 for a whole row
-  if (order == nullptr) {
-    if (g >= nrows) return;
-    lr = g;
-  } else {
-    const int64_t nchunks = (int64_t)counters[0];
-    if (g < nchunks) {
-      lr = items[2 * g + 0];
-      c = items[2 * g + 1];
-    } else {
-      const int64_t q = g - nchunks;
-      if (q >= nrows - (int64_t)counters[1]) return;
-      lr = order[q];
-    }
-  }
-  if constexpr (LPR == 64) {
-    lr = uniform64(lr);
-    c = uniform64(c);
-  }
-  const int64_t rs = (int64_t)rp[row_begin + lr];
-  const int64_t re = (int64_t)rp[row_begin + lr + 1];
-  int64_t j0 = rs, j1 = re;
-  if (c >= 0) {
-    // chunk c of num_chunks(len, chunk) = len / chunk; the last one (fewer than 2 * chunk
-    // nonzeros left from its start) takes the remainder.  No 64-bit division per work item.
-    j0 = rs + c * chunk;
-    j1 = (re - j0 - chunk < chunk) ? re : j0 + chunk;
-  }
-  for (int64_t c0 = 0; c0 < n; c0 += (int64_t)LPR * VEC) {
-    const int64_t cc = c0 + (int64_t)gl * VEC;
-    const bool active = cc < n;
-    A acc[VEC];
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) acc[e] = A(0);
-    accumulate<T, I, K>(col, val, vperm, B + cc, B, ldb, j0, j1, gl, gbase, active, acc);
-    if (active) {
-      if (c >= 0)
-        store_partial<A, VEC>(part + g * n + cc, acc);
-      else
-        store_row<T, VEC, K::NT>(C + lr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
-    }
-  }
-}
-
 // ---- small form: one launch, no plan, no workspace -------------------------------------------
 // Launches with few rows and little B-row traffic (use_small_form) run as ONE kernel.  Block b
 // owns rows [b*RPB, (b+1)*RPB), one lane-group per row.  A group takes its row when the row has at
@@ -772,6 +664,163 @@ __global__ void __launch_bounds__(64 * K::WPB)
   }
 }
 
+// ---- main kernel: one work list = hub chunks, then rows in bin order ------------------------
+// Without a plan (`order` == nullptr) the list is simply the rows in index order.
+template <typename T, typename I, typename K>
+__global__ void __launch_bounds__(64 * K::WPB)
+    spmm_main_kernel(const I* __restrict__ rp, const I* __restrict__ col,
+                     const T* __restrict__ val, const I* __restrict__ vperm,
+                     const T* __restrict__ B, int64_t ldb,
+                     T* __restrict__ C, int64_t ldc, int64_t row_begin, int64_t nrows, int64_t n,
+                     int64_t chunk, const unsigned long long* __restrict__ counters,
+                     const int64_t* __restrict__ items, const int64_t* __restrict__ order,
+                     typename Num<T>::acc* __restrict__ part, const T* __restrict__ bias,
+                     int act, int64_t wave_blocks) {
+  using A = typename Num<T>::acc;
+  constexpr int VEC = K::VEC, LPR = K::LPR, kWaves = K::WPB;
+  constexpr int GPW = 64 / LPR;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int gl = lane & (LPR - 1);
+  const int gbase = lane & ~(LPR - 1);
+  const int gsub = LPR == 64 ? 0 : lane / LPR;
+  if constexpr (K::WH && LPR < 64) {
+    // blocks [0, wave_blocks): one wave per hub chunk / heavy row (the plan's first items)
+    if ((int64_t)blockIdx.x < wave_blocks) {
+      const int64_t w = (int64_t)blockIdx.x * kWaves + wave;
+      const int64_t nchunks = (int64_t)counters[0];
+      const int64_t nheavy = (int64_t)counters[3] - (int64_t)counters[2];  // bin 0
+      if (w >= nchunks + nheavy) return;
+      int64_t wr, wc = -1;
+      if (w < nchunks) {
+        wr = items[2 * w + 0];
+        wc = items[2 * w + 1];
+      } else {
+        wr = order[w - nchunks];
+      }
+      wr = uniform64(wr);
+      wc = uniform64(wc);
+      const int64_t rs = (int64_t)rp[row_begin + wr];
+      const int64_t re = (int64_t)rp[row_begin + wr + 1];
+      int64_t j0 = rs, j1 = re;
+      if (wc >= 0) {
+        j0 = rs + wc * chunk;
+        j1 = (re - j0 - chunk < chunk) ? re : j0 + chunk;
+      }
+      for (int64_t c0 = 0; c0 < n; c0 += (int64_t)LPR * VEC) {
+        const int64_t cc = c0 + (int64_t)gl * VEC;
+        const bool active = cc < n;
+        A acc[VEC];
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[e] = A(0);
+        accumulate_wave<T, I, K>(col, val, vperm, B + cc, B, ldb, j0, j1, lane, gl, active, acc);
+        if (active && gsub == 0) {
+          if (wc >= 0)
+            store_partial<A, VEC>(part + w * n + cc, acc);
+          else
+            store_row<T, VEC, K::NT>(C + wr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
+        }
+      }
+      return;
+    }
+  }
+  if constexpr (K::BI) {
+    // blocks [0, wave_blocks): one block per hub chunk / heavy row (the plan's first items).
+    // A block returns or runs its item as a whole, so block_accumulate's barriers are uniform.
+    if ((int64_t)blockIdx.x < wave_blocks) {
+      __shared__ __attribute__((aligned(16))) SmallLds<T, I, K> lds;
+      constexpr int W = SmallForm<T, I, K>::W;
+      const int64_t w = blockIdx.x;
+      const int64_t nchunks = (int64_t)counters[0];
+      const int64_t nheavy = (int64_t)counters[3] - (int64_t)counters[2];  // bin 0
+      if (w >= nchunks + nheavy) return;
+      int64_t wr, wc = -1;
+      if (w < nchunks) {
+        wr = items[2 * w + 0];
+        wc = items[2 * w + 1];
+      } else {
+        wr = order[w - nchunks];
+      }
+      wr = uniform64(wr);
+      wc = uniform64(wc);
+      const int64_t rs = (int64_t)rp[row_begin + wr];
+      const int64_t re = (int64_t)rp[row_begin + wr + 1];
+      int64_t j0 = rs, j1 = re;
+      if (wc >= 0) {
+        j0 = rs + wc * chunk;
+        j1 = (re - j0 - chunk < chunk) ? re : j0 + chunk;
+      }
+      const int gb = wave * GPW + gsub;  // lane-group of the block
+      const bool chain = wave == 0 && gsub == 0;
+      for (int64_t c0 = 0; c0 < n; c0 += W) {
+        const int64_t cc = c0 + (int64_t)gl * VEC;
+        const bool active = cc < n;
+        A acc[VEC];
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[e] = A(0);
+        block_accumulate<T, I, K>(col, val, vperm, active ? B + cc : B, ldb, j0, j1, gb, gl,
+                                  chain, lds, acc);
+        if (chain && active) {
+          if (wc >= 0)
+            store_partial<A, VEC>(part + w * n + cc, acc);
+          else
+            store_row<T, VEC, K::NT>(C + wr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
+        }
+      }
+      return;
+    }
+  }
+  // one lane-group per work item; in the WH / BI forms these are the light rows after the wave /
+  // block items
+  int64_t g = ((int64_t)(blockIdx.x - ((K::WH || K::BI) ? wave_blocks : 0)) * kWaves + wave) * GPW +
+              gsub;
+  if constexpr ((K::WH && LPR < 64) || K::BI) {
+    if (order != nullptr) g += (int64_t)counters[0] + (int64_t)counters[3] - (int64_t)counters[2];
+  }
+  int64_t lr, c = -1;  // local row; chunk index or -1 for a whole row
+  if (order == nullptr) {
+    if (g >= nrows) return;
+    lr = g;
+  } else {
+    const int64_t nchunks = (int64_t)counters[0];
+    if (g < nchunks) {
+      lr = items[2 * g + 0];
+      c = items[2 * g + 1];
+    } else {
+      const int64_t q = g - nchunks;
+      if (q >= nrows - (int64_t)counters[1]) return;
+      lr = order[q];
+    }
+  }
+  if constexpr (LPR == 64) {
+    lr = uniform64(lr);
+    c = uniform64(c);
+  }
+  const int64_t rs = (int64_t)rp[row_begin + lr];
+  const int64_t re = (int64_t)rp[row_begin + lr + 1];
+  int64_t j0 = rs, j1 = re;
+  if (c >= 0) {
+    // chunk c of num_chunks(len, chunk) = len / chunk; the last one (fewer than 2 * chunk
+    // nonzeros left from its start) takes the remainder.  No 64-bit division per work item.
+    j0 = rs + c * chunk;
+    j1 = (re - j0 - chunk < chunk) ? re : j0 + chunk;
+  }
+  for (int64_t c0 = 0; c0 < n; c0 += (int64_t)LPR * VEC) {
+    const int64_t cc = c0 + (int64_t)gl * VEC;
+    const bool active = cc < n;
+    A acc[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc[e] = A(0);
+    accumulate<T, I, K>(col, val, vperm, B + cc, B, ldb, j0, j1, gl, gbase, active, acc);
+    if (active) {
+      if (c >= 0)
+        store_partial<A, VEC>(part + g * n + cc, acc);
+      else
+        store_row<T, VEC, K::NT>(C + lr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
+    }
+  }
+}
+
 // ---- hub reduce: C[hub row] = ((0 + part[chunk 0]) + part[chunk 1]) + ... (chunk order) ---------
 // One group of L lanes per hub (64/L hubs per wave); each lane owns VEC consecutive columns and
 // reads them as one 16-B vector per partial row, kPre partial rows in flight before the in-order
@@ -913,8 +962,14 @@ int launch_cfg(const Launch& L) {
   // Work list length <= hub chunks + rows; surplus groups exit at once.  The WH form puts one
   // wave per hub chunk / heavy row first (upper bound: every chunk and row), then the groups.
   const int64_t work = L.nrows + (plan ? w.max_chunks : 0);
-  const int64_t wave_blocks =
-      (K::WH && K::LPR < 64 && plan) ? (work + K::WPB - 1) / K::WPB : 0;
+  // The BI form puts one block per hub chunk / heavy row first (upper bound: every chunk and
+  // every row longer than the heavy threshold).
+  const int64_t heavy = L.sched.heavy == 0 ? auto_heavy(L.nrows, L.nnz) : L.sched.heavy;
+  const int64_t bi_items =
+      w.max_chunks + (heavy == INT64_MAX ? 0 : std::min<int64_t>(L.nrows, L.nnz / (heavy + 1) + 1));
+  const int64_t wave_blocks = (K::WH && K::LPR < 64 && plan) ? (work + K::WPB - 1) / K::WPB
+                              : (K::BI && plan)              ? bi_items
+                                                             : 0;
   const int64_t grid = wave_blocks + (work + GPB - 1) / GPB;
   OFX_REQUIRE(grid < (int64_t)UINT32_MAX, OFX_EINVAL, "spmm_csr: too many rows (%lld)",
               (long long)L.nrows);
@@ -980,13 +1035,32 @@ int launch_vec_small(const Launch& L, int lpr) {
   }
 }
 
+// Mid form (use_mid_form): block items first, then one lane-group per light row.  SR: the light
+// rows run the small-launch configuration (U = 32 / 16 loads in flight, next batch prefetched)
+// instead of the big-launch one (U = 8, 16 for one-element fp32 lanes).
+template <typename T, typename I, int VEC, bool SR>
+int launch_vec_mid(const Launch& L, int lpr) {
+  constexpr int U = SR ? (VEC * sizeof(T) <= 4 ? 32 : 16) : (VEC == 1 && sizeof(T) == 4 ? 16 : 8);
+  switch (lpr) {
+    case 4: return launch_cfg<T, I, Cfg<VEC, 4, U, 4, false, SR, false, false, true>>(L);
+    case 8: return launch_cfg<T, I, Cfg<VEC, 8, U, 4, false, SR, false, false, true>>(L);
+    case 16: return launch_cfg<T, I, Cfg<VEC, 16, U, 4, false, SR, false, false, true>>(L);
+    case 32: return launch_cfg<T, I, Cfg<VEC, 32, U, 4, false, SR, false, false, true>>(L);
+    case 64: return launch_cfg<T, I, Cfg<VEC, 64, U, 4, false, SR, false, false, true>>(L);
+    default: return fail(OFX_EINVAL, "spmm_csr: unsupported lanes-per-row %d", lpr);
+  }
+}
+
 template <typename T, typename I, int VEC>
 int launch_vec(const Launch& L, int lpr, bool nt) {
-  // forced variants (tests, tuning) keep the U = 8 configurations at every size
-  if ((L.nrows <= kSmallRows && L.sched.variant == 0 &&
-       (!nt || use_small_form(L.nrows, L.nnz, L.n, L.sched))) ||
-      L.sched.variant == kForceSmallVariant)
+  const int v = L.sched.variant;
+  if (v == kForceSmallVariant || (v == 0 && use_small_form(L.nrows, L.nnz, L.n, L.sched)))
     return launch_vec_small<T, I, VEC>(L, lpr);
+  if (v == kForceMidSmallVariant) return launch_vec_mid<T, I, VEC, true>(L, lpr);
+  if (v == kForceMidVariant || (v == 0 && use_mid_form(L.nrows, L.nnz, L.n, L.sched)))
+    return launch_vec_mid<T, I, VEC, false>(L, lpr);
+  // forced variants (tests, tuning) keep the U = 8 configurations at every size
+  if (L.nrows <= kSmallRows && v == 0 && !nt) return launch_vec_small<T, I, VEC>(L, lpr);
   switch (lpr) {
     case 4: return launch_cfg<T, I, Cfg<VEC, 4>>(L);
     case 8: return launch_cfg<T, I, Cfg<VEC, 8>>(L);
@@ -1007,12 +1081,11 @@ int launch_vec(const Launch& L, int lpr, bool nt) {
 
 template <typename T, typename I>
 int launch_typed(const Launch& L) {
-  const bool force_small = L.sched.variant == kForceSmallVariant;
-  if (L.sched.variant >= 10000 && !force_small)
-    return launch_tuned<T, I>(L, L.sched.variant - 10000);
+  const bool form = is_form_variant(L.sched.variant);  // auto configuration, forced form
+  if (L.sched.variant >= 10000 && !form) return launch_tuned<T, I>(L, L.sched.variant - 10000);
   // variant = VEC * 100 + LPR forces a configuration (tuning / tests); 0 = auto.
-  const int forced_vec = (L.sched.variant > 0 && !force_small) ? L.sched.variant / 100 : 0;
-  const int forced_lpr = (L.sched.variant > 0 && !force_small) ? L.sched.variant % 100 : 0;
+  const int forced_vec = (L.sched.variant > 0 && !form) ? L.sched.variant / 100 : 0;
+  const int forced_lpr = (L.sched.variant > 0 && !form) ? L.sched.variant % 100 : 0;
   // fp32 rows of <= 64 B: one element per lane over 16 lanes beats 4 lanes of float4 (+9% on
   // products-shaped N=16, scripts/ab.py); wider rows keep the widest vector
   const int vec = (!forced_vec && sizeof(T) == 4 && L.n <= 16) ? 1

@@ -38,6 +38,42 @@ inline bool use_small_form(int64_t nrows, int64_t nnz, int64_t n, const Schedule
   return s.variant == 0 && nrows <= kSmallRows && nnz <= kSmallFormElems / (n > 0 ? n : 1);
 }
 
+// Mid form (spmm_main_kernel with block items): launches above the small form and at most
+// kMidFormElems products.  Such a launch is short enough that its longest item sets its time:
+// a hub chunk or a long row summed by one lane-group is a chain of len / U dependent load rounds
+// (arxiv-shaped at N=16: a 7k-nonzero row held the launch at 600 us, profiles/r02j_probe_mid.json).
+// In the mid form every hub chunk and every row above the heavy threshold (the plan's bin 0,
+// at least kBlockItemMin nonzeros) is taken by a whole block (block_accumulate, the small form's
+// engine); the other rows keep one lane-group each.  Bits are unchanged: only who adds changes.
+constexpr int64_t kMidFormElems = int64_t(1) << 28;
+constexpr int64_t kBlockItemMin = 128;
+constexpr int kForceMidVariant = 30001;       // tuning: mid form at any size, big-launch rows
+constexpr int kForceMidSmallVariant = 30002;  // tuning: mid form, small-launch rows (U=32, PF)
+
+inline bool use_mid_form(int64_t nrows, int64_t nnz, int64_t n, const Schedule& s) {
+  if (s.variant == kForceMidVariant || s.variant == kForceMidSmallVariant) return true;
+  return s.variant == 0 && !use_small_form(nrows, nnz, n, s) &&
+         nnz <= kMidFormElems / (n > 0 ? n : 1);
+}
+
+// Tuning variants that force a form (small / mid) but keep the automatic configuration.
+inline bool is_form_variant(int v) {
+  return v == kForceSmallVariant || v == kForceMidVariant || v == kForceMidSmallVariant;
+}
+
+// The schedule a launch of `nrows` rows runs with: the mid form always plans (binned work list)
+// and raises the automatic heavy threshold to kBlockItemMin.  The workspace query, the planner
+// entry (ofx_spmm_csr_plan) and the launch all go through this, so a plan built once matches.
+inline Schedule launch_schedule(int64_t nrows, int64_t nnz, int64_t n, Schedule s) {
+  if (!use_mid_form(nrows, nnz, n, s)) return s;
+  s.force_bin = 1;
+  if (s.heavy == 0) {
+    const int64_t h = auto_heavy(nrows, nnz);
+    s.heavy = h > kBlockItemMin ? h : kBlockItemMin;
+  }
+  return s;
+}
+
 // Every (value, index) type pair: spmm_inst_<T>_<I>.hip (explicit instantiations).
 template <typename T, typename I>
 int launch_typed(const Launch& L);

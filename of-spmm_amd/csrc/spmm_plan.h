@@ -242,7 +242,7 @@ constexpr int64_t kMinBinRows = 16384;  // below this the grid is one wave of bl
 
 WsLayout ws_layout(int64_t nrows, int64_t nnz, int64_t n, size_t acc_bytes, const Schedule& s) {
   WsLayout w{};
-  const bool bin = s.heavy != INT64_MAX && nrows >= kMinBinRows;
+  const bool bin = s.heavy != INT64_MAX && (nrows >= kMinBinRows || s.force_bin);
   const bool hub = s.split != INT64_MAX && nnz > s.split;
   if (!bin && !hub) return w;  // identity work list: no plan, no workspace
   w.max_hubs = s.split == INT64_MAX ? 0 : nnz / (s.split + 1) + 1;
@@ -288,11 +288,7 @@ int launch_plan(hipStream_t stream, const I* rp, int64_t row_begin, int64_t nrow
                 const Schedule& sched, const WsLayout& w, char* ws, WorkList* wl) {
   // Heavy-bin threshold: rows above ~5x the mean degree go first (measured: products and the
   // 1M power-law config both peak at 4-6x the mean).  Order only, never numerics.
-  int64_t heavy = sched.heavy;
-  if (heavy == 0) {
-    const int64_t mean = nrows > 0 ? (nnz + nrows - 1) / nrows : 1;
-    heavy = 5 * mean < 16 ? 16 : 5 * mean;
-  }
+  const int64_t heavy = sched.heavy == 0 ? auto_heavy(nrows, nnz) : sched.heavy;
   worklist_of(w, ws, wl);
   auto* block_tot = reinterpret_cast<int64_t*>(ws + w.block_tot);
   const unsigned pgrid = (unsigned)w.plan_blocks;

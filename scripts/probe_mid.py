@@ -1,6 +1,7 @@
-"""Mid-size launches (above the small form's 2^20 products): the planned form (plan + main +
-reduce, five launches) against the small form forced at any size (tuning variant 30000, one
-launch), with the light/whole-block cut varied.  Prints one JSON object."""
+"""Mid-size launches (above the small form's 2^20 products): the default choice against the small
+form (tuning variant 30000, one launch) and the mid form (30001: block items + big-launch light
+rows; 30002: block items + prefetching light rows), with the block-item cut varied.  Prints one
+JSON object."""
 import json
 import sys
 
@@ -35,10 +36,13 @@ for name, (m, nnz) in graphs.items():
         b = synth.dense(0, m, n, device=dev)
         out = torch.empty((m, n), device=dev)
         ref = None
-        for label, opts in {"planned": None,
+        for label, opts in {"default": None,
                             "small": ops.make_options(variant=30000),
-                            "small_cut256": ops.make_options(variant=30000, heavy=256),
-                            "small_cut1024": ops.make_options(variant=30000, heavy=1024)}.items():
+                            "mid": ops.make_options(variant=30001),
+                            "mid_sr": ops.make_options(variant=30002),
+                            "mid_cut64": ops.make_options(variant=30001, heavy=64),
+                            "mid_cut512": ops.make_options(variant=30001, heavy=512),
+                            "mid_sr_cut512": ops.make_options(variant=30002, heavy=512)}.items():
             k = ops.SpmmCsrKernel(m, m, n, nnz, torch.int32, torch.float32, dev, opts)
             res[f"{name}_n{n}_{label}_us"] = t(lambda: k(rp, ci, v, b, out))
             if ref is None:

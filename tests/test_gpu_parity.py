@@ -557,3 +557,68 @@ def test_small_form_single_launch(device, dtype, idx, n):
         out5 = ops.spmm_csr_device(*d, m, k, options=ops.make_options(heavy=cut))
         torch.cuda.synchronize()
         assert_bitwise(out5, ref, f"light cut {cut}")
+
+
+@pytest.mark.parametrize("dtype,idx", [("f32", torch.int32), ("f32", torch.int64), ("bf16", torch.int32),
+                                       ("f16", torch.int64), ("f64", torch.int32)])
+@pytest.mark.parametrize("n", [1, 16, 17, 64, 128, 300])
+def test_mid_form_block_items(device, dtype, idx, n):
+    """Mid-size launches (above the small form, <= 2^28 products): every hub chunk and every row
+    above the heavy threshold is taken by a whole block (block_accumulate), the other rows by one
+    lane-group, after a plan.  Same bits as the oracle in the automatic choice and in each forced
+    form (30000 small, 30001 mid, 30002 mid with prefetching light rows), for row ranges, a plan
+    built once, the epilogue, gathered values, the ordered option and any heavy cut."""
+    rng = np.random.default_rng(1300 + n)
+    split = ops.default_split(n)
+    m, k = 5000, 24000
+    deg = rng.integers(0, 20, size=m)
+    special = [127, 128, 129, 1000, split, split + 1, 2 * split - 1, 2 * split + 7, 3 * split + 5,
+               min(9 * split, k)]
+    for i, d in enumerate(special):
+        deg[11 + 431 * i] = min(d, k)
+    deg[4000:4040] = rng.integers(130, 700, size=40)
+    rp, ci, v = random_csr(m, k, deg, rng, idx, DTYPES[dtype])
+    b = random_dense(k, n, rng, DTYPES[dtype])
+    nnz = ci.numel()
+    d = (rp.to(device), ci.to(device), v.to(device), b.to(device))
+    ref = oracle_spmm(rp, ci, v, b)
+    out = fs.spmm(d[0], d[1], d[2], m, k, d[3])
+    torch.cuda.synchronize()
+    assert_bitwise(out, ref, f"{dtype} n={n} auto (products {nnz * n})")
+    for variant in (30000, 30001, 30002):
+        opts = ops.make_options(variant=variant)
+        o = ops.spmm_csr_device(*d, m, k, options=opts)
+        torch.cuda.synchronize()
+        assert_bitwise(o, ref, f"form {variant}")
+        kern = ops.SpmmCsrKernel(m, k, n, nnz, idx, DTYPES[dtype], device, opts)
+        sub = torch.full((3100, n), float("nan"), dtype=DTYPES[dtype], device=device)
+        kern(*d, sub, row_begin=900, row_end=4000)
+        torch.cuda.synchronize()
+        assert_bitwise(sub, ref[900:4000], f"form {variant} row range")
+        if variant != 30000:  # a plan built once (the small form has none)
+            kp = ops.SpmmCsrKernel(m, k, n, nnz, idx, DTYPES[dtype], device, opts).plan(d[0], 0, m)
+            o2 = torch.full((m, n), float("nan"), dtype=DTYPES[dtype], device=device)
+            kp(*d, o2, 0, m, planned=True)
+            torch.cuda.synchronize()
+            assert_bitwise(o2, ref, f"form {variant} planned")
+        for cut in (1, 129, 100000):  # the block-item cut moves work, never bits
+            o3 = ops.spmm_csr_device(*d, m, k, options=ops.make_options(variant=variant, heavy=cut))
+            torch.cuda.synchronize()
+            assert_bitwise(o3, ref, f"form {variant} heavy cut {cut}")
+    opts = ops.make_options(variant=30001)
+    kern = ops.SpmmCsrKernel(m, k, n, nnz, idx, DTYPES[dtype], device, opts)
+    bias = random_dense(1, n, rng, DTYPES[dtype])[0]
+    out2 = torch.full((m, n), float("nan"), dtype=DTYPES[dtype], device=device)
+    kern(*d, out2, bias=bias.to(device), relu=True)
+    torch.cuda.synchronize()
+    assert_bitwise(out2, oracle.bias_act(ref, to_oracle(bias), "relu", dtype=dtype), "epilogue")
+    out3 = ops.spmm_csr_device(*d, m, k, options=ops.make_options(variant=30001, ordered=True))
+    torch.cuda.synchronize()
+    assert_bitwise(out3, oracle_spmm(rp, ci, v, b, ordered=True), "ordered")
+    perm = torch.from_numpy(rng.permutation(nnz).astype(np.int64)).to(idx)
+    vals_src = torch.empty_like(v)
+    vals_src[perm.long()] = v
+    out4 = ops.spmm_csr_gathered(d[0], d[1], vals_src.to(device), perm.to(device), d[3], m, k,
+                                 options=opts)
+    torch.cuda.synchronize()
+    assert_bitwise(out4, ref, "gathered values")
