@@ -517,35 +517,56 @@ __device__ __forceinline__ void block_accumulate(const I* __restrict__ col,
     if (stage) span_load((k + D) / S + 1, rc, rv);
     issue(k + D, b);
     if (chain) {
+      // full rounds of reads in flight, then one guarded round for the rest of the batch (a
+      // batch that is not a whole number of rounds pays one LDS wait for its tail, not one per
+      // product)
       int i = 0;
       if constexpr (SF::kColMajor) {
-        // column gl: 4 consecutive nonzeros per 16-B read, 8 reads in flight
+        // column gl: 4 consecutive nonzeros per 16-B read, QR reads in flight
+        constexpr int QR = 8;
         const A* cp = buf + gl * NBP;
-        for (; i + 32 <= cnt; i += 32) {
-          Pack<A, 4> x[8];
+        for (; i + 4 * QR <= cnt; i += 4 * QR) {
+          Pack<A, 4> x[QR];
 #pragma unroll
-          for (int q = 0; q < 8; ++q) x[q] = *reinterpret_cast<const Pack<A, 4>*>(cp + i + 4 * q);
+          for (int q = 0; q < QR; ++q) x[q] = *reinterpret_cast<const Pack<A, 4>*>(cp + i + 4 * q);
 #pragma unroll
-          for (int q = 0; q < 8; ++q)
+          for (int q = 0; q < QR; ++q)
 #pragma unroll
             for (int e = 0; e < 4; ++e) acc[0] = acc[0] + x[q].v[e];
         }
-        for (; i < cnt; ++i) acc[0] = acc[0] + cp[i];
-      } else {
-        for (; i + 16 <= cnt; i += 16) {
-          PA x[16];
+        if (i < cnt) {
+          Pack<A, 4> x[QR];
 #pragma unroll
-          for (int q = 0; q < 16; ++q)
+          for (int q = 0; q < QR; ++q)
+            if (i + 4 * q < cnt) x[q] = *reinterpret_cast<const Pack<A, 4>*>(cp + i + 4 * q);
+#pragma unroll
+          for (int q = 0; q < QR; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (i + 4 * q + e < cnt) acc[0] = acc[0] + x[q].v[e];
+        }
+      } else {
+        constexpr int QR = 16;
+        for (; i + QR <= cnt; i += QR) {
+          PA x[QR];
+#pragma unroll
+          for (int q = 0; q < QR; ++q)
             x[q] = *reinterpret_cast<const PA*>(buf + (i + q) * W + gl * VEC);
 #pragma unroll
-          for (int q = 0; q < 16; ++q)
+          for (int q = 0; q < QR; ++q)
 #pragma unroll
             for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + x[q].v[e];
         }
-        for (; i < cnt; ++i) {
-          const PA x = *reinterpret_cast<const PA*>(buf + i * W + gl * VEC);
+        if (i < cnt) {
+          PA x[QR];
 #pragma unroll
-          for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + x.v[e];
+          for (int q = 0; q < QR; ++q)
+            if (i + q < cnt) x[q] = *reinterpret_cast<const PA*>(buf + (i + q) * W + gl * VEC);
+#pragma unroll
+          for (int q = 0; q < QR; ++q)
+            if (i + q < cnt)
+#pragma unroll
+              for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + x[q].v[e];
         }
       }
     }
@@ -1030,7 +1051,7 @@ int launch_vec_small(const Launch& L, int lpr) {
     case 8: return launch_small_or_planned<T, I, Cfg<VEC, 8, U, 4, false, true, false, true>>(L);
     case 16: return launch_small_or_planned<T, I, Cfg<VEC, 16, U, 4, false, true, false, true>>(L);
     case 32: return launch_small_or_planned<T, I, Cfg<VEC, 32, U, 4, false, true, false, true>>(L);
-    case 64: return launch_small_or_planned<T, I, Cfg<VEC, 64, U>>(L);
+    case 64: return launch_small_or_planned<T, I, Cfg<VEC, 64, U, 4, false, false, false, false>>(L);
     default: return fail(OFX_EINVAL, "spmm_csr: unsupported lanes-per-row %d", lpr);
   }
 }
@@ -1057,8 +1078,12 @@ int launch_vec(const Launch& L, int lpr, bool nt) {
   if (v == kForceSmallVariant || (v == 0 && use_small_form(L.nrows, L.nnz, L.n, L.sched)))
     return launch_vec_small<T, I, VEC>(L, lpr);
   if (v == kForceMidSmallVariant) return launch_vec_mid<T, I, VEC, true>(L, lpr);
-  if (v == kForceMidVariant || (v == 0 && use_mid_form(L.nrows, L.nnz, L.n, L.sched)))
-    return launch_vec_mid<T, I, VEC, false>(L, lpr);
+  if (v == kForceMidVariant) return launch_vec_mid<T, I, VEC, false>(L, lpr);
+  // light rows of the mid form: the prefetching small-launch configuration above N = 16 (5-12%
+  // faster at N = 64 / 128 on 20k-170k-row power-law graphs), the big-launch one at N <= 16
+  // (profiles/r02n_probe_mid.json)
+  if (v == 0 && use_mid_form(L.nrows, L.nnz, L.n, L.sched))
+    return L.n > 16 ? launch_vec_mid<T, I, VEC, true>(L, lpr) : launch_vec_mid<T, I, VEC, false>(L, lpr);
   // forced variants (tests, tuning) keep the U = 8 configurations at every size
   if (L.nrows <= kSmallRows && v == 0 && !nt) return launch_vec_small<T, I, VEC>(L, lpr);
   switch (lpr) {

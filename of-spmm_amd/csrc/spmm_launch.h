@@ -46,7 +46,7 @@ inline bool use_small_form(int64_t nrows, int64_t nnz, int64_t n, const Schedule
 // at least kBlockItemMin nonzeros) is taken by a whole block (block_accumulate, the small form's
 // engine); the other rows keep one lane-group each.  Bits are unchanged: only who adds changes.
 constexpr int64_t kMidFormElems = int64_t(1) << 28;
-constexpr int64_t kBlockItemMin = 128;
+constexpr int64_t kBlockItemMin = 64;
 constexpr int kForceMidVariant = 30001;       // tuning: mid form at any size, big-launch rows
 constexpr int kForceMidSmallVariant = 30002;  // tuning: mid form, small-launch rows (U=32, PF)
 

@@ -58,25 +58,39 @@ __device__ __forceinline__ int plan_row(const I* __restrict__ rp, int64_t row_be
 }
 
 // Block-wide exclusive scan of kPlanVals int64 values (256 threads); returns the block totals.
+// Each wave scans with cross-lane moves (no barrier), the four wave totals meet in LDS: two
+// barriers instead of the sixteen of a shared-memory Hillis-Steele scan.
 __device__ __forceinline__ void block_scan_vals(int64_t (&v)[kPlanVals], int64_t (&tot)[kPlanVals]) {
-  __shared__ int64_t sh[kPlanVals][kBlock];
-  const int t = threadIdx.x;
+  constexpr int kWaves = kBlock / 64;
+  __shared__ int64_t wsum[kPlanVals][kWaves];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int64_t inc[kPlanVals];
 #pragma unroll
-  for (int i = 0; i < kPlanVals; ++i) sh[i][t] = v[i];
-  __syncthreads();
-  for (int off = 1; off < kBlock; off <<= 1) {
-    int64_t x[kPlanVals];
+  for (int i = 0; i < kPlanVals; ++i) inc[i] = v[i];
 #pragma unroll
-    for (int i = 0; i < kPlanVals; ++i) x[i] = t >= off ? sh[i][t - off] : 0;
-    __syncthreads();
+  for (int off = 1; off < 64; off <<= 1) {
 #pragma unroll
-    for (int i = 0; i < kPlanVals; ++i) sh[i][t] += x[i];
-    __syncthreads();
+    for (int i = 0; i < kPlanVals; ++i) {
+      const int64_t y = (int64_t)__shfl_up((long long)inc[i], off);
+      if (lane >= off) inc[i] += y;
+    }
   }
+  if (lane == 63) {
+#pragma unroll
+    for (int i = 0; i < kPlanVals; ++i) wsum[i][wv] = inc[i];
+  }
+  __syncthreads();
 #pragma unroll
   for (int i = 0; i < kPlanVals; ++i) {
-    tot[i] = sh[i][kBlock - 1];
-    v[i] = sh[i][t] - v[i];  // exclusive
+    int64_t pre = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      const int64_t x = wsum[i][w];
+      all += x;
+      if (w < wv) pre += x;
+    }
+    tot[i] = all;
+    v[i] = pre + inc[i] - v[i];  // exclusive
   }
   __syncthreads();
 }
@@ -231,6 +245,83 @@ __global__ void __launch_bounds__(kBlock)
                   order);
 }
 
+// plan_scan folded into plan_write for launches of at most kFusedPlanBlocks plan blocks (<= 256K
+// rows): every write block sums the per-block totals itself (its exclusive offset and the grand
+// totals, O(blocks) reads per block), so the planner is two launches instead of three.  Block 0
+// publishes the counters.  Same layout as the three-launch form.
+constexpr int64_t kFusedPlanBlocks = 256;
+
+template <typename I>
+__global__ void __launch_bounds__(kBlock)
+    spmm_plan_write_fused_kernel(const I* __restrict__ rp, int64_t row_begin, int64_t nrows,
+                                 int64_t split, int64_t chunk, int64_t heavy,
+                                 const int64_t* __restrict__ block_tot, int64_t nblocks,
+                                 unsigned long long* __restrict__ counters,
+                                 int64_t* __restrict__ hubs, int64_t* __restrict__ items,
+                                 int64_t* __restrict__ order) {
+  __shared__ unsigned long long s_off[kPlanVals], s_tot[kPlanVals], s_bin[kBins];
+  // the per-block totals and this block's row_ptr entries are loaded together (one memory
+  // round trip, not two)
+  int cls[kPlanRowsPerThread];
+  int64_t nc[kPlanRowsPerThread], v[kPlanVals], tot[kPlanVals], off[kPlanVals];
+  const int64_t base = (int64_t)blockIdx.x * kPlanRows + (int64_t)threadIdx.x * kPlanRowsPerThread;
+  int64_t po[kPlanVals] = {}, pt[kPlanVals] = {};
+  for (int64_t b = threadIdx.x; b < nblocks; b += kBlock) {
+#pragma unroll
+    for (int i = 0; i < kPlanVals; ++i) {
+      const int64_t x = block_tot[kPlanVals * b + i];
+      pt[i] += x;
+      if (b < (int64_t)blockIdx.x) po[i] += x;
+    }
+  }
+  plan_thread(rp, row_begin, nrows, base, split, chunk, heavy, cls, nc, v);
+  // wave sums of the partial offsets / totals, then one slot per wave (integer sums: any order
+  // gives the same value)
+  __shared__ int64_t w_off[kPlanVals][kBlock / 64], w_tot[kPlanVals][kBlock / 64];
+#pragma unroll
+  for (int i = 0; i < kPlanVals; ++i) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      po[i] += (int64_t)__shfl_xor((long long)po[i], m);
+      pt[i] += (int64_t)__shfl_xor((long long)pt[i], m);
+    }
+  }
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int i = 0; i < kPlanVals; ++i) {
+      w_off[i][threadIdx.x >> 6] = po[i];
+      w_tot[i][threadIdx.x >> 6] = pt[i];
+    }
+  }
+  block_scan_vals(v, tot);  // its barriers also publish the wave slots above
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < kPlanVals; ++i) {
+      int64_t a = 0, b = 0;
+      for (int w = 0; w < kBlock / 64; ++w) {
+        a += w_off[i][w];
+        b += w_tot[i][w];
+      }
+      s_off[i] = (unsigned long long)a;
+      s_tot[i] = (unsigned long long)b;
+    }
+    unsigned long long start = 0;
+    for (int b = 0; b < kBins; ++b) {
+      s_bin[b] = start;
+      start += s_tot[2 + b];
+    }
+    if (blockIdx.x == 0) {
+      counters[0] = s_tot[1];
+      counters[1] = s_tot[0];
+      for (int b = 0; b < kBins; ++b) counters[2 + b] = s_bin[b];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kPlanVals; ++i) off[i] = (int64_t)s_off[i];
+  plan_write_rows(cls, nc, v, off, s_bin, base, hubs, items, order);
+}
+
 struct WsLayout {
   size_t counters, block_tot, hubs, items, order, part, total;
   int64_t max_hubs, max_chunks, plan_blocks;
@@ -295,6 +386,13 @@ int launch_plan(hipStream_t stream, const I* rp, int64_t row_begin, int64_t nrow
   hipLaunchKernelGGL((spmm_plan_count_kernel<I>), dim3(pgrid), dim3(kBlock), 0, stream, rp,
                      row_begin, nrows, sched.split, sched.chunk, heavy, block_tot);
   OFX_HIP_CHECK(hipGetLastError());
+  if (w.plan_blocks <= kFusedPlanBlocks) {
+    hipLaunchKernelGGL((spmm_plan_write_fused_kernel<I>), dim3(pgrid), dim3(kBlock), 0, stream, rp,
+                       row_begin, nrows, sched.split, sched.chunk, heavy, block_tot,
+                       w.plan_blocks, wl->counters, wl->hubs, wl->items, wl->order);
+    OFX_HIP_CHECK(hipGetLastError());
+    return OFX_OK;
+  }
   hipLaunchKernelGGL(spmm_plan_scan_kernel, dim3(1), dim3(kBlock), 0, stream, block_tot,
                      w.plan_blocks, wl->counters);
   OFX_HIP_CHECK(hipGetLastError());

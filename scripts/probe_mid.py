@@ -40,9 +40,8 @@ for name, (m, nnz) in graphs.items():
                             "small": ops.make_options(variant=30000),
                             "mid": ops.make_options(variant=30001),
                             "mid_sr": ops.make_options(variant=30002),
-                            "mid_cut64": ops.make_options(variant=30001, heavy=64),
-                            "mid_cut512": ops.make_options(variant=30001, heavy=512),
-                            "mid_sr_cut512": ops.make_options(variant=30002, heavy=512)}.items():
+                            "mid_cut32": ops.make_options(variant=30001, heavy=32),
+                            "mid_sr_cut32": ops.make_options(variant=30002, heavy=32)}.items():
             k = ops.SpmmCsrKernel(m, m, n, nnz, torch.int32, torch.float32, dev, opts)
             res[f"{name}_n{n}_{label}_us"] = t(lambda: k(rp, ci, v, b, out))
             if ref is None:

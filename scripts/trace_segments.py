@@ -15,7 +15,8 @@ segs.append(cur)
 for i, s in enumerate(segs):
     dur = collections.defaultdict(list)
     for r in s:
-        dur[r["Kernel_Name"].split("(")[0][:80]].append(
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+        dur[name.split("(")[0][:90]].append(
             (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     calls = max(len(v) for v in dur.values())
     span = (int(s[-1]["End_Timestamp"]) - int(s[0]["Start_Timestamp"])) / 1e3
