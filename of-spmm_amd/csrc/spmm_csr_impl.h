@@ -376,6 +376,18 @@ __device__ __forceinline__ void store_partial(A* __restrict__ p, const A (&acc)[
   for (int e = 0; e < VEC; ++e) p[e] = acc[e];
 }
 
+// Block-engine sizes (compile-time knobs for A/B builds: scripts/ab_build.sh): bytes of products
+// per LDS buffer, nonzeros per batch, B-row loads per lane per batch.
+#ifndef OFX_BE_LDS
+#define OFX_BE_LDS 16384
+#endif
+#ifndef OFX_BE_NB_CAP
+#define OFX_BE_NB_CAP 128
+#endif
+#ifndef OFX_BE_UW_CAP
+#define OFX_BE_UW_CAP 8
+#endif
+
 // ---- small form: one launch, no plan, no workspace -------------------------------------------
 // Launches with few rows and little B-row traffic (use_small_form) run as ONE kernel.  Block b
 // owns rows [b*RPB, (b+1)*RPB), one lane-group per row.  A group takes its row when the row has at
@@ -395,10 +407,10 @@ struct SmallForm {
   static constexpr int RPB = GB;                          // rows per block
   static constexpr int D = 4;                             // batches of B-row loads in flight
   static constexpr int S = 8;                             // batches per (col, val) span
-  static constexpr int kLdsElems = 16384 / (int)sizeof(A);  // 16 KB of products per buffer
-  static constexpr int NB_RAW0 = kLdsElems / W < 128 ? kLdsElems / W : 128;
+  static constexpr int kLdsElems = OFX_BE_LDS / (int)sizeof(A);  // 16 KB of products per buffer
+  static constexpr int NB_RAW0 = kLdsElems / W < OFX_BE_NB_CAP ? kLdsElems / W : OFX_BE_NB_CAP;
   static constexpr int UW_RAW = NB_RAW0 / GB;
-  static constexpr int UW = UW_RAW > 8 ? 8 : (UW_RAW < 1 ? 1 : UW_RAW);  // loads per lane per batch
+  static constexpr int UW = UW_RAW > OFX_BE_UW_CAP ? OFX_BE_UW_CAP : (UW_RAW < 1 ? 1 : UW_RAW);  // loads per lane per batch
   static constexpr int NB = UW * GB;                      // nonzeros per batch
   static constexpr int SPAN = S * NB;                     // nonzeros per (col, val) span
   static constexpr int PT = (SPAN + kThreads - 1) / kThreads;  // span entries per thread
@@ -408,7 +420,7 @@ struct SmallForm {
   static constexpr int NBP = NB + 4;
   static constexpr int kBufElems = kColMajor ? W * NBP : NB * W;
   static_assert(S % D == 0 && S > D, "small form: span must hold whole rounds of the load ring");
-  static_assert(kBufElems * (int)sizeof(A) <= 16384 + 4 * W * (int)sizeof(A),
+  static_assert(kBufElems * (int)sizeof(A) <= OFX_BE_LDS + 4 * W * (int)sizeof(A),
                 "small form: LDS batch too large");
 };
 
