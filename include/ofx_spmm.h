@@ -275,6 +275,19 @@ int ofx_event_record(void* event, void* stream);
 int ofx_event_sync(void* event);
 int ofx_event_elapsed_ms(void* start, void* end, float* ms);
 int ofx_stream_wait_event(void* stream, void* event);
+/* hipGraph executable and stream capture: ep::CudaGraphExecutable (ep/cuda/cuda_stream.h:41-56,
+ * cuda_stream.cpp:49-80) and CudaStream::BeginGraphCapture / EndGraphCapture / IsGraphCapturing /
+ * LaunchGraph (cuda_stream.cpp:178-196).  end_capture updates a live executable in place
+ * (hipGraphExecUpdate) and re-instantiates only when the update is refused; exec == NULL
+ * discards the capture.  Capture mode is thread-local, as the reference's.                   */
+int ofx_graph_exec_create(void** exec);
+int ofx_graph_exec_destroy(void* exec);
+int ofx_graph_exec_stats(void* exec, int* instantiated, int64_t* instantiations, int64_t* updates,
+                         int64_t* launches);
+int ofx_stream_begin_capture(void* stream);
+int ofx_stream_is_capturing(void* stream, int* capturing);
+int ofx_stream_end_capture(void* stream, void* exec);
+int ofx_graph_launch(void* exec, void* stream);
 
 /* ---- RCCL all-gather (ccl::AllGather) ---------------------------------------------------- */
 #define OFX_UNIQUE_ID_BYTES 128
@@ -495,6 +508,16 @@ int ofx_spmm_job_run(void* job, void* stream, const void* row_ptr, const void* c
                      const void* values, const void* b_shard, void* out, void* tmp,
                      size_t tmp_bytes);
 int ofx_spmm_job_destroy(void* job);
+/* Graph mode of a compiled job (UserKernel::ForwardUserKernel, core/kernel/user_kernel.cpp:
+ * 676-707, with ONEFLOW_KERNEL_ENABLE_CUDA_GRAPH): the first run on a HIP placement is eager
+ * (the logical all-gather creates its communicator then); the next is captured (on the job's
+ * own stream) into a hipGraph that is launched on the caller's stream; a later run with the same
+ * tensor addresses launches the graph, one with different ones re-captures (an in-place
+ * executable update).  Host placements
+ * ignore graph mode.  Stats: captures, launches of a captured graph without re-capture, and
+ * captures that updated the executable in place.                                            */
+int ofx_spmm_job_set_graph(void* job, int enable);
+int ofx_spmm_job_graph_stats(void* job, int64_t* captures, int64_t* replays, int64_t* updates);
 
 #ifdef __cplusplus
 }

@@ -114,3 +114,117 @@ extern "C" int ofx_stream_wait_event(void* stream, void* event) {
                                    static_cast<hipEvent_t>(event), 0));
   return OFX_OK;
 }
+
+// ---- hipGraph executable + stream capture ----------------------------------------------------
+// ep::CudaGraphExecutable (oneflow/core/ep/cuda/cuda_stream.h:41-56, cuda_stream.cpp:49-80):
+// Update() first tries hipGraphExecUpdate on the live executable (same topology, new kernel
+// arguments) and re-instantiates only when the update is refused.  CudaStream's
+// BeginGraphCapture / EndGraphCapture / LaunchGraph (cuda_stream.cpp:178-196) capture in
+// thread-local mode, so other host threads keep launching eagerly meanwhile.
+namespace {
+struct GraphExec {
+  hipGraphExec_t exec = nullptr;
+  int device = -1;
+  int64_t instantiations = 0;  // full hipGraphInstantiate calls
+  int64_t updates = 0;         // in-place hipGraphExecUpdate successes
+  int64_t launches = 0;
+};
+}  // namespace
+
+extern "C" int ofx_graph_exec_create(void** exec) {
+  OFX_REQUIRE(exec, OFX_EINVAL, "graph_exec_create: NULL");
+  *exec = new GraphExec();
+  return OFX_OK;
+}
+extern "C" int ofx_graph_exec_destroy(void* exec) {
+  GraphExec* g = static_cast<GraphExec*>(exec);
+  if (!g) return OFX_OK;
+  if (g->exec) {
+    int cur = -1;
+    OFX_HIP_CHECK(hipGetDevice(&cur));
+    if (g->device >= 0 && g->device != cur) OFX_HIP_CHECK(hipSetDevice(g->device));
+    const hipError_t e = hipGraphExecDestroy(g->exec);
+    if (g->device >= 0 && g->device != cur) (void)hipSetDevice(cur);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      delete g;
+      return ofx::fail(OFX_EDEVICE, "hipGraphExecDestroy: %s", hipGetErrorString(e));
+    }
+  }
+  delete g;
+  return OFX_OK;
+}
+extern "C" int ofx_graph_exec_stats(void* exec, int* instantiated, int64_t* instantiations,
+                                    int64_t* updates, int64_t* launches) {
+  const GraphExec* g = static_cast<const GraphExec*>(exec);
+  OFX_REQUIRE(g, OFX_EINVAL, "graph_exec_stats: NULL executable");
+  if (instantiated) *instantiated = g->exec != nullptr;
+  if (instantiations) *instantiations = g->instantiations;
+  if (updates) *updates = g->updates;
+  if (launches) *launches = g->launches;
+  return OFX_OK;
+}
+extern "C" int ofx_stream_begin_capture(void* stream) {
+  OFX_REQUIRE(stream, OFX_EINVAL, "stream_begin_capture: the null stream cannot be captured");
+  OFX_HIP_CHECK(hipStreamBeginCapture(static_cast<hipStream_t>(stream),
+                                      hipStreamCaptureModeThreadLocal));
+  return OFX_OK;
+}
+extern "C" int ofx_stream_is_capturing(void* stream, int* capturing) {
+  OFX_REQUIRE(capturing, OFX_EINVAL, "stream_is_capturing: NULL");
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  OFX_HIP_CHECK(hipStreamIsCapturing(static_cast<hipStream_t>(stream), &st));
+  *capturing = st != hipStreamCaptureStatusNone;
+  return OFX_OK;
+}
+extern "C" int ofx_stream_end_capture(void* stream, void* exec) {
+  GraphExec* g = static_cast<GraphExec*>(exec);
+  hipGraph_t graph = nullptr;
+  const hipError_t ec = hipStreamEndCapture(static_cast<hipStream_t>(stream), &graph);
+  if (ec != hipSuccess || graph == nullptr) {  // capture invalidated by an unsupported call
+    (void)hipGetLastError();
+    if (graph) (void)hipGraphDestroy(graph);
+    return ofx::fail(OFX_EDEVICE, "hipStreamEndCapture: %s", hipGetErrorString(ec));
+  }
+  if (!g) {  // capture discarded on request (an error path of the caller)
+    OFX_HIP_CHECK(hipGraphDestroy(graph));
+    return OFX_OK;
+  }
+  int rc = OFX_OK;
+  bool done = false;
+  if (g->exec) {
+    hipGraphExecUpdateResult res = hipGraphExecUpdateError;
+    hipGraphNode_t err_node = nullptr;
+    const hipError_t eu = hipGraphExecUpdate(g->exec, graph, &err_node, &res);
+    if (eu == hipSuccess && res == hipGraphExecUpdateSuccess) {
+      ++g->updates;
+      done = true;
+    } else {
+      (void)hipGetLastError();
+      (void)hipGraphExecDestroy(g->exec);
+      g->exec = nullptr;
+    }
+  }
+  if (!done) {
+    const hipError_t ei = hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0);
+    if (ei != hipSuccess) {
+      (void)hipGetLastError();
+      g->exec = nullptr;
+      rc = ofx::fail(OFX_EDEVICE, "hipGraphInstantiate: %s", hipGetErrorString(ei));
+    } else {
+      ++g->instantiations;
+      (void)hipGetDevice(&g->device);
+    }
+  }
+  const hipError_t ed = hipGraphDestroy(graph);
+  if (rc == OFX_OK && ed != hipSuccess)
+    return ofx::fail(OFX_EDEVICE, "hipGraphDestroy: %s", hipGetErrorString(ed));
+  return rc;
+}
+extern "C" int ofx_graph_launch(void* exec, void* stream) {
+  GraphExec* g = static_cast<GraphExec*>(exec);
+  OFX_REQUIRE(g && g->exec, OFX_EINVAL, "graph_launch: executable not instantiated");
+  OFX_HIP_CHECK(hipGraphLaunch(g->exec, static_cast<hipStream_t>(stream)));
+  ++g->launches;
+  return OFX_OK;
+}

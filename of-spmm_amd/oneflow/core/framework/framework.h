@@ -25,6 +25,8 @@
 #include <utility>
 #include <vector>
 
+#include "ofx_spmm.h"
+
 namespace oneflow {
 
 // ---- common ----------------------------------------------------------------------------------
@@ -301,12 +303,49 @@ class CpuStream final : public Stream {
  private:
   int num_threads_;
 };
+// ep::CudaGraphExecutable for kHIP (ep/cuda/cuda_stream.h:41-56) over the C-ABI's hipGraph
+// executable (device_shim.cpp): Update() patches the live executable in place when it can.
+class HipGraphExecutable {
+ public:
+  HipGraphExecutable() { ofx_graph_exec_create(&exec_); }
+  ~HipGraphExecutable() { ofx_graph_exec_destroy(exec_); }
+  HipGraphExecutable(const HipGraphExecutable&) = delete;
+  HipGraphExecutable& operator=(const HipGraphExecutable&) = delete;
+  bool IsInstantiated() const {
+    int yes = 0;
+    ofx_graph_exec_stats(exec_, &yes, nullptr, nullptr, nullptr);
+    return yes != 0;
+  }
+  int64_t updates() const {
+    int64_t u = 0;
+    ofx_graph_exec_stats(exec_, nullptr, nullptr, &u, nullptr);
+    return u;
+  }
+  void* handle() const { return exec_; }
+
+ private:
+  void* exec_ = nullptr;
+};
+
 class HipStream final : public Stream {
  public:
   explicit HipStream(void* hip_stream, int device) : s_(hip_stream), device_(device) {}
   DeviceType device_type() const override { return DeviceType::kHIP; }
   void* hip_stream() const { return s_; }
   int device_index() const { return device_; }
+  // CudaStream::BeginGraphCapture / EndGraphCapture / IsGraphCapturing / LaunchGraph
+  // (cuda_stream.cpp:178-196); status codes instead of CHECKs (the C-ABI's error model).
+  int BeginGraphCapture() { return ofx_stream_begin_capture(s_); }
+  int EndGraphCapture(HipGraphExecutable* executable) {
+    return ofx_stream_end_capture(s_, executable ? executable->handle() : nullptr);
+  }
+  bool IsGraphCapturing() const {
+    int yes = 0;
+    return ofx_stream_is_capturing(s_, &yes) == 0 && yes != 0;
+  }
+  int LaunchGraph(const HipGraphExecutable* executable) {
+    return ofx_graph_launch(executable->handle(), s_);
+  }
 
  private:
   void* s_;

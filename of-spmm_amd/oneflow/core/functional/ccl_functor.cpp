@@ -144,10 +144,74 @@ class SpmmJob {
   const std::string& plan() const { return plan_; }
   size_t tmp_bytes() const { return gathered_bytes_ + spmm_tmp_bytes_; }
 
+  void set_graph(bool enable) {
+    graph_enabled_ = enable && pd_.device_type() == DeviceType::kHIP;
+    if (!graph_enabled_) graph_.reset();
+  }
+  void graph_stats(int64_t* captures, int64_t* replays, int64_t* updates) const {
+    if (captures) *captures = captures_;
+    if (replays) *replays = replays_;
+    if (updates) *updates = graph_ ? graph_->updates() : 0;
+  }
+
+  // UserKernel::ForwardUserKernel's graph branch (core/kernel/user_kernel.cpp:676-707): launch
+  // the captured graph while the tensors are unchanged; otherwise capture this run's launches
+  // on the stream (updating the executable in place), then launch it.
   int Run(void* stream, const void* row_ptr, const void* col_idx, const void* values,
           const void* b_shard, void* out, void* tmp, size_t tmp_bytes) {
     OFX_REQUIRE(tmp_bytes >= this->tmp_bytes() && (tmp || this->tmp_bytes() == 0), OFX_EWORKSPACE,
                 "spmm job: tmp of %zu bytes < %zu", tmp_bytes, this->tmp_bytes());
+    // CudaGraphSupport::IsReadyForCapture: the logical all-gather creates its RCCL communicator
+    // on its first run (not capturable), so the first run of a job is always eager.
+    if (!graph_enabled_ || !ready_) {
+      const int rc = Launches(stream, row_ptr, col_idx, values, b_shard, out, tmp);
+      if (rc == OFX_OK) ready_ = true;
+      return rc;
+    }
+    ep::HipStream caller(stream, device_);
+    OFX_REQUIRE(stream == nullptr || !caller.IsGraphCapturing(), OFX_EINVAL,
+                "spmm job: graph mode inside an outer capture; disable one of them");
+    const std::vector<const void*> key = {row_ptr, col_idx, values, b_shard, out, tmp};
+    if (graph_ && graph_->IsInstantiated() && key == graph_key_) {
+      ++replays_;
+      return caller.LaunchGraph(graph_.get());
+    }
+    // The launches are recorded on the job's own capture stream (a graph does not remember the
+    // stream it was captured on, and the caller's may be the null stream, which cannot be
+    // captured); the graph is then launched on the caller's stream, in its order.
+    if (!capture_stream_) {
+      const int rc = ofx_stream_create(&capture_stream_);
+      if (rc) return rc;
+    }
+    if (!graph_) graph_.reset(new ep::HipGraphExecutable());
+    ep::HipStream cap(capture_stream_, device_);
+    int rc = cap.BeginGraphCapture();
+    if (rc) return rc;
+    rc = Launches(capture_stream_, row_ptr, col_idx, values, b_shard, out, tmp);
+    if (rc) {
+      const std::string why = ofx_last_error();
+      cap.EndGraphCapture(nullptr);  // discard the partial capture
+      graph_key_.clear();
+      return ofx::fail(rc, "%s", why.c_str());
+    }
+    rc = cap.EndGraphCapture(graph_.get());
+    if (rc) {
+      graph_key_.clear();
+      return rc;
+    }
+    graph_key_ = key;
+    ++captures_;
+    return caller.LaunchGraph(graph_.get());
+  }
+
+  ~SpmmJob() {
+    graph_.reset();
+    if (capture_stream_) ofx_stream_destroy(capture_stream_);
+  }
+
+ private:
+  int Launches(void* stream, const void* row_ptr, const void* col_idx, const void* values,
+               const void* b_shard, void* out, void* tmp) {
     const void* b_full = b_shard;
     if (gather_kernel_) {
       user_op::Tensor t_in(b_shard_, (DataType)val_dtype_, const_cast<void*>(b_shard));
@@ -173,7 +237,6 @@ class SpmmJob {
                                           spmm_tmp_bytes_, 1, &h, &ax, pc_.parallel_id(), 0, nullptr);
   }
 
- private:
   Maybe<void> CompileGather(const Shape& b_logical, const std::string& stream_name) {
     const user_op::OpRegistryResult* op =
         user_op::UserOpRegistryMgr::Get().GetOpRegistryResult(gather_op_);
@@ -242,6 +305,11 @@ class SpmmJob {
   Shape b_shard_, b_full_;
   std::unique_ptr<user_op::OpKernel> gather_kernel_;
   std::shared_ptr<user_op::OpKernelState> gather_state_;
+  bool graph_enabled_ = false, ready_ = false;
+  void* capture_stream_ = nullptr;
+  std::unique_ptr<ep::HipGraphExecutable> graph_;
+  std::vector<const void*> graph_key_;
+  int64_t captures_ = 0, replays_ = 0;
 };
 
 }  // namespace
@@ -405,5 +473,18 @@ extern "C" int ofx_spmm_job_run(void* job, void* stream, const void* row_ptr, co
 
 extern "C" int ofx_spmm_job_destroy(void* job) {
   delete static_cast<SpmmJob*>(job);
+  return OFX_OK;
+}
+
+extern "C" int ofx_spmm_job_set_graph(void* job, int enable) {
+  OFX_REQUIRE(job, OFX_EINVAL, "spmm_job_set_graph: NULL job");
+  static_cast<SpmmJob*>(job)->set_graph(enable != 0);
+  return OFX_OK;
+}
+
+extern "C" int ofx_spmm_job_graph_stats(void* job, int64_t* captures, int64_t* replays,
+                                        int64_t* updates) {
+  OFX_REQUIRE(job, OFX_EINVAL, "spmm_job_graph_stats: NULL job");
+  static_cast<const SpmmJob*>(job)->graph_stats(captures, replays, updates);
   return OFX_OK;
 }

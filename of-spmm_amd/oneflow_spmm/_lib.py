@@ -125,6 +125,14 @@ def _load():
         "ofx_event_sync": ([p], i32),
         "ofx_event_elapsed_ms": ([p, p, ctypes.POINTER(ctypes.c_float)], i32),
         "ofx_stream_wait_event": ([p, p], i32),
+        "ofx_graph_exec_create": ([ctypes.POINTER(p)], i32),
+        "ofx_graph_exec_destroy": ([p], i32),
+        "ofx_graph_exec_stats": ([p, ctypes.POINTER(i32), ctypes.POINTER(i64), ctypes.POINTER(i64),
+                                  ctypes.POINTER(i64)], i32),
+        "ofx_stream_begin_capture": ([p], i32),
+        "ofx_stream_is_capturing": ([p, ctypes.POINTER(i32)], i32),
+        "ofx_stream_end_capture": ([p, p], i32),
+        "ofx_graph_launch": ([p, p], i32),
         "ofx_comm_get_unique_id": ([p], i32),
         "ofx_comm_init_rank": ([ctypes.POINTER(p), i32, p, i32], i32),
         "ofx_comm_destroy": ([p], i32),
@@ -170,6 +178,9 @@ def _load():
         "ofx_spmm_job_describe": ([p, p, sz, ctypes.POINTER(sz)], i32),
         "ofx_spmm_job_run": ([p, p, p, p, p, p, p, p, sz], i32),
         "ofx_spmm_job_destroy": ([p], i32),
+        "ofx_spmm_job_set_graph": ([p, i32], i32),
+        "ofx_spmm_job_graph_stats": ([p, ctypes.POINTER(i64), ctypes.POINTER(i64),
+                                      ctypes.POINTER(i64)], i32),
         "ofx_op_sbp_signatures": ([ctypes.c_char_p, ctypes.c_char_p, p, sz], i32),
     }
     for name, (args, res) in sigs.items():

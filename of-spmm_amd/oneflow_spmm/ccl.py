@@ -182,7 +182,8 @@ class SpmmJob:
     computes this rank's BalancedSplitter rows of out (S(0)).  Bits equal the single-device op."""
 
     def __init__(self, placement: PlacementSpec, m: int, k: int, n: int, nnz: int,
-                 idx_dtype: torch.dtype, dtype: torch.dtype, device, stream_name: str = ""):
+                 idx_dtype: torch.dtype, dtype: torch.dtype, device, stream_name: str = "",
+                 graph: bool = False):
         self.placement, self.m, self.k, self.n, self.nnz = placement, m, k, n, nnz
         self.dtype, self.idx_dtype, self.device = dtype, idx_dtype, torch.device(device)
         self._job = ctypes.c_void_p()
@@ -196,6 +197,23 @@ class SpmmJob:
         self._tmp = torch.empty(max(self.tmp_bytes, 1), dtype=torch.uint8, device=self.device)
         lo, hi = _balanced(m, placement.parallel_num, placement.parallel_id)
         self.row_range = (lo, hi)
+        if graph:
+            self.set_graph(True)
+
+    def set_graph(self, enable: bool = True):
+        """Graph mode (user_kernel.cpp:676-707): after one eager run, a run is captured into a
+        hipGraph and every later run with the same tensor addresses (pass `out=` to keep them)
+        is one graph launch on the current stream; host placements ignore it."""
+        check(LIB.ofx_spmm_job_set_graph(self._job, 1 if enable else 0), "spmm_job_set_graph")
+
+    @property
+    def graph_stats(self):
+        """{"captures", "replays", "updates"}: captured runs, graph launches without re-capture,
+        and captures that patched the executable in place."""
+        c, r, u = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        check(LIB.ofx_spmm_job_graph_stats(self._job, ctypes.byref(c), ctypes.byref(r),
+                                           ctypes.byref(u)), "spmm_job_graph_stats")
+        return {"captures": c.value, "replays": r.value, "updates": u.value}
 
     def __call__(self, row_ptr, col_idx, values, b_shard, out=None) -> torch.Tensor:
         if out is None:

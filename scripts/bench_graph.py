@@ -58,6 +58,31 @@ def main():
                       "graph_replay_ms_per_forward": round(replay, 4),
                       "speedup": round(eager / replay, 2), "bitexact": same}))
 
+    # one spmm_csr layer as the compiled job (the nn.Graph form): eager runs vs the job's own
+    # graph mode (captured once through the C-ABI's hipGraph executable, one launch per run);
+    # back-to-back rate and latency of a single synchronised call
+    from oneflow_spmm import ccl
+    ccl.install_control_plane()
+    pl = ccl.PlacementSpec("hip", 1, 0, (0,), (0,))
+    out = torch.empty((m, n), dtype=dt, device=dev)
+    res = {"config": args.config, "layer": "spmm_csr job"}
+    for mode in ("eager", "graph"):
+        job = ccl.SpmmJob(pl, m, k, n, nnz, torch.int32, dt, dev, graph=mode == "graph")
+        run = lambda: job(rp, ci, v, x, out=out)  # noqa: E731
+        run()
+        run()
+        res[f"{mode}_ms_back_to_back"] = round(per_iter_ms(run, args.iters), 4)
+
+        def one():
+            run()
+            torch.cuda.synchronize()
+        res[f"{mode}_ms_latency"] = round(per_iter_ms(one, args.iters), 4)
+        if mode == "graph":
+            res["graph_stats"] = job.graph_stats
+    res["op_layer_eager_ms_back_to_back"] = round(
+        per_iter_ms(lambda: fs.spmm(rp, ci, v, m, k, x), args.iters), 4)
+    print(json.dumps(res))
+
 
 if __name__ == "__main__":
     main()

@@ -145,6 +145,11 @@ def test_spmm_job_plan_and_one_device_cpu_run():
         job(rp, ci, v, b[:-1])
     with pytest.raises(ValueError, match="col_idx must be"):
         job(rp, ci.long(), v, b)
+    # graph mode is a device-stream feature: a host placement ignores it and runs eagerly
+    job.set_graph(True)
+    out2 = job(rp, ci, v, b)
+    assert np.array_equal(out2.numpy().view(np.uint32), ref.view(np.uint32))
+    assert job.graph_stats == {"captures": 0, "replays": 0, "updates": 0}
     # a HIP placement of 4 ranks compiles the logical collective into the plan (the RCCL
     # communicator is created on the first run, on the GPU)
     job4 = ccl.SpmmJob(PlacementSpec("hip", 4, 2), m, 4 * 65, n, ci.numel(), torch.int32,

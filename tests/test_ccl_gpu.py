@@ -62,3 +62,42 @@ def test_spmm_job_on_hip_bitexact_and_graph_replay(device, hip_placement, dt):
     g.replay()
     torch.cuda.synchronize()
     assert_bitwise(out, oracle_spmm(rp, ci, v, b2), "graph replay")
+
+
+@pytest.mark.parametrize("stream_kind", ["default", "side"])
+def test_spmm_job_native_graph_mode(device, hip_placement, stream_kind):
+    """The job's own graph mode (UserKernel::ForwardUserKernel's CUDA-graph branch,
+    user_kernel.cpp:676-707, over the C-ABI's hipGraph executable): run 1 eager, run 2 captured
+    and launched, later runs with the same tensors one graph launch each, new tensors re-capture
+    (an in-place executable update); every result bit-exact vs the oracle, on the null stream
+    and on a side stream."""
+    rng = np.random.default_rng(37)
+    m, k, n = 3000, 2500, 64
+    rp, ci, v = random_csr(m, k, power_law_degrees(m, 60000, k, rng), rng)
+    bs = [random_dense(k, n, rng) for _ in range(3)]
+    job = ccl.SpmmJob(hip_placement, m, k, n, ci.numel(), torch.int32, torch.float32, device,
+                      graph=True)
+    d = (rp.to(device), ci.to(device), v.to(device))
+    b = bs[0].to(device)
+    out = torch.empty((m, n), device=device)
+    stream = torch.cuda.current_stream(device) if stream_kind == "default" \
+        else torch.cuda.Stream(device)
+    with torch.cuda.stream(stream):
+        job(*d, b, out=out)                      # eager (IsReadyForCapture after the first run)
+        assert job.graph_stats["captures"] == 0
+        job(*d, b, out=out)                      # captured + launched
+        stream.synchronize()
+        assert_bitwise(out, oracle_spmm(rp, ci, v, bs[0]), "captured run")
+        for i in (1, 2):                         # replays read the new contents of b
+            b.copy_(bs[i].to(device))
+            out.fill_(float("nan"))
+            job(*d, b, out=out)
+            stream.synchronize()
+            assert_bitwise(out, oracle_spmm(rp, ci, v, bs[i]), f"replay {i}")
+        assert job.graph_stats == {"captures": 1, "replays": 2, "updates": 0}
+        out2 = torch.empty_like(out)             # new address: re-capture, executable updated
+        job(*d, b, out=out2)
+        job(*d, b, out=out2)
+        stream.synchronize()
+        assert_bitwise(out2, oracle_spmm(rp, ci, v, bs[2]), "re-captured run")
+        assert job.graph_stats == {"captures": 2, "replays": 3, "updates": 1}
