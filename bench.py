@@ -434,7 +434,10 @@ def main():
             "host": hc,
             "sample": f"{what} x{reps} runs ({t_cpu:.1f} s), oracle/spmm_oracle.c OpenMP {best} "
                       f"threads (the fastest of {sorted(runs)} threads; the process may use "
-                      f"{usable} of {hc['nproc']} cores), same inputs and schedule"}
+                      f"{usable} of {hc['nproc']} cores), same inputs and schedule",
+            # BASELINE.md section 3's all-core run, stated beside the fastest one
+            "all_cores": {"threads": nt_all, "value": round(runs[nt_all][0], 3),
+                          "unit": "GFLOP/s"}}
         result["extra"]["cpu_by_threads"] = {
             str(t_): {"value": round(g_, 3), "unit": "GFLOP/s", "runs": r_, "seconds": round(s_, 1)}
             for t_, (g_, r_, s_) in sorted(runs.items())}
