@@ -427,17 +427,17 @@ def main():
             runs[usable] = time_oracle(usable, 10.0, 5)
         if threads not in runs:
             runs[threads] = time_oracle(threads, 5.0, 3)
+        # the all-core run is the headline; the fastest run (the cores a
+        # cgroup quota actually grants the process) is stated beside it
         best = max(runs, key=lambda t_: runs[t_][0])
-        cpu_gflops, reps, t_cpu = runs[best]
+        cpu_gflops, reps, t_cpu = runs[nt_all]
         result["cpu_baseline"] = {
-            "value": round(cpu_gflops, 3), "unit": "GFLOP/s", "cores": best, "kind": "port",
+            "value": round(cpu_gflops, 3), "unit": "GFLOP/s", "cores": nt_all, "kind": "port",
             "host": hc,
-            "sample": f"{what} x{reps} runs ({t_cpu:.1f} s), oracle/spmm_oracle.c OpenMP {best} "
-                      f"threads (the fastest of {sorted(runs)} threads; the process may use "
-                      f"{usable} of {hc['nproc']} cores), same inputs and schedule",
-            # BASELINE.md section 3's all-core run, stated beside the fastest one
-            "all_cores": {"threads": nt_all, "value": round(runs[nt_all][0], 3),
-                          "unit": "GFLOP/s"}}
+            "sample": f"{what} x{reps} runs ({t_cpu:.1f} s), oracle/spmm_oracle.c OpenMP {nt_all} "
+                      f"threads on {hc['nproc']} host cores (the process may use {usable} of them: "
+                      f"cgroup quota {hc['cgroup_cpu_quota']}), same inputs and schedule",
+            "fastest": {"threads": best, "value": round(runs[best][0], 3), "unit": "GFLOP/s"}}
         result["extra"]["cpu_by_threads"] = {
             str(t_): {"value": round(g_, 3), "unit": "GFLOP/s", "runs": r_, "seconds": round(s_, 1)}
             for t_, (g_, r_, s_) in sorted(runs.items())}
