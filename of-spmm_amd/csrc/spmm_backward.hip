@@ -369,9 +369,19 @@ struct SddmmArgs {
   size_t ws_bytes;
 };
 
+// Work layout only: every dv[j] is its own dot product, so how rows are cut into items never
+// changes a bit.  The forward's default split (65536 / n, part of ITS numeric contract) made the
+// narrow kernel's hub chunks 1-2k (N=64) and 2-4k (N=32) nonzeros long: one lane-group walks a
+// chunk in chunk / U dependent rounds, and on a power-law graph those chains set the launch time
+// (1M power-law, N=32: 1.67 ms, slower than N=64).  Items of at most kSddmmChunk nonzeros keep the
+// chains short; the wide kernel (n > 2048, one wave per item) keeps the forward's cut.
+constexpr int64_t kSddmmChunk = 256;
+constexpr int64_t kMaxNarrowN = 256 * kLeaf;  // sddmm_aligned's narrow configurations
+
 Schedule sddmm_schedule(int64_t n) {
-  // Work layout only (no numeric effect): hub rows cut like the forward's default.
-  return resolve_schedule(n, nullptr);
+  Schedule s = resolve_schedule(n, nullptr);
+  if (n <= kMaxNarrowN) s.split = s.chunk = kSddmmChunk;
+  return s;
 }
 
 #ifndef OFX_SD_U
