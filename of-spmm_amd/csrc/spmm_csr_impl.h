@@ -1084,6 +1084,22 @@ int launch_vec_mid(const Launch& L, int lpr) {
   }
 }
 
+// Big launches at N <= 16 fp32 whose longest item outlasts the memory traffic.  A hub chunk of up
+// to 2 * split nonzeros is one lane-group's chain of 2 * split / U dependent load rounds (~1.3 us
+// each under load); when the launch's B-row lines (one 128-B line per nonzero, "Narrow rows")
+// take less than that at ~6 TB/s, the chain sets the time, and 32 loads in flight with the next
+// (col, val) batch prefetched halve it (tuning variant 10022).  1M power-law, N = 16: 0.88 ->
+// 0.61 ms; products-shaped N = 16 (bandwidth-bound) keeps U = 16, where variant 10022 is 16%
+// slower (profiles/r02_wh_big_sizes.jsonl).  Same bits (U and the prefetch only change issue).
+// The same holds at N = 32 fp32 (128-B rows, 8 loads in flight per lane of 8 lanes): 16 loads
+// in flight with the batch prefetched.
+inline bool chain_bound(const Launch& L, int u, int64_t row_bytes) {
+  if (L.sched.split == INT64_MAX) return false;
+  const double chain_us = 2.0 * (double)L.sched.split / (double)u * 1.3;
+  const double lines_us = (double)L.nnz * (double)(row_bytes < 128 ? 128 : row_bytes) / 6.0e6;
+  return lines_us < chain_us;
+}
+
 template <typename T, typename I, int VEC>
 int launch_vec(const Launch& L, int lpr, bool nt) {
   const int v = L.sched.variant;
@@ -1100,11 +1116,18 @@ int launch_vec(const Launch& L, int lpr, bool nt) {
   if (L.nrows <= kSmallRows && v == 0 && !nt) return launch_vec_small<T, I, VEC>(L, lpr);
   switch (lpr) {
     case 4: return launch_cfg<T, I, Cfg<VEC, 4>>(L);
-    case 8: return launch_cfg<T, I, Cfg<VEC, 8>>(L);
+    case 8:
+      if constexpr (VEC == 4 && sizeof(T) == 4) {
+        if (v == 0 && chain_bound(L, 8, L.n * 4)) return launch_cfg<T, I, Cfg<4, 8, 16, 4, false, true>>(L);
+      }
+      return launch_cfg<T, I, Cfg<VEC, 8>>(L);
     case 16:
       // fp32 rows of <= 64 B (one element per lane): 16 loads in flight instead of 8, -1.2% on
       // products-shaped N = 16 (tuning variant 10021, profiles/r02_ab_n16_bnt.log), same bits
-      if constexpr (VEC == 1 && sizeof(T) == 4) return launch_cfg<T, I, Cfg<1, 16, 16>>(L);
+      if constexpr (VEC == 1 && sizeof(T) == 4) {
+        if (v == 0 && chain_bound(L, 16, L.n * 4)) return launch_cfg<T, I, Cfg<1, 16, 32, 4, false, true>>(L);
+        return launch_cfg<T, I, Cfg<1, 16, 16>>(L);
+      }
       return launch_cfg<T, I, Cfg<VEC, 16>>(L);
     case 32:
       return nt ? launch_cfg<T, I, Cfg<VEC, 32, 8, 4, true>>(L) : launch_cfg<T, I, Cfg<VEC, 32>>(L);

@@ -248,6 +248,23 @@ def test_baseline_configs_bitexact(device, name):
     assert ok, worst
 
 
+@pytest.mark.parametrize("n,alt_variant", [(16, 10021), (32, 408)])
+def test_plaw1m_chain_bound_config_bitexact(device, n, alt_variant):
+    """1M power-law at N=16 / 32: the big launch whose hub chains outlast its memory traffic runs
+    twice the loads in flight with the (col, val) batch prefetched (chain_bound); the whole output
+    bit for bit against the oracle and against the plain configuration of that width."""
+    cfg = fs.synth.CONFIGS["plaw1m"]
+    m, k, nnz = cfg["m"], cfg["k"], cfg["nnz"]
+    rp, ci, v = fs.synth.csr(m, k, nnz)
+    b = fs.synth.dense(0, k, n)
+    d = (rp.to(device), ci.to(device), v.to(device), b.to(device))
+    out = fs.spmm(*d[:3], m, k, d[3])
+    alt = ops.spmm_csr_device(*d, m, k, options=ops.make_options(variant=alt_variant))
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int32), alt.view(torch.int32))
+    assert_bitwise(out, oracle_spmm(rp, ci, v, b), f"plaw1m n={n}")
+
+
 @pytest.mark.slow
 def test_products_scale_sampled_rows(device):
     """ogbn-products-shaped (2.45M rows, 123.7M nnz, N=128): every hub row and a contiguous
