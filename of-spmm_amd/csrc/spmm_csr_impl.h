@@ -1100,6 +1100,18 @@ inline bool chain_bound(const Launch& L, int u, int64_t row_bytes) {
   return lines_us < chain_us;
 }
 
+// Mid-form launches at N <= 16 fp32 past ~8M nonzeros: the mid form's time grows with the
+// nonzeros (its lines at ~2.4 TB/s: 2-15M-nonzero power-law graphs, profiles/r02_mid_vs_chain*.jsonl)
+// while the prefetching U = 32 configuration is held at its longest chain (2 * split / 32 rounds
+// of ~1.75 us, ~0.45 ms at split 4096), so past the crossing the chain configuration is faster:
+// 11M nonzeros 0.57 -> 0.46 ms, 15M 0.80 -> 0.46 ms; 8M is even.  Same bits.
+inline bool chain_beats_mid(const Launch& L) {
+  if (L.sched.split == INT64_MAX) return false;
+  const double chain_us = 2.0 * (double)L.sched.split / 32.0 * 1.75;
+  const double mid_us = (double)L.nnz * 128.0 / 2.4e6;
+  return mid_us > chain_us;
+}
+
 template <typename T, typename I, int VEC>
 int launch_vec(const Launch& L, int lpr, bool nt) {
   const int v = L.sched.variant;
@@ -1110,8 +1122,12 @@ int launch_vec(const Launch& L, int lpr, bool nt) {
   // light rows of the mid form: the prefetching small-launch configuration above N = 16 (5-12%
   // faster at N = 64 / 128 on 20k-170k-row power-law graphs), the big-launch one at N <= 16
   // (profiles/r02n_probe_mid.json)
-  if (v == 0 && use_mid_form(L.nrows, L.nnz, L.n, L.sched))
+  if (v == 0 && use_mid_form(L.nrows, L.nnz, L.n, L.sched)) {
+    if constexpr (VEC == 1 && sizeof(T) == 4) {
+      if (lpr == 16 && chain_beats_mid(L)) return launch_cfg<T, I, Cfg<1, 16, 32, 4, false, true>>(L);
+    }
     return L.n > 16 ? launch_vec_mid<T, I, VEC, true>(L, lpr) : launch_vec_mid<T, I, VEC, false>(L, lpr);
+  }
   // forced variants (tests, tuning) keep the U = 8 configurations at every size
   if (L.nrows <= kSmallRows && v == 0 && !nt) return launch_vec_small<T, I, VEC>(L, lpr);
   switch (lpr) {

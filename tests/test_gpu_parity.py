@@ -265,6 +265,23 @@ def test_plaw1m_chain_bound_config_bitexact(device, n, alt_variant):
     assert_bitwise(out, oracle_spmm(rp, ci, v, b), f"plaw1m n={n}")
 
 
+def test_mid_size_n16_chain_config_bitexact(device):
+    """A 15M-nonzero power-law graph at N=16 sits in the mid form's size range, but its hub
+    chains make the prefetching U = 32 configuration faster (chain_beats_mid): the output bit for
+    bit against the oracle, the plain U = 16 configuration and the forced mid form."""
+    m = k = 750_000
+    nnz, n = 15_000_000, 16
+    rp, ci, v = fs.synth.csr(m, k, nnz)
+    b = fs.synth.dense(0, k, n)
+    d = (rp.to(device), ci.to(device), v.to(device), b.to(device))
+    out = fs.spmm(*d[:3], m, k, d[3])
+    for variant in (10021, 30002):
+        alt = ops.spmm_csr_device(*d, m, k, options=ops.make_options(variant=variant))
+        torch.cuda.synchronize()
+        assert torch.equal(out.view(torch.int32), alt.view(torch.int32)), variant
+    assert_bitwise(out, oracle_spmm(rp, ci, v, b), "15M n=16")
+
+
 @pytest.mark.slow
 def test_products_scale_sampled_rows(device):
     """ogbn-products-shaped (2.45M rows, 123.7M nnz, N=128): every hub row and a contiguous
