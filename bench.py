@@ -10,8 +10,8 @@ Workload (config.workload): ogbn-products-shaped synthetic power-law CSR (2,449,
 value = 2*nnz*N FLOPs per step (whole job) / max-over-ranks step time, in GFLOP/s.
 
 Extra objects: `roofline` (dominant kernel spmm_main, HIP events on its stream, algorithmic
-gather-model bytes) and `cpu_baseline` (the oracle's C restatement on the host
-cores, rank 0 at N=1 only, bounded sample).
+gather-model bytes) and `cpu_baseline` (the operator's kCPU kernel, SURVEY.md §8d
+row a2, on the host cores this process may use, plus a 1-thread run; rank 0 at N=1 only).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config products] [--no-cpu-baseline]
 """
@@ -102,9 +102,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")),
                     help="host threads for input generation and the secondary CPU numbers")
-    ap.add_argument("--cpu-baseline-threads", type=int, default=os.cpu_count() or 1,
-                    help="threads of the headline cpu_baseline (default: every host core, "
-                         "BASELINE.md section 3)")
+    ap.add_argument("--cpu-baseline-threads", type=int, default=0,
+                    help="threads of the cpu_baseline (default: the cores this process may use, "
+                         "min(nproc, affinity, cgroup quota); never more)")
     ap.add_argument("--variant", type=int, default=0, help="force a kernel variant (VEC*100+LPR)")
     ap.add_argument("--comm", choices=["rccl", "rccl-p2p"], default=None,
                     help="all-gather schedule for N>1 (default: measured at setup, faster kept)")
@@ -387,7 +387,7 @@ def main():
             "tune_errors": getattr(rs, "tune_errors", {}) or None,
             "nnz_per_rank_max_over_mean": round(float(nz[0]) / (float(nz[1]) / world), 4)})
 
-    # ---- CPU baseline: oracle restatement on the host cores (rank 0, N=1 only) ---------------
+    # ---- CPU baseline (rank 0, N=1 only): the operator's own kCPU kernel ------
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         from oracle import oracle
         # bounded sample: the first rows holding <= 130M nonzeros (all of products; rows are
@@ -396,80 +396,65 @@ def main():
         nnz_s = int(rp_full[r_s])
         flops_s = 2.0 * nnz_s * n
         what = "full workload" if r_s == m else f"rows [0,{r_s}) = {nnz_s} nnz"
-        rp_np = rp_full[: r_s + 1]
-        ci_np = cols[:nnz_s].astype(np.int64)
-        v_np = vals.numpy() if dt != torch.bfloat16 else vals.view(torch.int16).numpy().view(np.uint16)
-        v_np = v_np[:nnz_s]
         h_b = synth.dense(0, k, n, dt)
-        b_np = h_b.numpy() if dt != torch.bfloat16 else h_b.view(torch.int16).numpy().view(np.uint16)
-        dname = result["dtype"]
-
-        def time_oracle(nt, budget_s, max_reps):
-            oracle.spmm(rp_np, ci_np, v_np, b_np, dtype=dname, nthreads=nt, row_end=min(r_s, 100000))
-            reps_, t_ = 0, 0.0
-            while t_ < budget_s and reps_ < max_reps:
-                t1 = time.perf_counter()
-                oracle.spmm(rp_np, ci_np, v_np, b_np, dtype=dname, nthreads=nt)
-                t_ += time.perf_counter() - t1
-                reps_ += 1
-            return flops_s * reps_ / t_ / 1e9, reps_, t_
-
-        # headline: every host core, and the cores this process may
-        # actually use (a cgroup CPU quota throttles an all-core run on the GPU box: 16 CPUs of a
-        # 256-core host); the faster of the two is the baseline, both are reported
+        h_rp = torch.from_numpy(rp_full.astype(np.int32))
+        h_ci = torch.from_numpy(cols)
+        h_out = torch.empty((r_s, n), dtype=dt)
+        # the cores this process may use: min(nproc, affinity, cgroup quota).  On the GPU box a
+        # 16-CPU quota sits on a 256-core host; more threads than the quota only add throttling
+        # (round 2 measured 256 threads at a third of the 16-thread rate), so none are used.
         hc = host_cpu()
         usable = min(x for x in (hc["nproc"] or 1, hc["affinity"],
                                  int(np.ceil(hc["cgroup_cpu_quota"])) if hc["cgroup_cpu_quota"]
                                  else None) if x)
-        nt_all = args.cpu_baseline_threads
-        runs = {nt_all: time_oracle(nt_all, 10.0, 5)}
-        if usable != nt_all:
-            runs[usable] = time_oracle(usable, 10.0, 5)
-        if threads not in runs:
-            runs[threads] = time_oracle(threads, 5.0, 3)
-        # the all-core run is the headline; the fastest run (the cores a
-        # cgroup quota actually grants the process) is stated beside it
-        best = max(runs, key=lambda t_: runs[t_][0])
-        cpu_gflops, reps, t_cpu = runs[nt_all]
+        nt_cpu = min(args.cpu_baseline_threads or usable, usable)
+
+        def time_a2(nt, row_end, budget_s, max_reps):
+            kw = dict(out=h_out[:row_end], row_end=row_end, num_threads=nt)
+            ops.spmm_csr_cpu(h_rp, h_ci, vals, h_b, m, k, **kw)  # warm-up (page-in)
+            reps_, t_ = 0, 0.0
+            while t_ < budget_s and reps_ < max_reps:
+                t1 = time.perf_counter()
+                ops.spmm_csr_cpu(h_rp, h_ci, vals, h_b, m, k, **kw)
+                t_ += time.perf_counter() - t1
+                reps_ += 1
+            return 2.0 * float(rp_full[row_end]) * n * reps_ / t_ / 1e9, reps_, t_
+
+        cpu_gflops, reps, t_cpu = time_a2(nt_cpu, r_s, 6.0, 5)
+        bitexact = bool(torch.equal(h_out.view(torch.uint8), out[:r_s].cpu().view(torch.uint8)))
+        # one thread (OneFlow's default CPU_THREADING_RUNTIME=SEQ, CMakeLists.txt:54, and the
+        # launcher's OMP_NUM_THREADS=1, launch.py:117-118) on the first rows holding ~1/16 of the
+        # sample's nonzeros
+        r1 = int(np.searchsorted(rp_full[: r_s + 1], rp_full[r_s] // 16))
+        g1, reps1, t1s = time_a2(1, r1, 4.0, 2)
         result["cpu_baseline"] = {
-            "value": round(cpu_gflops, 3), "unit": "GFLOP/s", "cores": nt_all, "kind": "port",
-            "host": hc,
-            "sample": f"{what} x{reps} runs ({t_cpu:.1f} s), oracle/spmm_oracle.c OpenMP {nt_all} "
-                      f"threads on {hc['nproc']} host cores (the process may use {usable} of them: "
-                      f"cgroup quota {hc['cgroup_cpu_quota']}), same inputs and schedule",
-            "fastest": {"threads": best, "value": round(runs[best][0], 3), "unit": "GFLOP/s"}}
-        result["extra"]["cpu_by_threads"] = {
-            str(t_): {"value": round(g_, 3), "unit": "GFLOP/s", "runs": r_, "seconds": round(s_, 1)}
-            for t_, (g_, r_, s_) in sorted(runs.items())}
-        # single thread (OneFlow's default CPU_THREADING_RUNTIME=SEQ) on the first
-        # rows holding ~1/16 of the sample's nonzeros
-        r1 = int(np.searchsorted(rp_np, rp_np[-1] // 16))
+            "value": round(cpu_gflops, 3), "unit": "GFLOP/s", "cores": nt_cpu, "kind": "port",
+            "implementation": "ofx_spmm_csr_cpu: the operator's DeviceType::kCPU kernel (SURVEY.md "
+                              "§8a row a2; OpenMP row-parallel, the reference's gather -> mul -> "
+                              "segment-sum order, same hub schedule as the GPU)",
+            "host": {**hc, "usable_cores": usable},
+            "sample": f"{what} x{reps} runs ({t_cpu:.1f} s), {nt_cpu} OpenMP threads = the cores "
+                      f"this process may use ({hc['nproc']} host cores, affinity {hc['affinity']}, "
+                      f"cgroup quota {hc['cgroup_cpu_quota']}); same inputs and schedule as the GPU",
+            "bitexact_vs_gpu": bitexact,
+            "one_thread": {"value": round(g1, 3), "unit": "GFLOP/s", "cores": 1,
+                           "sample": f"rows [0,{r1}) = {int(rp_full[r1])} nnz x{reps1} runs "
+                                     f"({t1s:.1f} s)"}}
+        # the oracle's C restatement (test infrastructure; the checker, timed for reference only)
+        rp_np = rp_full[: r_s + 1]
+        ci_np = cols[:nnz_s].astype(np.int64)
+        v_np = vals.numpy() if dt != torch.bfloat16 else vals.view(torch.int16).numpy().view(np.uint16)
+        v_np = v_np[:nnz_s]
+        b_np = h_b.numpy() if dt != torch.bfloat16 else h_b.view(torch.int16).numpy().view(np.uint16)
+        oracle.spmm(rp_np, ci_np, v_np, b_np, dtype=result["dtype"], nthreads=nt_cpu,
+                    row_end=min(r_s, 100000))
         t1 = time.perf_counter()
-        oracle.spmm(rp_np, ci_np, v_np, b_np, dtype=dname, nthreads=1, row_end=r1)
-        t_1 = time.perf_counter() - t1
-        result["extra"]["cpu_1thread"] = {
-            "value": round(2.0 * float(rp_np[r1]) * n / t_1 / 1e9, 3), "unit": "GFLOP/s", "cores": 1,
-            "sample": f"rows [0,{r1}) = {int(rp_np[r1])} nnz, one run ({t_1:.1f} s)"}
-        del ci_np, b_np
-        # the operator's own DeviceType::kCPU kernel (SURVEY.md §8d's a2), same threads and
-        # sample, on host tensors; bit-identical to the GPU result by contract
-        h_rp = torch.from_numpy(rp_full.astype(np.int32))
-        h_ci = torch.from_numpy(cols)
-        h_out = torch.empty((r_s, n), dtype=dt)
-        kw = dict(out=h_out, row_end=r_s, num_threads=threads)
-        ops.spmm_csr_cpu(h_rp, h_ci, vals, h_b, m, k, **kw)
-        reps2, t_a2 = 0, 0.0
-        while t_a2 < 5.0 and reps2 < 3:
-            t1 = time.perf_counter()
-            ops.spmm_csr_cpu(h_rp, h_ci, vals, h_b, m, k, **kw)
-            t_a2 += time.perf_counter() - t1
-            reps2 += 1
-        result["extra"]["cpu_op_kernel"] = {
-            "value": round(flops_s * reps2 / t_a2 / 1e9, 3), "unit": "GFLOP/s", "cores": threads,
-            "sample": f"{what} x{reps2} runs ({t_a2:.1f} s), ofx_spmm_csr_cpu (the kCPU kernel)",
-            "bitexact_vs_gpu": bool(torch.equal(h_out.view(torch.uint8),
-                                                out[:r_s].cpu().view(torch.uint8)))}
-        del h_rp, h_ci, h_b, h_out
+        oracle.spmm(rp_np, ci_np, v_np, b_np, dtype=result["dtype"], nthreads=nt_cpu)
+        t_o = time.perf_counter() - t1
+        result["extra"]["cpu_oracle"] = {
+            "value": round(flops_s / t_o / 1e9, 3), "unit": "GFLOP/s", "cores": nt_cpu,
+            "sample": f"{what}, one run ({t_o:.1f} s), oracle/spmm_oracle.c (the tests' checker)"}
+        del ci_np, b_np, h_rp, h_ci, h_b, h_out
         # BASELINE configs[0]: the Cora-shaped problem on the OneFlow CPU op path (plumbing)
         cc = synth.CONFIGS["cora"]
         c_rp, c_ci, c_v = synth.csr(cc["m"], cc["k"], cc["nnz"], threads=threads)

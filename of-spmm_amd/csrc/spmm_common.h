@@ -140,12 +140,16 @@ OFX_HD bool is_value_dtype(int dt) {
 
 // ---- schedule ---------------------------------------------------------------------------
 // Default split threshold: rows with more than T nonzeros are cut into chunks of T, where
-// T = clamp(65536 / n, 128, 8192) rounded down to a power of two (T*n ~ 64K multiply-adds
+// T = clamp(65536 / n, 128, 512) rounded down to a power of two (T*n <= 64K multiply-adds
 // per chunk).  This is a fixed function of n and part of the numeric contract.
+// The 512 cap (round 3; was 8192) bounds a chunk's in-order chain at every width: at N = 16 a
+// 4096-8191-nonzero chunk was one lane-group's chain of 256-512 dependent load rounds, which
+// set the time of power-law launches of modest size (1M rows at N = 16 ran slower than N = 64).
+// N >= 128 keeps its threshold (512 at N = 128, 256 at N = 256).
 OFX_HD int64_t default_split(int64_t n) {
-  int64_t t = n > 0 ? (int64_t)65536 / n : 8192;
+  int64_t t = n > 0 ? (int64_t)65536 / n : 512;
   if (t < 128) t = 128;
-  if (t > 8192) t = 8192;
+  if (t > 512) t = 512;
   int64_t p = 128;
   while (p * 2 <= t) p *= 2;
   return p;

@@ -129,10 +129,11 @@ int spmm_entry(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k,
   OFX_REQUIRE(row_ptr && c, OFX_EINVAL, "spmm_csr: NULL row_ptr or output");
   OFX_REQUIRE(nnz == 0 || (col_idx && values && b), OFX_EINVAL,
               "spmm_csr: NULL col_idx/values/b with nnz=%lld", (long long)nnz);
+  const int64_t nnz_est = launch_nnz(m, nrows, nnz);
   Launch L{static_cast<hipStream_t>(stream), row_ptr, col_idx, values, b, c, ldb, ldc,
-           row_begin, nrows, n, nnz, launch_schedule(nrows, nnz, n, resolve_schedule(n, opts)),
+           row_begin, nrows, n, nnz, launch_schedule(nrows, nnz_est, n, resolve_schedule(n, opts)),
            workspace, workspace_bytes,
-           bias, act, k, values_perm};
+           bias, act, k, values_perm, nnz_est};
   if (idx_dtype == OFX_DT_INT32) return launch_idx<int32_t>(val_dtype, L);
   return launch_idx<int64_t>(val_dtype, L);
 }
@@ -174,8 +175,9 @@ extern "C" int ofx_spmm_csr_plan(void* stream, int idx_dtype, int val_dtype, int
               (long long)row_end, (long long)m);
   const int64_t nrows = row_end - row_begin;
   if (nrows == 0 || n == 0) return OFX_OK;  // the launch writes nothing either
-  const Schedule s = launch_schedule(nrows, nnz, n, resolve_schedule(n, opts));
-  if (use_small_form(nrows, nnz, n, s)) return OFX_OK;  // the small form needs no plan
+  const int64_t nnz_est = launch_nnz(m, nrows, nnz);  // as the launch estimates it
+  const Schedule s = launch_schedule(nrows, nnz_est, n, resolve_schedule(n, opts));
+  if (use_small_form(nrows, nnz_est, n, s)) return OFX_OK;  // the small form needs no plan
   const plan::WsLayout w = plan::ws_layout(nrows, nnz, n, acc_bytes_of(val_dtype), s);
   if (w.total == 0) return OFX_OK;  // identity work list: nothing to plan
   OFX_REQUIRE(row_ptr != nullptr, OFX_EINVAL, "spmm_csr_plan: NULL row_ptr");
@@ -187,9 +189,9 @@ extern "C" int ofx_spmm_csr_plan(void* stream, int idx_dtype, int val_dtype, int
   char* ws = static_cast<char*>(workspace);
   if (idx_dtype == OFX_DT_INT32)
     return plan::launch_plan<int32_t>(st, static_cast<const int32_t*>(row_ptr), row_begin, nrows,
-                                      nnz, s, w, ws, &wl);
+                                      nnz_est, s, w, ws, &wl);
   return plan::launch_plan<int64_t>(st, static_cast<const int64_t*>(row_ptr), row_begin, nrows,
-                                    nnz, s, w, ws, &wl);
+                                    nnz_est, s, w, ws, &wl);
 }
 
 extern "C" int ofx_spmm_csr_fused(void* stream, int idx_dtype, int val_dtype, int64_t m,

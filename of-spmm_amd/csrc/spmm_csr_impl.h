@@ -444,6 +444,11 @@ struct SmallLds {
 //   products are in LDS.
 //   Products of consecutive batches alternate between two LDS buffers, so one barrier per batch
 //   orders the writes of batch k against the adds of batch k (after it) and of batch k - 1.
+// Chunked traversal (kpc > 0): [j0, j1) is a whole split row whose chunks are kpc batches long
+// (chunk = kpc * NB) and whose last chunk (nc - 1) takes the remainder.  The adder closes a chunk
+// at each chunk boundary (total = total + acc; acc = +0) and returns total + the last chunk's
+// sum: the contract's bits (each chunk from +0 in order, the partials in chunk order from +0)
+// in one pipelined pass instead of one pass per chunk.
 template <typename T, typename I, typename K>
 __device__ __forceinline__ void block_accumulate(const I* __restrict__ col,
                                                  const T* __restrict__ val,
@@ -451,7 +456,8 @@ __device__ __forceinline__ void block_accumulate(const I* __restrict__ col,
                                                  const T* __restrict__ Bs, int64_t ldb,
                                                  int64_t j0, int64_t j1, int gb, int gl,
                                                  bool chain, SmallLds<T, I, K>& sh,
-                                                 typename Num<T>::acc (&acc)[K::VEC]) {
+                                                 typename Num<T>::acc (&acc)[K::VEC],
+                                                 int64_t kpc = 0, int64_t nc = 0) {
 #pragma clang fp contract(off)
   using SF = SmallForm<T, I, K>;
   using A = typename Num<T>::acc;
@@ -485,6 +491,9 @@ __device__ __forceinline__ void block_accumulate(const I* __restrict__ col,
   };
   I rc[PT];  // the next span's (col, val), in flight until staged
   A rv[PT];
+  A total[VEC];  // chunked traversal: the closed chunks' sum, in chunk order from +0
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) total[e] = A(0);
   // B rows of batch kb (B row 0 for a batch past the end: its span buffer may hold anything)
   auto issue = [&](int64_t kb, P (&b)[UW]) {
     const int off = (int)((kb / S) & 1) * SPAN + (int)(kb % S) * NB;
@@ -529,6 +538,13 @@ __device__ __forceinline__ void block_accumulate(const I* __restrict__ col,
     if (stage) span_load((k + D) / S + 1, rc, rv);
     issue(k + D, b);
     if (chain) {
+      if (kpc > 0 && k > 0 && k % kpc == 0 && k / kpc < nc) {  // batch k opens a new chunk
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          total[e] = total[e] + acc[e];
+          acc[e] = A(0);
+        }
+      }
       // full rounds of reads in flight, then one guarded round for the rest of the batch (a
       // batch that is not a whole number of rounds pays one LDS wait for its tail, not one per
       // product)
@@ -616,6 +632,10 @@ __device__ __forceinline__ void block_accumulate(const I* __restrict__ col,
   if (k0 + 4 < nb) step(k0 + 4, b0, false);
   if (k0 + 5 < nb) step(k0 + 5, b1, false);
   if (k0 + 6 < nb) step(k0 + 6, b2, false);
+  if (kpc > 0) {
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc[e] = total[e] + acc[e];
+  }
   __syncthreads();  // the next call's first batch writes buffer 0, which the adds may still read
 }
 
@@ -669,6 +689,8 @@ __global__ void __launch_bounds__(64 * K::WPB)
     const int64_t re = (int64_t)rp[row_begin + hr + 1];
     const bool split_row = re - rs > split;
     const int64_t nc = split_row ? num_chunks(re - rs, chunk) : 1;
+    // chunks of whole batches: the row in one chunked pass (block_accumulate)
+    const bool one_pass = split_row && chunk % SF::NB == 0;
     for (int64_t c0 = 0; c0 < n; c0 += W) {
       const int64_t cc = c0 + (int64_t)gl * VEC;
       const bool active = cc < n;
@@ -676,6 +698,14 @@ __global__ void __launch_bounds__(64 * K::WPB)
       A total[VEC], acc[VEC];
 #pragma unroll
       for (int e = 0; e < VEC; ++e) total[e] = A(0);
+      if (one_pass) {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[e] = A(0);
+        block_accumulate<T, I, K>(col, val, vperm, Bs, ldb, rs, re, gb, gl, chain, lds, acc,
+                                  chunk / SF::NB, nc);
+        if (chain && active) store_row<T, VEC, K::NT>(C + hr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
+        continue;
+      }
       for (int64_t ci = 0; ci < nc; ++ci) {
         int64_t j0 = rs, j1 = re;
         if (split_row) {
@@ -984,7 +1014,7 @@ int launch_cfg(const Launch& L) {
     if (L.sched.planned) {
       plan::worklist_of(w, static_cast<char*>(L.ws), &wl);
     } else {
-      const int rc = launch_plan<I>(L.stream, rp, L.row_begin, L.nrows, L.nnz, L.sched, w,
+      const int rc = launch_plan<I>(L.stream, rp, L.row_begin, L.nrows, L.nnz_est, L.sched, w,
                                     static_cast<char*>(L.ws), &wl);
       if (rc) return rc;
     }
@@ -997,7 +1027,7 @@ int launch_cfg(const Launch& L) {
   const int64_t work = L.nrows + (plan ? w.max_chunks : 0);
   // The BI form puts one block per hub chunk / heavy row first (upper bound: every chunk and
   // every row longer than the heavy threshold).
-  const int64_t heavy = L.sched.heavy == 0 ? auto_heavy(L.nrows, L.nnz) : L.sched.heavy;
+  const int64_t heavy = L.sched.heavy == 0 ? auto_heavy(L.nrows, L.nnz_est) : L.sched.heavy;
   const int64_t bi_items =
       w.max_chunks + (heavy == INT64_MAX ? 0 : std::min<int64_t>(L.nrows, L.nnz / (heavy + 1) + 1));
   const int64_t wave_blocks = (K::WH && K::LPR < 64 && plan) ? (work + K::WPB - 1) / K::WPB
@@ -1040,7 +1070,7 @@ int launch_small(const Launch& L) {
 
 template <typename T, typename I, typename K>
 int launch_small_or_planned(const Launch& L) {
-  if (use_small_form(L.nrows, L.nnz, L.n, L.sched)) return launch_small<T, I, K>(L);
+  if (use_small_form(L.nrows, L.nnz_est, L.n, L.sched)) return launch_small<T, I, K>(L);
   return launch_cfg<T, I, K>(L);
 }
 
@@ -1068,6 +1098,21 @@ int launch_vec_small(const Launch& L, int lpr) {
   }
 }
 
+// The planned form with the small-launch configuration (wave items for hub chunks and heavy rows,
+// U = 32 / 16 loads in flight, next batch prefetched) at any size: tuning variant 30004.
+template <typename T, typename I, int VEC>
+int launch_vec_wave(const Launch& L, int lpr) {
+  constexpr int U = VEC * sizeof(T) <= 4 ? 32 : 16;
+  switch (lpr) {
+    case 4: return launch_cfg<T, I, Cfg<VEC, 4, U, 4, false, true, false, true>>(L);
+    case 8: return launch_cfg<T, I, Cfg<VEC, 8, U, 4, false, true, false, true>>(L);
+    case 16: return launch_cfg<T, I, Cfg<VEC, 16, U, 4, false, true, false, true>>(L);
+    case 32: return launch_cfg<T, I, Cfg<VEC, 32, U, 4, false, true, false, true>>(L);
+    case 64: return launch_cfg<T, I, Cfg<VEC, 64, U, 4, false, false, false, false>>(L);
+    default: return fail(OFX_EINVAL, "spmm_csr: unsupported lanes-per-row %d", lpr);
+  }
+}
+
 // Mid form (use_mid_form): block items first, then one lane-group per light row.  SR: the light
 // rows run the small-launch configuration (U = 32 / 16 loads in flight, next batch prefetched)
 // instead of the big-launch one (U = 8, 16 for one-element fp32 lanes).
@@ -1084,66 +1129,29 @@ int launch_vec_mid(const Launch& L, int lpr) {
   }
 }
 
-// Big launches at N <= 16 fp32 whose longest item outlasts the memory traffic.  A hub chunk of up
-// to 2 * split nonzeros is one lane-group's chain of 2 * split / U dependent load rounds (~1.3 us
-// each under load); when the launch's B-row lines (one 128-B line per nonzero, "Narrow rows")
-// take less than that at ~6 TB/s, the chain sets the time, and 32 loads in flight with the next
-// (col, val) batch prefetched halve it (tuning variant 10022).  1M power-law, N = 16: 0.88 ->
-// 0.61 ms; products-shaped N = 16 (bandwidth-bound) keeps U = 16, where variant 10022 is 16%
-// slower (profiles/r02_wh_big_sizes.jsonl).  Same bits (U and the prefetch only change issue).
-// The same holds at N = 32 fp32 (128-B rows, 8 loads in flight per lane of 8 lanes): 16 loads
-// in flight with the batch prefetched.
-inline bool chain_bound(const Launch& L, int u, int64_t row_bytes) {
-  if (L.sched.split == INT64_MAX) return false;
-  const double chain_us = 2.0 * (double)L.sched.split / (double)u * 1.3;
-  const double lines_us = (double)L.nnz * (double)(row_bytes < 128 ? 128 : row_bytes) / 6.0e6;
-  return lines_us < chain_us;
-}
-
-// Mid-form launches at N <= 16 fp32 past ~8M nonzeros: the mid form's time grows with the
-// nonzeros (its lines at ~2.4 TB/s: 2-15M-nonzero power-law graphs, profiles/r02_mid_vs_chain*.jsonl)
-// while the prefetching U = 32 configuration is held at its longest chain (2 * split / 32 rounds
-// of ~1.75 us, ~0.45 ms at split 4096), so past the crossing the chain configuration is faster:
-// 11M nonzeros 0.57 -> 0.46 ms, 15M 0.80 -> 0.46 ms; 8M is even.  Same bits.
-inline bool chain_beats_mid(const Launch& L) {
-  if (L.sched.split == INT64_MAX) return false;
-  const double chain_us = 2.0 * (double)L.sched.split / 32.0 * 1.75;
-  const double mid_us = (double)L.nnz * 128.0 / 2.4e6;
-  return mid_us > chain_us;
-}
-
 template <typename T, typename I, int VEC>
 int launch_vec(const Launch& L, int lpr, bool nt) {
   const int v = L.sched.variant;
-  if (v == kForceSmallVariant || (v == 0 && use_small_form(L.nrows, L.nnz, L.n, L.sched)))
+  if (v == kForceSmallVariant || (v == 0 && use_small_form(L.nrows, L.nnz_est, L.n, L.sched)))
     return launch_vec_small<T, I, VEC>(L, lpr);
   if (v == kForceMidSmallVariant) return launch_vec_mid<T, I, VEC, true>(L, lpr);
   if (v == kForceMidVariant) return launch_vec_mid<T, I, VEC, false>(L, lpr);
+  if (v == kForceWaveVariant) return launch_vec_wave<T, I, VEC>(L, lpr);
   // light rows of the mid form: the prefetching small-launch configuration above N = 16 (5-12%
   // faster at N = 64 / 128 on 20k-170k-row power-law graphs), the big-launch one at N <= 16
   // (profiles/r02n_probe_mid.json)
-  if (v == 0 && use_mid_form(L.nrows, L.nnz, L.n, L.sched)) {
-    if constexpr (VEC == 1 && sizeof(T) == 4) {
-      if (lpr == 16 && chain_beats_mid(L)) return launch_cfg<T, I, Cfg<1, 16, 32, 4, false, true>>(L);
-    }
+  if (v == 0 && use_mid_form(L.nrows, L.nnz_est, L.n, L.sched)) {
     return L.n > 16 ? launch_vec_mid<T, I, VEC, true>(L, lpr) : launch_vec_mid<T, I, VEC, false>(L, lpr);
   }
   // forced variants (tests, tuning) keep the U = 8 configurations at every size
   if (L.nrows <= kSmallRows && v == 0 && !nt) return launch_vec_small<T, I, VEC>(L, lpr);
   switch (lpr) {
     case 4: return launch_cfg<T, I, Cfg<VEC, 4>>(L);
-    case 8:
-      if constexpr (VEC == 4 && sizeof(T) == 4) {
-        if (v == 0 && chain_bound(L, 8, L.n * 4)) return launch_cfg<T, I, Cfg<4, 8, 16, 4, false, true>>(L);
-      }
-      return launch_cfg<T, I, Cfg<VEC, 8>>(L);
+    case 8: return launch_cfg<T, I, Cfg<VEC, 8>>(L);
     case 16:
       // fp32 rows of <= 64 B (one element per lane): 16 loads in flight instead of 8, -1.2% on
       // products-shaped N = 16 (tuning variant 10021, profiles/r02_ab_n16_bnt.log), same bits
-      if constexpr (VEC == 1 && sizeof(T) == 4) {
-        if (v == 0 && chain_bound(L, 16, L.n * 4)) return launch_cfg<T, I, Cfg<1, 16, 32, 4, false, true>>(L);
-        return launch_cfg<T, I, Cfg<1, 16, 16>>(L);
-      }
+      if constexpr (VEC == 1 && sizeof(T) == 4) return launch_cfg<T, I, Cfg<1, 16, 16>>(L);
       return launch_cfg<T, I, Cfg<VEC, 16>>(L);
     case 32:
       return nt ? launch_cfg<T, I, Cfg<VEC, 32, 8, 4, true>>(L) : launch_cfg<T, I, Cfg<VEC, 32>>(L);

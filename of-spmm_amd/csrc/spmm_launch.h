@@ -22,7 +22,20 @@ struct Launch {
   int act;
   int64_t b_rows;  // k: rows of B (cache-footprint choice of load hints)
   const void* vperm;  // NULL, or I[nnz]: nonzero j's value is val[vperm[j]] (A^T of a gradient)
+  int64_t nnz_est;    // this launch's nonzeros, estimated (launch_nnz): the form choice and the
+                      // automatic heavy threshold; `nnz` (the matrix's) bounds the workspace
 };
+
+// Nonzeros of a launch over `nrows` of the matrix's `m` rows: nnz * nrows / m.  row_ptr lives on
+// the device, so the exact count is not known to the host; a row range of these graphs (rows
+// randomly permuted; BalancedSplitter ranges measured within 3% of the mean nnz) holds about its
+// share.  The form heuristics use it so that a rank's slice of an S(0) split is treated as the
+// launch it is (with the matrix's nnz an 11M-nonzero graph on 8 ranks took the
+// single-GPU crossovers at 1.4M local nonzeros).  The workspace bounds keep the matrix's nnz.
+inline int64_t launch_nnz(int64_t m, int64_t nrows, int64_t nnz) {
+  if (m <= 0 || nrows >= m) return nnz;
+  return (int64_t)((__int128)nnz * nrows / m);
+}
 
 // Small form (spmm_small_kernel): one launch when the launch has at most kSmallRows rows and at
 // most kSmallFormElems products (nnz * n).  Its longest row then costs at most that many products
@@ -56,9 +69,14 @@ inline bool use_mid_form(int64_t nrows, int64_t nnz, int64_t n, const Schedule& 
          nnz <= kMidFormElems / (n > 0 ? n : 1);
 }
 
-// Tuning variants that force a form (small / mid) but keep the automatic configuration.
+constexpr int kForceBigVariant = 30003;   // tuning: the planned big form, bandwidth configuration
+constexpr int kForceWaveVariant = 30004;  // tuning: the planned form with wave items (U=32, PF)
+
+// Tuning variants that force a form (small / mid / big / wave) but keep the automatic
+// configuration.
 inline bool is_form_variant(int v) {
-  return v == kForceSmallVariant || v == kForceMidVariant || v == kForceMidSmallVariant;
+  return v == kForceSmallVariant || v == kForceMidVariant || v == kForceMidSmallVariant ||
+         v == kForceBigVariant || v == kForceWaveVariant;
 }
 
 // The schedule a launch of `nrows` rows runs with: the mid form always plans (binned work list)

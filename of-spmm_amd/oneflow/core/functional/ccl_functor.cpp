@@ -76,6 +76,31 @@ Maybe<void> CheckContiguous(const ofx_tensor_desc* t, const char* name) {
 }
 
 // Streams of the kernels: a HIP stream handle for kHIP, the host for kCPU.
+// Makes `device` current for its scope and restores the caller's device (a negative device, a
+// host placement, changes nothing).
+struct DeviceGuard {
+  int prev = -1, rc = OFX_OK;
+  explicit DeviceGuard(int device) {
+    if (device < 0) return;
+    if (hipGetDevice(&prev) != hipSuccess) {
+      rc = ofx::fail(OFX_EDEVICE, "spmm job: hipGetDevice failed");
+      prev = -1;
+      return;
+    }
+    if (prev == device) {
+      prev = -1;
+      return;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+      rc = ofx::fail(OFX_EDEVICE, "spmm job: hipSetDevice(%d) failed", device);
+      prev = -1;
+    }
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
 struct StreamPair {
   ep::CpuStream cpu{0};
   ep::HipStream hip;
@@ -144,9 +169,17 @@ class SpmmJob {
   const std::string& plan() const { return plan_; }
   size_t tmp_bytes() const { return gathered_bytes_ + spmm_tmp_bytes_; }
 
-  void set_graph(bool enable) {
+  // Graph mode is validated at one rank only (tests/test_ccl_gpu.py): a multi-rank capture
+  // records ncclAllGather into the graph, and that capture/replay has not run on hardware yet
+  // (the driver's 8-GPU node is the first place it could), so P > 1 is refused until it has.
+  int set_graph(bool enable) {
+    OFX_REQUIRE(!enable || pd_.parallel_num() == 1, OFX_EUNSUPPORTED,
+                "spmm job: graph mode with %lld ranks (a captured RCCL all-gather) is not "
+                "validated on hardware; run the %lld-rank job eagerly",
+                (long long)pd_.parallel_num(), (long long)pd_.parallel_num());
     graph_enabled_ = enable && pd_.device_type() == DeviceType::kHIP;
     if (!graph_enabled_) graph_.reset();
+    return OFX_OK;
   }
   void graph_stats(int64_t* captures, int64_t* replays, int64_t* updates) const {
     if (captures) *captures = captures_;
@@ -178,7 +211,11 @@ class SpmmJob {
     }
     // The launches are recorded on the job's own capture stream (a graph does not remember the
     // stream it was captured on, and the caller's may be the null stream, which cannot be
-    // captured); the graph is then launched on the caller's stream, in its order.
+    // captured); the graph is then launched on the caller's stream, in its order.  The capture
+    // stream, the capture and the instantiation belong to the job's device, whatever device
+    // the caller has current (restored on return).
+    DeviceGuard guard(device_);
+    if (guard.rc) return guard.rc;
     if (!capture_stream_) {
       const int rc = ofx_stream_create(&capture_stream_);
       if (rc) return rc;
@@ -478,8 +515,7 @@ extern "C" int ofx_spmm_job_destroy(void* job) {
 
 extern "C" int ofx_spmm_job_set_graph(void* job, int enable) {
   OFX_REQUIRE(job, OFX_EINVAL, "spmm_job_set_graph: NULL job");
-  static_cast<SpmmJob*>(job)->set_graph(enable != 0);
-  return OFX_OK;
+  return static_cast<SpmmJob*>(job)->set_graph(enable != 0);
 }
 
 extern "C" int ofx_spmm_job_graph_stats(void* job, int64_t* captures, int64_t* replays,

@@ -50,9 +50,10 @@ def lib():
 
 def default_split(n: int) -> int:
     """Restates the operator's documented default hub-row threshold:
-    T = clamp(65536 // n, 128, 8192) rounded down to a power of two."""
-    t = 65536 // n if n > 0 else 8192
-    t = min(max(t, 128), 8192)
+    T = clamp(65536 // n, 128, 512) rounded down to a power of two (the cap was 8192 before
+    round 3)."""
+    t = 65536 // n if n > 0 else 512
+    t = min(max(t, 128), 512)
     p = 128
     while p * 2 <= t:
         p *= 2

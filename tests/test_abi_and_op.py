@@ -121,9 +121,9 @@ def _hub_problem(n=128, seed=3):
 
 def test_op_column_split_keeps_logical_schedule():
     """under S(1) every rank runs the hub schedule of the logical N (split =
-    default_split(128) = 512, not default_split(32) = 2048): each slice is bit-identical to the
+    default_split(512) = 128, not default_split(128) = 512): each slice is bit-identical to the
     single-device op's columns."""
-    n = 128
+    n = 512
     m, k, rp, ci, v, b = _hub_problem(n)
     full = fs.spmm(rp, ci, v, m, k, b)
     assert fs.ops.default_split(n // 4) != fs.ops.default_split(n)

@@ -157,6 +157,11 @@ def test_spmm_job_plan_and_one_device_cpu_run():
     assert "_nccl_logical_all_gather(src S(0), dst B" in job4.plan
     assert "(65,16) on this rank" in job4.plan and "rows [150,225)" in job4.plan
     assert job4.tmp_bytes >= 4 * 65 * n * 2
+    # a multi-rank capture (ncclAllGather inside a hipGraph) is not validated on
+    # hardware, so graph mode is refused at P > 1 (eager runs stay available)
+    with pytest.raises(OfxError, match="graph mode with 4 ranks"):
+        job4.set_graph(True)
+    job4.set_graph(False)
     with pytest.raises(OfxError, match="K % P != 0"):
         ccl.SpmmJob(PlacementSpec("hip", 4, 0), m, 261, n, ci.numel(), torch.int32,
                     torch.float32, "cpu")

@@ -87,7 +87,8 @@ def test_bf16_rounding_helpers():
     assert back[0] == 1.0 and back[1] == 1.0  # tie to even
     assert back[2] == np.float32(1.0078125)
     assert np.isnan(back[-1]) and np.isinf(back[-2])
-    assert oracle.default_split(128) == 512 and oracle.default_split(1) == 8192
+    assert oracle.default_split(128) == 512 and oracle.default_split(1) == 512
+    assert oracle.default_split(16) == 512 and oracle.default_split(64) == 512
     assert oracle.default_split(256) == 256 and oracle.default_split(1024) == 128
 
 
