@@ -68,6 +68,25 @@ def host_cpu() -> dict:
             "cgroup_cpu_quota": quota}
 
 
+class Mark:
+    """A point on the launch stream: a HIP event (GPU), or the host clock after the work issued
+    so far has finished (the CPU rehearsal, where every call is synchronous)."""
+
+    def __init__(self, on_gpu: bool):
+        self.on_gpu = on_gpu
+        self.ev = torch.cuda.Event(enable_timing=True) if on_gpu else None
+        self.t = 0.0
+
+    def record(self):
+        if self.on_gpu:
+            self.ev.record()
+        else:
+            self.t = time.perf_counter()
+
+    def ms_to(self, later: "Mark") -> float:
+        return self.ev.elapsed_time(later.ev) if self.on_gpu else (later.t - self.t) * 1e3
+
+
 def _claim_stdout():
     """Route fd 1 to stderr for the whole run (RCCL and the HIP runtime print banners on stdout)
     and return a writer on the real stdout for the one JSON line of the bench contract."""
@@ -119,10 +138,17 @@ def main():
                          "performance number)")
     ap.add_argument("--force-rowsplit", action="store_true",
                     help="run the N>1 code path (RCCL all-gather + local SpMM) even with one rank")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu: rehearse the N>1 path on host tensors with the kCPU kernel (needs "
+                         "--backend gloo; not a performance number)")
+    ap.add_argument("--tune-budget", type=float, default=120.0,
+                    help="seconds of exchange-candidate timing at setup (N>1); the candidates run "
+                         "in order of their modelled time, the rest are skipped")
     args = ap.parse_args()
     _spawn_ranks_if_needed(args.gpus)
     out_stream = _claim_stdout()
 
+    t_wall0 = time.time()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -130,10 +156,21 @@ def main():
         log(f"[bench] error: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
         sys.exit(2)
     rehearsal = args.backend == "gloo"
-    dev_index = local_rank % torch.cuda.device_count() if rehearsal else local_rank
-    torch.cuda.set_device(dev_index)
-    device = torch.device("cuda", dev_index)
+    on_gpu = args.device == "cuda"
+    if not on_gpu and not rehearsal:
+        log("[bench] error: --device cpu is a rehearsal of the multi-rank path: use --backend gloo")
+        sys.exit(2)
+    if on_gpu:
+        dev_index = local_rank % torch.cuda.device_count() if rehearsal else local_rank
+        torch.cuda.set_device(dev_index)
+        device = torch.device("cuda", dev_index)
+    else:
+        device = torch.device("cpu")
     red_dev = "cpu" if rehearsal else device  # where the timing reductions run
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
     rowsplit = world > 1 or args.force_rowsplit
     if rowsplit:
         if world == 1:
@@ -152,7 +189,7 @@ def main():
     from oneflow_spmm import ops, synth
     from oneflow_spmm.distributed import RowSplitSpmm
 
-    cfg = synth.CONFIGS[args.config]
+    cfg = {**synth.CONFIGS, **synth.EXTRA_CONFIGS}[args.config]
     m, k, nnz, n, dt = cfg["m"], cfg["k"], cfg["nnz"], cfg["n"], cfg["dtype"]
     s_v = torch.empty(0, dtype=dt).element_size()
     threads = args.cpu_threads
@@ -173,7 +210,7 @@ def main():
     out = torch.empty((rows, n), dtype=dt, device=device)
     log(f"[bench] inputs for rank {rank}: rows {rows} nnz {nnz_local} built in {time.time() - t0:.1f}s")
 
-    events = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    events = [Mark(on_gpu) for _ in range(3)]
     opts = ops.make_options(variant=args.variant) if args.variant else None
     if not rowsplit:
         d_b = synth.dense(0, k, n, dt, device=device)
@@ -206,7 +243,7 @@ def main():
         # exchange: all-gather (ring / point-to-point) x pipeline depth (column blocks gathered
         # while the previous block computes), or halo-only rows; measured here, untimed, the
         # fastest kept (every candidate gives the same bytes)
-        comm_times = {}
+        comm_times, tune_s = {}, None
         if args.comm or args.pipeline or args.exchange != "auto":
             rs.exchange = args.exchange if args.exchange != "auto" else "allgather"
             if rs.exchange not in ("allgather", "halo") and rs.exchange not in rs.grids:
@@ -217,9 +254,13 @@ def main():
                 rs.set_pipeline(1)
                 rs.set_halo_pipeline(args.pipeline or 1)
         else:
-            comm_times = rs.tune(out, force=args.force_rowsplit)
-            log("[bench] exchange candidates (ms, max over ranks): " +
-                ", ".join(f"{kk} {vv:.3f}" for kk, vv in sorted(comm_times.items(), key=lambda x: x[1])))
+            t_tune = time.time()
+            comm_times = rs.tune(out, force=args.force_rowsplit, budget_s=args.tune_budget)
+            tune_s = time.time() - t_tune
+            log("[bench] exchange candidates (ms, max over ranks; model-predicted): " +
+                ", ".join(f"{kk} {vv:.3f} ({rs.tune_report[kk]['predicted_ms']:.3f})"
+                          for kk, vv in sorted(comm_times.items(), key=lambda x: x[1])))
+        setup_s = time.time() - t0
         log(f"[bench] exchange kept: {rs.exchange} / {rs.comm_kind} / pipeline "
             f"{rs.halo_chunks if rs.exchange == 'halo' else rs.chunks}")
 
@@ -229,20 +270,19 @@ def main():
     # ---- warmup + timed region -----------------------------------------------------------------
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     if rowsplit:
         dist.barrier()
-    torch.cuda.synchronize()
-    ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    sync()
+    ev_start, ev_end = Mark(on_gpu), Mark(on_gpu)
     t_start = time.perf_counter()
     ev_start.record()
     for _ in range(args.steps):
         step()
     ev_end.record()
-    torch.cuda.synchronize()
     if rowsplit:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t_start
     if rowsplit:
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
@@ -255,7 +295,7 @@ def main():
     # ---- dominant-kernel timing: events on the launch stream around the SpMM launches ---------
     # N=1: the op call (plan + main + reduce; main dominates).  N>1: the local SpMM after the
     # gather.  Measured over a separate short run so the timed region above has no extra events.
-    torch.cuda.synchronize()
+    sync()
     spmm_ms, gather_ms = [], []
     for _ in range(max(args.steps, 5)):
         if not rowsplit:
@@ -268,16 +308,16 @@ def main():
             events[1].record()
             rs.compute_phase(out)
             events[2].record()
-        torch.cuda.synchronize()
-        spmm_ms.append(events[1].elapsed_time(events[2]))
+        sync()
+        spmm_ms.append(events[1].ms_to(events[2]))
         if rowsplit:
-            gather_ms.append(events[0].elapsed_time(events[1]))
+            gather_ms.append(events[0].ms_to(events[1]))
     kern_ms_separate = float(np.mean(spmm_ms))
     kern_ms = kern_ms_separate
     if not rowsplit:
         # N=1: the op's launches are the only work on the launch stream, so the HIP events that
         # bracket the timed region on that stream give the average op duration directly
-        kern_ms = ev_start.elapsed_time(ev_end) / args.steps
+        kern_ms = ev_start.ms_to(ev_end) / args.steps
     gather_mean = float(np.mean(gather_ms)) if gather_ms else 0.0
     phase = {"spmm_ms_max": kern_ms, "gather_ms_max": gather_mean}
     if rowsplit and world > 1:
@@ -286,9 +326,9 @@ def main():
         phase = {"spmm_ms_max": float(t[0]), "gather_ms_max": float(t[1])}
     # cold-cache SpMM: a 512 MB scratch write evicts the 256 MB Infinity Cache
     # and the L2s before each launch; median of 5.  The timed region above is the warm number.
-    scratch = torch.empty(512 << 20, dtype=torch.uint8, device=device)
     cold = []
-    for i in range(5):
+    scratch = torch.empty(512 << 20, dtype=torch.uint8, device=device) if on_gpu else None
+    for i in range(5 if on_gpu else 0):
         scratch.fill_(i)
         if not rowsplit:
             events[1].record()
@@ -298,10 +338,10 @@ def main():
             events[1].record()
             rs.compute_phase(out)
             events[2].record()
-        torch.cuda.synchronize()
-        cold.append(events[1].elapsed_time(events[2]))
+        sync()
+        cold.append(events[1].ms_to(events[2]))
     del scratch
-    cold_ms = float(np.median(cold))
+    cold_ms = float(np.median(cold)) if cold else float("nan")
     bytes_launch = alg_bytes(rows, nnz_local, n, s_v)
     if rowsplit and rs.exchange in rs.grids:  # the grid's SpMM: its row group x N/C columns
         gp = rs.grids[rs.exchange]
@@ -353,8 +393,8 @@ def main():
                      "alg_bytes_per_launch": bytes_launch, "kernel_ms": round(kern_ms, 4)},
     }
     result["extra"] = {"kernel_ms_events_separate_run": round(kern_ms_separate, 4),
-                       "kernel_ms_cold_median": round(cold_ms, 4),
-                       "gbs_cold": round(bytes_launch / (cold_ms * 1e-3) / 1e9, 1)}
+                       "kernel_ms_cold_median": round(cold_ms, 4) if cold else None,
+                       "gbs_cold": round(bytes_launch / (cold_ms * 1e-3) / 1e9, 1) if cold else None}
     if rowsplit:
         nz = torch.tensor([nnz_local, nnz_local], dtype=torch.float64, device=red_dev)
         if world > 1:
@@ -385,7 +425,30 @@ def main():
             "allgather_tune_ms": {kk: (round(vv, 4) if np.isfinite(vv) else None)
                                   for kk, vv in comm_times.items()},
             "tune_errors": getattr(rs, "tune_errors", {}) or None,
+            # every candidate: model time (xGMI assumption), the model refitted to
+            # the first measurement, the measured time (max over ranks) and whether it ran
+            "tune_candidates": getattr(rs, "tune_report", {}) or None,
+            "tune_rate_fit_gbs": round(rs.tune_rate_fit / 1e9, 2)
+            if getattr(rs, "tune_rate_fit", None) else None,
+            "tune_seconds": round(tune_s, 2) if tune_s is not None else None,
+            "setup_seconds": round(setup_s, 2),
             "nnz_per_rank_max_over_mean": round(float(nz[0]) / (float(nz[1]) / world), 4)})
+        # memory of the run: peak device memory (torch's allocator, this process) and peak host
+        # RSS per rank, max and sum over ranks
+        import resource
+        peak = torch.tensor([torch.cuda.max_memory_allocated(device) / 1e9 if on_gpu else 0.0,
+                             resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6],
+                            dtype=torch.float64, device=red_dev)
+        peak_sum = peak.clone()
+        if world > 1:
+            dist.all_reduce(peak, op=dist.ReduceOp.MAX)
+            dist.all_reduce(peak_sum, op=dist.ReduceOp.SUM)
+        result["extra"]["memory_gb"] = {
+            "device_peak_max_rank": round(float(peak[0]), 2),
+            "device_peak_sum": round(float(peak_sum[0]), 2),
+            "host_rss_peak_max_rank": round(float(peak[1]), 2),
+            "host_rss_peak_sum": round(float(peak_sum[1]), 2)}
+        result["extra"]["wall_seconds_to_line"] = round(time.time() - t_wall0, 1)
 
     # ---- CPU baseline (rank 0, N=1 only): the operator's own kCPU kernel ------
     if world == 1 and rank == 0 and not args.no_cpu_baseline:

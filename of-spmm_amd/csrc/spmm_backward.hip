@@ -48,6 +48,19 @@ __global__ void __launch_bounds__(kBlock) expand_rows_kernel(const I* __restrict
   for (int64_t j = (int64_t)rp[r] + lane; j < (int64_t)rp[r + 1]; j += 64) row_of[j] = (I)r;
 }
 
+// Sort keys of the transpose: the column, or k for a column outside [0, k) (the forward zero-fills
+// its gathered row, so such a nonzero touches no row of B and belongs to no row of A^T; sorted
+// past row_ptr_T[k], it is never read).
+template <typename I>
+__global__ void transpose_keys_kernel(const I* __restrict__ col, int64_t nnz, int64_t k,
+                                      I* __restrict__ keys) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nnz; j += stride) {
+    const int64_t c = (int64_t)col[j];
+    keys[j] = (I)((uint64_t)c < (uint64_t)k ? c : k);
+  }
+}
+
 // out_rp[c] = first position of column >= c in the sorted keys (binary search).
 template <typename I>
 __global__ void col_ptr_kernel(const I* __restrict__ keys, int64_t nnz, int64_t k,
@@ -114,14 +127,18 @@ int transpose(hipStream_t s, int64_t m, int64_t k, int64_t nnz, const I* rp, con
   I* keys_out = static_cast<I*>(ws);
   I* vals_in = keys_out + nnz;
   I* row_of = vals_in + nnz;
+  I* keys_in = row_of + nnz;
   void* cub_tmp = static_cast<char*>(ws) + plan::align_up(4 * (size_t)nnz * sizeof(I), 256);
   hipLaunchKernelGGL((iota_kernel<I>), dim3(g_nnz), dim3(kBlock), 0, s, vals_in, nnz);
   OFX_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL((expand_rows_kernel<I>), dim3((unsigned)((m + 3) / 4)), dim3(kBlock), 0, s,
                      rp, m, row_of);
   OFX_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL((transpose_keys_kernel<I>), dim3(g_nnz), dim3(kBlock), 0, s, col, nnz, k,
+                     keys_in);
+  OFX_HIP_CHECK(hipGetLastError());
   // stable LSD radix sort of (col, j): entries of one column keep ascending j == ascending row
-  OFX_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub, col, keys_out, vals_in, out_perm,
+  OFX_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub, keys_in, keys_out, vals_in, out_perm,
                                                    (int)nnz, 0, bits_for(k + 1), s));
   hipLaunchKernelGGL((col_ptr_kernel<I>), dim3((unsigned)((k + 1 + kBlock - 1) / kBlock)),
                      dim3(kBlock), 0, s, keys_out, nnz, k, out_rp);
@@ -205,8 +222,8 @@ __device__ __forceinline__ bool sddmm_item(const I* __restrict__ rp, int64_t g, 
 template <typename T, typename I, int LG, int L, int U, bool ALIGNED>
 __global__ void __launch_bounds__(kBlock)
     sddmm_kernel(const I* __restrict__ rp, const I* __restrict__ col, const T* __restrict__ dC,
-                 int64_t ldc, const T* __restrict__ B, int64_t ldb, T* __restrict__ out,
-                 int64_t row_begin, int64_t nrows, int64_t n, int64_t chunk,
+                 int64_t ldc, const T* __restrict__ B, int64_t ldb, int64_t kb,
+                 T* __restrict__ out, int64_t row_begin, int64_t nrows, int64_t n, int64_t chunk,
                  const unsigned long long* __restrict__ counters, const int64_t* __restrict__ items,
                  const int64_t* __restrict__ order) {
 #pragma clang fp contract(off)
@@ -237,9 +254,11 @@ __global__ void __launch_bounds__(kBlock)
       for (int u = 0; u < U; ++u) {
         const int64_t cu = (int64_t)__shfl((int64_t)myc, gbase + ((k + u) & (LG - 1)), 64);
         if (k + u < cnt) {
+          // a column outside [0, k): the forward gathered a zero row (zero_row_leaves)
           const T* brow = B + cu * ldb;
+          const bool in = (uint64_t)cu < (uint64_t)kb;
 #pragma unroll
-          for (int l = 0; l < L; ++l) load_leaf<T, ALIGNED>(brow, (int64_t)(gl * L + l) * kLeaf, n, bv[u][l]);
+          for (int l = 0; l < L; ++l) load_leaf<T, ALIGNED>(brow, in ? (int64_t)(gl * L + l) * kLeaf : n, n, bv[u][l]);
         }
       }
 #pragma unroll
@@ -280,8 +299,9 @@ constexpr int kMaxTilesLog = 6;  // n <= 2048 * 64 = 131072
 template <typename T, typename I, bool ALIGNED>
 __global__ void __launch_bounds__(kBlock)
     sddmm_wide_kernel(const I* __restrict__ rp, const I* __restrict__ col, const T* __restrict__ dC,
-                      int64_t ldc, const T* __restrict__ B, int64_t ldb, T* __restrict__ out,
-                      int64_t row_begin, int64_t nrows, int64_t n, int64_t chunk, int tiles,
+                      int64_t ldc, const T* __restrict__ B, int64_t ldb, int64_t kb,
+                      T* __restrict__ out, int64_t row_begin, int64_t nrows, int64_t n,
+                      int64_t chunk, int tiles,
                       const unsigned long long* __restrict__ counters,
                       const int64_t* __restrict__ items, const int64_t* __restrict__ order) {
 #pragma clang fp contract(off)
@@ -311,8 +331,9 @@ __global__ void __launch_bounds__(kBlock)
           const int64_t cu = (int64_t)__shfl((int64_t)myc, (k + u) & 63, 64);
           if (k + u < cnt) {
             const T* brow = B + cu * ldb;
+            const bool in = (uint64_t)cu < (uint64_t)kb;  // else a zero row
 #pragma unroll
-            for (int l = 0; l < L; ++l) load_leaf<T, ALIGNED>(brow, (leaf0 + l) * kLeaf, n, bv[u][l]);
+            for (int l = 0; l < L; ++l) load_leaf<T, ALIGNED>(brow, in ? (leaf0 + l) * kLeaf : n, n, bv[u][l]);
           }
         }
 #pragma unroll
@@ -364,7 +385,7 @@ struct SddmmArgs {
   hipStream_t s;
   const void *rp, *col, *dC, *B;
   void* out;
-  int64_t ldc, ldb, row_begin, nrows, n, nnz;
+  int64_t ldc, ldb, row_begin, nrows, n, nnz, k;
   void* ws;
   size_t ws_bytes;
 };
@@ -411,7 +432,7 @@ int sddmm_cfg(const SddmmArgs& a) {
   const int64_t grid = (work + GPB - 1) / GPB;
   hipLaunchKernelGGL((sddmm_kernel<T, I, LG, L, U, ALIGNED>), dim3((unsigned)grid), dim3(kBlock), 0,
                      a.s, static_cast<const I*>(a.rp), static_cast<const I*>(a.col),
-                     static_cast<const T*>(a.dC), a.ldc, static_cast<const T*>(a.B), a.ldb,
+                     static_cast<const T*>(a.dC), a.ldc, static_cast<const T*>(a.B), a.ldb, a.k,
                      static_cast<T*>(a.out), a.row_begin, a.nrows, a.n,
                      w.total > 0 ? sched.chunk : INT64_MAX, wl.counters, wl.items, wl.order);
   OFX_HIP_CHECK(hipGetLastError());
@@ -449,7 +470,7 @@ int sddmm_aligned(const SddmmArgs& a) {
   const int64_t grid = (work + kBlock / 64 - 1) / (kBlock / 64);
   hipLaunchKernelGGL((sddmm_wide_kernel<T, I, ALIGNED>), dim3((unsigned)grid), dim3(kBlock), 0, a.s,
                      static_cast<const I*>(a.rp), static_cast<const I*>(a.col),
-                     static_cast<const T*>(a.dC), a.ldc, static_cast<const T*>(a.B), a.ldb,
+                     static_cast<const T*>(a.dC), a.ldc, static_cast<const T*>(a.B), a.ldb, a.k,
                      static_cast<T*>(a.out), a.row_begin, a.nrows, a.n,
                      w.total > 0 ? sched.chunk : INT64_MAX, (int)tiles, wl.counters, wl.items,
                      wl.order);
@@ -570,7 +591,7 @@ extern "C" int ofx_sddmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t
               "sddmm_csr: NULL pointer");
   if (n == 0) return fail(OFX_EINVAL, "sddmm_csr: n == 0 (use a zero fill)");
   SddmmArgs args{static_cast<hipStream_t>(stream), row_ptr, col_idx, a, b, out, lda, ldb,
-                 row_begin, row_end - row_begin, n, nnz, workspace, workspace_bytes};
+                 row_begin, row_end - row_begin, n, nnz, k, workspace, workspace_bytes};
   if (idx_dtype == OFX_DT_INT32) return sddmm_idx<int32_t>(val_dtype, args);
   return sddmm_idx<int64_t>(val_dtype, args);
 }

@@ -19,55 +19,69 @@
 namespace ofx {
 namespace {
 
+// A column outside [0, k): the reference CPU gather zero-fills the gathered row of an index >= the
+// table size (oneflow/user/kernels/gather_kernel_util.cpp:84-89), so the nonzero adds val * 0; a
+// negative index fails its CHECK_GE (:80), reported here as OFX_EINVAL (`neg`).
 template <typename T, typename I>
-void row_sum(const I* col, const T* val, const T* B, int64_t ldb, int64_t n, int64_t j0,
-             int64_t j1, typename Num<T>::acc* acc) {
+void row_sum(const I* col, const T* val, const T* B, int64_t ldb, int64_t k, int64_t n,
+             int64_t j0, int64_t j1, typename Num<T>::acc* acc, bool* neg) {
 #pragma clang fp contract(off)
   using A = typename Num<T>::acc;
   for (int64_t c = 0; c < n; ++c) acc[c] = A(0);
   for (int64_t j = j0; j < j1; ++j) {
     const A v = Num<T>::load(val[j]);
-    const T* brow = B + (int64_t)col[j] * ldb;
-    for (int64_t c = 0; c < n; ++c) acc[c] = acc[c] + Num<T>::mul(v, Num<T>::load(brow[c]));
+    const int64_t cj = (int64_t)col[j];
+    if (cj >= 0 && cj < k) {
+      const T* brow = B + cj * ldb;
+      for (int64_t c = 0; c < n; ++c) acc[c] = acc[c] + Num<T>::mul(v, Num<T>::load(brow[c]));
+    } else {  // the zero-filled gathered row
+      if (cj < 0) *neg = true;
+      for (int64_t c = 0; c < n; ++c) acc[c] = acc[c] + Num<T>::mul(v, A(0));
+    }
   }
 }
 
 template <typename T, typename I>
-int cpu_spmm(int nthreads, int64_t n, const I* rp, const I* col, const T* val, const T* B,
-             int64_t ldb, T* C, int64_t ldc, int64_t row_begin, int64_t row_end,
+int cpu_spmm(int nthreads, int64_t k, int64_t n, const I* rp, const I* col, const T* val,
+             const T* B, int64_t ldb, T* C, int64_t ldc, int64_t row_begin, int64_t row_end,
              const Schedule& s, const T* bias, int act) {
 #pragma clang fp contract(off)
   using A = typename Num<T>::acc;
   const int64_t rows = row_end - row_begin;
-#pragma omp parallel num_threads(nthreads)
+  bool any_neg = false;
+#pragma omp parallel num_threads(nthreads) reduction(|| : any_neg)
   {
     std::vector<A> acc(n), part(n);
+    bool neg = false;
 #pragma omp for schedule(dynamic, 64)
     for (int64_t g = 0; g < rows; ++g) {
       const int64_t r = row_begin + g;
       const int64_t j0 = (int64_t)rp[r], j1 = (int64_t)rp[r + 1];
       const int64_t len = j1 - j0;
       if (len <= s.split) {
-        row_sum<T, I>(col, val, B, ldb, n, j0, j1, acc.data());
+        row_sum<T, I>(col, val, B, ldb, k, n, j0, j1, acc.data(), &neg);
       } else {
         const int64_t nc = num_chunks(len, s.chunk);
         for (int64_t c = 0; c < n; ++c) acc[c] = A(0);
-        for (int64_t k = 0; k < nc; ++k) {
-          const int64_t a = j0 + k * s.chunk;
-          const int64_t b = (k == nc - 1) ? j1 : a + s.chunk;
-          row_sum<T, I>(col, val, B, ldb, n, a, b, part.data());
+        for (int64_t q = 0; q < nc; ++q) {
+          const int64_t a = j0 + q * s.chunk;
+          const int64_t e = (q == nc - 1) ? j1 : a + s.chunk;
+          row_sum<T, I>(col, val, B, ldb, k, n, a, e, part.data(), &neg);
           for (int64_t c = 0; c < n; ++c) acc[c] = acc[c] + part[c];
         }
       }
       T* out = C + g * ldc;
       for (int64_t c = 0; c < n; ++c) out[c] = epilogue<T>(acc[c], bias, c, act);
     }
+    any_neg = any_neg || neg;
   }
+  OFX_REQUIRE(!any_neg, OFX_EINVAL,
+              "spmm_csr_cpu: negative column index (gather_kernel_util.cpp:80 CHECK_GE(idx, 0))");
   return OFX_OK;
 }
 
 template <typename I>
-int cpu_dispatch(int nthreads, int val_dtype, int64_t n, const void* rp, const void* col,
+int cpu_dispatch(int nthreads, int val_dtype, int64_t k, int64_t n, const void* rp, const void* col,
                  const void* val, const void* b, int64_t ldb, void* c, int64_t ldc,
                  int64_t row_begin, int64_t row_end, const Schedule& s, const void* bias,
                  int act) {
@@ -75,16 +89,16 @@ int cpu_dispatch(int nthreads, int val_dtype, int64_t n, const void* rp, const v
   const I* ci = static_cast<const I*>(col);
   switch (val_dtype) {
     case OFX_DT_FLOAT:
-      return cpu_spmm<float, I>(nthreads, n, r, ci, (const float*)val, (const float*)b, ldb,
+      return cpu_spmm<float, I>(nthreads, k, n, r, ci, (const float*)val, (const float*)b, ldb,
                                 (float*)c, ldc, row_begin, row_end, s, (const float*)bias, act);
     case OFX_DT_DOUBLE:
-      return cpu_spmm<double, I>(nthreads, n, r, ci, (const double*)val, (const double*)b, ldb,
+      return cpu_spmm<double, I>(nthreads, k, n, r, ci, (const double*)val, (const double*)b, ldb,
                                  (double*)c, ldc, row_begin, row_end, s, (const double*)bias, act);
     case OFX_DT_BFLOAT16:
-      return cpu_spmm<bf16, I>(nthreads, n, r, ci, (const bf16*)val, (const bf16*)b, ldb,
+      return cpu_spmm<bf16, I>(nthreads, k, n, r, ci, (const bf16*)val, (const bf16*)b, ldb,
                                (bf16*)c, ldc, row_begin, row_end, s, (const bf16*)bias, act);
     case OFX_DT_FLOAT16:
-      return cpu_spmm<f16, I>(nthreads, n, r, ci, (const f16*)val, (const f16*)b, ldb, (f16*)c,
+      return cpu_spmm<f16, I>(nthreads, k, n, r, ci, (const f16*)val, (const f16*)b, ldb, (f16*)c,
                               ldc, row_begin, row_end, s, (const f16*)bias, act);
     default: return fail(OFX_EUNSUPPORTED, "spmm_csr_cpu: unsupported value dtype %d", val_dtype);
   }
@@ -118,9 +132,9 @@ int spmm_cpu_entry(int num_threads, int idx_dtype, int val_dtype, int64_t m, int
   const int nt = num_threads > 0 ? num_threads : omp_get_max_threads();
   const Schedule s = resolve_schedule(n, opts);
   if (idx_dtype == OFX_DT_INT32)
-    return cpu_dispatch<int32_t>(nt, val_dtype, n, row_ptr, col_idx, values, b, ldb, c, ldc,
+    return cpu_dispatch<int32_t>(nt, val_dtype, k, n, row_ptr, col_idx, values, b, ldb, c, ldc,
                                  row_begin, row_end, s, bias, act);
-  return cpu_dispatch<int64_t>(nt, val_dtype, n, row_ptr, col_idx, values, b, ldb, c, ldc,
+  return cpu_dispatch<int64_t>(nt, val_dtype, k, n, row_ptr, col_idx, values, b, ldb, c, ldc,
                                row_begin, row_end, s, bias, act);
 }
 }  // namespace
@@ -187,21 +201,27 @@ namespace {
 template <typename I>
 void cpu_transpose(int64_t m, int64_t k, int64_t nnz, const I* rp, const I* col, I* out_rp,
                    I* out_col, I* out_perm) {
-  std::vector<int64_t> cnt(k + 1, 0);
-  for (int64_t j = 0; j < nnz; ++j) ++cnt[(int64_t)col[j] + 1];
-  for (int64_t c = 0; c < k; ++c) cnt[c + 1] += cnt[c];
+  // key k for a column outside [0, k): after row_ptr_T[k], never read (csrc/spmm_backward.hip
+  // transpose_keys_kernel)
+  auto key = [&](int64_t j) {
+    const int64_t c = (int64_t)col[j];
+    return (uint64_t)c < (uint64_t)k ? c : k;
+  };
+  std::vector<int64_t> cnt(k + 2, 0);
+  for (int64_t j = 0; j < nnz; ++j) ++cnt[key(j) + 1];
+  for (int64_t c = 0; c <= k; ++c) cnt[c + 1] += cnt[c];
   for (int64_t c = 0; c <= k; ++c) out_rp[c] = (I)cnt[c];
   for (int64_t r = 0; r < m; ++r)  // rows ascending -> stable within each column
     for (int64_t j = (int64_t)rp[r]; j < (int64_t)rp[r + 1]; ++j) {
-      const int64_t pos = cnt[(int64_t)col[j]]++;
+      const int64_t pos = cnt[key(j)]++;
       out_col[pos] = (I)r;
       out_perm[pos] = (I)j;
     }
 }
 
 template <typename T, typename I>
-void cpu_sddmm(int nthreads, int64_t n, const I* rp, const I* col, const T* a, int64_t lda,
-               const T* b, int64_t ldb, T* out, int64_t row_begin, int64_t row_end) {
+void cpu_sddmm(int nthreads, int64_t k, int64_t n, const I* rp, const I* col, const T* a,
+               int64_t lda, const T* b, int64_t ldb, T* out, int64_t row_begin, int64_t row_end) {
 #pragma clang fp contract(off)
   using A = typename Num<T>::acc;
   const int64_t leaves = (n + 7) / 8;
@@ -210,11 +230,13 @@ void cpu_sddmm(int nthreads, int64_t n, const I* rp, const I* col, const T* a, i
 #pragma omp parallel num_threads(nthreads)
   {
     std::vector<A> leaf(padded);
+    const std::vector<T> zero(n, Num<T>::store(A(0)));  // the zero-filled row of a column outside [0, k)
 #pragma omp for schedule(dynamic, 64)
     for (int64_t r = row_begin; r < row_end; ++r) {
       const T* arow = a + (r - row_begin) * lda;
       for (int64_t j = (int64_t)rp[r]; j < (int64_t)rp[r + 1]; ++j) {
-        const T* brow = b + (int64_t)col[j] * ldb;
+        const int64_t cj = (int64_t)col[j];
+        const T* brow = (uint64_t)cj < (uint64_t)k ? b + cj * ldb : zero.data();
         for (int64_t l = 0; l < padded; ++l) {
           A s = A(0);
           for (int64_t e = 8 * l; e < 8 * l + 8 && e < n; ++e)
@@ -287,16 +309,16 @@ extern "C" int ofx_sddmm_csr_cpu(int num_threads, int idx_dtype, int val_dtype, 
     const I* ci = (const I*)col_idx;
     switch (val_dtype) {
       case OFX_DT_FLOAT:
-        cpu_sddmm<float, I>(nt, n, rp, ci, (const float*)a, lda, (const float*)b, ldb, (float*)out, row_begin, row_end);
+        cpu_sddmm<float, I>(nt, k, n, rp, ci, (const float*)a, lda, (const float*)b, ldb, (float*)out, row_begin, row_end);
         break;
       case OFX_DT_DOUBLE:
-        cpu_sddmm<double, I>(nt, n, rp, ci, (const double*)a, lda, (const double*)b, ldb, (double*)out, row_begin, row_end);
+        cpu_sddmm<double, I>(nt, k, n, rp, ci, (const double*)a, lda, (const double*)b, ldb, (double*)out, row_begin, row_end);
         break;
       case OFX_DT_BFLOAT16:
-        cpu_sddmm<bf16, I>(nt, n, rp, ci, (const bf16*)a, lda, (const bf16*)b, ldb, (bf16*)out, row_begin, row_end);
+        cpu_sddmm<bf16, I>(nt, k, n, rp, ci, (const bf16*)a, lda, (const bf16*)b, ldb, (bf16*)out, row_begin, row_end);
         break;
       default:
-        cpu_sddmm<f16, I>(nt, n, rp, ci, (const f16*)a, lda, (const f16*)b, ldb, (f16*)out, row_begin, row_end);
+        cpu_sddmm<f16, I>(nt, k, n, rp, ci, (const f16*)a, lda, (const f16*)b, ldb, (f16*)out, row_begin, row_end);
         break;
     }
   };

@@ -69,11 +69,13 @@ struct alignas(sizeof(T) * VEC) Pack {
 // WH: small launches: hub chunks and heavy rows take a whole wave each (the wave's 64/LPR groups
 // interleave the nonzeros of one item), the light rows one group each (accumulate_wave).
 // BI: the mid form: hub chunks and heavy rows take a whole block each (block_accumulate).
+// BUF: B rows through raw buffer loads with the hardware range check (B < 4 GiB, BRows); the
+// global-load form (BUF = false) serves larger B in the bandwidth configurations only.
 template <int VEC_, int LPR_, int U_ = 8, int WPB_ = 4, bool NT_ = false, bool PF_ = false,
-          bool BNT_ = false, bool WH_ = false, bool BI_ = false>
+          bool BNT_ = false, bool WH_ = false, bool BI_ = false, bool BUF_ = true>
 struct Cfg {
   static constexpr int VEC = VEC_, LPR = LPR_, U = U_, WPB = WPB_;
-  static constexpr bool NT = NT_, PF = PF_, BNT = BNT_, WH = WH_, BI = BI_;
+  static constexpr bool NT = NT_, PF = PF_, BNT = BNT_, WH = WH_, BI = BI_, BUF = BUF_;
   // loads in flight per lane of the wave-item form: G * UW * VEC cross-lane moves per batch are
   // unrolled, so UW keeps that at <= 256 (4..32)
   static constexpr int G = LPR < 64 ? 64 / LPR : 1;
@@ -142,6 +144,85 @@ __device__ __forceinline__ int64_t shfl(int64_t v, int src) {
 __device__ __forceinline__ float shfl(float v, int src) { return __shfl(v, src); }
 __device__ __forceinline__ double shfl(double v, int src) { return __shfl(v, src); }
 
+// The zero row of out-of-range columns.  The reference gather zero-fills the gathered row of an
+// index outside the table (CPU: idx >= size, oneflow/user/kernels/gather_kernel_util.cpp:84-89;
+// CUDA: any index outside [0, size), gather_kernel_util.cu:36), so such a nonzero adds val * 0
+// (+-0, or NaN for a non-finite value): the bits of loading zeros.  A lane whose column is out of
+// range loads a VEC slot of this zero-initialised buffer instead of a B row, so nothing outside B
+// is read and no per-element select is needed (one 64-bit address select per nonzero).
+constexpr int64_t kZeroRowBytes = 16384;
+__device__ __attribute__((aligned(256))) uint32_t g_zero_row[kZeroRowBytes / 4];
+
+// B-row loads of one lane in one column pass (columns [c0, c0 + W); cc = the lane's first column,
+// c0 for a lane past n), with the reference gather's zero fill of a column outside [0, k).
+//   BUF (B < 4 GiB: every configuration but the papers-scale one): raw buffer loads through one
+//   descriptor over B's k rows.  The byte offset of column c is min(c, k) * ldb_bytes + the lane's
+//   column bytes; row k lies past the descriptor's range, and the hardware returns zeros for it.
+//   So an out-of-range column costs nothing beyond one clamp (v_min_u32 for int32 indices), and
+//   the address is 32-bit arithmetic instead of a 64-bit multiply-add per load.
+//   !BUF: global loads; an out-of-range column loads this lane's slot of g_zero_row instead (a
+//   64-bit select per load).
+template <typename T, bool BUF>
+struct BRows {
+  const T* base;  // !BUF: B + cc
+  const T* zero;  // !BUF: this lane's slot of g_zero_row
+  int64_t ldb, k;
+  __amdgpu_buffer_rsrc_t rsrc;  // BUF: B[0 .. k) rows
+  uint32_t ldb_bytes, cc_bytes, k32;
+  template <typename I>
+  __device__ __forceinline__ uint32_t clamp_row(I c) const {
+#ifdef OFX_AB_NO_ZERO_FILL  // A/B builds only (scripts/ab_build.sh): no bound
+    return (uint32_t)c;
+#else
+    if constexpr (sizeof(I) == 4) return __builtin_elementwise_min((uint32_t)c, k32);
+    else return (uint64_t)c < (uint64_t)k ? (uint32_t)c : k32;
+#endif
+  }
+  __device__ __forceinline__ const T* row(int64_t c) const {
+    return (uint64_t)c < (uint64_t)k ? base + c * ldb : zero;
+  }
+  template <bool NTB, typename P, typename I>
+  __device__ __forceinline__ P load(I c) const {
+    if constexpr (BUF) {
+      const uint32_t off = clamp_row(c) * ldb_bytes + cc_bytes;
+      constexpr int aux = NTB ? 2 : 0;  // nt
+      if constexpr (sizeof(P) == 16) {
+        return __builtin_bit_cast(P, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, aux));
+      } else if constexpr (sizeof(P) == 8) {
+        return __builtin_bit_cast(P, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, aux));
+      } else if constexpr (sizeof(P) == 4) {
+        return __builtin_bit_cast(P, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, aux));
+      } else {
+        static_assert(sizeof(P) == 2, "B-row slice of 2, 4, 8 or 16 bytes");
+        return __builtin_bit_cast(P, __builtin_amdgcn_raw_buffer_load_b16(rsrc, off, 0, aux));
+      }
+    } else {
+      return ld_brow<NTB, P>(row((int64_t)c));
+    }
+  }
+};
+template <typename T, bool BUF>
+__device__ __forceinline__ BRows<T, BUF> brows(const T* B, int64_t c0, int64_t cc, bool active,
+                                               int64_t ldb, int64_t k) {
+  BRows<T, BUF> r;
+  const int64_t lc = active ? cc : c0;
+  r.base = B + lc;
+  r.zero = reinterpret_cast<const T*>(g_zero_row) + (lc - c0);
+  r.ldb = ldb;
+  r.k = k;
+  if constexpr (BUF) {
+    // the launch guarantees (k + 1) * ldb * sizeof(T) < 2^32; all descriptor inputs are kernel
+    // arguments (wave-uniform), so no waterfall loop is emitted around the loads
+    r.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(B), 0,
+                                               (int)(uint32_t)(k * ldb * (int64_t)sizeof(T)),
+                                               0x00020000);
+    r.ldb_bytes = (uint32_t)(ldb * (int64_t)sizeof(T));
+    r.cc_bytes = (uint32_t)(lc * (int64_t)sizeof(T));
+    r.k32 = (uint32_t)k;
+  }
+  return r;
+}
+
 __device__ __forceinline__ int64_t uniform64(int64_t v) {
   const uint64_t u = (uint64_t)v;
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
@@ -154,9 +235,8 @@ __device__ __forceinline__ int64_t uniform64(int64_t v) {
 template <typename T, typename I, typename K>
 __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* __restrict__ val,
                                            const I* __restrict__ vperm,
-                                           const T* __restrict__ Bc, const T* __restrict__ B0,
-                                           int64_t ldb, int64_t j0,
-                                           int64_t j1, int gl, int gbase, bool active,
+                                           const BRows<T, K::BUF>& br, int64_t j0, int64_t j1,
+                                           int gl, int gbase, bool active,
                                            typename Num<T>::acc (&acc)[K::VEC]) {
 #pragma clang fp contract(off)
   constexpr int VEC = K::VEC, LPR = K::LPR, kUnroll = K::U;
@@ -174,7 +254,7 @@ __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* _
           const int64_t cu = (int64_t)ld_stream<K::NT>(col + j + u);
           const int64_t jv = vperm ? (int64_t)ld_stream<K::NT>(vperm + j + u) : j + u;
           vv[u] = Num<T>::load(ld_stream<K::NT>(val + jv));
-          if (active) bv[u] = ld_brow<K::BNT, P>(Bc + cu * ldb);
+          if (active) bv[u] = br.template load<K::BNT, P>(cu);
         }
       }
 #pragma unroll
@@ -195,7 +275,7 @@ __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* _
       const int n_ = (int)((j1 - jb) < BATCH ? (j1 - jb) : BATCH);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        c[r] = 0;
+        c[r] = 0;  // slots past the row end: row 0 (the zero row if k == 0), discarded
         v[r] = 0;
         const int idx = r * LPR + gl;
         if (idx < n_) {
@@ -232,27 +312,26 @@ __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* _
           // every load (slots past the row end read B row 0, inactive lanes read from B's first
           // columns; both discarded below), so the group pays one LDS wait and one memory round
           // trip per batch instead of one ds_bpermute wait per load.
-          int64_t cuv[kUnroll];
+          I cuv[kUnroll];
 #pragma unroll
           for (int u = 0; u < kUnroll; ++u) {
             const int src = gbase + ((k + u) & (LPR - 1));
             const int r = R > 1 ? u / LPR : 0;
-            cuv[u] = (int64_t)shfl(myc[r], src);
+            cuv[u] = shfl(myc[r], src);
             vv[u] = shfl(myv[r], src);
           }
-          const T* Bs = active ? Bc : B0;
 #pragma unroll
           for (int u = 0; u < kUnroll; ++u)
-            bv[u] = ld_brow<K::BNT, P>(Bs + (k + u < cnt ? cuv[u] : 0) * ldb);
+            bv[u] = br.template load<K::BNT, P>(k + u < cnt ? cuv[u] : I(0));
         } else {
 #pragma unroll
           for (int u = 0; u < kUnroll; ++u) {
             // R > 1: the batch is exactly kUnroll long, so k == 0 and the register is static
             const int src = gbase + ((k + u) & (LPR - 1));
             const int r = R > 1 ? u / LPR : 0;
-            const int64_t cu = (int64_t)shfl(myc[r], src);
+            const I cu = shfl(myc[r], src);
             vv[u] = shfl(myv[r], src);
-            if (k + u < cnt && active) bv[u] = ld_brow<K::BNT, P>(Bc + cu * ldb);
+            if (k + u < cnt && active) bv[u] = br.template load<K::BNT, P>(cu);
           }
         }
 #pragma unroll
@@ -276,9 +355,8 @@ __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* _
 template <typename T, typename I, typename K>
 __device__ __forceinline__ void accumulate_wave(const I* __restrict__ col, const T* __restrict__ val,
                                                 const I* __restrict__ vperm,
-                                                const T* __restrict__ Bc, const T* __restrict__ B0,
-                                                int64_t ldb, int64_t j0, int64_t j1, int lane,
-                                                int gl, bool active,
+                                                const BRows<T, K::BUF>& br,
+                                                int64_t j0, int64_t j1, int lane, int gl,
                                                 typename Num<T>::acc (&acc)[K::VEC]) {
 #pragma clang fp contract(off)
   constexpr int VEC = K::VEC, LPR = K::LPR, U = K::UW, G = 64 / LPR;
@@ -305,7 +383,6 @@ __device__ __forceinline__ void accumulate_wave(const I* __restrict__ col, const
   I nxc[R];
   A nxv[R];
   if (j0 < j1) load_batch(j0, nxc, nxv);
-  const T* Bs = active ? Bc : B0;
   for (int64_t jb = j0; jb < j1; jb += BATCH) {
     const int cnt = (int)((j1 - jb) < BATCH ? (j1 - jb) : BATCH);
     I myc[R];
@@ -329,7 +406,7 @@ __device__ __forceinline__ void accumulate_wave(const I* __restrict__ col, const
     P bv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      bv[u] = ld_brow<K::BNT, P>(Bs + (G * u + q < cnt ? (int64_t)cuv[u] : 0) * ldb);
+      bv[u] = br.template load<K::BNT, P>(G * u + q < cnt ? cuv[u] : I(0));
     // per u: this group's product, the G groups' products fetched with ds_bpermute (all issued
     // before the first add, so their latency overlaps), then added in nonzero order
 #pragma unroll
@@ -453,7 +530,7 @@ template <typename T, typename I, typename K>
 __device__ __forceinline__ void block_accumulate(const I* __restrict__ col,
                                                  const T* __restrict__ val,
                                                  const I* __restrict__ vperm,
-                                                 const T* __restrict__ Bs, int64_t ldb,
+                                                 const BRows<T, K::BUF>& br,
                                                  int64_t j0, int64_t j1, int gb, int gl,
                                                  bool chain, SmallLds<T, I, K>& sh,
                                                  typename Num<T>::acc (&acc)[K::VEC],
@@ -500,8 +577,8 @@ __device__ __forceinline__ void block_accumulate(const I* __restrict__ col,
     const int64_t live = -(int64_t)(kb < nb);
 #pragma unroll
     for (int u = 0; u < UW; ++u) {
-      const int64_t c = (int64_t)sh.scol[off + GB * u + gb] & live;
-      b[u] = ld_brow<K::BNT, P>(Bs + c * ldb);
+      const I c = sh.scol[off + GB * u + gb] & (I)live;
+      b[u] = br.template load<K::BNT, P>(c);
     }
   };
   // batch k: products of the B rows in `b` -> LDS; (span staging); barrier; B rows of batch
@@ -643,8 +720,9 @@ template <typename T, typename I, typename K>
 __global__ void __launch_bounds__(64 * K::WPB)
     spmm_small_kernel(const I* __restrict__ rp, const I* __restrict__ col,
                       const T* __restrict__ val, const I* __restrict__ vperm,
-                      const T* __restrict__ B, int64_t ldb, T* __restrict__ C, int64_t ldc,
-                      int64_t row_begin, int64_t nrows, int64_t n, int64_t split, int64_t chunk,
+                      const T* __restrict__ B, int64_t ldb, int64_t kb, T* __restrict__ C,
+                      int64_t ldc, int64_t row_begin, int64_t nrows, int64_t n, int64_t split,
+                      int64_t chunk,
                       int64_t light, const T* __restrict__ bias, int act) {
   using SF = SmallForm<T, I, K>;
   using A = typename Num<T>::acc;
@@ -675,7 +753,8 @@ __global__ void __launch_bounds__(64 * K::WPB)
         A acc[VEC];
 #pragma unroll
         for (int e = 0; e < VEC; ++e) acc[e] = A(0);
-        accumulate<T, I, K>(col, val, vperm, B + cc, B, ldb, rs, re, gl, gbase, active, acc);
+        accumulate<T, I, K>(col, val, vperm, brows<T, K::BUF>(B, c0, cc, active, ldb, kb), rs, re, gl, gbase,
+                            active, acc);
         if (active) store_row<T, VEC, K::NT>(C + lr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
       }
     }
@@ -694,14 +773,14 @@ __global__ void __launch_bounds__(64 * K::WPB)
     for (int64_t c0 = 0; c0 < n; c0 += W) {
       const int64_t cc = c0 + (int64_t)gl * VEC;
       const bool active = cc < n;
-      const T* Bs = active ? B + cc : B;
+      const BRows<T, K::BUF> br = brows<T, K::BUF>(B, c0, cc, active, ldb, kb);
       A total[VEC], acc[VEC];
 #pragma unroll
       for (int e = 0; e < VEC; ++e) total[e] = A(0);
       if (one_pass) {
 #pragma unroll
         for (int e = 0; e < VEC; ++e) acc[e] = A(0);
-        block_accumulate<T, I, K>(col, val, vperm, Bs, ldb, rs, re, gb, gl, chain, lds, acc,
+        block_accumulate<T, I, K>(col, val, vperm, br, rs, re, gb, gl, chain, lds, acc,
                                   chunk / SF::NB, nc);
         if (chain && active) store_row<T, VEC, K::NT>(C + hr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
         continue;
@@ -714,7 +793,7 @@ __global__ void __launch_bounds__(64 * K::WPB)
         }
 #pragma unroll
         for (int e = 0; e < VEC; ++e) acc[e] = A(0);
-        block_accumulate<T, I, K>(col, val, vperm, Bs, ldb, j0, j1, gb, gl, chain, lds, acc);
+        block_accumulate<T, I, K>(col, val, vperm, br, j0, j1, gb, gl, chain, lds, acc);
         if (split_row) {
 #pragma unroll
           for (int e = 0; e < VEC; ++e) total[e] = total[e] + acc[e];
@@ -733,7 +812,7 @@ template <typename T, typename I, typename K>
 __global__ void __launch_bounds__(64 * K::WPB)
     spmm_main_kernel(const I* __restrict__ rp, const I* __restrict__ col,
                      const T* __restrict__ val, const I* __restrict__ vperm,
-                     const T* __restrict__ B, int64_t ldb,
+                     const T* __restrict__ B, int64_t ldb, int64_t kb,
                      T* __restrict__ C, int64_t ldc, int64_t row_begin, int64_t nrows, int64_t n,
                      int64_t chunk, const unsigned long long* __restrict__ counters,
                      const int64_t* __restrict__ items, const int64_t* __restrict__ order,
@@ -776,7 +855,8 @@ __global__ void __launch_bounds__(64 * K::WPB)
         A acc[VEC];
 #pragma unroll
         for (int e = 0; e < VEC; ++e) acc[e] = A(0);
-        accumulate_wave<T, I, K>(col, val, vperm, B + cc, B, ldb, j0, j1, lane, gl, active, acc);
+        accumulate_wave<T, I, K>(col, val, vperm, brows<T, K::BUF>(B, c0, cc, active, ldb, kb), j0, j1, lane, gl,
+                                 acc);
         if (active && gsub == 0) {
           if (wc >= 0)
             store_partial<A, VEC>(part + w * n + cc, acc);
@@ -821,7 +901,7 @@ __global__ void __launch_bounds__(64 * K::WPB)
         A acc[VEC];
 #pragma unroll
         for (int e = 0; e < VEC; ++e) acc[e] = A(0);
-        block_accumulate<T, I, K>(col, val, vperm, active ? B + cc : B, ldb, j0, j1, gb, gl,
+        block_accumulate<T, I, K>(col, val, vperm, brows<T, K::BUF>(B, c0, cc, active, ldb, kb), j0, j1, gb, gl,
                                   chain, lds, acc);
         if (chain && active) {
           if (wc >= 0)
@@ -874,7 +954,8 @@ __global__ void __launch_bounds__(64 * K::WPB)
     A acc[VEC];
 #pragma unroll
     for (int e = 0; e < VEC; ++e) acc[e] = A(0);
-    accumulate<T, I, K>(col, val, vperm, B + cc, B, ldb, j0, j1, gl, gbase, active, acc);
+    accumulate<T, I, K>(col, val, vperm, brows<T, K::BUF>(B, c0, cc, active, ldb, kb), j0, j1, gl, gbase, active,
+                        acc);
     if (active) {
       if (c >= 0)
         store_partial<A, VEC>(part + g * n + cc, acc);
@@ -1030,14 +1111,17 @@ int launch_cfg(const Launch& L) {
   const int64_t heavy = L.sched.heavy == 0 ? auto_heavy(L.nrows, L.nnz_est) : L.sched.heavy;
   const int64_t bi_items =
       w.max_chunks + (heavy == INT64_MAX ? 0 : std::min<int64_t>(L.nrows, L.nnz / (heavy + 1) + 1));
-  const int64_t wave_blocks = (K::WH && K::LPR < 64 && plan) ? (work + K::WPB - 1) / K::WPB
+  // wave items (one wave each) and block items (one block each) are bounded alike: hub chunks
+  // plus the rows above the heavy threshold
+  const int64_t wave_blocks = (K::WH && K::LPR < 64 && plan) ? (bi_items + K::WPB - 1) / K::WPB
                               : (K::BI && plan)              ? bi_items
                                                              : 0;
   const int64_t grid = wave_blocks + (work + GPB - 1) / GPB;
   OFX_REQUIRE(grid < (int64_t)UINT32_MAX, OFX_EINVAL, "spmm_csr: too many rows (%lld)",
               (long long)L.nrows);
   hipLaunchKernelGGL((spmm_main_kernel<T, I, K>), dim3((unsigned)grid), dim3(64 * K::WPB), 0,
-                     L.stream, rp, col, val, static_cast<const I*>(L.vperm), B, L.ldb, C, L.ldc,
+                     L.stream, rp, col, val, static_cast<const I*>(L.vperm), B, L.ldb, L.b_rows, C,
+                     L.ldc,
                      L.row_begin, L.nrows, L.n,
                      plan ? L.sched.chunk : INT64_MAX, counters, items, order, part,
                      static_cast<const T*>(L.bias), L.act, wave_blocks);
@@ -1061,7 +1145,8 @@ int launch_small(const Launch& L) {
   hipLaunchKernelGGL((spmm_small_kernel<T, I, K>), dim3((unsigned)grid), dim3(64 * K::WPB), 0,
                      L.stream, static_cast<const I*>(L.rp), static_cast<const I*>(L.col),
                      static_cast<const T*>(L.val), static_cast<const I*>(L.vperm),
-                     static_cast<const T*>(L.b), L.ldb, static_cast<T*>(L.c), L.ldc, L.row_begin,
+                     static_cast<const T*>(L.b), L.ldb, L.b_rows, static_cast<T*>(L.c), L.ldc,
+                     L.row_begin,
                      L.nrows, L.n, L.sched.split, L.sched.chunk, light,
                      static_cast<const T*>(L.bias), L.act);
   OFX_HIP_CHECK(hipGetLastError());
@@ -1098,16 +1183,17 @@ int launch_vec_small(const Launch& L, int lpr) {
   }
 }
 
-// The planned form with the small-launch configuration (wave items for hub chunks and heavy rows,
-// U = 32 / 16 loads in flight, next batch prefetched) at any size: tuning variant 30004.
-template <typename T, typename I, int VEC>
-int launch_vec_wave(const Launch& L, int lpr) {
+// The prefetching form (use_prefetch_form): U = 32 / 16 loads in flight per lane, the next batch's
+// (col, val) prefetched; WH: hub chunks and heavy rows take a whole wave (wave items).  Tuning
+// variants 30004 (WH) / 30005 force it at any size.
+template <typename T, typename I, int VEC, bool WH>
+int launch_vec_pf(const Launch& L, int lpr) {
   constexpr int U = VEC * sizeof(T) <= 4 ? 32 : 16;
   switch (lpr) {
-    case 4: return launch_cfg<T, I, Cfg<VEC, 4, U, 4, false, true, false, true>>(L);
-    case 8: return launch_cfg<T, I, Cfg<VEC, 8, U, 4, false, true, false, true>>(L);
-    case 16: return launch_cfg<T, I, Cfg<VEC, 16, U, 4, false, true, false, true>>(L);
-    case 32: return launch_cfg<T, I, Cfg<VEC, 32, U, 4, false, true, false, true>>(L);
+    case 4: return launch_cfg<T, I, Cfg<VEC, 4, U, 4, false, true, false, WH>>(L);
+    case 8: return launch_cfg<T, I, Cfg<VEC, 8, U, 4, false, true, false, WH>>(L);
+    case 16: return launch_cfg<T, I, Cfg<VEC, 16, U, 4, false, true, false, WH>>(L);
+    case 32: return launch_cfg<T, I, Cfg<VEC, 32, U, 4, false, true, false, WH>>(L);
     case 64: return launch_cfg<T, I, Cfg<VEC, 64, U, 4, false, false, false, false>>(L);
     default: return fail(OFX_EINVAL, "spmm_csr: unsupported lanes-per-row %d", lpr);
   }
@@ -1129,22 +1215,61 @@ int launch_vec_mid(const Launch& L, int lpr) {
   }
 }
 
+// B's byte offsets fit the buffer descriptor's 32 bits (BRows): row k (the zero row) included.
+template <typename T>
+bool buffer_rows_ok(const Launch& L) {
+  return (unsigned __int128)(L.b_rows + 1) * (unsigned __int128)L.ldb * sizeof(T) <
+         ((unsigned __int128)1 << 32);
+}
+
+// B of 4 GiB or more (papers-scale): the bandwidth configurations with global loads (BUF = false).
+template <typename T, typename I, int VEC>
+int launch_vec_global(const Launch& L, int lpr, bool nt) {
+  switch (lpr) {
+    case 4: return launch_cfg<T, I, Cfg<VEC, 4, 8, 4, false, false, false, false, false, false>>(L);
+    case 8: return launch_cfg<T, I, Cfg<VEC, 8, 8, 4, false, false, false, false, false, false>>(L);
+    case 16:
+      if constexpr (VEC == 1 && sizeof(T) == 4)
+        return launch_cfg<T, I, Cfg<1, 16, 16, 4, false, false, false, false, false, false>>(L);
+      return launch_cfg<T, I, Cfg<VEC, 16, 8, 4, false, false, false, false, false, false>>(L);
+    case 32:
+      return nt ? launch_cfg<T, I, Cfg<VEC, 32, 8, 4, true, false, false, false, false, false>>(L)
+                : launch_cfg<T, I, Cfg<VEC, 32, 8, 4, false, false, false, false, false, false>>(L);
+    case 64:
+      return nt ? launch_cfg<T, I, Cfg<VEC, 64, 8, 4, true, false, false, false, false, false>>(L)
+                : launch_cfg<T, I, Cfg<VEC, 64, 8, 4, false, false, false, false, false, false>>(L);
+    default: return fail(OFX_EINVAL, "spmm_csr: unsupported lanes-per-row %d", lpr);
+  }
+}
+
 template <typename T, typename I, int VEC>
 int launch_vec(const Launch& L, int lpr, bool nt) {
   const int v = L.sched.variant;
+  if (!buffer_rows_ok<T>(L)) {
+    OFX_REQUIRE(v == 0 || v == kForceBigVariant || (v > 0 && v < 10000), OFX_EINVAL,
+                "spmm_csr: variant %d needs B under 4 GiB (k=%lld, ldb=%lld)", v,
+                (long long)L.b_rows, (long long)L.ldb);
+    return launch_vec_global<T, I, VEC>(L, lpr, nt);
+  }
   if (v == kForceSmallVariant || (v == 0 && use_small_form(L.nrows, L.nnz_est, L.n, L.sched)))
     return launch_vec_small<T, I, VEC>(L, lpr);
   if (v == kForceMidSmallVariant) return launch_vec_mid<T, I, VEC, true>(L, lpr);
   if (v == kForceMidVariant) return launch_vec_mid<T, I, VEC, false>(L, lpr);
-  if (v == kForceWaveVariant) return launch_vec_wave<T, I, VEC>(L, lpr);
+  if (v == kForceWaveVariant) return launch_vec_pf<T, I, VEC, true>(L, lpr);
+  if (v == kForcePrefetchVariant) return launch_vec_pf<T, I, VEC, false>(L, lpr);
   // light rows of the mid form: the prefetching small-launch configuration above N = 16 (5-12%
   // faster at N = 64 / 128 on 20k-170k-row power-law graphs), the big-launch one at N <= 16
   // (profiles/r02n_probe_mid.json)
   if (v == 0 && use_mid_form(L.nrows, L.nnz_est, L.n, L.sched)) {
     return L.n > 16 ? launch_vec_mid<T, I, VEC, true>(L, lpr) : launch_vec_mid<T, I, VEC, false>(L, lpr);
   }
-  // forced variants (tests, tuning) keep the U = 8 configurations at every size
-  if (L.nrows <= kSmallRows && v == 0 && !nt) return launch_vec_small<T, I, VEC>(L, lpr);
+  // prefetching form: wave items at 16 < N <= 64 only (profiles/r03d_probe_forms.jsonl: at N = 16
+  // they cost more than they save, arxiv-shaped 206 against 96 us; at N = 32 / 64 they win or tie,
+  // 100 / 124 against 155 / 135 us; at N = 128 the form without them is 4-8% faster)
+  if (v == 0 && use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched))
+    return (L.n > 16 && L.n <= 64) ? launch_vec_pf<T, I, VEC, true>(L, lpr)
+                                   : launch_vec_pf<T, I, VEC, false>(L, lpr);
+  // the bandwidth configuration (forced variants keep it at every size)
   switch (lpr) {
     case 4: return launch_cfg<T, I, Cfg<VEC, 4>>(L);
     case 8: return launch_cfg<T, I, Cfg<VEC, 8>>(L);
@@ -1166,7 +1291,11 @@ int launch_vec(const Launch& L, int lpr, bool nt) {
 template <typename T, typename I>
 int launch_typed(const Launch& L) {
   const bool form = is_form_variant(L.sched.variant);  // auto configuration, forced form
-  if (L.sched.variant >= 10000 && !form) return launch_tuned<T, I>(L, L.sched.variant - 10000);
+  if (L.sched.variant >= 10000 && !form) {
+    OFX_REQUIRE(buffer_rows_ok<T>(L), OFX_EINVAL,
+                "spmm_csr: tuning variant %d needs B under 4 GiB", L.sched.variant);
+    return launch_tuned<T, I>(L, L.sched.variant - 10000);
+  }
   // variant = VEC * 100 + LPR forces a configuration (tuning / tests); 0 = auto.
   const int forced_vec = (L.sched.variant > 0 && !form) ? L.sched.variant / 100 : 0;
   const int forced_lpr = (L.sched.variant > 0 && !form) ? L.sched.variant % 100 : 0;

@@ -37,27 +37,39 @@ inline int64_t launch_nnz(int64_t m, int64_t nrows, int64_t nnz) {
   return (int64_t)((__int128)nnz * nrows / m);
 }
 
-// Small form (spmm_small_kernel): one launch when the launch has at most kSmallRows rows and at
-// most kSmallFormElems products (nnz * n).  Its longest row then costs at most that many products
-// of one block's in-order adds, against the planned form's three planning launches + reduce.
-// A fixed function of (rows, nnz, n, variant): the workspace query and the launch agree.
+// Which form a launch takes is a fixed function of (rows, estimated nnz, n, variant), so the
+// workspace query, the plan-once entry and the launch agree.  The thresholds are counts, set from
+// the round-3 forms sweep over power-law graphs of 89k-124M nonzeros at N = 16-128 (every form
+// forced on every graph, same box; profiles/r03b_probe_forms.jsonl, DESIGN.md §3 "Forms"), and a
+// GPU test runs each rule on both sides of its threshold.
+//
+// Small form (spmm_small_kernel): one launch when the launch has at most kSmallRows rows, at most
+// kSmallFormNnz nonzeros and at most kSmallFormElems products (nnz * n).  A block adds its long
+// rows one after another, so the form pays for a long row with a serial chain; the nonzero cap
+// keeps the power-law maximum degree small (PubMed-shaped, 89k nonzeros: 18.7 / 22.6 / 27.8 us at
+// N = 16 / 32 / 64 against 24-31 us planned; 20k rows with 400k nonzeros and a 5,065-nonzero row:
+// 54 us against 38 us in the mid form).
 constexpr int64_t kSmallRows = 32768;
-constexpr int64_t kSmallFormElems = int64_t(1) << 20;
+constexpr int64_t kSmallFormNnz = int64_t(1) << 17;
+constexpr int64_t kSmallFormElems = int64_t(1) << 23;
 constexpr int kSmallLight = 2;  // rows of more than kSmallLight * U nonzeros take the whole block
 constexpr int kForceSmallVariant = 30000;  // tuning: the small form at any size (probes only)
 
 inline bool use_small_form(int64_t nrows, int64_t nnz, int64_t n, const Schedule& s) {
   if (s.variant == kForceSmallVariant) return true;
-  return s.variant == 0 && nrows <= kSmallRows && nnz <= kSmallFormElems / (n > 0 ? n : 1);
+  return s.variant == 0 && nrows <= kSmallRows && nnz <= kSmallFormNnz &&
+         nnz <= kSmallFormElems / (n > 0 ? n : 1);
 }
 
-// Mid form (spmm_main_kernel with block items): launches above the small form and at most
-// kMidFormElems products.  Such a launch is short enough that its longest item sets its time:
-// a hub chunk or a long row summed by one lane-group is a chain of len / U dependent load rounds
-// (arxiv-shaped at N=16: a 7k-nonzero row held the launch at 600 us, profiles/r02j_probe_mid.json).
-// In the mid form every hub chunk and every row above the heavy threshold (the plan's bin 0,
-// at least kBlockItemMin nonzeros) is taken by a whole block (block_accumulate, the small form's
-// engine); the other rows keep one lane-group each.  Bits are unchanged: only who adds changes.
+// Mid form (spmm_main_kernel with block items): launches of at most kSmallRows rows above the small
+// form and at most kMidFormElems products.  Every hub chunk and every row above the heavy threshold
+// (the plan's bin 0, at least kBlockItemMin nonzeros) is taken by a whole block (block_accumulate,
+// the small form's engine); the other rows keep one lane-group each.  Bits are unchanged: only who
+// adds changes.  Few rows means few lane-groups, so a long row summed by one group would hold the
+// launch (20k rows, 400k nonzeros: 38-51 us here against 53-91 us with wave items and 88-147 us
+// in the bandwidth configuration).  With more rows the block items' LDS (33-41 KB per block, on
+// every block of the launch) costs more than it saves (arxiv-shaped, 169k rows: 112 us at N = 16
+// against 78 us in the prefetching form).
 constexpr int64_t kMidFormElems = int64_t(1) << 28;
 constexpr int64_t kBlockItemMin = 64;
 constexpr int kForceMidVariant = 30001;       // tuning: mid form at any size, big-launch rows
@@ -65,18 +77,33 @@ constexpr int kForceMidSmallVariant = 30002;  // tuning: mid form, small-launch 
 
 inline bool use_mid_form(int64_t nrows, int64_t nnz, int64_t n, const Schedule& s) {
   if (s.variant == kForceMidVariant || s.variant == kForceMidSmallVariant) return true;
-  return s.variant == 0 && !use_small_form(nrows, nnz, n, s) &&
+  return s.variant == 0 && nrows <= kSmallRows && !use_small_form(nrows, nnz, n, s) &&
          nnz <= kMidFormElems / (n > 0 ? n : 1);
 }
 
+// Prefetching form (planned, U = 32 / 16 loads in flight per lane with the next (col, val) batch
+// loaded during the current one; above N = 16 hub chunks and heavy rows take a whole wave):
+// launches of more rows than the mid form and at most kPrefetchNnz nonzeros.  Such a launch is
+// too short for its traffic to hide the chains of its longest items, so more loads in flight per
+// chain win; past it, the bandwidth configuration's occupancy wins.  Measured crossover between
+// 2M nonzeros (prefetching 73 / 93 / 118 / 160 us at N = 16 / 32 / 64 / 128 against 109 / 172 /
+// 165 / 195 us) and 5M (149 / 209 / 274 / 391 us against 118 / 188 / 217 / 353 us).
+constexpr int64_t kPrefetchNnz = int64_t(3) << 20;
+
+inline bool use_prefetch_form(int64_t nrows, int64_t nnz, int64_t n, const Schedule& s) {
+  return s.variant == 0 && !use_small_form(nrows, nnz, n, s) && !use_mid_form(nrows, nnz, n, s) &&
+         nnz <= kPrefetchNnz;
+}
+
 constexpr int kForceBigVariant = 30003;   // tuning: the planned big form, bandwidth configuration
-constexpr int kForceWaveVariant = 30004;  // tuning: the planned form with wave items (U=32, PF)
+constexpr int kForceWaveVariant = 30004;  // tuning: the prefetching form with wave items
+constexpr int kForcePrefetchVariant = 30005;  // tuning: the prefetching form without wave items
 
 // Tuning variants that force a form (small / mid / big / wave) but keep the automatic
 // configuration.
 inline bool is_form_variant(int v) {
   return v == kForceSmallVariant || v == kForceMidVariant || v == kForceMidSmallVariant ||
-         v == kForceBigVariant || v == kForceWaveVariant;
+         v == kForceBigVariant || v == kForceWaveVariant || v == kForcePrefetchVariant;
 }
 
 // The schedule a launch of `nrows` rows runs with: the mid form always plans (binned work list)

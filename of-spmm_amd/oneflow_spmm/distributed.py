@@ -217,6 +217,7 @@ class GridPlan:
         self.c_grp = torch.empty((sub, m_g, w), dtype=dt, device=dev)
         self.recv_c = torch.empty((sub, cn, m_r, w), dtype=dt, device=dev)
         self.csr = (row_ptr, col_idx, values)
+        self.nnz_group = int(row_ptr[self.ghi]) - int(row_ptr[self.glo])  # the model's SpMM bytes
         peer = [p != r for p in range(G)]
         mate = [p != r and p // cn == self.g for p in range(G)]
         m_of = lambda p: self.m_rng[p][1] - self.m_rng[p][0]  # noqa: E731
@@ -838,16 +839,61 @@ class RowSplitSpmm:
         return self.compute(row_ptr, cols["allgather"], values, out)
 
     # -- schedule choice -------------------------------------------------------------------------
-    def tune(self, out, pipelines=(1, 2, 4), reps: int = 3, force: bool = False) -> dict:
+    # A-priori model of one step per exchange candidate: bytes this rank receives
+    # at R_X plus the local SpMM's gather-model bytes at R_HBM (B rows of fewer than 128 B cost a
+    # whole 128-B line, "Narrow rows"); with D pipeline blocks / sub-blocks the two overlap:
+    # max(x, s) + min(x, s) / D.  R_X is an xGMI assumption (RCCL reaching 300 GB/s of ingress per
+    # GPU over 7 links of ~153 GB/s); `tune` refits it to the first measured candidate before it
+    # prunes.
+    R_X = 300e9
+    R_HBM = 6.0e12
+
+    def _spmm_bytes(self, rows, nnz, w, blocks=1):
+        e = torch.empty(0, dtype=self.dtype).element_size()
+        return blocks * (4 * (rows + 1) + (4 + e) * nnz + max(e * w, 128) * nnz + e * rows * w)
+
+    def _candidate_model(self, name, chunks):
+        """(bytes received per step, local SpMM bytes, overlap depth) of a candidate."""
+        e = torch.empty(0, dtype=self.dtype).element_size()
+        rows = self.row_range[1] - self.row_range[0]
+        if name in self.grids:
+            gp = self.grids[name]
+            b_el, c_el = gp.exchange_rows()
+            return ((b_el + c_el) * e, self._spmm_bytes(gp.ghi - gp.glo, gp.nnz_group, gp.w, gp.sub),
+                    gp.sub)
+        if name == "halo":
+            recv = self.halo.halo_rows * self.n * e
+        else:
+            recv = (self.k_padded - self.pad) * self.n * e
+        return recv, self._spmm_bytes(rows, self.nnz_local, self.n // chunks, chunks), chunks
+
+    @staticmethod
+    def _model_ms(recv, spmm, depth, r_x, r_h):
+        x, t = recv / r_x * 1e3, spmm / r_h * 1e3
+        return x + t if depth <= 1 else max(x, t) + min(x, t) / depth
+
+    def tune(self, out, pipelines=(1, 2, 4), reps: int = 3, force: bool = False,
+             budget_s: float | None = None, prune: float = 3.0,
+             first: tuple = ("grid2x4/s2",)) -> dict:
         """Times every exchange on this node with the real step over the bound CSR: all-gather
         (ring / point-to-point) x pipeline depth, the halo exchange and the grid plans if built.
         Keeps the fastest.  Timings are max-reduced over ranks, so all ranks choose the same; every
-        candidate produces the same bytes.  Returns {"<comm>/p<C>" | "halo" | "nsplit[/s<S>]" |
-        "grid<R>x<C>[/s<S>]": ms}.  One rank has nothing to exchange, so it keeps its setting unless
-        `force` (tests).  With torch.distributed as the transport (gloo on CPU, the tests) the
-        all-gather candidates are its collectives and the clock is the host's."""
+        candidate produces the same bytes.  Returns {"<comm>/p<C>" | "halo[/p<C>]" | "nsplit[/s<S>]"
+        | "grid<R>x<C>[/s<S>]": ms} of the candidates measured.
+
+        Order and bounds (so the first 8-GPU run ends in bounded time): the candidates named in
+        `first` (the 2x4 grid with sub-block overlap, DESIGN.md §4's expected best at 8 GPUs), then
+        the rest in ascending model time (_model_ms).  After the first measurement R_X is refitted
+        to it; a candidate whose refitted model time exceeds `prune` x the best measured time is
+        skipped, and once `budget_s` seconds have passed (max over ranks) the rest are skipped.
+        Every decision uses max-reduced values, so all ranks take the same path.  The record is in
+        `self.tune_report`: per candidate the model time, the measured time and the status.
+        One rank has nothing to exchange, so it keeps its setting unless `force` (tests).  With
+        torch.distributed as the transport (gloo on CPU, the tests) the all-gather candidates are
+        its collectives and the clock is the host's."""
         if self._bound is None:
             raise RuntimeError("tune: bind() the CSR first")
+        self.tune_report = {}
         if self.world == 1 and not force:
             return {}
         native = self.comm_kind.startswith("rccl")
@@ -855,6 +901,11 @@ class RowSplitSpmm:
         base = "rccl" if native else "torch"
         on_gpu = self.device.type == "cuda"
         red_dev = self.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+
+        def max_over_ranks(v: float) -> float:
+            t = torch.tensor([v], dtype=torch.float64, device=red_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            return float(t.item())
 
         def measure():
             # A candidate that raises on any rank (a host-side error, deterministic across ranks)
@@ -879,33 +930,81 @@ class RowSplitSpmm:
                     ms = (time.perf_counter() - t0) * 1e3 / reps
             except Exception as e:  # noqa: BLE001 -- reported, candidate dropped
                 self.tune_errors[f"{self.exchange}/{self.comm_kind}/p{self.chunks}"] = repr(e)
-            t = torch.tensor([ms], dtype=torch.float64, device=red_dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-            return float(t.item())
+            return max_over_ranks(ms)
+
+        # the candidates: (name, setter)
+        cands = []
+        for chunks in pipelines:
+            if self.n % chunks == 0:
+                for kind in kinds:
+                    def ag(chunks=chunks, kind=kind):
+                        self.exchange = "allgather"
+                        self.set_pipeline(chunks)
+                        self.comm_kind = kind
+                    cands.append((f"{kind}/p{chunks}", ag, "allgather", chunks))
+        if self.halo is not None:
+            for chunks in pipelines:
+                if self.n % chunks == 0:
+                    def hl(chunks=chunks):
+                        self.set_pipeline(1)
+                        self.set_halo_pipeline(chunks)
+                        self.exchange, self.comm_kind = "halo", base
+                    cands.append(("halo" if chunks == 1 else f"halo/p{chunks}", hl, "halo", chunks))
+        for name in self.grids:
+            def gr(name=name):
+                self.set_pipeline(1)
+                self.exchange, self.comm_kind = name, base
+            cands.append((name, gr, name, 1))
+        # the model inputs of every candidate, max-reduced over ranks: the order and every skip
+        # decision below are then the same on all ranks (their collectives stay matched)
+        model = {c[0]: self._candidate_model(c[2], c[3]) for c in cands}
+        names = sorted(model)
+        mt = torch.tensor([[model[nm][0], model[nm][1]] for nm in names], dtype=torch.float64,
+                          device=red_dev)
+        dist.all_reduce(mt, op=dist.ReduceOp.MAX, group=self.group)
+        model = {nm: (float(mt[i, 0]), float(mt[i, 1]), model[nm][2]) for i, nm in enumerate(names)}
+        prior = {nm: self._model_ms(*model[nm], self.R_X, self.R_HBM) for nm in model}
+        cands.sort(key=lambda c: (c[0] not in first, prior[c[0]], c[0]))
 
         times = {}
         self.tune_errors = {}
-        self.exchange = "allgather"
-        for chunks in pipelines:
-            if self.n % chunks:
+        r_x = self.R_X
+        t_start = time.perf_counter()
+        for name, setter, _, _ in cands:
+            rec = {"predicted_ms": round(prior[name], 4), "recv_mb": round(model[name][0] / 1e6, 2),
+                   "spmm_mb": round(model[name][1] / 1e6, 2)}
+            self.tune_report[name] = rec
+            best = min(times.values()) if times else float("inf")
+            fitted = self._model_ms(*model[name], r_x, self.R_HBM)
+            rec["refit_predicted_ms"] = round(fitted, 4)
+            if (budget_s is not None and times
+                    and max_over_ranks(time.perf_counter() - t_start) > budget_s):
+                rec["status"] = "skipped: budget"
                 continue
-            self.set_pipeline(chunks)
-            for kind in kinds:
-                self.comm_kind = kind
-                times[f"{kind}/p{chunks}"] = measure()
-        if self.halo is not None:
-            for chunks in pipelines:
-                if self.n % chunks:
-                    continue
-                self.set_halo_pipeline(chunks)
-                self.exchange, self.comm_kind = "halo", base
-                times["halo" if chunks == 1 else f"halo/p{chunks}"] = measure()
-        for name in self.grids:
-            self.exchange, self.comm_kind = name, base
-            times[name] = measure()
-        best = min(times, key=times.get)
-        if not math.isfinite(times[best]):
+            if math.isfinite(best) and fitted > prune * best:
+                rec["status"] = "skipped: model"
+                continue
+            setter()
+            ms = measure()
+            rec["measured_ms"] = round(ms, 4) if math.isfinite(ms) else None
+            rec["status"] = "measured" if math.isfinite(ms) else "error"
+            if math.isfinite(ms):
+                times[name] = ms
+                if len(times) == 1:  # refit the exchange rate to the first measurement
+                    recv, spmm, depth = model[name]
+                    t_ms = spmm / self.R_HBM * 1e3
+                    if depth <= 1:
+                        x_ms = ms - t_ms
+                    elif ms - t_ms / depth >= t_ms:  # exchange-bound: ms = x + t / D
+                        x_ms = ms - t_ms / depth
+                    else:  # SpMM-bound: ms = t + x / D
+                        x_ms = depth * (ms - t_ms)
+                    if recv > 0 and x_ms > 0:
+                        r_x = recv / (x_ms * 1e-3)
+        self.tune_rate_fit = r_x
+        if not times:
             raise RuntimeError(f"RowSplitSpmm.tune: every exchange failed: {self.tune_errors}")
+        best = min(times, key=times.get)
         if self.halo is not None:
             self.set_halo_pipeline(int(best.split("/p")[1]) if best.startswith("halo/p") else 1)
         if best.startswith("halo"):

@@ -28,6 +28,8 @@ CONFIGS = {
 # row_ptr offsets and every nonzero position past 2^31 need 64-bit indices end to end).
 EXTRA_CONFIGS = {
     "int64_max": dict(m=40_000_000, k=40_000_000, nnz=2_300_000_000, n=16, dtype=torch.float32),
+    # the CPU rehearsal of the multi-rank bench path (bench.py --device cpu, tests)
+    "tiny": dict(m=20_000, k=20_000, nnz=200_000, n=32, dtype=torch.float32),
 }
 
 

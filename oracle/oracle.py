@@ -40,10 +40,11 @@ def lib():
     if _LIB is None:
         _LIB = ctypes.CDLL(build())
         i64, p, c_int = ctypes.c_int64, ctypes.c_void_p, ctypes.c_int
-        _LIB.orc_spmm_f64.argtypes = [i64, i64, i64, p, p, p, p, i64, p, i64, i64, i64, i64, i64, c_int]
-        _LIB.orc_spmm_f32.argtypes = _LIB.orc_spmm_f64.argtypes + [c_int]
+        base = [i64, i64, i64, p, p, p, p, i64, p, i64, i64, i64, i64, i64, c_int]
+        _LIB.orc_spmm_f64.argtypes = base + [c_int]  # + neg_zero
+        _LIB.orc_spmm_f32.argtypes = base + [c_int, c_int]  # + round16, neg_zero
         _LIB.orc_round16.argtypes = [p, i64, c_int]
-        _LIB.orc_spmm_f32_ref64.argtypes = [i64, p, p, p, p, i64, p, p, i64, i64, c_int]
+        _LIB.orc_spmm_f32_ref64.argtypes = [i64, p, p, p, p, i64, p, p, i64, i64, c_int, i64]
         _LIB.orc_balanced_range.argtypes = [i64, i64, i64, ctypes.POINTER(i64), ctypes.POINTER(i64)]
     return _LIB
 
@@ -103,9 +104,12 @@ def _p(a):
 
 
 def spmm(row_ptr, col_idx, values, b, *, dtype="f32", row_begin=0, row_end=None, split=0, chunk=0,
-         ordered=False, nthreads=None, k=None):
+         ordered=False, nthreads=None, k=None, negative="error"):
     """Oracle SpMM.  dtype in {"f32","f64","bf16","f16"}; bf16 arrays are uint16 bit patterns.
-    Returns C rows [row_begin, row_end) in the storage dtype (bf16 -> uint16 bits)."""
+    Returns C rows [row_begin, row_end) in the storage dtype (bf16 -> uint16 bits).
+    A column >= k gathers a zero-filled row (gather_kernel_util.cpp:84-89: the nonzero adds
+    val * 0).  A negative column raises (the CPU gather's CHECK_GE, :80) unless
+    negative="zero": the CUDA gather's semantics (gather_kernel_util.cu:36), the device kernel's."""
     m = len(row_ptr) - 1
     row_end = m if row_end is None else row_end
     n = b.shape[1]
@@ -120,7 +124,7 @@ def spmm(row_ptr, col_idx, values, b, *, dtype="f32", row_begin=0, row_end=None,
         bb = np.ascontiguousarray(b, dtype=np.float64)
         out = np.zeros((rows, n), dtype=np.float64)
         rc = lib().orc_spmm_f64(m, k, n, _p(rp), _p(ci), _p(v), _p(bb), n, _p(out), n,
-                                row_begin, row_end, s, c, nt)
+                                row_begin, row_end, s, c, nt, int(negative == "zero"))
     else:
         if dtype == "bf16":
             v, bb = bf16_bits_to_f32(np.asarray(values)), bf16_bits_to_f32(np.asarray(b))
@@ -130,9 +134,10 @@ def spmm(row_ptr, col_idx, values, b, *, dtype="f32", row_begin=0, row_end=None,
         v, bb = np.ascontiguousarray(v), np.ascontiguousarray(bb)
         out = np.zeros((rows, n), dtype=np.float32)
         rc = lib().orc_spmm_f32(m, k, n, _p(rp), _p(ci), _p(v), _p(bb), n, _p(out), n,
-                                row_begin, row_end, s, c, nt, _ROUND16.get(dtype, 0))
+                                row_begin, row_end, s, c, nt, _ROUND16.get(dtype, 0),
+                                int(negative == "zero"))
     if rc != 0:
-        raise ValueError("oracle: column index out of range")
+        raise ValueError("oracle: negative column index (CHECK_GE(idx, 0))")
     if dtype == "bf16":
         return f32_to_bf16_bits(out)
     if dtype == "f16":
@@ -209,7 +214,8 @@ def relu_bias_grad(y, dy, *, relu: bool, dtype="f32"):
 
 
 def ref64(row_ptr, col_idx, values_f32, b_f32, *, row_begin=0, row_end=None, nthreads=None):
-    """fp64 product C64 and |.|-sum bound of an fp32 (or upcast 16-bit) problem."""
+    """fp64 product C64 and |.|-sum bound of an fp32 (or upcast 16-bit) problem (columns outside
+    [0, K) gather a zero row)."""
     m = len(row_ptr) - 1
     row_end = m if row_end is None else row_end
     n = b_f32.shape[1]
@@ -221,7 +227,7 @@ def ref64(row_ptr, col_idx, values_f32, b_f32, *, row_begin=0, row_end=None, nth
     c64 = np.zeros((rows, n))
     ab = np.zeros((rows, n))
     lib().orc_spmm_f32_ref64(n, _p(rp), _p(ci), _p(v), _p(bb), n, _p(c64), _p(ab), row_begin,
-                             row_end, nthreads or min(os.cpu_count() or 1, 16))
+                             row_end, nthreads or min(os.cpu_count() or 1, 16), bb.shape[0])
     return c64, ab
 
 
@@ -238,14 +244,15 @@ def _lib_sddmm():
     L = lib()
     if not getattr(L, "_sddmm_set", False):
         i64, p, c_int = ctypes.c_int64, ctypes.c_void_p, ctypes.c_int
-        L.orc_sddmm_f32.argtypes = [i64, p, p, p, i64, p, i64, p, i64, i64, c_int]
+        L.orc_sddmm_f32.argtypes = [i64, p, p, p, i64, p, i64, p, i64, i64, c_int, i64]
         L.orc_sddmm_f64.argtypes = L.orc_sddmm_f32.argtypes
         L._sddmm_set = True
     return L
 
 
 def sddmm(row_ptr, col_idx, a, b, *, dtype="f32", row_begin=0, row_end=None, nthreads=None):
-    """out[j] = <a[row(j)-row_begin], b[col[j]]> in the operator's pairwise-leaf order.
+    """out[j] = <a[row(j)-row_begin], b[col[j]]> in the operator's pairwise-leaf order (a column
+    outside [0, K) reads the forward's zero-filled row).
     a holds rows [row_begin, row_end); bf16 arrays are uint16 bit patterns."""
     m = len(row_ptr) - 1
     row_end = m if row_end is None else row_end
@@ -259,7 +266,7 @@ def sddmm(row_ptr, col_idx, a, b, *, dtype="f32", row_begin=0, row_end=None, nth
         bb = np.ascontiguousarray(b, dtype=np.float64)
         out = np.zeros(nnz, dtype=np.float64)
         _lib_sddmm().orc_sddmm_f64(n, _p(rp), _p(ci), _p(aa), n, _p(bb), n, _p(out), row_begin,
-                                   row_end, nt)
+                                   row_end, nt, bb.shape[0])
         return out
     if dtype == "bf16":
         aa, bb = bf16_bits_to_f32(np.asarray(a)), bf16_bits_to_f32(np.asarray(b))
@@ -267,7 +274,8 @@ def sddmm(row_ptr, col_idx, a, b, *, dtype="f32", row_begin=0, row_end=None, nth
         aa, bb = np.asarray(a).astype(np.float32), np.asarray(b).astype(np.float32)
     aa, bb = np.ascontiguousarray(aa), np.ascontiguousarray(bb)
     out = np.zeros(nnz, dtype=np.float32)
-    _lib_sddmm().orc_sddmm_f32(n, _p(rp), _p(ci), _p(aa), n, _p(bb), n, _p(out), row_begin, row_end, nt)
+    _lib_sddmm().orc_sddmm_f32(n, _p(rp), _p(ci), _p(aa), n, _p(bb), n, _p(out), row_begin, row_end, nt,
+                               bb.shape[0])
     if dtype == "bf16":
         return f32_to_bf16_bits(out)
     if dtype == "f16":
@@ -277,13 +285,16 @@ def sddmm(row_ptr, col_idx, a, b, *, dtype="f32", row_begin=0, row_end=None, nth
 
 def transpose(row_ptr, col_idx, k):
     """CSR -> CSR of the transpose by a stable sort on the column (entries of each new row keep
-    ascending original row order).  Returns (row_ptr_T, col_idx_T = original rows, perm)."""
+    ascending original row order).  Returns (row_ptr_T, col_idx_T = original rows, perm).
+    A column outside [0, k) sorts as k: after row_ptr_T[k], in no row (the forward's zero-filled
+    gather reads no row of b, so d b gets nothing from it)."""
     rp = np.asarray(row_ptr, dtype=np.int64)
     ci = np.asarray(col_idx, dtype=np.int64)
     rows = np.repeat(np.arange(len(rp) - 1, dtype=np.int64), np.diff(rp))
-    perm = np.argsort(ci, kind="stable")
+    key = np.where((ci >= 0) & (ci < k), ci, k)
+    perm = np.argsort(key, kind="stable")
     rp_t = np.zeros(k + 1, dtype=np.int64)
-    rp_t[1:] = np.cumsum(np.bincount(ci, minlength=k))
+    rp_t[1:] = np.cumsum(np.bincount(key, minlength=k + 1)[:k])
     return rp_t, rows[perm], perm
 
 

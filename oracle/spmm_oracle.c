@@ -9,7 +9,10 @@
  * torch.sparse_csr in tests/golden/make_golden.py:
  *
  *   gather     oneflow/user/kernels/gather_kernel_util.cpp:72-92
- *              out[i,:] = in[idx[i],:]   (CHECK_GE(idx, 0); rows outside the shard zero-filled)
+ *              out[i,:] = in[idx[i],:]   (CHECK_GE(idx, 0) -> error here; an index >= the table
+ *              size gathers a zero-filled row, :84-89, so its nonzero adds val * 0.  The CUDA
+ *              gather, gather_kernel_util.cu:36, zero-fills negative indices too: orc_* take
+ *              `neg_zero` = 1 for that semantics, the device kernel's)
  *   multiply   elementwise val[i] * out[i,:]  (one fp rounding)
  *   segsum     oneflow/user/kernels/unsorted_segment_sum_kernel_util.cpp:29-45
  *              out zero-filled (Memset, unsorted_segment_sum_kernel.cpp:95-96), then for i in
@@ -25,6 +28,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #pragma GCC optimize("no-fast-math")
@@ -90,13 +94,16 @@ void orc_round16(float* x, int64_t n, int round16) {
   for (int64_t i = 0; i < n; ++i) x[i] = orc_mul(x[i], 1.0f, round16);
 }
 
+/* The gathered row of column c: B's row, or the zero-filled row of an index outside [0, k). */
+#define ORC_ROW(b, c, ldb, k, zero) (((uint64_t)(c) < (uint64_t)(k)) ? (b) + (c) * (ldb) : (zero))
+
 /* One segment [j0, j1) of row sums, f32 mul-then-add, from +0 (gather -> mul -> segsum). */
-static void seg_f32(const int64_t* col, const float* val, const float* b, int64_t ldb, int64_t n,
-                    int64_t j0, int64_t j1, float* acc, int round16) {
+static void seg_f32(const int64_t* col, const float* val, const float* b, int64_t ldb, int64_t k,
+                    const float* zero, int64_t n, int64_t j0, int64_t j1, float* acc, int round16) {
   for (int64_t c = 0; c < n; ++c) acc[c] = 0.0f;
   if (round16 == ORC_R_NONE) { /* fp32: a branch-free loop the compiler vectorises over c */
     for (int64_t j = j0; j < j1; ++j) {
-      const float* from = b + col[j] * ldb; /* gather */
+      const float* from = ORC_ROW(b, col[j], ldb, k, zero); /* gather */
       const float v = val[j];
       for (int64_t c = 0; c < n; ++c) {
         const float prod = v * from[c]; /* multiply (rounded; built -ffp-contract=off) */
@@ -107,7 +114,7 @@ static void seg_f32(const int64_t* col, const float* val, const float* b, int64_
   }
   if (round16 == ORC_R_BF16) { /* the same rounding as orc_round_bf16, written as a select */
     for (int64_t j = j0; j < j1; ++j) {
-      const float* from = b + col[j] * ldb;
+      const float* from = ORC_ROW(b, col[j], ldb, k, zero);
       const float v = val[j];
       for (int64_t c = 0; c < n; ++c) {
         const float p = v * from[c];
@@ -124,7 +131,7 @@ static void seg_f32(const int64_t* col, const float* val, const float* b, int64_
     return;
   }
   for (int64_t j = j0; j < j1; ++j) {
-    const float* from = b + col[j] * ldb; /* gather */
+    const float* from = ORC_ROW(b, col[j], ldb, k, zero); /* gather */
     for (int64_t c = 0; c < n; ++c) {
       const float prod = orc_mul(val[j], from[c], round16); /* multiply, stored in T */
       acc[c] = acc[c] + prod;                                /* segment-sum */
@@ -133,10 +140,10 @@ static void seg_f32(const int64_t* col, const float* val, const float* b, int64_
 }
 
 static void seg_f64(const int64_t* col, const double* val, const double* b, int64_t ldb,
-                    int64_t n, int64_t j0, int64_t j1, double* acc) {
+                    int64_t k, const double* zero, int64_t n, int64_t j0, int64_t j1, double* acc) {
   for (int64_t c = 0; c < n; ++c) acc[c] = 0.0;
   for (int64_t j = j0; j < j1; ++j) {
-    const double* from = b + col[j] * ldb;
+    const double* from = ORC_ROW(b, col[j], ldb, k, zero);
     for (int64_t c = 0; c < n; ++c) {
       const double prod = val[j] * from[c];
       acc[c] = acc[c] + prod;
@@ -145,16 +152,18 @@ static void seg_f64(const int64_t* col, const double* val, const double* b, int6
 }
 
 /* C (rows [row_begin,row_end), written from C[0]) = A @ B in f32 with the given schedule.
- * Returns 0, or -1 on an out-of-range column (the reference's CHECK_GE / bounds). */
+ * Returns 0, or -1 on a negative column (the reference's CHECK_GE) unless neg_zero; a column
+ * >= k gathers a zero row. */
 int orc_spmm_f32(int64_t m, int64_t k, int64_t n, const int64_t* rp, const int64_t* col,
                  const float* val, const float* b, int64_t ldb, float* c, int64_t ldc,
                  int64_t row_begin, int64_t row_end, int64_t split, int64_t chunk,
-                 int nthreads, int round16) {
-  int bad = 0;
+                 int nthreads, int round16, int neg_zero) {
   (void)m;
-  for (int64_t j = rp[row_begin]; j < rp[row_end]; ++j)
-    if (col[j] < 0 || col[j] >= k) bad = 1;
-  if (bad) return -1;
+  if (!neg_zero)
+    for (int64_t j = rp[row_begin]; j < rp[row_end]; ++j)
+      if (col[j] < 0) return -1;
+  float* zero = (float*)calloc((size_t)(n > 0 ? n : 1), sizeof(float));
+  if (!zero) return -2;
 #pragma omp parallel num_threads(nthreads)
   {
     float* part = (float*)__builtin_alloca(sizeof(float) * (n > 0 ? n : 1));
@@ -163,31 +172,33 @@ int orc_spmm_f32(int64_t m, int64_t k, int64_t n, const int64_t* rp, const int64
       float* out = c + (r - row_begin) * ldc;
       const int64_t j0 = rp[r], j1 = rp[r + 1], len = j1 - j0;
       if (len <= split) {
-        seg_f32(col, val, b, ldb, n, j0, j1, out, round16);
+        seg_f32(col, val, b, ldb, k, zero, n, j0, j1, out, round16);
       } else {
         const int64_t nc = len / chunk;
         for (int64_t x = 0; x < n; ++x) out[x] = 0.0f;
         for (int64_t q = 0; q < nc; ++q) {
           const int64_t a = j0 + q * chunk;
           const int64_t e = (q == nc - 1) ? j1 : a + chunk;
-          seg_f32(col, val, b, ldb, n, a, e, part, round16);
+          seg_f32(col, val, b, ldb, k, zero, n, a, e, part, round16);
           for (int64_t x = 0; x < n; ++x) out[x] = out[x] + part[x];
         }
       }
     }
   }
+  free(zero);
   return 0;
 }
 
 int orc_spmm_f64(int64_t m, int64_t k, int64_t n, const int64_t* rp, const int64_t* col,
                  const double* val, const double* b, int64_t ldb, double* c, int64_t ldc,
                  int64_t row_begin, int64_t row_end, int64_t split, int64_t chunk,
-                 int nthreads) {
-  int bad = 0;
+                 int nthreads, int neg_zero) {
   (void)m;
-  for (int64_t j = rp[row_begin]; j < rp[row_end]; ++j)
-    if (col[j] < 0 || col[j] >= k) bad = 1;
-  if (bad) return -1;
+  if (!neg_zero)
+    for (int64_t j = rp[row_begin]; j < rp[row_end]; ++j)
+      if (col[j] < 0) return -1;
+  double* zero = (double*)calloc((size_t)(n > 0 ? n : 1), sizeof(double));
+  if (!zero) return -2;
 #pragma omp parallel num_threads(nthreads)
   {
     double* part = (double*)__builtin_alloca(sizeof(double) * (n > 0 ? n : 1));
@@ -196,19 +207,20 @@ int orc_spmm_f64(int64_t m, int64_t k, int64_t n, const int64_t* rp, const int64
       double* out = c + (r - row_begin) * ldc;
       const int64_t j0 = rp[r], j1 = rp[r + 1], len = j1 - j0;
       if (len <= split) {
-        seg_f64(col, val, b, ldb, n, j0, j1, out);
+        seg_f64(col, val, b, ldb, k, zero, n, j0, j1, out);
       } else {
         const int64_t nc = len / chunk;
         for (int64_t x = 0; x < n; ++x) out[x] = 0.0;
         for (int64_t q = 0; q < nc; ++q) {
           const int64_t a = j0 + q * chunk;
           const int64_t e = (q == nc - 1) ? j1 : a + chunk;
-          seg_f64(col, val, b, ldb, n, a, e, part);
+          seg_f64(col, val, b, ldb, k, zero, n, a, e, part);
           for (int64_t x = 0; x < n; ++x) out[x] = out[x] + part[x];
         }
       }
     }
   }
+  free(zero);
   return 0;
 }
 
@@ -216,13 +228,14 @@ int orc_spmm_f64(int64_t m, int64_t k, int64_t n, const int64_t* rp, const int64
  * used by the tolerance check |C - C64| <= rtol * absum. */
 void orc_spmm_f32_ref64(int64_t n, const int64_t* rp, const int64_t* col, const float* val,
                         const float* b, int64_t ldb, double* c64, double* absum,
-                        int64_t row_begin, int64_t row_end, int nthreads) {
+                        int64_t row_begin, int64_t row_end, int nthreads, int64_t k) {
 #pragma omp parallel for schedule(dynamic, 64) num_threads(nthreads)
   for (int64_t r = row_begin; r < row_end; ++r) {
     double* o = c64 + (r - row_begin) * n;
     double* a = absum + (r - row_begin) * n;
     for (int64_t x = 0; x < n; ++x) o[x] = a[x] = 0.0;
     for (int64_t j = rp[r]; j < rp[r + 1]; ++j) {
+      if ((uint64_t)col[j] >= (uint64_t)k) continue; /* a zero-filled row: adds (+-)0 */
       const float* from = b + col[j] * ldb;
       for (int64_t x = 0; x < n; ++x) {
         o[x] += (double)val[j] * (double)from[x];
@@ -244,8 +257,10 @@ static int64_t pow2_at_least(int64_t x) {
 
 void orc_sddmm_f32(int64_t n, const int64_t* rp, const int64_t* col, const float* a, int64_t lda,
                    const float* b, int64_t ldb, float* out, int64_t row_begin, int64_t row_end,
-                   int nthreads) {
+                   int nthreads, int64_t k) {
   const int64_t leaves = (n + 7) / 8, padded = pow2_at_least(leaves);
+  float* zero = (float*)calloc((size_t)(n > 0 ? n : 1), sizeof(float));
+  if (!zero) return;
 #pragma omp parallel num_threads(nthreads)
   {
     float* leaf = (float*)__builtin_alloca(sizeof(float) * padded);
@@ -253,7 +268,7 @@ void orc_sddmm_f32(int64_t n, const int64_t* rp, const int64_t* col, const float
     for (int64_t r = row_begin; r < row_end; ++r) {
       const float* ar = a + (r - row_begin) * lda;
       for (int64_t j = rp[r]; j < rp[r + 1]; ++j) {
-        const float* br = b + col[j] * ldb;
+        const float* br = ORC_ROW(b, col[j], ldb, k, zero); /* the forward's gathered row */
         for (int64_t l = 0; l < padded; ++l) {
           float s = 0.0f;
           for (int64_t e = 8 * l; e < 8 * l + 8 && e < n; ++e) {
@@ -268,12 +283,15 @@ void orc_sddmm_f32(int64_t n, const int64_t* rp, const int64_t* col, const float
       }
     }
   }
+  free(zero);
 }
 
 void orc_sddmm_f64(int64_t n, const int64_t* rp, const int64_t* col, const double* a, int64_t lda,
                    const double* b, int64_t ldb, double* out, int64_t row_begin, int64_t row_end,
-                   int nthreads) {
+                   int nthreads, int64_t k) {
   const int64_t leaves = (n + 7) / 8, padded = pow2_at_least(leaves);
+  double* zero = (double*)calloc((size_t)(n > 0 ? n : 1), sizeof(double));
+  if (!zero) return;
 #pragma omp parallel num_threads(nthreads)
   {
     double* leaf = (double*)__builtin_alloca(sizeof(double) * padded);
@@ -281,7 +299,7 @@ void orc_sddmm_f64(int64_t n, const int64_t* rp, const int64_t* col, const doubl
     for (int64_t r = row_begin; r < row_end; ++r) {
       const double* ar = a + (r - row_begin) * lda;
       for (int64_t j = rp[r]; j < rp[r + 1]; ++j) {
-        const double* br = b + col[j] * ldb;
+        const double* br = ORC_ROW(b, col[j], ldb, k, zero);
         for (int64_t l = 0; l < padded; ++l) {
           double s = 0.0;
           for (int64_t e = 8 * l; e < 8 * l + 8 && e < n; ++e) {
@@ -296,4 +314,5 @@ void orc_sddmm_f64(int64_t n, const int64_t* rp, const int64_t* col, const doubl
       }
     }
   }
+  free(zero);
 }

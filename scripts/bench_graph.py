@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Eager op-layer calls vs one hipGraph replay (oneflow_spmm.SpmmGraph) for a two-layer GCN
-forward: fused_spmm(+bias, relu) then spmm, on a BASELINE-shaped graph.  Small graphs (Cora) are
-launch- and host-bound in eager mode; the graph removes the per-op host work.
+"""The compiled spmm_csr job (oneflow_spmm.ccl.SpmmJob, the nn.Graph form of one layer): eager
+runs against the job's native graph mode (ofx_spmm_job_set_graph: captured once through the
+device C-ABI's hipGraph executable, one graph launch per run), on a BASELINE-shaped graph; plus
+the eager two-layer GCN forward through the op layer for reference.
 
     python scripts/bench_graph.py [--config cora] [--iters 200]
 """
@@ -50,13 +51,8 @@ def main():
 
     with torch.no_grad():
         eager = per_iter_ms(lambda: gcn(x), args.iters)
-        g = fs.SpmmGraph(gcn, x)
-        replay = per_iter_ms(lambda: g.graph.replay(), args.iters)
-        same = bool(torch.equal(g.run(x).view(torch.uint8), gcn(x).view(torch.uint8)))
     print(json.dumps({"config": args.config, "m": m, "nnz": nnz, "n": n, "layers": 2,
-                      "eager_ms_per_forward": round(eager, 4),
-                      "graph_replay_ms_per_forward": round(replay, 4),
-                      "speedup": round(eager / replay, 2), "bitexact": same}))
+                      "eager_ms_per_forward": round(eager, 4)}))
 
     # one spmm_csr layer as the compiled job (the nn.Graph form): eager runs vs the job's own
     # graph mode (captured once through the C-ABI's hipGraph executable, one launch per run);

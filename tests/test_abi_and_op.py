@@ -228,11 +228,13 @@ def test_direct_abi_argument_checks():
     assert sz.value == 0  # every row is in the lightest degree bin: no plan, no workspace
     assert L.ofx_spmm_csr_workspace_size(5, 2, 10, 10, 128, 100000, None, ctypes.byref(sz)) == 0
     assert sz.value > 0
-    # the small form (one launch, no plan): <= 32768 rows and <= 2^20 products nnz * n
+    # the small form (one launch, no plan): <= 32768 rows, <= 2^17 nonzeros and <= 2^23
+    # products nnz * n (spmm_launch.h)
     for m, n, nnz, small in [(32768, 16, 65536, True), (32769, 16, 65536, False),
-                             (2708, 16, 10556, True), (2708, 64, 10556, True),
-                             (2708, 128, 10556, False), (1000, 300, 3495, True),
-                             (1000, 300, 3496, False)]:
+                             (2708, 16, 10556, True), (2708, 128, 10556, True),
+                             (19717, 64, 88648, True), (19717, 128, 88648, False),
+                             (20000, 16, 131072, True), (20000, 16, 131073, False),
+                             (1000, 300, 27962, True), (1000, 300, 27963, False)]:
         assert L.ofx_spmm_csr_workspace_size(5, 2, m, m, n, nnz, None, ctypes.byref(sz)) == 0
         assert (sz.value == 0) == small, (m, n, nnz)
     rc = L.ofx_spmm_csr(None, 5, 2, 4, 4, 4, 0, None, None, None, None, 4, None, 4, 3, 2, None, 0, None)

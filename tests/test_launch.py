@@ -103,3 +103,49 @@ def test_bench_multi_rank_rehearsal_on_one_gpu():
     assert line["config"]["parallelism"].startswith("REHEARSAL")
     assert len(line["extra"]["allgather_tune_ms"]) >= 5
 
+
+
+def _bench_line(p):
+    import json
+    assert p.returncode == 0, p.stderr[-3000:]
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+_SPAWN_ENV_DROP = ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")
+
+
+def test_bench_eight_rank_rehearsal_pinned_grid2x4_s2():
+    """the driver's 8-GPU bench path rehearsed with 8 ranks on the host
+    (self-spawn, gloo, RowSplitSpmm over host tensors with the kCPU kernel): --exchange
+    grid2x4/s2 is accepted and runs, every rank joins, one JSON line with the memory record."""
+    p = _bench(["--gpus", "8", "--backend", "gloo", "--device", "cpu", "--config", "tiny",
+                "--exchange", "grid2x4/s2", "--steps", "1", "--warmup", "0"],
+               {"OMP_NUM_THREADS": "1"}, drop=_SPAWN_ENV_DROP)
+    line = _bench_line(p)
+    assert line["n_gpus"] == 8 and line["extra"]["ranks_seen"] == 8
+    assert line["extra"]["exchange"] == "grid2x4/s2"
+    assert line["config"]["parallelism"].startswith("REHEARSAL")
+    assert line["extra"]["memory_gb"]["host_rss_peak_sum"] > 0
+    assert line["value"] > 0
+
+
+def test_bench_eight_rank_tune_is_ordered_and_bounded():
+    """tune() at 8 ranks: grid2x4/s2 is measured first, every candidate is reported with its model
+    time, and a zero budget stops after the first measurement (the rest 'skipped: budget')."""
+    p = _bench(["--gpus", "8", "--backend", "gloo", "--device", "cpu", "--config", "tiny",
+                "--steps", "1", "--warmup", "0", "--tune-budget", "0"],
+               {"OMP_NUM_THREADS": "1"}, drop=_SPAWN_ENV_DROP)
+    line = _bench_line(p)
+    cands = line["extra"]["tune_candidates"]
+    assert len(cands) >= 12  # 3 all-gather depths (gloo: one kind), 3 halo, 6 grids
+    assert all("predicted_ms" in c for c in cands.values())
+    measured = [k for k, c in cands.items() if c["status"] == "measured"]
+    assert measured == ["grid2x4/s2"]
+    assert all(c["status"] == "skipped: budget" for k, c in cands.items() if k != "grid2x4/s2")
+    assert line["extra"]["exchange"] == "grid2x4/s2"
+
+
+def test_bench_eight_ranks_refuses_a_short_launch():
+    p = _bench(["--gpus", "8", "--device", "cpu", "--backend", "gloo"],
+               {"WORLD_SIZE": "4", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode == 2 and "WORLD_SIZE=4" in p.stderr and p.stdout == ""
