@@ -255,7 +255,7 @@ def main():
                 rs.set_halo_pipeline(args.pipeline or 1)
         else:
             t_tune = time.time()
-            comm_times = rs.tune(out, force=args.force_rowsplit, budget_s=args.tune_budget)
+            comm_times = rs.tune(out, force=args.force_rowsplit, budget_s=args.tune_budget, log=log)
             tune_s = time.time() - t_tune
             log("[bench] exchange candidates (ms, max over ranks; model-predicted): " +
                 ", ".join(f"{kk} {vv:.3f} ({rs.tune_report[kk]['predicted_ms']:.3f})"

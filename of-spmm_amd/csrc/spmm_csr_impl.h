@@ -814,7 +814,8 @@ __global__ void __launch_bounds__(64 * K::WPB)
                      const T* __restrict__ val, const I* __restrict__ vperm,
                      const T* __restrict__ B, int64_t ldb, int64_t kb,
                      T* __restrict__ C, int64_t ldc, int64_t row_begin, int64_t nrows, int64_t n,
-                     int64_t chunk, const unsigned long long* __restrict__ counters,
+                     int64_t split, int64_t chunk, int64_t heavy,
+                     const unsigned long long* __restrict__ counters,
                      const int64_t* __restrict__ items, const int64_t* __restrict__ order,
                      typename Num<T>::acc* __restrict__ part, const T* __restrict__ bias,
                      int act, int64_t wave_blocks) {
@@ -920,19 +921,28 @@ __global__ void __launch_bounds__(64 * K::WPB)
   if constexpr ((K::WH && LPR < 64) || K::BI) {
     if (order != nullptr) g += (int64_t)counters[0] + (int64_t)counters[3] - (int64_t)counters[2];
   }
+  // Work items with a plan: hub chunks, then the heavy rows (bin 0 of `order`), then every row by
+  // its index -- a group whose row is a hub or heavy row (done by the items before) exits.  Taking
+  // the light rows by index instead of through `order` removes one dependent load from each light
+  // row's chain (order[q] -> row_ptr -> (col, val) -> B rows), which is what bounds the short
+  // rows of a latency-bound launch; the rows keep index order, as in the plan's light bin.
   int64_t lr, c = -1;  // local row; chunk index or -1 for a whole row
+  bool by_index = false;
   if (order == nullptr) {
     if (g >= nrows) return;
     lr = g;
   } else {
     const int64_t nchunks = (int64_t)counters[0];
+    const int64_t nheavy = (int64_t)counters[3] - (int64_t)counters[2];  // bin 0
     if (g < nchunks) {
       lr = items[2 * g + 0];
       c = items[2 * g + 1];
+    } else if (g < nchunks + nheavy) {
+      lr = order[g - nchunks];
     } else {
-      const int64_t q = g - nchunks;
-      if (q >= nrows - (int64_t)counters[1]) return;
-      lr = order[q];
+      lr = g - nchunks - nheavy;
+      if (lr >= nrows) return;
+      by_index = true;
     }
   }
   if constexpr (LPR == 64) {
@@ -941,6 +951,7 @@ __global__ void __launch_bounds__(64 * K::WPB)
   }
   const int64_t rs = (int64_t)rp[row_begin + lr];
   const int64_t re = (int64_t)rp[row_begin + lr + 1];
+  if (by_index && (re - rs > split || re - rs > heavy)) return;  // a hub or a heavy row
   int64_t j0 = rs, j1 = re;
   if (c >= 0) {
     // chunk c of num_chunks(len, chunk) = len / chunk; the last one (fewer than 2 * chunk
@@ -1103,14 +1114,14 @@ int launch_cfg(const Launch& L) {
   unsigned long long* counters = wl.counters;
   int64_t *hub = wl.hubs, *items = wl.items, *order = wl.order;
   A* part = reinterpret_cast<A*>(wl.part);
-  // Work list length <= hub chunks + rows; surplus groups exit at once.  The WH form puts one
-  // wave per hub chunk / heavy row first (upper bound: every chunk and row), then the groups.
-  const int64_t work = L.nrows + (plan ? w.max_chunks : 0);
-  // The BI form puts one block per hub chunk / heavy row first (upper bound: every chunk and
-  // every row longer than the heavy threshold).
+  // Work items: hub chunks, heavy rows, then every row by index (surplus groups exit at once).
+  // The WH / BI forms put one wave / block per hub chunk and heavy row first (upper bound: every
+  // chunk and every row longer than the heavy threshold), then the groups of the rows.
   const int64_t heavy = L.sched.heavy == 0 ? auto_heavy(L.nrows, L.nnz_est) : L.sched.heavy;
-  const int64_t bi_items =
-      w.max_chunks + (heavy == INT64_MAX ? 0 : std::min<int64_t>(L.nrows, L.nnz / (heavy + 1) + 1));
+  const int64_t heavy_bound =
+      heavy == INT64_MAX ? 0 : std::min<int64_t>(L.nrows, L.nnz / (heavy + 1) + 1);
+  const int64_t bi_items = w.max_chunks + heavy_bound;
+  const int64_t work = L.nrows + (plan ? bi_items : 0);
   // wave items (one wave each) and block items (one block each) are bounded alike: hub chunks
   // plus the rows above the heavy threshold
   const int64_t wave_blocks = (K::WH && K::LPR < 64 && plan) ? (bi_items + K::WPB - 1) / K::WPB
@@ -1122,8 +1133,8 @@ int launch_cfg(const Launch& L) {
   hipLaunchKernelGGL((spmm_main_kernel<T, I, K>), dim3((unsigned)grid), dim3(64 * K::WPB), 0,
                      L.stream, rp, col, val, static_cast<const I*>(L.vperm), B, L.ldb, L.b_rows, C,
                      L.ldc,
-                     L.row_begin, L.nrows, L.n,
-                     plan ? L.sched.chunk : INT64_MAX, counters, items, order, part,
+                     L.row_begin, L.nrows, L.n, plan ? L.sched.split : INT64_MAX,
+                     plan ? L.sched.chunk : INT64_MAX, heavy, counters, items, order, part,
                      static_cast<const T*>(L.bias), L.act, wave_blocks);
   OFX_HIP_CHECK(hipGetLastError());
   if (plan && w.max_hubs > 0)

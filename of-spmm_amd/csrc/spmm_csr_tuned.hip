@@ -44,6 +44,13 @@ int launch_tuned(const Launch& L, int id) {
       case 23: return launch_cfg<T, I, Cfg<1, 16, 32, 4, false, true, false, true>>(L);
       case 24: return launch_cfg<T, I, Cfg<4, 16, 16, 4, false, true>>(L);
       case 25: return launch_cfg<T, I, Cfg<4, 16, 16, 4, false, true, false, true>>(L);
+      // mid-size launches at N = 16: four lanes of float4 per row (16 rows per wave) instead of
+      // sixteen one-element lanes, with / without the prefetch and wave items
+      case 26: return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true>>(L);
+      case 27: return launch_cfg<T, I, Cfg<4, 4, 16, 4, false, true>>(L);
+      case 28: return launch_cfg<T, I, Cfg<2, 8, 8, 4, false, true>>(L);
+      case 29: return launch_cfg<T, I, Cfg<4, 4, 16, 4, false, true, false, true>>(L);
+      case 30: return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, true>>(L);
       default: break;
     }
   }

@@ -874,7 +874,7 @@ class RowSplitSpmm:
 
     def tune(self, out, pipelines=(1, 2, 4), reps: int = 3, force: bool = False,
              budget_s: float | None = None, prune: float = 3.0,
-             first: tuple = ("grid2x4/s2",)) -> dict:
+             first: tuple = ("grid2x4/s2",), log=None) -> dict:
         """Times every exchange on this node with the real step over the bound CSR: all-gather
         (ring / point-to-point) x pipeline depth, the halo exchange and the grid plans if built.
         Keeps the fastest.  Timings are max-reduced over ranks, so all ranks choose the same; every
@@ -988,6 +988,9 @@ class RowSplitSpmm:
             ms = measure()
             rec["measured_ms"] = round(ms, 4) if math.isfinite(ms) else None
             rec["status"] = "measured" if math.isfinite(ms) else "error"
+            if log is not None:
+                log(f"[tune] {name}: {ms:.3f} ms (model {prior[name]:.3f}, refit {fitted:.3f}; "
+                    f"{time.perf_counter() - t_start:.1f} s)")
             if math.isfinite(ms):
                 times[name] = ms
                 if len(times) == 1:  # refit the exchange rate to the first measurement

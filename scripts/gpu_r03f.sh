@@ -1,5 +1,5 @@
-# round 3, GPU call f: buffer-load B rows: full GPU suite, same-box A/B against the previous
-# commit's kernels, forms sweep
+# round 3, GPU call f: buffer-load B rows + light rows by index: full GPU suite, same-box A/B
+# against the previous commit's kernels, N=16 mid-size configurations, forms sweep
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -12,5 +12,6 @@ for lib in base main base main; do
   timeout -k 10 300 python -u scripts/probe_split.py --no-old --graphs p2m,plaw1m,products --widths 64,128 --variants 416,432 --rounds 3 >> gpurun_out/r03f_ab_$lib.jsonl 2>> gpurun_out/r03f_ab.err || { tail -20 gpurun_out/r03f_ab.err; exit 1; }
 done
 unset OFX_SPMM_LIB
+timeout -k 10 600 python -u scripts/probe_split.py --no-old --graphs pubmed,small20k,arxiv,g60k,p2m,p5m,plaw1m --widths 16 --variants 0,10021,10022,10026,10027,10028,10029,10030,10029h-1,10029h128,30004h-1,30005h-1,404 > gpurun_out/r03f_probe_n16.jsonl 2> gpurun_out/r03f_probe_n16.err || { tail -20 gpurun_out/r03f_probe_n16.err; exit 1; }
 timeout -k 10 600 python -u scripts/probe_split.py --no-old --variants 0,30003,30004,30005 > gpurun_out/r03f_probe_forms.jsonl 2> gpurun_out/r03f_probe_forms.err || { tail -20 gpurun_out/r03f_probe_forms.err; exit 1; }
 echo all done

@@ -75,14 +75,17 @@ def main():
             b = synth.dense(0, m, n, device=dev)
             out = torch.empty((m, n), device=dev)
             kern = {}
-            for vv in [int(x) for x in args.variants.split(",")]:
+            for spec in args.variants.split(","):
+                # "<variant>" or "<variant>h<heavy threshold>" (h-1: no heavy bin)
+                vs, _, hs = spec.partition("h")
+                vv, heavy = int(vs), int(hs) if hs else 0
                 if vv in (10021, 10022) and n != 16:
                     continue  # one-element fp32 lanes: N <= 16 only
                 if vv == 30000 and nnz * n > (1 << 26):
                     continue  # the small form's block-wide chains: far too slow beyond this
                 try:
-                    kern[str(vv)] = ops.SpmmCsrKernel(m, m, n, nnz, rp.dtype, b.dtype, dev,
-                                                      ops.make_options(variant=vv))
+                    kern[spec] = ops.SpmmCsrKernel(m, m, n, nnz, rp.dtype, b.dtype, dev,
+                                                   ops.make_options(variant=vv, heavy=heavy))
                 except Exception as e:  # noqa: BLE001  (a variant not applicable to this N)
                     print(f"[probe_split] skip {vv} at n={n}: {e}", file=sys.stderr)
             if not args.no_old:

@@ -15,7 +15,7 @@ def short(name):
     return name.split("(")[0]
 
 
-def main(src, tag, dst="profiles"):
+def main(src, tag, dst="profiles", alg_bytes=None):
     stats = []
     for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
         stats.append({"kernel": short(r["Name"]), "full_name": r["Name"], "calls": int(r["Calls"]),
@@ -44,6 +44,16 @@ def main(src, tag, dst="profiles"):
     if traffic:
         rd = traffic.get("read_bytes_by_request_size", traffic.get("read_bytes_corrected_x2"))
         traffic["beyond_l2_bytes_per_launch"] = rd + traffic.get("write_size_bytes", 0)
+    if alg_bytes:
+        # the gather model's bytes per launch against the measured beyond-L2 bytes,
+        # and the dominant kernel's rate / fraction of the 8 TB/s HBM spec at its average duration
+        avg_us = max(stats, key=lambda s: s["pct"])["avg_us"]
+        traffic["algorithmic_bytes_per_launch"] = float(alg_bytes)
+        if "beyond_l2_bytes_per_launch" in traffic:
+            traffic["beyond_l2_over_algorithmic"] = traffic["beyond_l2_bytes_per_launch"] / float(alg_bytes)
+        traffic["dominant_kernel_avg_us"] = avg_us
+        traffic["achieved_gbs_gather_model"] = float(alg_bytes) / (avg_us * 1e-6) / 1e9
+        traffic["frac_of_8tbs"] = traffic["achieved_gbs_gather_model"] / 8000.0
     out = {"tag": tag, "dominant_kernel": main_k, "kernels": stats, "pmc_avg_per_dispatch": pmc_avg,
            "traffic": traffic}
     os.makedirs(dst, exist_ok=True)
@@ -58,9 +68,12 @@ def main(src, tag, dst="profiles"):
             f.write(f"- **{k}**: " + ", ".join(f"{n}={v:.4g}" for n, v in sorted(d.items())) + "\n")
         f.write("\n## Traffic of the dominant kernel per launch\n\n")
         for n, v in traffic.items():
-            f.write(f"- {n}: {v:.4g} bytes ({v / 1e9:.3f} GB)\n")
+            if n.endswith("bytes") or n.endswith("per_launch"):
+                f.write(f"- {n}: {v:.4g} bytes ({v / 1e9:.3f} GB)\n")
+            else:
+                f.write(f"- {n}: {v:.4g}\n")
     print(json.dumps(traffic))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], alg_bytes=float(sys.argv[3]) if len(sys.argv) > 3 else None)
