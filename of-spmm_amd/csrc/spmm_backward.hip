@@ -42,10 +42,10 @@ __global__ void iota_kernel(I* __restrict__ out, int64_t n) {
 template <typename I>
 __global__ void __launch_bounds__(kBlock) expand_rows_kernel(const I* __restrict__ rp, int64_t m,
                                                              I* __restrict__ row_of) {
-  const int64_t r = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-  if (r >= m) return;
   const int lane = threadIdx.x & 63;
-  for (int64_t j = (int64_t)rp[r] + lane; j < (int64_t)rp[r + 1]; j += 64) row_of[j] = (I)r;
+  const int64_t stride = (int64_t)gridDim.x * (kBlock / 64);
+  for (int64_t r = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); r < m; r += stride)
+    for (int64_t j = (int64_t)rp[r] + lane; j < (int64_t)rp[r + 1]; j += 64) row_of[j] = (I)r;
 }
 
 // Sort keys of the transpose: the column, or k for a column outside [0, k) (the forward zero-fills
@@ -131,7 +131,8 @@ int transpose(hipStream_t s, int64_t m, int64_t k, int64_t nnz, const I* rp, con
   void* cub_tmp = static_cast<char*>(ws) + plan::align_up(4 * (size_t)nnz * sizeof(I), 256);
   hipLaunchKernelGGL((iota_kernel<I>), dim3(g_nnz), dim3(kBlock), 0, s, vals_in, nnz);
   OFX_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL((expand_rows_kernel<I>), dim3((unsigned)((m + 3) / 4)), dim3(kBlock), 0, s,
+  hipLaunchKernelGGL((expand_rows_kernel<I>), dim3((unsigned)std::min<int64_t>((m + 3) / 4, 1 << 20)),
+                     dim3(kBlock), 0, s,
                      rp, m, row_of);
   OFX_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL((transpose_keys_kernel<I>), dim3(g_nnz), dim3(kBlock), 0, s, col, nnz, k,
@@ -219,20 +220,23 @@ __device__ __forceinline__ bool sddmm_item(const I* __restrict__ rp, int64_t g, 
   return j0 < j1;
 }
 
+// Grid pieces: a launch holds fewer than 2^32 threads (papers-scale row counts would not).
+constexpr int64_t kLaunchBlocks = ((int64_t)1 << 31) / kBlock;
+
 template <typename T, typename I, int LG, int L, int U, bool ALIGNED>
 __global__ void __launch_bounds__(kBlock)
     sddmm_kernel(const I* __restrict__ rp, const I* __restrict__ col, const T* __restrict__ dC,
                  int64_t ldc, const T* __restrict__ B, int64_t ldb, int64_t kb,
                  T* __restrict__ out, int64_t row_begin, int64_t nrows, int64_t n, int64_t chunk,
                  const unsigned long long* __restrict__ counters, const int64_t* __restrict__ items,
-                 const int64_t* __restrict__ order) {
+                 const int64_t* __restrict__ order, int64_t block_base) {
 #pragma clang fp contract(off)
   using A = typename Num<T>::acc;
   constexpr int GPW = 64 / LG;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int gl = lane & (LG - 1);
-  const int64_t g = ((int64_t)blockIdx.x * (kBlock / 64) + wave) * GPW + lane / LG;
+  const int64_t g = ((block_base + (int64_t)blockIdx.x) * (kBlock / 64) + wave) * GPW + lane / LG;
   int64_t lr, j0, j1;
   if (!sddmm_item<I>(rp, g, row_begin, nrows, chunk, counters, items, order, &lr, &j0, &j1)) return;
   // dC row, this lane's leaves
@@ -303,12 +307,14 @@ __global__ void __launch_bounds__(kBlock)
                       T* __restrict__ out, int64_t row_begin, int64_t nrows, int64_t n,
                       int64_t chunk, int tiles,
                       const unsigned long long* __restrict__ counters,
-                      const int64_t* __restrict__ items, const int64_t* __restrict__ order) {
+                      const int64_t* __restrict__ items, const int64_t* __restrict__ order,
+                      int64_t block_base) {
 #pragma clang fp contract(off)
   using A = typename Num<T>::acc;
   constexpr int L = kWideLeaves / 64, U = 2;
   const int lane = threadIdx.x & 63;
-  const int64_t g = (int64_t)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t g = (block_base + (int64_t)blockIdx.x) * (kBlock / 64) +
+                    __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int64_t lr, j0, j1;
   if (!sddmm_item<I>(rp, g, row_begin, nrows, chunk, counters, items, order, &lr, &j0, &j1)) return;
   const T* arow = dC + lr * ldc;
@@ -430,12 +436,15 @@ int sddmm_cfg(const SddmmArgs& a) {
   }
   const int64_t work = a.nrows + (w.total > 0 ? w.max_chunks : 0);
   const int64_t grid = (work + GPB - 1) / GPB;
-  hipLaunchKernelGGL((sddmm_kernel<T, I, LG, L, U, ALIGNED>), dim3((unsigned)grid), dim3(kBlock), 0,
-                     a.s, static_cast<const I*>(a.rp), static_cast<const I*>(a.col),
-                     static_cast<const T*>(a.dC), a.ldc, static_cast<const T*>(a.B), a.ldb, a.k,
-                     static_cast<T*>(a.out), a.row_begin, a.nrows, a.n,
-                     w.total > 0 ? sched.chunk : INT64_MAX, wl.counters, wl.items, wl.order);
-  OFX_HIP_CHECK(hipGetLastError());
+  for (int64_t b0 = 0; b0 < grid; b0 += kLaunchBlocks) {  // < 2^31 threads per launch
+    hipLaunchKernelGGL((sddmm_kernel<T, I, LG, L, U, ALIGNED>),
+                       dim3((unsigned)std::min(kLaunchBlocks, grid - b0)), dim3(kBlock), 0, a.s,
+                       static_cast<const I*>(a.rp), static_cast<const I*>(a.col),
+                       static_cast<const T*>(a.dC), a.ldc, static_cast<const T*>(a.B), a.ldb, a.k,
+                       static_cast<T*>(a.out), a.row_begin, a.nrows, a.n,
+                       w.total > 0 ? sched.chunk : INT64_MAX, wl.counters, wl.items, wl.order, b0);
+    OFX_HIP_CHECK(hipGetLastError());
+  }
   return OFX_OK;
 }
 
@@ -468,13 +477,16 @@ int sddmm_aligned(const SddmmArgs& a) {
   }
   const int64_t work = a.nrows + (w.total > 0 ? w.max_chunks : 0);
   const int64_t grid = (work + kBlock / 64 - 1) / (kBlock / 64);
-  hipLaunchKernelGGL((sddmm_wide_kernel<T, I, ALIGNED>), dim3((unsigned)grid), dim3(kBlock), 0, a.s,
-                     static_cast<const I*>(a.rp), static_cast<const I*>(a.col),
-                     static_cast<const T*>(a.dC), a.ldc, static_cast<const T*>(a.B), a.ldb, a.k,
-                     static_cast<T*>(a.out), a.row_begin, a.nrows, a.n,
-                     w.total > 0 ? sched.chunk : INT64_MAX, (int)tiles, wl.counters, wl.items,
-                     wl.order);
-  OFX_HIP_CHECK(hipGetLastError());
+  for (int64_t b0 = 0; b0 < grid; b0 += kLaunchBlocks) {  // < 2^31 threads per launch
+    hipLaunchKernelGGL((sddmm_wide_kernel<T, I, ALIGNED>),
+                       dim3((unsigned)std::min(kLaunchBlocks, grid - b0)), dim3(kBlock), 0, a.s,
+                       static_cast<const I*>(a.rp), static_cast<const I*>(a.col),
+                       static_cast<const T*>(a.dC), a.ldc, static_cast<const T*>(a.B), a.ldb, a.k,
+                       static_cast<T*>(a.out), a.row_begin, a.nrows, a.n,
+                       w.total > 0 ? sched.chunk : INT64_MAX, (int)tiles, wl.counters, wl.items,
+                       wl.order, b0);
+    OFX_HIP_CHECK(hipGetLastError());
+  }
   return OFX_OK;
 }
 

@@ -71,16 +71,33 @@ struct alignas(sizeof(T) * VEC) Pack {
 // BI: the mid form: hub chunks and heavy rows take a whole block each (block_accumulate).
 // BUF: B rows through raw buffer loads with the hardware range check (B < 4 GiB, BRows); the
 // global-load form (BUF = false) serves larger B in the bandwidth configurations only.
+// HL (with WH): the wave items run in HL-lane groups of one element per lane with HU loads in
+// flight (WaveMap), not in the light rows' VEC x LPR groups.  Narrow rows then take 4-lane groups
+// of 16-B loads (16 light rows per wave at few registers) while a hub chunk still gets a whole
+// wave with few cross-lane moves per product: the kernel's register count (the larger of the two
+// paths) stays at the light path's.
 template <int VEC_, int LPR_, int U_ = 8, int WPB_ = 4, bool NT_ = false, bool PF_ = false,
-          bool BNT_ = false, bool WH_ = false, bool BI_ = false, bool BUF_ = true>
+          bool BNT_ = false, bool WH_ = false, bool BI_ = false, bool BUF_ = true, int HL_ = 0,
+          int HU_ = 16>
 struct Cfg {
   static constexpr int VEC = VEC_, LPR = LPR_, U = U_, WPB = WPB_;
   static constexpr bool NT = NT_, PF = PF_, BNT = BNT_, WH = WH_, BI = BI_, BUF = BUF_;
+  static constexpr int HL = HL_, HU = HU_;
   // loads in flight per lane of the wave-item form: G * UW * VEC cross-lane moves per batch are
   // unrolled, so UW keeps that at <= 256 (4..32)
   static constexpr int G = LPR < 64 ? 64 / LPR : 1;
   static constexpr int UW_RAW = 256 / (G * VEC);
   static constexpr int UW = UW_RAW > 32 ? 32 : (UW_RAW < 4 ? 4 : UW_RAW);
+};
+
+// The lane mapping of the wave items (accumulate_wave): the light rows' one, or HL lanes of one
+// element each (HL > 0).
+template <typename K>
+struct WaveMap {
+  static constexpr int VEC = K::HL > 0 ? 1 : K::VEC;
+  static constexpr int LPR = K::HL > 0 ? K::HL : K::LPR;
+  static constexpr int UW = K::HL > 0 ? K::HU : K::UW;
+  static constexpr bool BNT = K::BNT, BUF = K::BUF;
 };
 
 template <typename X>
@@ -818,9 +835,10 @@ __global__ void __launch_bounds__(64 * K::WPB)
                      const unsigned long long* __restrict__ counters,
                      const int64_t* __restrict__ items, const int64_t* __restrict__ order,
                      typename Num<T>::acc* __restrict__ part, const T* __restrict__ bias,
-                     int act, int64_t wave_blocks) {
+                     int act, int64_t wave_blocks, int64_t block_base) {
   using A = typename Num<T>::acc;
   constexpr int VEC = K::VEC, LPR = K::LPR, kWaves = K::WPB;
+  const int64_t bid = block_base + (int64_t)blockIdx.x;  // launches of > 2^31 threads are cut
   constexpr int GPW = 64 / LPR;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -829,40 +847,45 @@ __global__ void __launch_bounds__(64 * K::WPB)
   const int gsub = LPR == 64 ? 0 : lane / LPR;
   if constexpr (K::WH && LPR < 64) {
     // blocks [0, wave_blocks): one wave per hub chunk / heavy row (the plan's first items)
-    if ((int64_t)blockIdx.x < wave_blocks) {
-      const int64_t w = (int64_t)blockIdx.x * kWaves + wave;
+    using KW = WaveMap<K>;
+    constexpr int WV = KW::VEC, WL = KW::LPR;
+    if (bid < wave_blocks) {
+      // the wave_blocks * WPB waves stride over the items (the grid bound is an estimate; the
+      // plan's counters hold the count), so the launch carries no blocks that only exit
+      const int wgl = lane & (WL - 1);
       const int64_t nchunks = (int64_t)counters[0];
       const int64_t nheavy = (int64_t)counters[3] - (int64_t)counters[2];  // bin 0
-      if (w >= nchunks + nheavy) return;
-      int64_t wr, wc = -1;
-      if (w < nchunks) {
-        wr = items[2 * w + 0];
-        wc = items[2 * w + 1];
-      } else {
-        wr = order[w - nchunks];
-      }
-      wr = uniform64(wr);
-      wc = uniform64(wc);
-      const int64_t rs = (int64_t)rp[row_begin + wr];
-      const int64_t re = (int64_t)rp[row_begin + wr + 1];
-      int64_t j0 = rs, j1 = re;
-      if (wc >= 0) {
-        j0 = rs + wc * chunk;
-        j1 = (re - j0 - chunk < chunk) ? re : j0 + chunk;
-      }
-      for (int64_t c0 = 0; c0 < n; c0 += (int64_t)LPR * VEC) {
-        const int64_t cc = c0 + (int64_t)gl * VEC;
-        const bool active = cc < n;
-        A acc[VEC];
+      for (int64_t w = bid * kWaves + wave; w < nchunks + nheavy; w += wave_blocks * kWaves) {
+        int64_t wr, wc = -1;
+        if (w < nchunks) {
+          wr = items[2 * w + 0];
+          wc = items[2 * w + 1];
+        } else {
+          wr = order[w - nchunks];
+        }
+        wr = uniform64(wr);
+        wc = uniform64(wc);
+        const int64_t rs = (int64_t)rp[row_begin + wr];
+        const int64_t re = (int64_t)rp[row_begin + wr + 1];
+        int64_t j0 = rs, j1 = re;
+        if (wc >= 0) {
+          j0 = rs + wc * chunk;
+          j1 = (re - j0 - chunk < chunk) ? re : j0 + chunk;
+        }
+        for (int64_t c0 = 0; c0 < n; c0 += (int64_t)WL * WV) {
+          const int64_t cc = c0 + (int64_t)wgl * WV;
+          const bool active = cc < n;
+          A acc[WV];
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) acc[e] = A(0);
-        accumulate_wave<T, I, K>(col, val, vperm, brows<T, K::BUF>(B, c0, cc, active, ldb, kb), j0, j1, lane, gl,
-                                 acc);
-        if (active && gsub == 0) {
-          if (wc >= 0)
-            store_partial<A, VEC>(part + w * n + cc, acc);
-          else
-            store_row<T, VEC, K::NT>(C + wr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
+          for (int e = 0; e < WV; ++e) acc[e] = A(0);
+          accumulate_wave<T, I, KW>(col, val, vperm, brows<T, K::BUF>(B, c0, cc, active, ldb, kb),
+                                    j0, j1, lane, wgl, acc);
+          if (active && lane < WL) {
+            if (wc >= 0)
+              store_partial<A, WV>(part + w * n + cc, acc);
+            else
+              store_row<T, WV, K::NT>(C + wr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
+          }
         }
       }
       return;
@@ -871,10 +894,10 @@ __global__ void __launch_bounds__(64 * K::WPB)
   if constexpr (K::BI) {
     // blocks [0, wave_blocks): one block per hub chunk / heavy row (the plan's first items).
     // A block returns or runs its item as a whole, so block_accumulate's barriers are uniform.
-    if ((int64_t)blockIdx.x < wave_blocks) {
+    if (bid < wave_blocks) {
       __shared__ __attribute__((aligned(16))) SmallLds<T, I, K> lds;
       constexpr int W = SmallForm<T, I, K>::W;
-      const int64_t w = blockIdx.x;
+      const int64_t w = bid;
       const int64_t nchunks = (int64_t)counters[0];
       const int64_t nheavy = (int64_t)counters[3] - (int64_t)counters[2];  // bin 0
       if (w >= nchunks + nheavy) return;
@@ -916,7 +939,7 @@ __global__ void __launch_bounds__(64 * K::WPB)
   }
   // one lane-group per work item; in the WH / BI forms these are the light rows after the wave /
   // block items
-  int64_t g = ((int64_t)(blockIdx.x - ((K::WH || K::BI) ? wave_blocks : 0)) * kWaves + wave) * GPW +
+  int64_t g = ((bid - ((K::WH || K::BI) ? wave_blocks : 0)) * kWaves + wave) * GPW +
               gsub;
   if constexpr ((K::WH && LPR < 64) || K::BI) {
     if (order != nullptr) g += (int64_t)counters[0] + (int64_t)counters[3] - (int64_t)counters[2];
@@ -1121,22 +1144,28 @@ int launch_cfg(const Launch& L) {
   const int64_t heavy_bound =
       heavy == INT64_MAX ? 0 : std::min<int64_t>(L.nrows, L.nnz / (heavy + 1) + 1);
   const int64_t bi_items = w.max_chunks + heavy_bound;
-  const int64_t work = L.nrows + (plan ? bi_items : 0);
   // wave items (one wave each) and block items (one block each) are bounded alike: hub chunks
-  // plus the rows above the heavy threshold
-  const int64_t wave_blocks = (K::WH && K::LPR < 64 && plan) ? (bi_items + K::WPB - 1) / K::WPB
-                              : (K::BI && plan)              ? bi_items
-                                                             : 0;
+  // plus the rows above the heavy threshold.  The wave items loop (a wave strides over them), so
+  // their blocks are capped at kWaveItemBlocks; the light rows then need one group per row.
+  constexpr int64_t kWaveItemBlocks = 2048;
+  const bool wh = K::WH && K::LPR < 64 && plan;
+  const int64_t wave_blocks = wh ? std::min<int64_t>((bi_items + K::WPB - 1) / K::WPB, kWaveItemBlocks)
+                              : (K::BI && plan) ? bi_items
+                                                : 0;
+  const int64_t work = L.nrows + (plan && !wh && !K::BI ? bi_items : 0);
   const int64_t grid = wave_blocks + (work + GPB - 1) / GPB;
-  OFX_REQUIRE(grid < (int64_t)UINT32_MAX, OFX_EINVAL, "spmm_csr: too many rows (%lld)",
-              (long long)L.nrows);
-  hipLaunchKernelGGL((spmm_main_kernel<T, I, K>), dim3((unsigned)grid), dim3(64 * K::WPB), 0,
-                     L.stream, rp, col, val, static_cast<const I*>(L.vperm), B, L.ldb, L.b_rows, C,
-                     L.ldc,
-                     L.row_begin, L.nrows, L.n, plan ? L.sched.split : INT64_MAX,
-                     plan ? L.sched.chunk : INT64_MAX, heavy, counters, items, order, part,
-                     static_cast<const T*>(L.bias), L.act, wave_blocks);
-  OFX_HIP_CHECK(hipGetLastError());
+  // A launch holds fewer than 2^32 threads (papers-scale: 111M rows + items at 8 groups per block
+  // would not): the grid goes out in pieces of kLaunchBlocks, each told its first block.
+  constexpr int64_t kLaunchBlocks = ((int64_t)1 << 31) / (64 * K::WPB);
+  for (int64_t b0 = 0; b0 < grid; b0 += kLaunchBlocks) {
+    const int64_t nb = std::min(kLaunchBlocks, grid - b0);
+    hipLaunchKernelGGL((spmm_main_kernel<T, I, K>), dim3((unsigned)nb), dim3(64 * K::WPB), 0,
+                       L.stream, rp, col, val, static_cast<const I*>(L.vperm), B, L.ldb, L.b_rows,
+                       C, L.ldc, L.row_begin, L.nrows, L.n, plan ? L.sched.split : INT64_MAX,
+                       plan ? L.sched.chunk : INT64_MAX, heavy, counters, items, order, part,
+                       static_cast<const T*>(L.bias), L.act, wave_blocks, b0);
+    OFX_HIP_CHECK(hipGetLastError());
+  }
   if (plan && w.max_hubs > 0)
     return launch_reduce<T>(L.stream, w.max_hubs, L.n, counters, hub, part, C, L.ldc,
                             static_cast<const T*>(L.bias), L.act);
@@ -1297,6 +1326,26 @@ int launch_vec(const Launch& L, int lpr, bool nt) {
   }
 }
 
+// Rows of 64 B in fp32 (N = 16) above the mid form: four lanes of float4 per light row (16 rows
+// per wave, few registers, so many rows in flight: what bounds these launches) and the hub chunks
+// and heavy rows as wave items in 16-lane one-element groups (HL), so a 512-nonzero chunk is not
+// one 4-lane chain.  Up to kPrefetchNnz: U = 4 with 16 wave-item loads in flight per lane (arxiv-
+// shaped 71 -> 46 us, 2M nonzeros 65 -> 56 us); past it 2-lane float2 groups of U = 8 with 8 (5M
+// 111 -> 92 us, 1M power-law 406 -> 353 us, products 2,241 -> 2,184 us; a uniform-degree 20M graph
+// 396 -> 402 us).  profiles/r03n_graph.jsonl.  Same bits: only who adds changes.
+template <typename T, typename I>
+int launch_narrow(const Launch& L) {
+  if (L.nnz_est <= kPrefetchNnz)
+    return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, true, false, true, false, true, 16, 16>>(L);
+  return launch_cfg<T, I, Cfg<2, 8, 8, 4, false, true, false, true, false, true, 16, 8>>(L);
+}
+
+bool use_narrow_form(const Launch& L, int elem_bytes) {
+  return L.sched.variant == 0 && elem_bytes == 4 && L.n == 16 && pick_vec(4, L, 0) == 4 &&
+         !use_small_form(L.nrows, L.nnz_est, L.n, L.sched) &&
+         !use_mid_form(L.nrows, L.nnz_est, L.n, L.sched);
+}
+
 }  // namespace
 
 template <typename T, typename I>
@@ -1307,11 +1356,15 @@ int launch_typed(const Launch& L) {
                 "spmm_csr: tuning variant %d needs B under 4 GiB", L.sched.variant);
     return launch_tuned<T, I>(L, L.sched.variant - 10000);
   }
+  if constexpr (sizeof(T) == 4) {
+    if (use_narrow_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L)) return launch_narrow<T, I>(L);
+  }
   // variant = VEC * 100 + LPR forces a configuration (tuning / tests); 0 = auto.
   const int forced_vec = (L.sched.variant > 0 && !form) ? L.sched.variant / 100 : 0;
   const int forced_lpr = (L.sched.variant > 0 && !form) ? L.sched.variant % 100 : 0;
-  // fp32 rows of <= 64 B: one element per lane over 16 lanes beats 4 lanes of float4 (+9% on
-  // products-shaped N=16, scripts/ab.py); wider rows keep the widest vector
+  // fp32 rows of <= 64 B outside the narrow form (the small / mid forms, N < 16, forced forms):
+  // one element per lane over 16 lanes (+9% against 4 lanes of float4 in the round-2 bandwidth
+  // configuration, scripts/ab.py); wider rows keep the widest vector
   const int vec = (!forced_vec && sizeof(T) == 4 && L.n <= 16) ? 1
                                                                  : pick_vec((int)sizeof(T), L, forced_vec);
   OFX_REQUIRE(vec > 0, OFX_EINVAL,

@@ -51,6 +51,15 @@ int launch_tuned(const Launch& L, int id) {
       case 28: return launch_cfg<T, I, Cfg<2, 8, 8, 4, false, true>>(L);
       case 29: return launch_cfg<T, I, Cfg<4, 4, 16, 4, false, true, false, true>>(L);
       case 30: return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, true>>(L);
+      // ... and with wave items in 16-lane one-element groups (HL = 16, HU loads in flight)
+      case 31: return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, true, false, true, false, true, 16, 16>>(L);
+      case 32: return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 16, 16>>(L);
+      case 33: return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, true, false, true, false, true, 16, 8>>(L);
+      case 34: return launch_cfg<T, I, Cfg<2, 8, 8, 4, false, true, false, true, false, true, 16, 16>>(L);
+      case 35: return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, false, false, true, false, true, 16, 16>>(L);
+      case 36: return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, true, false, true, false, true, 16, 32>>(L);
+      case 37: return launch_cfg<T, I, Cfg<2, 8, 8, 4, false, true, false, true, false, true, 16, 8>>(L);
+      case 38: return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 16, 8>>(L);
       default: break;
     }
   }

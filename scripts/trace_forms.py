@@ -21,8 +21,9 @@ from oneflow_spmm import ops, synth  # noqa: E402
 dev = torch.device("cuda", 0)
 cache = {}
 for spec in sys.argv[1:]:
-    name, n, variant = spec.split(":")
-    n, variant = int(n), int(variant)
+    name, n, vs = spec.split(":")
+    v, _, hs = vs.partition("h")  # "<variant>" or "<variant>h<heavy threshold>"
+    n, variant, heavy = int(n), int(v), (int(hs) if hs else 0)
     m, nnz = GRAPHS[name]
     if name not in cache:
         rp, ci, v = synth.csr(m, m, nnz, threads=16)
@@ -31,7 +32,7 @@ for spec in sys.argv[1:]:
     b = synth.dense(0, m, n, device=dev)
     out = torch.empty((m, n), device=dev)
     k = ops.SpmmCsrKernel(m, m, n, nnz, torch.int32, torch.float32, dev,
-                          ops.make_options(variant=variant))
+                          ops.make_options(variant=variant, heavy=heavy))
     for _ in range(200):
         k(rp, ci, v, b, out)
     torch.cuda.synchronize()

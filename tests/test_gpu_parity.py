@@ -53,7 +53,7 @@ def test_forced_variants_bitexact(device, variant):
 
 
 @pytest.mark.parametrize("n", [16, 128])
-@pytest.mark.parametrize("tuned", list(range(1, 18)) + list(range(21, 31)))
+@pytest.mark.parametrize("tuned", list(range(1, 18)) + list(range(21, 39)))
 def test_tuning_table_bitexact(device, tuned, n):
     """Every entry of the tuning table (variant 10000 + id, spmm_csr.hip launch_tuned) computes
     the contract's bits: only the launch shape and loads in flight differ."""
@@ -591,6 +591,58 @@ def test_small_form_single_launch(device, dtype, idx, n):
         out5 = ops.spmm_csr_device(*d, m, k, options=ops.make_options(heavy=cut))
         torch.cuda.synchronize()
         assert_bitwise(out5, ref, f"light cut {cut}")
+
+
+@pytest.mark.parametrize("idx", [torch.int32, torch.int64])
+@pytest.mark.parametrize("mean_deg", [25, 90])
+def test_narrow_form_n16(device, idx, mean_deg):
+    """fp32 N = 16 above the mid form (launch_narrow): 4-lane float4 light rows with 16-lane wave
+    items up to kPrefetchNnz nonzeros (mean degree 25: 1M), 2-lane float2 ones past it (90: 3.6M).
+    Same bits as the oracle for the whole matrix, a row range, a plan built once, heavy cuts, the
+    epilogue and gathered values, and as the forced bandwidth configuration."""
+    rng = np.random.default_rng(1700 + mean_deg)
+    n, m, k = 16, 40_000, 40_000
+    split = ops.default_split(n)
+    deg = rng.integers(0, 2 * mean_deg, size=m)
+    for i, d in enumerate([split, split + 1, 2 * split - 1, 2 * split, 5 * split + 3, 20_000]):
+        deg[7 + 5003 * i] = d
+    deg[30_000:30_300] = rng.integers(100, 500, size=300)
+    rp, ci, v = random_csr(m, k, deg, rng, idx, torch.float32)
+    b = random_dense(k, n, rng)
+    nnz = ci.numel()
+    assert (nnz > (3 << 20)) == (mean_deg == 90)
+    d = (rp.to(device), ci.to(device), v.to(device), b.to(device))
+    ref = oracle_spmm(rp, ci, v, b)
+    out = fs.spmm(*d[:3], m, k, d[3])
+    torch.cuda.synchronize()
+    assert_bitwise(out, ref, f"narrow auto nnz={nnz}")
+    kern = ops.SpmmCsrKernel(m, k, n, nnz, idx, torch.float32, device)
+    sub = torch.full((20_000, n), float("nan"), device=device)
+    kern(*d, sub, row_begin=10_000, row_end=30_000)
+    kp = ops.SpmmCsrKernel(m, k, n, nnz, idx, torch.float32, device).plan(d[0], 0, m)
+    o2 = torch.full((m, n), float("nan"), device=device)
+    kp(*d, o2, 0, m, planned=True)
+    torch.cuda.synchronize()
+    assert_bitwise(sub, ref[10_000:30_000], "row range")
+    assert_bitwise(o2, ref, "planned")
+    for cut in (1, 129, 100_000):
+        o3 = ops.spmm_csr_device(*d, m, k, options=ops.make_options(heavy=cut))
+        torch.cuda.synchronize()
+        assert_bitwise(o3, ref, f"heavy cut {cut}")
+    big = ops.spmm_csr_device(*d, m, k, options=ops.make_options(variant=30003))
+    torch.cuda.synchronize()
+    assert torch.equal(big.view(torch.int32), out.view(torch.int32))
+    bias = random_dense(1, n, rng)[0]
+    o4 = torch.full((m, n), float("nan"), device=device)
+    kern(*d, o4, bias=bias.to(device), relu=True)
+    torch.cuda.synchronize()
+    assert_bitwise(o4, oracle.bias_act(ref, to_oracle(bias), "relu", dtype="f32"), "epilogue")
+    perm = torch.from_numpy(rng.permutation(nnz).astype(np.int64)).to(idx)
+    vals_src = torch.empty_like(v)
+    vals_src[perm.long()] = v
+    o5 = ops.spmm_csr_gathered(d[0], d[1], vals_src.to(device), perm.to(device), d[3], m, k)
+    torch.cuda.synchronize()
+    assert_bitwise(o5, ref, "gathered values")
 
 
 @pytest.mark.parametrize("dtype,idx", [("f32", torch.int32), ("f32", torch.int64), ("bf16", torch.int32),
