@@ -944,11 +944,22 @@ __global__ void __launch_bounds__(64 * K::WPB)
   if constexpr ((K::WH && LPR < 64) || K::BI) {
     if (order != nullptr) g += (int64_t)counters[0] + (int64_t)counters[3] - (int64_t)counters[2];
   }
-  // Work items with a plan: hub chunks, then the heavy rows (bin 0 of `order`), then every row by
-  // its index -- a group whose row is a hub or heavy row (done by the items before) exits.  Taking
-  // the light rows by index instead of through `order` removes one dependent load from each light
-  // row's chain (order[q] -> row_ptr -> (col, val) -> B rows), which is what bounds the short
-  // rows of a latency-bound launch; the rows keep index order, as in the plan's light bin.
+  // Work items with a plan: hub chunks, then the heavy rows (bin 0 of `order`), then the light
+  // rows in index order, taken one of two ways (the same rows, the same bits):
+  //   by index  every row index gets a group, and a group whose row is a hub or heavy row (done
+  //             by the items before) exits.  No order[q] load in the light row's chain (order ->
+  //             row_ptr -> (col, val) -> B rows), which is what bounds the short rows of a
+  //             latency-bound launch; but an exited group leaves its lanes idle while the other
+  //             groups of its wave work, so it pays only when few rows are excluded;
+  //   by order  the plan's light bin (order[q]), dense.
+  // By index when hubs + heavy rows are at most 1/kIdxExcluded of the rows (power-law graphs:
+  // 1.7-1.8%; Reddit-shaped: 53% hubs, where it cost 9%).
+  constexpr int64_t kIdxExcluded = 16;
+#if defined(OFX_LIGHT_ORDER)
+  constexpr bool kIdx = false;  // A/B builds only (scripts/ab_build.sh)
+#else
+  constexpr bool kIdx = true;
+#endif
   int64_t lr, c = -1;  // local row; chunk index or -1 for a whole row
   bool by_index = false;
   if (order == nullptr) {
@@ -956,12 +967,20 @@ __global__ void __launch_bounds__(64 * K::WPB)
     lr = g;
   } else {
     const int64_t nchunks = (int64_t)counters[0];
+    const int64_t nhubs = (int64_t)counters[1];
     const int64_t nheavy = (int64_t)counters[3] - (int64_t)counters[2];  // bin 0
+#if defined(OFX_LIGHT_INDEX)
+    const bool idx = true;
+#else
+    const bool idx = kIdx && (nhubs + nheavy) * kIdxExcluded <= nrows;
+#endif
     if (g < nchunks) {
       lr = items[2 * g + 0];
       c = items[2 * g + 1];
-    } else if (g < nchunks + nheavy) {
-      lr = order[g - nchunks];
+    } else if (g < nchunks + nheavy || !idx) {
+      const int64_t q = g - nchunks;
+      if (q >= nrows - nhubs) return;
+      lr = order[q];
     } else {
       lr = g - nchunks - nheavy;
       if (lr >= nrows) return;

@@ -60,6 +60,13 @@ int launch_tuned(const Launch& L, int id) {
       case 36: return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, true, false, true, false, true, 16, 32>>(L);
       case 37: return launch_cfg<T, I, Cfg<2, 8, 8, 4, false, true, false, true, false, true, 16, 8>>(L);
       case 38: return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 16, 8>>(L);
+      // N = 32 / 64: float4 light rows in 8 / 16 lanes with HL wave items (16 or 32 lanes)
+      case 39: return launch_cfg<T, I, Cfg<4, 8, 4, 4, false, true, false, true, false, true, 16, 16>>(L);
+      case 40: return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, true, false, true, false, true, 32, 8>>(L);
+      case 41: return launch_cfg<T, I, Cfg<4, 16, 4, 4, false, true, false, true, false, true, 16, 16>>(L);
+      case 42: return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, true, false, true, false, true, 32, 8>>(L);
+      case 43: return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, true>>(L);
+      case 44: return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, true>>(L);
       default: break;
     }
   }

@@ -53,7 +53,7 @@ def test_forced_variants_bitexact(device, variant):
 
 
 @pytest.mark.parametrize("n", [16, 128])
-@pytest.mark.parametrize("tuned", list(range(1, 18)) + list(range(21, 39)))
+@pytest.mark.parametrize("tuned", list(range(1, 18)) + list(range(21, 45)))
 def test_tuning_table_bitexact(device, tuned, n):
     """Every entry of the tuning table (variant 10000 + id, spmm_csr.hip launch_tuned) computes
     the contract's bits: only the launch shape and loads in flight differ."""
