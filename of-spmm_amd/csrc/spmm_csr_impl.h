@@ -1329,6 +1329,9 @@ int launch_vec(const Launch& L, int lpr, bool nt) {
     return (L.n > 16 && L.n <= 64) ? launch_vec_pf<T, I, VEC, true>(L, lpr)
                                    : launch_vec_pf<T, I, VEC, false>(L, lpr);
   // the bandwidth configuration (forced variants keep it at every size)
+#ifdef OFX_AB_GLOBAL_LOADS  // A/B builds only (scripts/ab_build.sh): global loads, not buffer loads
+  return launch_vec_global<T, I, VEC>(L, lpr, nt);
+#endif
   switch (lpr) {
     case 4: return launch_cfg<T, I, Cfg<VEC, 4>>(L);
     case 8: return launch_cfg<T, I, Cfg<VEC, 8>>(L);
