@@ -825,8 +825,13 @@ __global__ void __launch_bounds__(64 * K::WPB)
 
 // ---- main kernel: one work list = hub chunks, then rows in bin order ------------------------
 // Without a plan (`order` == nullptr) the list is simply the rows in index order.
+#ifdef OFX_AB_WPE  // A/B builds only (scripts/ab_build.sh): waves per SIMD the registers must allow
+#define OFX_MAIN_WPE __attribute__((amdgpu_waves_per_eu(OFX_AB_WPE)))
+#else
+#define OFX_MAIN_WPE
+#endif
 template <typename T, typename I, typename K>
-__global__ void __launch_bounds__(64 * K::WPB)
+__global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
     spmm_main_kernel(const I* __restrict__ rp, const I* __restrict__ col,
                      const T* __restrict__ val, const I* __restrict__ vperm,
                      const T* __restrict__ B, int64_t ldb, int64_t kb,
