@@ -348,7 +348,15 @@ __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* _
             const int r = R > 1 ? u / LPR : 0;
             const I cu = shfl(myc[r], src);
             vv[u] = shfl(myv[r], src);
-            if (k + u < cnt && active) bv[u] = br.template load<K::BNT, P>(cu);
+            if constexpr (K::BUF) {
+              // branch-free issue: a slot past the row end (or a lane past n) loads row k, which
+              // lies outside the buffer, so the range check returns zeros with no memory access.
+              // Loads under per-slot branches made hipcc wait vmcnt(0) before each bf16 / f16
+              // load (one B row in flight per lane instead of U)
+              bv[u] = br.template load<K::BNT, P>(k + u < cnt && active ? cu : (I)br.k32);
+            } else {
+              if (k + u < cnt && active) bv[u] = br.template load<K::BNT, P>(cu);
+            }
           }
         }
 #pragma unroll
