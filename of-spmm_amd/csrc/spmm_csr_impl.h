@@ -1122,8 +1122,8 @@ int launch_reduce(hipStream_t s, int64_t max_hubs, int64_t n, const unsigned lon
   return launch_reduce_vec<T, 1>(s, max_hubs, n, counters, hubs, part, C, ldc, bias, act);
 }
 
-int pick_vec(int elem_bytes, const Launch& L, int forced_vec) {
-  const int maxvec = 16 / elem_bytes;
+int pick_vec(int elem_bytes, const Launch& L, int forced_vec, int cap = 16) {
+  const int maxvec = std::min(16 / elem_bytes, cap);
   for (int v = maxvec; v >= 1; v /= 2) {
     if (forced_vec && v != forced_vec) continue;
     const size_t vb = (size_t)v * elem_bytes;
@@ -1400,8 +1400,19 @@ int launch_typed(const Launch& L) {
   // fp32 rows of <= 64 B outside the narrow form (the small / mid forms, N < 16, forced forms):
   // one element per lane over 16 lanes (+9% against 4 lanes of float4 in the round-2 bandwidth
   // configuration, scripts/ab.py); wider rows keep the widest vector
+  // 16-bit rows of at most 128 B (N <= 64) in the bandwidth configuration: at least 16 lanes per
+  // row (VEC = N / 16: 2-8 B per lane) instead of the widest vector over 4-8 lanes; products bf16
+  // N = 8 / 16 / 32 / 64 -8 / -7 / -6 / -13%, Reddit-shaped N = 16 / 32 / 64 -27 / -19 / -6%
+  // (profiles/r03y_lanes_*.jsonl; fp32 keeps its layouts, DESIGN.md §3 tuning record)
+  const bool narrow16 = !forced_vec && sizeof(T) == 2 && L.n <= 64 && L.sched.variant == 0 &&
+                        !use_small_form(L.nrows, L.nnz_est, L.n, L.sched) &&
+                        !use_mid_form(L.nrows, L.nnz_est, L.n, L.sched) &&
+                        !use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched);
+  int cap16 = 1;  // the largest power of two <= N / 16
+  while (cap16 * 32 <= L.n) cap16 *= 2;
   const int vec = (!forced_vec && sizeof(T) == 4 && L.n <= 16) ? 1
-                                                                 : pick_vec((int)sizeof(T), L, forced_vec);
+                  : narrow16 ? pick_vec((int)sizeof(T), L, 0, cap16)
+                             : pick_vec((int)sizeof(T), L, forced_vec);
   OFX_REQUIRE(vec > 0, OFX_EINVAL,
               "spmm_csr: variant %d not applicable (n=%lld ldb=%lld ldc=%lld or pointer alignment)",
               L.sched.variant, (long long)L.n, (long long)L.ldb, (long long)L.ldc);

@@ -17,7 +17,7 @@ sys.path[:0] = [os.path.join(ROOT, "of-spmm_amd"), ROOT]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-DT = {"f32": torch.float32, "bf16": torch.bfloat16, "f64": torch.float64}
+DT = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16, "f64": torch.float64}
 
 
 def main():

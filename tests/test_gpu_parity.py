@@ -708,3 +708,29 @@ def test_mid_form_block_items(device, dtype, idx, n):
                                  options=opts)
     torch.cuda.synchronize()
     assert_bitwise(out4, ref, "gathered values")
+
+
+@pytest.mark.parametrize("dtype,idx", [("bf16", torch.int32), ("f16", torch.int64)])
+@pytest.mark.parametrize("n", [8, 16, 24, 48, 64])
+def test_narrow_16bit_bandwidth_layout(device, dtype, idx, n):
+    """16-bit rows of <= 128 B in the bandwidth configuration (above kPrefetchNnz nonzeros) take
+    N / 16 elements per lane over >= 16 lanes (launch_typed, narrow16; rounded down to a power of
+    two: N = 24 / 48 -> 1 / 2) instead of the widest vector.  Lane layout only: the same bits as
+    the oracle and as the widest-vector configuration forced."""
+    rng = np.random.default_rng(4100 + n)
+    m, k = 120_000, 90_000
+    deg = rng.integers(0, 60, size=m)
+    deg[17] = 3000  # a hub row (split)
+    rp, ci, v = random_csr(m, k, deg, rng, idx, DTYPES[dtype])
+    assert ci.numel() > (3 << 20)
+    b = random_dense(k, n, rng, DTYPES[dtype])
+    d = (rp.to(device), ci.to(device), v.to(device), b.to(device))
+    ref = oracle_spmm(rp, ci, v, b)
+    out = fs.spmm(d[0], d[1], d[2], m, k, d[3])
+    torch.cuda.synchronize()
+    assert_bitwise(out, ref, f"{dtype} n={n} auto")
+    wide = 8 if n % 8 == 0 else (4 if n % 4 == 0 else 2)
+    lpr = max(4, 1 << (n // wide - 1).bit_length())
+    o2 = ops.spmm_csr_device(*d, m, k, options=ops.make_options(variant=wide * 100 + lpr))
+    torch.cuda.synchronize()
+    assert torch.equal(o2.view(torch.int16), out.view(torch.int16))
