@@ -160,6 +160,22 @@ __device__ __forceinline__ int64_t shfl(int64_t v, int src) {
 }
 __device__ __forceinline__ float shfl(float v, int src) { return __shfl(v, src); }
 __device__ __forceinline__ double shfl(double v, int src) { return __shfl(v, src); }
+// Lane `src` (wave-uniform) of v, as a scalar.
+__device__ __forceinline__ int32_t readlane(int32_t v, int src) {
+  return __builtin_amdgcn_readlane(v, src);
+}
+__device__ __forceinline__ int64_t readlane(int64_t v, int src) {
+  const uint64_t u = (uint64_t)v;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, src);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), src);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ float readlane(float v, int src) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
+}
+__device__ __forceinline__ double readlane(double v, int src) {
+  return __builtin_bit_cast(double, readlane(__builtin_bit_cast(int64_t, v), src));
+}
 
 // The zero row of out-of-range columns.  The reference gather zero-fills the gathered row of an
 // index outside the table (CPU: idx >= size, oneflow/user/kernels/gather_kernel_util.cpp:84-89;
@@ -260,6 +276,55 @@ __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* _
   using A = typename Num<T>::acc;
   using P = Pack<T, VEC>;
   if constexpr (LPR == 64) {
+#if !defined(OFX_AB_LPR64_SCALAR)
+    // j0/j1 are wave-uniform.  Batches of 64 nonzeros: the (col, val) pairs are loaded coalesced,
+    // one per lane, the next batch's during this one; each nonzero's pair reaches the wave as
+    // scalars through v_readlane (no LDS), and U B rows are in flight per lane, issued branch-free
+    // where B is one buffer (slots past the row end load row k: zeros from the range check, no
+    // memory access).  The scalar-cache form this replaces (s_load of each col / val) paid two
+    // dependent round trips per U nonzeros (OFX_AB_LPR64_SCALAR keeps it for A/B builds).
+    auto load_batch = [&](int64_t jb, I& c, A& v) {
+      const int n_ = (int)((j1 - jb) < 64 ? (j1 - jb) : 64);
+      c = 0;
+      v = A(0);
+      if (gl < n_) {
+        c = ld_stream<K::NT>(col + jb + gl);
+        const int64_t jv = vperm ? (int64_t)ld_stream<K::NT>(vperm + jb + gl) : jb + gl;
+        v = Num<T>::load(ld_stream<K::NT>(val + jv));
+      }
+    };
+    I nxc;
+    A nxv;
+    if (j0 < j1) load_batch(j0, nxc, nxv);
+    for (int64_t jb = j0; jb < j1; jb += 64) {
+      const int cnt = (int)((j1 - jb) < 64 ? (j1 - jb) : 64);
+      const I myc = nxc;
+      const A myv = nxv;
+      if (jb + 64 < j1) load_batch(jb + 64, nxc, nxv);  // in flight during this batch
+      for (int k = 0; k < cnt; k += kUnroll) {
+        P bv[kUnroll];
+        A vv[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+          const int s = k + u;  // wave-uniform, < 64
+          const I cu = readlane(myc, s);
+          vv[u] = readlane(myv, s);
+          if constexpr (K::BUF) {
+            bv[u] = br.template load<K::BNT, P>(s < cnt && active ? cu : (I)br.k32);
+          } else {
+            if (s < cnt && active) bv[u] = br.template load<K::BNT, P>(cu);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+          if (k + u < cnt && active) {
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + Num<T>::mul(vv[u], Num<T>::load(bv[u].v[e]));
+          }
+        }
+      }
+    }
+#else
     // j0/j1 are wave-uniform: col/val come through the scalar cache.
     for (int64_t j = j0; j < j1; j += kUnroll) {
       const int cnt = (int)((j1 - j) < kUnroll ? (j1 - j) : kUnroll);
@@ -282,6 +347,7 @@ __device__ __forceinline__ void accumulate(const I* __restrict__ col, const T* _
         }
       }
     }
+#endif
   } else {
     // A batch is R * LPR nonzeros: each lane loads R (col, val) pairs coalesced, the group
     // broadcasts them with ds_bpermute.  R > 1 only when more B-row loads are kept in flight

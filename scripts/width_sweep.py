@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--config", default="products")
     ap.add_argument("--widths", default="1,2,4,8,16,32,64,128,256,512")
     ap.add_argument("--dtypes", default="f32,bf16")
+    ap.add_argument("--idx", default="int32", choices=["int32", "int64"])
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default="0",
@@ -40,6 +41,8 @@ def main():
     m, k, nnz = cfg["m"], cfg["k"], cfg["nnz"]
     dev = torch.device("cuda", 0)
     rp, ci, v32 = synth.csr(m, k, nnz, val_dtype=torch.float32, threads=16)
+    if args.idx == "int64":
+        rp, ci = rp.to(torch.int64), ci.to(torch.int64)
     d_rp, d_ci = rp.to(dev), ci.to(dev)
     rows_chk = 2000
     for dname in args.dtypes.split(","):
@@ -84,7 +87,7 @@ def main():
                     ts.append(e0.elapsed_time(e1) / args.reps)
                 ms = float(np.median(ts))
                 ab = alg_bytes(m, nnz, n, b.element_size())
-                print(json.dumps({"config": args.config, "dtype": dname, "n": n, "variant": var,
+                print(json.dumps({"config": args.config, "dtype": dname, "idx": args.idx, "n": n, "variant": var,
                                   "ms": round(ms, 4),
                                   "gflops": round(2.0 * nnz * n / (ms * 1e-3) / 1e9, 1),
                                   "gather_model_gbs": round(ab / (ms * 1e-3) / 1e9, 1),
