@@ -76,12 +76,14 @@ struct alignas(sizeof(T) * VEC) Pack {
 // of 16-B loads (16 light rows per wave at few registers) while a hub chunk still gets a whole
 // wave with few cross-lane moves per product: the kernel's register count (the larger of the two
 // paths) stays at the light path's.
+// SH (bandwidth configurations, fp32): n need not be a multiple of VEC; the lane holding a row's
+// last columns takes the VEC-wide window ending at column n - 1 (16-B accesses at 4-B alignment).
 template <int VEC_, int LPR_, int U_ = 8, int WPB_ = 4, bool NT_ = false, bool PF_ = false,
           bool BNT_ = false, bool WH_ = false, bool BI_ = false, bool BUF_ = true, int HL_ = 0,
-          int HU_ = 16>
+          int HU_ = 16, bool SH_ = false>
 struct Cfg {
   static constexpr int VEC = VEC_, LPR = LPR_, U = U_, WPB = WPB_;
-  static constexpr bool NT = NT_, PF = PF_, BNT = BNT_, WH = WH_, BI = BI_, BUF = BUF_;
+  static constexpr bool NT = NT_, PF = PF_, BNT = BNT_, WH = WH_, BI = BI_, BUF = BUF_, SH = SH_;
   static constexpr int HL = HL_, HU = HU_;
   // loads in flight per lane of the wave-item form: G * UW * VEC cross-lane moves per batch are
   // unrolled, so UW keeps that at <= 256 (4..32)
@@ -1081,8 +1083,14 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
     j1 = (re - j0 - chunk < chunk) ? re : j0 + chunk;
   }
   for (int64_t c0 = 0; c0 < n; c0 += (int64_t)LPR * VEC) {
-    const int64_t cc = c0 + (int64_t)gl * VEC;
+    int64_t cc = c0 + (int64_t)gl * VEC;
     const bool active = cc < n;
+    if constexpr (K::SH) {
+      // n not a multiple of VEC: the lane holding the row's last columns takes the window ending
+      // at column n - 1; its first columns repeat its neighbour's (the same sums in the same order,
+      // written twice with the same bits)
+      if (active && cc + VEC > n) cc = n - VEC;
+    }
     A acc[VEC];
 #pragma unroll
     for (int e = 0; e < VEC; ++e) acc[e] = A(0);
@@ -1427,6 +1435,34 @@ int launch_vec(const Launch& L, int lpr, bool nt) {
   }
 }
 
+// fp32 rows whose width is not a multiple of 4 above N = 64 in the bandwidth configuration:
+// 16-B lanes with the last window shifted (Cfg::SH) instead of one element per lane, which needs
+// several 64-lane passes there: products N = 99 / 301 10.6 / 31.2 -> 8.5 / 25.2 ms.  At 17-63
+// columns one pass of single elements is as fast or faster (N = 41 / 47 / 63: 4.6 / 5.0 / 6.1 ms
+// against 4.8 / 5.2 / 6.2; such rows cost whole 128-B lines either way); profiles/r03ad_sweep.jsonl.
+template <typename T, typename I>
+int launch_shift(const Launch& L, bool nt) {
+  const int lpr = pick_lpr(L.n, 4);
+  switch (lpr) {
+    case 8: return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L);
+    case 16: return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L);
+    case 32:
+      return nt ? launch_cfg<T, I, Cfg<4, 32, 8, 4, true, false, false, false, false, true, 0, 16, true>>(L)
+                : launch_cfg<T, I, Cfg<4, 32, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L);
+    default:
+      return nt ? launch_cfg<T, I, Cfg<4, 64, 8, 4, true, false, false, false, false, true, 0, 16, true>>(L)
+                : launch_cfg<T, I, Cfg<4, 64, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L);
+  }
+}
+
+bool use_shift_form(const Launch& L, int elem_bytes) {
+  return L.sched.variant == 0 && elem_bytes == 4 && L.n > 64 && L.n % 4 != 0 &&
+         !use_small_form(L.nrows, L.nnz_est, L.n, L.sched) &&
+         !use_mid_form(L.nrows, L.nnz_est, L.n, L.sched) &&
+         !use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched) &&
+         ((uintptr_t)L.b % 4) == 0 && ((uintptr_t)L.c % 4) == 0;
+}
+
 // Rows of 64 B in fp32 (N = 16) above the mid form: four lanes of float4 per light row (16 rows
 // per wave, few registers, so many rows in flight: what bounds these launches) and the hub chunks
 // and heavy rows as wave items in 16-lane one-element groups (HL), so a 512-nonzero chunk is not
@@ -1459,6 +1495,8 @@ int launch_typed(const Launch& L) {
   }
   if constexpr (sizeof(T) == 4) {
     if (use_narrow_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L)) return launch_narrow<T, I>(L);
+    if (use_shift_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
+      return launch_shift<T, I>(L, (L.b_rows * L.ldb * (int64_t)sizeof(T)) > kNtBytes);
   }
   // variant = VEC * 100 + LPR forces a configuration (tuning / tests); 0 = auto.
   const int forced_vec = (L.sched.variant > 0 && !form) ? L.sched.variant / 100 : 0;

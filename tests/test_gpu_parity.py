@@ -734,3 +734,44 @@ def test_narrow_16bit_bandwidth_layout(device, dtype, idx, n):
     o2 = ops.spmm_csr_device(*d, m, k, options=ops.make_options(variant=wide * 100 + lpr))
     torch.cuda.synchronize()
     assert torch.equal(o2.view(torch.int16), out.view(torch.int16))
+
+
+@pytest.mark.parametrize("idx", [torch.int32, torch.int64])
+@pytest.mark.parametrize("n", [17, 18, 41, 47, 63, 99, 301])
+def test_shifted_window_odd_widths(device, idx, n):
+    """fp32 widths that are not a multiple of 4 above N = 64 in the bandwidth configuration (above
+    kPrefetchNnz nonzeros) run 16-B lanes whose last window ends at column n - 1 (Cfg::SH; the
+    shifted lane repeats its neighbour's first columns with the same bits).  Bit-exact against the
+    oracle for contiguous B / C, strided views with a 4-B-offset base (ldb, ldc > n), the fused
+    epilogue, hub rows, and against the one-element-per-lane configuration forced."""
+    rng = np.random.default_rng(5100 + n)
+    m, k = 120_000, 90_000
+    deg = rng.integers(0, 60, size=m)
+    deg[17] = 3000
+    deg[9_999] = 700
+    rp, ci, v = random_csr(m, k, deg, rng, idx, torch.float32)
+    assert ci.numel() > (3 << 20)
+    b = random_dense(k, n, rng)
+    d = (rp.to(device), ci.to(device), v.to(device), b.to(device))
+    ref = oracle_spmm(rp, ci, v, b)
+    out = fs.spmm(d[0], d[1], d[2], m, k, d[3])
+    torch.cuda.synchronize()
+    assert_bitwise(out, ref, f"n={n} auto")
+    lpr = min(64, max(4, 1 << (n - 1).bit_length()))
+    o1 = ops.spmm_csr_device(*d, m, k, options=ops.make_options(variant=100 + lpr))
+    torch.cuda.synchronize()
+    assert torch.equal(o1.view(torch.int32), out.view(torch.int32))
+    # strided views, base offset by one element (4 B): B[:, 1:n+1] of a (k, n+3) buffer
+    bbig = torch.zeros((k, n + 3), dtype=torch.float32, device=device)
+    bbig[:, 1:n + 1] = d[3]
+    cbig = torch.full((m, n + 5), float("nan"), device=device)
+    ops.spmm_csr_device(d[0], d[1], d[2], bbig[:, 1:n + 1], m, k, out=cbig[:, 3:n + 3])
+    torch.cuda.synchronize()
+    assert_bitwise(cbig[:, 3:n + 3], ref, f"n={n} strided, offset base")
+    assert torch.isnan(cbig[:, :3]).all() and torch.isnan(cbig[:, n + 3:]).all()
+    bias = random_dense(1, n, rng)[0]
+    kern = ops.SpmmCsrKernel(m, k, n, ci.numel(), idx, torch.float32, device)
+    o3 = torch.full((m, n), float("nan"), device=device)
+    kern(*d, o3, bias=bias.to(device), relu=True)
+    torch.cuda.synchronize()
+    assert_bitwise(o3, oracle.bias_act(ref, to_oracle(bias), "relu", dtype="f32"), "epilogue")
