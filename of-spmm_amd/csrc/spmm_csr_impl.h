@@ -1520,7 +1520,16 @@ int launch_typed(const Launch& L) {
   OFX_REQUIRE(vec > 0, OFX_EINVAL,
               "spmm_csr: variant %d not applicable (n=%lld ldb=%lld ldc=%lld or pointer alignment)",
               L.sched.variant, (long long)L.n, (long long)L.ldb, (long long)L.ldc);
-  const int lpr = forced_lpr ? forced_lpr : pick_lpr(L.n, vec);
+  int lpr = forced_lpr ? forced_lpr : pick_lpr(L.n, vec);
+  // rows of fewer than 8 single-element lanes in the bandwidth configuration: 8-lane groups (idle
+  // lanes included), not 4-lane ones; fp32 N = 1 / 2 / 3 / 4 on products -11 / -9 / -8 / -9%, on
+  // the 1M power-law graph N = 1 / 4 -10 / -22%.  16 lanes won on products at N = 2-8 by 2-8% but
+  // lost on the power-law graph by 4-48% (profiles/r03af_sweep.jsonl)
+  if (!forced_lpr && vec == 1 && lpr < 8 && L.sched.variant == 0 &&
+      !use_small_form(L.nrows, L.nnz_est, L.n, L.sched) &&
+      !use_mid_form(L.nrows, L.nnz_est, L.n, L.sched) &&
+      !use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched))
+    lpr = 8;
   const bool nt = (L.b_rows * L.ldb * (int64_t)sizeof(T)) > kNtBytes;
   switch (vec) {
     case 1: return launch_vec<T, I, 1>(L, lpr, nt);

@@ -737,7 +737,7 @@ def test_narrow_16bit_bandwidth_layout(device, dtype, idx, n):
 
 
 @pytest.mark.parametrize("idx", [torch.int32, torch.int64])
-@pytest.mark.parametrize("n", [17, 18, 41, 47, 63, 99, 301])
+@pytest.mark.parametrize("n", [1, 3, 5, 17, 18, 41, 47, 63, 99, 301])
 def test_shifted_window_odd_widths(device, idx, n):
     """fp32 widths that are not a multiple of 4 above N = 64 in the bandwidth configuration (above
     kPrefetchNnz nonzeros) run 16-B lanes whose last window ends at column n - 1 (Cfg::SH; the
