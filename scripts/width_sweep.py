@@ -23,6 +23,8 @@ DT = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16, "f64":
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="products")
+    ap.add_argument("--graph", default="", help="rows:nonzeros of a synthetic power-law graph "
+                                                   "(rows = cols) instead of --config")
     ap.add_argument("--widths", default="1,2,4,8,16,32,64,128,256,512")
     ap.add_argument("--dtypes", default="f32,bf16")
     ap.add_argument("--idx", default="int32", choices=["int32", "int64"])
@@ -37,8 +39,13 @@ def main():
     from bench import alg_bytes
     from oracle import oracle
 
-    cfg = synth.CONFIGS[args.config]
-    m, k, nnz = cfg["m"], cfg["k"], cfg["nnz"]
+    if args.graph:
+        m, nnz = (int(x) for x in args.graph.split(":"))
+        k = m
+        args.config = f"graph{m}x{nnz}"
+    else:
+        cfg = synth.CONFIGS[args.config]
+        m, k, nnz = cfg["m"], cfg["k"], cfg["nnz"]
     dev = torch.device("cuda", 0)
     rp, ci, v32 = synth.csr(m, k, nnz, val_dtype=torch.float32, threads=16)
     if args.idx == "int64":
