@@ -41,6 +41,51 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
+class PhaseWatch:
+    """Per-rank phase log and deadline.  Every rank prints each phase it
+    enters, with its elapsed time, to stderr; a watchdog thread ends a rank whose phase outlives
+    its limit: it names the phase, aborts the native RCCL communicator (so peers blocked on this
+    rank fail rather than hang) and exits with EXIT_STALL.  A rank that has touched the GPU only
+    ever exits; it is never re-exec'd."""
+
+    EXIT_STALL = 75
+
+    def __init__(self, rank: int, world: int, scale: float = 1.0):
+        import threading
+        self.rank, self.world, self.scale = rank, world, scale
+        self.t0 = time.monotonic()
+        self.name, self.started, self.deadline = "start", self.t0, None
+        self.on_abort = []  # callables run before the exit (communicator abort)
+        self._lock = threading.Lock()
+        threading.Thread(target=self._watch, name="phase-watch", daemon=True).start()
+
+    def phase(self, name: str, limit_s: float | None = None):
+        now = time.monotonic()
+        limit = None if limit_s is None else limit_s * self.scale
+        with self._lock:
+            self.name, self.started = name, now
+            self.deadline = None if limit is None else now + limit
+        print(f"[rank {self.rank}/{self.world}] {now - self.t0:8.1f} s  phase: {name}"
+              + (f" (limit {limit:.0f} s)" if limit is not None else ""), file=sys.stderr, flush=True)
+
+    def _watch(self):
+        while True:
+            time.sleep(0.25)
+            with self._lock:
+                name, started, deadline = self.name, self.started, self.deadline
+            if deadline is None or time.monotonic() <= deadline:
+                continue
+            print(f"[rank {self.rank}/{self.world}] STALLED: phase '{name}' still running after "
+                  f"{time.monotonic() - started:.0f} s (limit {deadline - started:.0f} s); aborting "
+                  f"the communicator and exiting {self.EXIT_STALL}", file=sys.stderr, flush=True)
+            for f in self.on_abort:
+                try:
+                    f()
+                except Exception as e:  # noqa: BLE001 -- exiting anyway
+                    print(f"[rank {self.rank}] abort hook failed: {e!r}", file=sys.stderr, flush=True)
+            os._exit(self.EXIT_STALL)
+
+
 def alg_bytes(rows: int, nnz: int, n: int, s_v: int, s_i: int = 4) -> int:
     """Gather model: row_ptr once, col/val once, one B row per nonzero, C once."""
     return s_i * (rows + 1) + (s_i + s_v) * nnz + s_v * nnz * n + s_v * rows * n
@@ -96,7 +141,7 @@ def _claim_stdout():
     return os.fdopen(real, "w")
 
 
-def _spawn_ranks_if_needed(gpus: int):
+def _spawn_ranks_if_needed(gpus: int, deadline_s: float):
     """`python bench.py --gpus N` without a launcher: start the N ranks here (the environment
     contract of oneflow.distributed.launch, python/oneflow/distributed/launch.py:103-140) and exit
     with their status.  Runs before anything touches the GPU; the package is not imported (its
@@ -108,8 +153,10 @@ def _spawn_ranks_if_needed(gpus: int):
         "ofx_launch", os.path.join(ROOT, "of-spmm_amd", "oneflow_spmm", "launch.py"))
     launch = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(launch)
-    log(f"[bench] --gpus {gpus} without a launcher: spawning {gpus} local ranks")
-    sys.exit(launch.spawn_local_ranks(gpus, [os.path.abspath(__file__), *sys.argv[1:]]))
+    log(f"[bench] --gpus {gpus} without a launcher: spawning {gpus} local ranks "
+        f"(deadline {deadline_s:.0f} s)")
+    sys.exit(launch.spawn_local_ranks(gpus, [os.path.abspath(__file__), *sys.argv[1:]],
+                                      timeout=deadline_s))
 
 
 def main():
@@ -141,11 +188,20 @@ def main():
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: rehearse the N>1 path on host tensors with the kCPU kernel (needs "
                          "--backend gloo; not a performance number)")
+    ap.add_argument("--deadline", type=float, default=1800.0,
+                    help="seconds the whole multi-rank run may take when bench.py spawns its ranks; "
+                         "past it the ranks are terminated and the exit status is 124")
+    ap.add_argument("--phase-timeout-scale", type=float,
+                    default=float(os.environ.get("OFX_PHASE_TIMEOUT_SCALE", "1")),
+                    help="multiplies every per-rank phase limit (N>1: a rank stalled in a phase "
+                         "past its limit names it and exits 75)")
+    ap.add_argument("--stall-test", default=os.environ.get("OFX_BENCH_STALL", ""),
+                    help="tests only: 'rank:phase' makes that rank sleep in that phase")
     ap.add_argument("--tune-budget", type=float, default=120.0,
                     help="seconds of exchange-candidate timing at setup (N>1); the candidates run "
                          "in order of their modelled time, the rest are skipped")
     args = ap.parse_args()
-    _spawn_ranks_if_needed(args.gpus)
+    _spawn_ranks_if_needed(args.gpus, args.deadline)
     out_stream = _claim_stdout()
 
     t_wall0 = time.time()
@@ -172,6 +228,16 @@ def main():
         if on_gpu:
             torch.cuda.synchronize()
     rowsplit = world > 1 or args.force_rowsplit
+    watch = PhaseWatch(rank, world, args.phase_timeout_scale) if rowsplit else None
+    stall_rank, _, stall_phase = args.stall_test.partition(":")
+
+    def enter_phase(name, limit_s):
+        if watch is None:
+            return
+        watch.phase(name, limit_s)
+        if stall_phase and int(stall_rank) == rank and name.startswith(stall_phase):
+            time.sleep(1e6)  # the watchdog ends this rank
+    enter_phase("process group init", 300)
     if rowsplit:
         if world == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -195,6 +261,7 @@ def main():
     threads = args.cpu_threads
 
     # ---- inputs (this rank's rows only), resident in HBM before timing -------------------------
+    enter_phase("inputs", 900)
     t0 = time.time()
     rp_full = synth.row_ptr(m, k, nnz)
     lo, hi = fs._C.balanced_range(m, world, rank)
@@ -223,12 +290,15 @@ def main():
             def step():
                 kern(d_rp, d_ci, d_v, d_b, out)
     else:
+        enter_phase("communicator init", 400)
         try:
             rs = RowSplitSpmm(m, k, n, nnz_local, dt, torch.int32, device,
                               comm="torch" if rehearsal else "auto")
         except fs.OfxError as e:  # own RCCL communicator refused: torch.distributed's (also RCCL)
             log(f"[bench] native RCCL communicator unavailable ({e}); using torch.distributed")
             rs = RowSplitSpmm(m, k, n, nnz_local, dt, torch.int32, device, comm="torch")
+        watch.on_abort.append(rs.abort)
+        enter_phase("bind (shards, remap, plans, halo and grid layouts)", 900)
         klo, khi = rs.k_range
         rs.load_shard(synth.dense(klo, khi, n, dt, device=device))
         full = None
@@ -255,7 +325,8 @@ def main():
                 rs.set_halo_pipeline(args.pipeline or 1)
         else:
             t_tune = time.time()
-            comm_times = rs.tune(out, force=args.force_rowsplit, budget_s=args.tune_budget, log=log)
+            comm_times = rs.tune(out, force=args.force_rowsplit, budget_s=args.tune_budget, log=log,
+                                 on_candidate=lambda nm: enter_phase(f"tune: {nm}", 180))
             tune_s = time.time() - t_tune
             log("[bench] exchange candidates (ms, max over ranks; model-predicted): " +
                 ", ".join(f"{kk} {vv:.3f} ({rs.tune_report[kk]['predicted_ms']:.3f})"
@@ -268,12 +339,14 @@ def main():
             rs.step(out)
 
     # ---- warmup + timed region -----------------------------------------------------------------
+    enter_phase("warmup", 300)
     for _ in range(args.warmup):
         step()
     sync()
     if rowsplit:
         dist.barrier()
     sync()
+    enter_phase("timed steps", 600)
     ev_start, ev_end = Mark(on_gpu), Mark(on_gpu)
     t_start = time.perf_counter()
     ev_start.record()
@@ -292,6 +365,7 @@ def main():
     flops = 2.0 * nnz * n
     value = flops * args.steps / elapsed / 1e9
 
+    enter_phase("phase timing and report", 600)
     # ---- dominant-kernel timing: events on the launch stream around the SpMM launches ---------
     # N=1: the op call (plan + main + reduce; main dominates).  N>1: the local SpMM after the
     # gather.  Measured over a separate short run so the timed region above has no extra events.
@@ -424,6 +498,12 @@ def main():
             "remote_rows_total": (rs.k - (khi - klo)),
             "allgather_tune_ms": {kk: (round(vv, 4) if np.isfinite(vv) else None)
                                   for kk, vv in comm_times.items()},
+            # the north star's configuration (plain row split + one all-gather of B), always
+            # measured by tune() whichever exchange wins: ms per step and its aggregate rate
+            "rowsplit_allgather_p1": ({"ms": round(comm_times[ag1], 4),
+                                       "gflops": round(flops / (comm_times[ag1] * 1e-3) / 1e9, 2)}
+                                      if (ag1 := f"{'torch' if rehearsal else 'rccl'}/p1") in comm_times
+                                      and np.isfinite(comm_times[ag1]) else None),
             "tune_errors": getattr(rs, "tune_errors", {}) or None,
             # every candidate: model time (xGMI assumption), the model refitted to
             # the first measurement, the measured time (max over ranks) and whether it ran
@@ -535,8 +615,11 @@ def main():
     if rank == 0:
         print(json.dumps(result), file=out_stream, flush=True)
     if rowsplit:
+        enter_phase("shutdown", 120)
         rs.close()
         dist.destroy_process_group()
+        if watch is not None:
+            watch.phase("done")
 
 
 if __name__ == "__main__":

@@ -140,6 +140,14 @@ int ofx_spmm_csr_plan(void* stream, int idx_dtype, int val_dtype, int64_t m, int
                       int64_t nnz, const void* row_ptr, int64_t row_begin, int64_t row_end,
                       void* workspace, size_t workspace_bytes, const ofx_spmm_options* opts);
 
+/* Bounds-checked builds only (OFX_DEBUG_BOUNDS, `make -C of-spmm_amd debug`): every global access
+ * of the forward kernels is checked against its launch's allocations before it is made, and an
+ * access outside all of them is skipped and recorded.  Synchronises the device and copies the
+ * first violation to out[8] = {violations, site (file tag * 100000 + line), address, bytes,
+ * block, thread, launch tag, 0}; reset != 0 clears the record.  A release build returns
+ * OFX_EUNSUPPORTED.  No reference counterpart (a debugging aid of this port).                  */
+int ofx_debug_bounds_read(uint64_t* out, int reset);
+
 /* Fused epilogue: out = act(A @ B + bias), bit-identical to the
  * composition spmm_csr -> bias_add (BroadcastElementwiseBinary kAdd over axis 1,
  * oneflow/user/kernels/bias_add_kernel.cpp:25-53) -> relu (UnaryFunctor<kRelu>,
@@ -293,6 +301,18 @@ int ofx_graph_launch(void* exec, void* stream);
 #define OFX_UNIQUE_ID_BYTES 128
 int ofx_comm_get_unique_id(void* uid_out /* OFX_UNIQUE_ID_BYTES */);
 int ofx_comm_init_rank(void** comm, int nranks, const void* uid, int rank);
+/* ofx_comm_init_rank with a deadline: a non-blocking communicator (ncclCommInitRankConfig with
+ * config.blocking = 0) whose set-up is polled (ncclCommGetAsyncError); if a peer has not joined
+ * within timeout_s seconds the communicator is aborted (ncclCommAbort) and OFX_ECOMM returned
+ * with the wait named.  Every later call on it (all-gathers, send/recv groups, finalize) is
+ * bounded by the same timeout and aborts the communicator when it expires.  Replaces the
+ * unbounded EagerNcclCommMgr::CreateNcclComm (eager_nccl_comm_manager.cpp:57-80).           */
+int ofx_comm_init_rank_deadline(void** comm, int nranks, const void* uid, int rank,
+                                double timeout_s);
+/* ncclCommAbort: drops the communicator's pending operations so that peers waiting on this rank
+ * fail too (a rank's watchdog calls it before exiting). */
+int ofx_comm_abort(void* comm);
+/* ncclCommFinalize (waited for) + ncclCommDestroy. */
 int ofx_comm_destroy(void* comm);
 /* ncclCommCount / ncclCommUserRank of a communicator. */
 int ofx_comm_count(void* comm, int* nranks, int* rank);

@@ -10,15 +10,35 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstring>
+#include <thread>
 
 #include "ofx_internal.h"
 #include "spmm_common.h"
 
+// A call on a communicator.  Communicators made by ofx_comm_init_rank_deadline are non-blocking
+// (ncclConfig_t.blocking = 0): any call on them may return ncclInProgress, and the operation is
+// then complete once ncclCommGetAsyncError stops reporting ncclInProgress (comm_wait, bounded by
+// the communicator's deadline).  Blocking communicators return ncclSuccess or an error.
 #define OFX_NCCL_CHECK(expr)                                                                   \
   do {                                                                                         \
     ncclResult_t ofx_r_ = (expr);                                                              \
     if (ofx_r_ != ncclSuccess)                                                                 \
+      return ::ofx::fail(OFX_ECOMM, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(ofx_r_), \
+                         __FILE__, __LINE__);                                                  \
+  } while (0)
+#define OFX_NCCL_CALL(comm, expr)                                                              \
+  do {                                                                                         \
+    const int ofx_rc_ = comm_wait((comm), (expr), #expr);                                      \
+    if (ofx_rc_ != OFX_OK) return ofx_rc_;                                                     \
+  } while (0)
+// Between ncclGroupStart and ncclGroupEnd a call only records its operation: ncclInProgress
+// there is not waited for (the group's ncclGroupEnd is, through OFX_NCCL_CALL).
+#define OFX_NCCL_GROUPED(expr)                                                                 \
+  do {                                                                                         \
+    ncclResult_t ofx_r_ = (expr);                                                              \
+    if (ofx_r_ != ncclSuccess && ofx_r_ != ncclInProgress)                                     \
       return ::ofx::fail(OFX_ECOMM, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(ofx_r_), \
                          __FILE__, __LINE__);                                                  \
   } while (0)
@@ -36,6 +56,39 @@ bool nccl_dtype(int dt, ncclDataType_t* out) {
     case OFX_DT_BFLOAT16: *out = ncclBfloat16; return true;
     default: return false;
   }
+}
+
+// Seconds a call on a non-blocking communicator may stay in progress (ofx_comm_init_rank_deadline
+// sets it; the reference's blocking NCCL calls have no bound).
+double g_call_timeout_s = 300.0;
+
+double seconds_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// Completes a call that returned ncclInProgress (non-blocking communicator): polls the
+// communicator's state until it leaves ncclInProgress, or aborts it after g_call_timeout_s so
+// that peers blocked on this rank fail as well instead of hanging.
+int comm_wait(ncclComm_t c, ncclResult_t r, const char* what) {
+  if (r == ncclSuccess) return OFX_OK;
+  if (r != ncclInProgress)
+    return ofx::fail(OFX_ECOMM, "%s failed: %s", what, ncclGetErrorString(r));
+  const auto t0 = std::chrono::steady_clock::now();
+  ncclResult_t st = ncclInProgress;
+  while (true) {
+    const ncclResult_t q = ncclCommGetAsyncError(c, &st);
+    if (q != ncclSuccess)
+      return ofx::fail(OFX_ECOMM, "%s: ncclCommGetAsyncError failed: %s", what, ncclGetErrorString(q));
+    if (st != ncclInProgress) break;
+    if (seconds_since(t0) > g_call_timeout_s) {
+      ncclCommAbort(c);
+      return ofx::fail(OFX_ECOMM, "%s: still in progress after %.0f s; communicator aborted", what,
+                       g_call_timeout_s);
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+  if (st != ncclSuccess) return ofx::fail(OFX_ECOMM, "%s failed: %s", what, ncclGetErrorString(st));
+  return OFX_OK;
 }
 }  // namespace
 
@@ -59,8 +112,67 @@ extern "C" int ofx_comm_init_rank(void** comm, int nranks, const void* uid, int 
   return OFX_OK;
 }
 
+// ofx_comm_init_rank with a deadline: a non-blocking communicator
+// (ncclCommInitRankConfig, config.blocking = 0) whose set-up is polled with
+// ncclCommGetAsyncError; a rank whose peers have not all joined within `timeout_s` seconds aborts
+// the communicator (ncclCommAbort) and returns OFX_ECOMM naming the wait, instead of blocking
+// forever inside ncclCommInitRank.  Every later call on the communicator is bounded the same way
+// (OFX_NCCL_CALL).  The reference's EagerNcclCommMgr::CreateNcclComm
+// (oneflow/core/job/eager_nccl_comm_manager.cpp:57-80) blocks without a bound.
+extern "C" int ofx_comm_init_rank_deadline(void** comm, int nranks, const void* uid, int rank,
+                                           double timeout_s) {
+  OFX_REQUIRE(comm && uid && nranks > 0 && rank >= 0 && rank < nranks && timeout_s > 0, OFX_EINVAL,
+              "comm_init_rank_deadline: bad arguments (nranks=%d rank=%d timeout=%g)", nranks, rank,
+              timeout_s);
+  g_call_timeout_s = timeout_s;
+  ncclUniqueId id;
+  std::memcpy(&id, uid, sizeof(id));
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  ncclComm_t c = nullptr;
+  const ncclResult_t r = ncclCommInitRankConfig(&c, nranks, id, rank, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    if (c != nullptr) ncclCommAbort(c);
+    return ofx::fail(OFX_ECOMM, "comm_init_rank_deadline: ncclCommInitRankConfig failed: %s",
+                     ncclGetErrorString(r));
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  ncclResult_t st = r;
+  while (st == ncclInProgress) {
+    const ncclResult_t q = ncclCommGetAsyncError(c, &st);
+    if (q != ncclSuccess) st = q;
+    if (st != ncclInProgress) break;
+    if (seconds_since(t0) > timeout_s) {
+      ncclCommAbort(c);
+      return ofx::fail(OFX_ECOMM,
+                       "comm_init_rank_deadline: rank %d of %d: communicator not set up after %.0f s "
+                       "(a peer did not join); aborted", rank, nranks, timeout_s);
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  }
+  if (st != ncclSuccess) {
+    ncclCommAbort(c);
+    return ofx::fail(OFX_ECOMM, "comm_init_rank_deadline: rank %d of %d: %s", rank, nranks,
+                     ncclGetErrorString(st));
+  }
+  *comm = c;
+  return OFX_OK;
+}
+
+// Aborts a communicator (ncclCommAbort): its pending operations are dropped and peers blocked on
+// it fail.  Called by a rank's phase watchdog before it exits (bench.py).
+extern "C" int ofx_comm_abort(void* comm) {
+  if (comm) OFX_NCCL_CHECK(ncclCommAbort(static_cast<ncclComm_t>(comm)));
+  return OFX_OK;
+}
+
+// Finalize (flushes the communicator's operations; a non-blocking communicator may report
+// ncclInProgress, waited for with the call deadline), then destroy.
 extern "C" int ofx_comm_destroy(void* comm) {
-  if (comm) OFX_NCCL_CHECK(ncclCommDestroy(static_cast<ncclComm_t>(comm)));
+  if (comm == nullptr) return OFX_OK;
+  ncclComm_t c = static_cast<ncclComm_t>(comm);
+  OFX_NCCL_CALL(c, ncclCommFinalize(c));
+  OFX_NCCL_CHECK(ncclCommDestroy(c));
   return OFX_OK;
 }
 
@@ -77,8 +189,8 @@ extern "C" int ofx_allgather(void* stream, const void* in, void* out, size_t cou
   ncclDataType_t t;
   OFX_REQUIRE(nccl_dtype(dtype, &t), OFX_EUNSUPPORTED, "allgather: unsupported dtype %d", dtype);
   OFX_REQUIRE(comm && (count == 0 || (in && out)), OFX_EINVAL, "allgather: NULL argument");
-  OFX_NCCL_CHECK(ncclAllGather(in, out, count, t, static_cast<ncclComm_t>(comm),
-                               static_cast<hipStream_t>(stream)));
+  ncclComm_t c = static_cast<ncclComm_t>(comm);
+  OFX_NCCL_CALL(c, ncclAllGather(in, out, count, t, c, static_cast<hipStream_t>(stream)));
   return OFX_OK;
 }
 
@@ -100,10 +212,10 @@ extern "C" int ofx_allgather_p2p(void* stream, void* buf, size_t count, int dtyp
   OFX_NCCL_CHECK(ncclGroupStart());
   for (int d = 1; d < nranks; ++d) {  // peers in a rotated order so links are loaded evenly
     const int to = (rank + d) % nranks, from = (rank - d + nranks) % nranks;
-    OFX_NCCL_CHECK(ncclSend(base + (size_t)rank * count * esz, count, t, to, c, s));
-    OFX_NCCL_CHECK(ncclRecv(base + (size_t)from * count * esz, count, t, from, c, s));
+    OFX_NCCL_GROUPED(ncclSend(base + (size_t)rank * count * esz, count, t, to, c, s));
+    OFX_NCCL_GROUPED(ncclRecv(base + (size_t)from * count * esz, count, t, from, c, s));
   }
-  OFX_NCCL_CHECK(ncclGroupEnd());
+  OFX_NCCL_CALL(c, ncclGroupEnd());
   return OFX_OK;
 }
 
@@ -132,13 +244,13 @@ extern "C" int ofx_exchange_rows(void* stream, void* comm, int dtype, int64_t n,
   for (int d = 1; d < nranks; ++d) {
     const int to = (rank + d) % nranks, from = (rank - d + nranks) % nranks;
     if (send_counts[to] > 0)
-      OFX_NCCL_CHECK(ncclSend(sb + (size_t)send_offsets[to] * row_bytes,
-                              (size_t)(send_counts[to] * n), t, to, c, s));
+      OFX_NCCL_GROUPED(ncclSend(sb + (size_t)send_offsets[to] * row_bytes,
+                                (size_t)(send_counts[to] * n), t, to, c, s));
     if (recv_counts[from] > 0)
-      OFX_NCCL_CHECK(ncclRecv(rb + (size_t)recv_offsets[from] * row_bytes,
-                              (size_t)(recv_counts[from] * n), t, from, c, s));
+      OFX_NCCL_GROUPED(ncclRecv(rb + (size_t)recv_offsets[from] * row_bytes,
+                                (size_t)(recv_counts[from] * n), t, from, c, s));
   }
-  OFX_NCCL_CHECK(ncclGroupEnd());
+  OFX_NCCL_CALL(c, ncclGroupEnd());
   return OFX_OK;
 }
 

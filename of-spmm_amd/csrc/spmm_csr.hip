@@ -19,6 +19,7 @@
 #include "spmm_common.h"
 #include "spmm_plan.h"
 #include "spmm_launch.h"
+#include "dbg_bounds.h"
 
 namespace ofx {
 namespace {
@@ -185,6 +186,14 @@ extern "C" int ofx_spmm_csr_plan(void* stream, int idx_dtype, int val_dtype, int
               "spmm_csr_plan: workspace of %zu bytes is smaller than the %zu bytes required",
               workspace_bytes, w.total);
   hipStream_t st = static_cast<hipStream_t>(stream);
+#ifdef OFX_DEBUG_BOUNDS
+  {  // the planner's allocations (dbg_bounds.h): row_ptr and the workspace
+    dbg::HostBounds hb;
+    hb.add(row_ptr, (uint64_t)((row_end + 1) * (idx_dtype == OFX_DT_INT32 ? 4 : 8)));
+    hb.add(workspace, workspace_bytes);
+    OFX_REQUIRE(hb.publish(st, 3ull << 48) == 0, OFX_EDEVICE, "spmm_csr_plan: debug bounds");
+  }
+#endif
   plan::WorkList wl{};
   char* ws = static_cast<char*>(workspace);
   if (idx_dtype == OFX_DT_INT32)
@@ -280,4 +289,36 @@ extern "C" int ofx_synth_dense(void* stream, int val_dtype, int64_t r_begin, int
   }
   OFX_HIP_CHECK(hipGetLastError());
   return OFX_OK;
+}
+
+// ---- OFX_DEBUG_BOUNDS builds (dbg_bounds.h) ----------------------------------------------------
+#ifdef OFX_DEBUG_BOUNDS
+namespace ofx {
+// the first violation of any launch: kHitWords device words, zeroed once
+unsigned long long* dbg_hit_words() {
+  static unsigned long long* words = nullptr;
+  if (words == nullptr) {
+    void* p = nullptr;
+    if (hipMalloc(&p, dbg::kHitWords * sizeof(unsigned long long)) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, dbg::kHitWords * sizeof(unsigned long long)) != hipSuccess) return nullptr;
+    words = static_cast<unsigned long long*>(p);
+  }
+  return words;
+}
+}  // namespace ofx
+#endif
+
+extern "C" int ofx_debug_bounds_read(uint64_t* out, int reset) {
+#ifdef OFX_DEBUG_BOUNDS
+  OFX_REQUIRE(out != nullptr, OFX_EINVAL, "debug_bounds_read: out is NULL");
+  unsigned long long* w = dbg_hit_words();
+  OFX_REQUIRE(w != nullptr, OFX_EDEVICE, "debug_bounds_read: no hit buffer");
+  OFX_HIP_CHECK(hipDeviceSynchronize());
+  OFX_HIP_CHECK(hipMemcpy(out, w, dbg::kHitWords * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (reset) OFX_HIP_CHECK(hipMemset(w, 0, dbg::kHitWords * sizeof(uint64_t)));
+  return OFX_OK;
+#else
+  (void)out, (void)reset;
+  return fail(OFX_EUNSUPPORTED, "debug_bounds_read: a release build (build with OFX_DEBUG_BOUNDS)");
+#endif
 }

@@ -42,6 +42,7 @@
 #include "spmm_common.h"
 #include "spmm_plan.h"
 #include "spmm_launch.h"
+#include "dbg_bounds.h"
 
 namespace ofx {
 namespace {
@@ -116,7 +117,12 @@ struct RawOf<f16> {
 };
 
 template <bool NT, typename X>
-__device__ __forceinline__ X ld_stream(const X* p) {
+__device__ __forceinline__ X ld_stream(const X* p, int line = __builtin_LINE()) {
+#ifdef OFX_DEBUG_BOUNDS
+  if (!dok(p, sizeof(X), line)) return X{};
+#else
+  (void)line;
+#endif
   if constexpr (NT) {
     using R = typename RawOf<X>::type;
     const R r = __builtin_nontemporal_load(reinterpret_cast<const R*>(p));
@@ -232,7 +238,9 @@ struct BRows {
         return __builtin_bit_cast(P, __builtin_amdgcn_raw_buffer_load_b16(rsrc, off, 0, aux));
       }
     } else {
-      return ld_brow<NTB, P>(row((int64_t)c));
+      const T* q = row((int64_t)c);
+      if (!OFX_DOK(q, sizeof(P))) return P{};  // OFX_DEBUG_BOUNDS builds only
+      return ld_brow<NTB, P>(q);
     }
   }
 };
@@ -467,9 +475,9 @@ __device__ __forceinline__ void accumulate_wave(const I* __restrict__ col, const
       v[r] = 0;
       const int idx = r * 64 + lane;
       if (idx < n_) {
-        c[r] = col[jb + idx];
-        const int64_t jv = vperm ? (int64_t)vperm[jb + idx] : jb + idx;
-        v[r] = Num<T>::load(val[jv]);
+        c[r] = OFX_LD(col + (jb + idx));
+        const int64_t jv = vperm ? (int64_t)OFX_LD(vperm + (jb + idx)) : jb + idx;
+        v[r] = Num<T>::load(OFX_LD(val + jv));
       }
     }
   };
@@ -524,6 +532,7 @@ __device__ __forceinline__ void accumulate_wave(const I* __restrict__ col, const
 template <typename T, int VEC, bool NT>
 __device__ __forceinline__ void store_row(T* __restrict__ p, const typename Num<T>::acc (&acc)[VEC],
                                           const T* __restrict__ bias, int act) {
+  if (!OFX_DOK(p, sizeof(Pack<T, VEC>)) || (bias && !OFX_DOK(bias, sizeof(T) * VEC))) return;  // debug
   Pack<T, VEC> o;
   if (bias == nullptr && act == OFX_ACT_NONE) {  // uniform: the plain op pays one branch
 #pragma unroll
@@ -542,6 +551,7 @@ __device__ __forceinline__ void store_row(T* __restrict__ p, const typename Num<
 
 template <typename A, int VEC>
 __device__ __forceinline__ void store_partial(A* __restrict__ p, const A (&acc)[VEC]) {
+  if (!OFX_DOK(p, sizeof(A) * VEC)) return;  // OFX_DEBUG_BOUNDS builds only
 #pragma unroll
   for (int e = 0; e < VEC; ++e) p[e] = acc[e];
 }
@@ -645,8 +655,8 @@ __device__ __forceinline__ void block_accumulate(const I* __restrict__ col,
       const int64_t j = j0 + s * SPAN + e;
       // past j1: nonzero j1 - 1 again (a valid row; its products are never added)
       const int64_t jc = j < j1 ? j : j1 - 1;
-      c[p] = col[jc];
-      v[p] = Num<T>::load(val[vperm ? (int64_t)vperm[jc] : jc]);
+      c[p] = OFX_LD(col + jc);
+      v[p] = Num<T>::load(OFX_LD(val + (vperm ? (int64_t)OFX_LD(vperm + jc) : jc)));
     }
   };
   auto span_store = [&](int64_t s, const I (&c)[PT], const A (&v)[PT]) {
@@ -834,8 +844,8 @@ __global__ void __launch_bounds__(64 * K::WPB)
   __syncthreads();
   const int64_t lr = row0 + gb;
   if (lr < nrows) {
-    const int64_t rs = (int64_t)rp[row_begin + lr];
-    const int64_t re = (int64_t)rp[row_begin + lr + 1];
+    const int64_t rs = (int64_t)OFX_LD(rp + (row_begin + lr));
+    const int64_t re = (int64_t)OFX_LD(rp + (row_begin + lr + 1));
     const int64_t len = re - rs;
     if (len > light || len > split) {
       if (gl == 0) heavy_rows[atomicAdd(&nheavy, 1)] = gb;
@@ -857,8 +867,8 @@ __global__ void __launch_bounds__(64 * K::WPB)
   const bool chain = wave == 0 && q == 0;
   for (int h = 0; h < nh; ++h) {
     const int64_t hr = row0 + heavy_rows[h];
-    const int64_t rs = (int64_t)rp[row_begin + hr];
-    const int64_t re = (int64_t)rp[row_begin + hr + 1];
+    const int64_t rs = (int64_t)OFX_LD(rp + (row_begin + hr));
+    const int64_t re = (int64_t)OFX_LD(rp + (row_begin + hr + 1));
     const bool split_row = re - rs > split;
     const int64_t nc = split_row ? num_chunks(re - rs, chunk) : 1;
     // chunks of whole batches: the row in one chunked pass (block_accumulate)
@@ -934,20 +944,20 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
       // the wave_blocks * WPB waves stride over the items (the grid bound is an estimate; the
       // plan's counters hold the count), so the launch carries no blocks that only exit
       const int wgl = lane & (WL - 1);
-      const int64_t nchunks = (int64_t)counters[0];
-      const int64_t nheavy = (int64_t)counters[3] - (int64_t)counters[2];  // bin 0
+      const int64_t nchunks = (int64_t)OFX_LD(counters + 0);
+      const int64_t nheavy = (int64_t)OFX_LD(counters + 3) - (int64_t)OFX_LD(counters + 2);  // bin 0
       for (int64_t w = bid * kWaves + wave; w < nchunks + nheavy; w += wave_blocks * kWaves) {
         int64_t wr, wc = -1;
         if (w < nchunks) {
-          wr = items[2 * w + 0];
-          wc = items[2 * w + 1];
+          wr = OFX_LD(items + (2 * w + 0));
+          wc = OFX_LD(items + (2 * w + 1));
         } else {
-          wr = order[w - nchunks];
+          wr = OFX_LD(order + (w - nchunks));
         }
         wr = uniform64(wr);
         wc = uniform64(wc);
-        const int64_t rs = (int64_t)rp[row_begin + wr];
-        const int64_t re = (int64_t)rp[row_begin + wr + 1];
+        const int64_t rs = (int64_t)OFX_LD(rp + (row_begin + wr));
+        const int64_t re = (int64_t)OFX_LD(rp + (row_begin + wr + 1));
         int64_t j0 = rs, j1 = re;
         if (wc >= 0) {
           j0 = rs + wc * chunk;
@@ -979,20 +989,20 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
       __shared__ __attribute__((aligned(16))) SmallLds<T, I, K> lds;
       constexpr int W = SmallForm<T, I, K>::W;
       const int64_t w = bid;
-      const int64_t nchunks = (int64_t)counters[0];
-      const int64_t nheavy = (int64_t)counters[3] - (int64_t)counters[2];  // bin 0
+      const int64_t nchunks = (int64_t)OFX_LD(counters + 0);
+      const int64_t nheavy = (int64_t)OFX_LD(counters + 3) - (int64_t)OFX_LD(counters + 2);  // bin 0
       if (w >= nchunks + nheavy) return;
       int64_t wr, wc = -1;
       if (w < nchunks) {
-        wr = items[2 * w + 0];
-        wc = items[2 * w + 1];
+        wr = OFX_LD(items + (2 * w + 0));
+        wc = OFX_LD(items + (2 * w + 1));
       } else {
-        wr = order[w - nchunks];
+        wr = OFX_LD(order + (w - nchunks));
       }
       wr = uniform64(wr);
       wc = uniform64(wc);
-      const int64_t rs = (int64_t)rp[row_begin + wr];
-      const int64_t re = (int64_t)rp[row_begin + wr + 1];
+      const int64_t rs = (int64_t)OFX_LD(rp + (row_begin + wr));
+      const int64_t re = (int64_t)OFX_LD(rp + (row_begin + wr + 1));
       int64_t j0 = rs, j1 = re;
       if (wc >= 0) {
         j0 = rs + wc * chunk;
@@ -1023,7 +1033,9 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
   int64_t g = ((bid - ((K::WH || K::BI) ? wave_blocks : 0)) * kWaves + wave) * GPW +
               gsub;
   if constexpr ((K::WH && LPR < 64) || K::BI) {
-    if (order != nullptr) g += (int64_t)counters[0] + (int64_t)counters[3] - (int64_t)counters[2];
+    if (order != nullptr)
+      g += (int64_t)OFX_LD(counters + 0) + (int64_t)OFX_LD(counters + 3) -
+           (int64_t)OFX_LD(counters + 2);
   }
   // Work items with a plan: hub chunks, then the heavy rows (bin 0 of `order`), then the light
   // rows in index order, taken one of two ways (the same rows, the same bits):
@@ -1047,21 +1059,21 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
     if (g >= nrows) return;
     lr = g;
   } else {
-    const int64_t nchunks = (int64_t)counters[0];
-    const int64_t nhubs = (int64_t)counters[1];
-    const int64_t nheavy = (int64_t)counters[3] - (int64_t)counters[2];  // bin 0
+    const int64_t nchunks = (int64_t)OFX_LD(counters + 0);
+    const int64_t nhubs = (int64_t)OFX_LD(counters + 1);
+    const int64_t nheavy = (int64_t)OFX_LD(counters + 3) - (int64_t)OFX_LD(counters + 2);  // bin 0
 #if defined(OFX_LIGHT_INDEX)
     const bool idx = true;
 #else
     const bool idx = kIdx && (nhubs + nheavy) * kIdxExcluded <= nrows;
 #endif
     if (g < nchunks) {
-      lr = items[2 * g + 0];
-      c = items[2 * g + 1];
+      lr = OFX_LD(items + (2 * g + 0));
+      c = OFX_LD(items + (2 * g + 1));
     } else if (g < nchunks + nheavy || !idx) {
       const int64_t q = g - nchunks;
       if (q >= nrows - nhubs) return;
-      lr = order[q];
+      lr = OFX_LD(order + q);
     } else {
       lr = g - nchunks - nheavy;
       if (lr >= nrows) return;
@@ -1072,8 +1084,8 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
     lr = uniform64(lr);
     c = uniform64(c);
   }
-  const int64_t rs = (int64_t)rp[row_begin + lr];
-  const int64_t re = (int64_t)rp[row_begin + lr + 1];
+  const int64_t rs = (int64_t)OFX_LD(rp + (row_begin + lr));
+  const int64_t re = (int64_t)OFX_LD(rp + (row_begin + lr + 1));
   if (by_index && (re - rs > split || re - rs > heavy)) return;  // a hub or a heavy row
   int64_t j0 = rs, j1 = re;
   if (c >= 0) {
@@ -1124,13 +1136,13 @@ __global__ void __launch_bounds__(kBlock)
   using A = typename Num<T>::acc;
   using P = Pack<A, VEC>;
   constexpr int kPre = 16;  // partial rows in flight per lane (the adds stay in chunk order)
-  const int64_t nhubs = (int64_t)counters[1];
+  const int64_t nhubs = (int64_t)OFX_LD(counters + 1);
   const int gl = threadIdx.x % L;
   const int64_t groups = (int64_t)gridDim.x * (kBlock / L);
   for (int64_t h = (int64_t)blockIdx.x * (kBlock / L) + threadIdx.x / L; h < nhubs; h += groups) {
-    const int64_t lr = hubs[3 * h + 0];
-    const int64_t slot = hubs[3 * h + 1];
-    const int64_t nc = hubs[3 * h + 2];
+    const int64_t lr = OFX_LD(hubs + (3 * h + 0));
+    const int64_t slot = OFX_LD(hubs + (3 * h + 1));
+    const int64_t nc = OFX_LD(hubs + (3 * h + 2));
     for (int64_t c = (int64_t)gl * VEC; c < n; c += (int64_t)L * VEC) {
       const A* p = part + slot * n + c;
       A acc[VEC];
@@ -1140,7 +1152,7 @@ __global__ void __launch_bounds__(kBlock)
       for (; q + kPre <= nc; q += kPre) {
         P v[kPre];
 #pragma unroll
-        for (int u = 0; u < kPre; ++u) v[u] = *reinterpret_cast<const P*>(p + (q + u) * n);
+        for (int u = 0; u < kPre; ++u) v[u] = OFX_LD(reinterpret_cast<const P*>(p + (q + u) * n));
 #pragma unroll
         for (int u = 0; u < kPre; ++u) {
 #pragma unroll
@@ -1148,12 +1160,13 @@ __global__ void __launch_bounds__(kBlock)
         }
       }
       for (; q < nc; ++q) {
-        const P v = *reinterpret_cast<const P*>(p + q * n);
+        const P v = OFX_LD(reinterpret_cast<const P*>(p + q * n));
 #pragma unroll
         for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + v.v[e];
       }
+      if (bias && !OFX_DOK(bias + c, sizeof(T) * VEC)) continue;  // OFX_DEBUG_BOUNDS builds only
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) C[lr * ldc + c + e] = epilogue<T>(acc[e], bias, c + e, act);
+      for (int e = 0; e < VEC; ++e) OFX_ST(&C[lr * ldc + c + e], epilogue<T>(acc[e], bias, c + e, act));
     }
   }
 }
@@ -1215,6 +1228,38 @@ int pick_lpr(int64_t n, int vec) {
   return l;
 }
 
+#ifdef OFX_DEBUG_BOUNDS
+// OFX_DEBUG_BOUNDS builds: the launch's allocations (dbg_bounds.h), published on its stream before
+// its kernels, and its configuration as the tag recorded with a violation:
+// VEC | LPR << 8 | U << 16 | flags << 24 (NT PF BNT WH BI BUF SH) | HL << 32 | HU << 40 | kind << 48
+template <typename T, typename I, typename K>
+int debug_publish(const Launch& L, unsigned long long kind) {
+  dbg::HostBounds hb;
+  const int64_t si = (int64_t)sizeof(I), st = (int64_t)sizeof(T);
+  hb.add(L.rp, (uint64_t)((L.row_begin + L.nrows + 1) * si));
+  hb.add(L.col, (uint64_t)(L.nnz * si));
+  hb.add(L.val, (uint64_t)(L.nnz * st));
+  hb.add(L.vperm, (uint64_t)(L.nnz * si));
+  if (L.b_rows > 0) hb.add(L.b, (uint64_t)(((L.b_rows - 1) * L.ldb + L.n) * st));
+  hb.add(L.c, (uint64_t)(((L.nrows - 1) * L.ldc + L.n) * st));
+  hb.add(L.ws, L.ws_bytes);
+  hb.add(L.bias, (uint64_t)(L.n * st));
+  void* zero = nullptr;
+  OFX_HIP_CHECK(hipGetSymbolAddress(&zero, HIP_SYMBOL(g_zero_row)));
+  hb.add(zero, kZeroRowBytes);
+  const unsigned long long flags = (unsigned long long)K::NT | (unsigned long long)K::PF << 1 |
+                                   (unsigned long long)K::BNT << 2 | (unsigned long long)K::WH << 3 |
+                                   (unsigned long long)K::BI << 4 | (unsigned long long)K::BUF << 5 |
+                                   (unsigned long long)K::SH << 6;
+  const unsigned long long tag = (unsigned long long)K::VEC | (unsigned long long)K::LPR << 8 |
+                                 (unsigned long long)K::U << 16 | flags << 24 |
+                                 (unsigned long long)K::HL << 32 | (unsigned long long)K::HU << 40 |
+                                 kind << 48;
+  OFX_REQUIRE(hb.publish(L.stream, tag) == 0, OFX_EDEVICE, "spmm_csr: debug bounds not published");
+  return OFX_OK;
+}
+#endif
+
 template <typename T, typename I, typename K>
 int launch_cfg(const Launch& L) {
   using A = typename Num<T>::acc;
@@ -1227,6 +1272,9 @@ int launch_cfg(const Launch& L) {
   T* C = static_cast<T*>(L.c);
   const WsLayout w = ws_layout(L.nrows, L.nnz, L.n, sizeof(A), L.sched);
   const bool plan = w.total > 0;
+#ifdef OFX_DEBUG_BOUNDS
+  if (const int rc = debug_publish<T, I, K>(L, 1)) return rc;
+#endif
   WorkList wl{};
   if (plan) {
     OFX_REQUIRE(L.ws != nullptr && L.ws_bytes >= w.total, OFX_EWORKSPACE,
@@ -1286,6 +1334,9 @@ int launch_small(const Launch& L) {
   const int64_t light =
       (L.sched.heavy > 0 && L.sched.heavy != INT64_MAX) ? L.sched.heavy : (int64_t)kSmallLight * K::U;
   const int64_t grid = (L.nrows + SF::RPB - 1) / SF::RPB;
+#ifdef OFX_DEBUG_BOUNDS
+  if (const int rc = debug_publish<T, I, K>(L, 2)) return rc;
+#endif
   OFX_REQUIRE(grid < (int64_t)UINT32_MAX, OFX_EINVAL, "spmm_csr: too many rows (%lld)",
               (long long)L.nrows);
   hipLaunchKernelGGL((spmm_small_kernel<T, I, K>), dim3((unsigned)grid), dim3(64 * K::WPB), 0,

@@ -9,6 +9,7 @@
 
 #include "ofx_internal.h"
 #include "spmm_common.h"
+#include "dbg_bounds.h"
 
 namespace ofx {
 namespace plan {
@@ -45,7 +46,8 @@ __device__ __forceinline__ int plan_row(const I* __restrict__ rp, int64_t row_be
                                         int64_t& nc) {
   nc = 0;
   if (g >= nrows) return -2;  // no row
-  const int64_t len = (int64_t)rp[row_begin + g + 1] - (int64_t)rp[row_begin + g];
+  const int64_t len = (int64_t)OFX_LDP(rp + (row_begin + g + 1)) -
+                      (int64_t)OFX_LDP(rp + (row_begin + g));
   if (len > split) {
     nc = num_chunks(len, chunk);
     return -1;  // hub
@@ -129,7 +131,8 @@ __global__ void __launch_bounds__(kBlock)
   block_scan_vals(v, tot);
   if (threadIdx.x == 0) {
 #pragma unroll
-    for (int i = 0; i < kPlanVals; ++i) block_tot[kPlanVals * blockIdx.x + i] = tot[i];
+    for (int i = 0; i < kPlanVals; ++i)
+      OFX_STP(block_tot + (kPlanVals * blockIdx.x + i), tot[i]);
   }
 }
 
@@ -149,24 +152,24 @@ __global__ void __launch_bounds__(kBlock)
 #pragma unroll 8
   for (int64_t b = b0; b < b1; ++b) {
 #pragma unroll
-    for (int i = 0; i < kPlanVals; ++i) v[i] += block_tot[kPlanVals * b + i];
+    for (int i = 0; i < kPlanVals; ++i) v[i] += OFX_LDP(block_tot + (kPlanVals * b + i));
   }
   block_scan_vals(v, tot);  // v: exclusive offset of this thread's run
 #pragma unroll 8
   for (int64_t b = b0; b < b1; ++b) {
 #pragma unroll
     for (int i = 0; i < kPlanVals; ++i) {
-      const int64_t x = block_tot[kPlanVals * b + i];
-      block_tot[kPlanVals * b + i] = v[i];
+      const int64_t x = OFX_LDP(block_tot + (kPlanVals * b + i));
+      OFX_STP(block_tot + (kPlanVals * b + i), v[i]);
       v[i] += x;
     }
   }
   if (threadIdx.x == 0) {
-    counters[0] = (unsigned long long)tot[1];
-    counters[1] = (unsigned long long)tot[0];
+    OFX_STP(counters + 0, (unsigned long long)tot[1]);
+    OFX_STP(counters + 1, (unsigned long long)tot[0]);
     int64_t start = 0;
     for (int b = 0; b < kBins; ++b) {
-      counters[2 + b] = (unsigned long long)start;
+      OFX_STP(counters + (2 + b), (unsigned long long)start);
       start += tot[2 + b];
     }
   }
@@ -192,13 +195,13 @@ __device__ __forceinline__ void plan_write_rows(const int (&cls)[kPlanRowsPerThr
     const int64_t g = base + q;
     first[q] = slot;
     if (cls[q] == -1) {
-      hubs[3 * hi + 0] = g;
-      hubs[3 * hi + 1] = slot;
-      hubs[3 * hi + 2] = nc[q];
+      OFX_STP(hubs + (3 * hi + 0), g);
+      OFX_STP(hubs + (3 * hi + 1), slot);
+      OFX_STP(hubs + (3 * hi + 2), nc[q]);
       if (nc[q] <= kOwnItems) {
         for (int64_t c = 0; c < nc[q]; ++c) {
-          items[2 * (slot + c) + 0] = g;
-          items[2 * (slot + c) + 1] = c;
+          OFX_STP(items + (2 * (slot + c) + 0), g);
+          OFX_STP(items + (2 * (slot + c) + 1), c);
         }
       }
       ++hi;
@@ -206,7 +209,7 @@ __device__ __forceinline__ void plan_write_rows(const int (&cls)[kPlanRowsPerThr
     } else if (cls[q] >= 0) {
 #pragma unroll
       for (int b = 0; b < kBins; ++b)
-        if (cls[q] == b) order[pos[b]++] = g;
+        if (cls[q] == b) OFX_STP(order + (pos[b]++), g);
     }
   }
   // Hubs with many chunks: the whole wave writes their (row, chunk) items, 64 lanes strided
@@ -221,8 +224,8 @@ __device__ __forceinline__ void plan_write_rows(const int (&cls)[kPlanRowsPerThr
       const int64_t s0 = (int64_t)__shfl((long long)first[q], src);
       const int64_t ncs = (int64_t)__shfl((long long)nc[q], src);
       for (int64_t c = threadIdx.x & 63; c < ncs; c += 64) {
-        items[2 * (s0 + c) + 0] = g;
-        items[2 * (s0 + c) + 1] = c;
+        OFX_STP(items + (2 * (s0 + c) + 0), g);
+        OFX_STP(items + (2 * (s0 + c) + 1), c);
       }
     }
   }
@@ -269,7 +272,7 @@ __global__ void __launch_bounds__(kBlock)
   for (int64_t b = threadIdx.x; b < nblocks; b += kBlock) {
 #pragma unroll
     for (int i = 0; i < kPlanVals; ++i) {
-      const int64_t x = block_tot[kPlanVals * b + i];
+      const int64_t x = OFX_LDP(block_tot + (kPlanVals * b + i));
       pt[i] += x;
       if (b < (int64_t)blockIdx.x) po[i] += x;
     }
@@ -311,9 +314,9 @@ __global__ void __launch_bounds__(kBlock)
       start += s_tot[2 + b];
     }
     if (blockIdx.x == 0) {
-      counters[0] = s_tot[1];
-      counters[1] = s_tot[0];
-      for (int b = 0; b < kBins; ++b) counters[2 + b] = s_bin[b];
+      OFX_STP(counters + 0, s_tot[1]);
+      OFX_STP(counters + 1, s_tot[0]);
+      for (int b = 0; b < kBins; ++b) OFX_STP(counters + (2 + b), s_bin[b]);
     }
   }
   __syncthreads();

@@ -82,6 +82,7 @@ def _load():
         "ofx_relu_bias_grad": ([p, i32, i64, i64, p, i64, p, i64, p, i64, p, i32, p, sz], i32),
         "ofx_relu_bias_grad_cpu": ([i32, i32, i64, i64, p, i64, p, i64, p, i64, p, i32], i32),
         "ofx_spmm_csr_plan": ([p, i32, i32, i64, i64, i64, i64, p, i64, i64, p, sz, popt], i32),
+        "ofx_debug_bounds_read": ([ctypes.POINTER(u64), i32], i32),
         "ofx_spmm_csr_fused": ([p, i32, i32, i64, i64, i64, i64, p, p, p, p, i64, p, i64, i64, i64,
                                 p, i32, p, sz, popt], i32),
         "ofx_spmm_csr_fused_cpu": ([i32, i32, i32, i64, i64, i64, i64, p, p, p, p, i64, p, i64, i64,
@@ -135,6 +136,8 @@ def _load():
         "ofx_graph_launch": ([p, p], i32),
         "ofx_comm_get_unique_id": ([p], i32),
         "ofx_comm_init_rank": ([ctypes.POINTER(p), i32, p, i32], i32),
+        "ofx_comm_init_rank_deadline": ([ctypes.POINTER(p), i32, p, i32, ctypes.c_double], i32),
+        "ofx_comm_abort": ([p], i32),
         "ofx_comm_destroy": ([p], i32),
         "ofx_comm_count": ([p, ctypes.POINTER(i32), ctypes.POINTER(i32)], i32),
         "ofx_allgather": ([p, p, p, sz, i32, p], i32),

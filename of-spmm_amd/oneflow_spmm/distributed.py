@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 import time
 
 import torch
@@ -525,8 +526,20 @@ class RowSplitSpmm:
         uid = ctypes.create_string_buffer(obj[0], UNIQUE_ID_BYTES)
         comm = ctypes.c_void_p()
         check(LIB.ofx_set_device(self.device.index if self.device.index is not None else 0), "set_device")
-        check(LIB.ofx_comm_init_rank(ctypes.byref(comm), self.world, uid, self.rank), "comm_init_rank")
+        # bounded: a peer that never joins ends this rank with a named error (and an aborted
+        # communicator) instead of a hang inside the set-up; OFX_COMM_TIMEOUT seconds, 300 default
+        check(LIB.ofx_comm_init_rank_deadline(ctypes.byref(comm), self.world, uid, self.rank,
+                                              self.comm_timeout_s), "comm_init_rank_deadline")
         self._comm = comm
+
+    comm_timeout_s = float(os.environ.get("OFX_COMM_TIMEOUT", "300"))
+
+    def abort(self):
+        """ncclCommAbort of the native communicator (a stalled rank's watchdog, before it exits):
+        peers blocked on this rank then fail instead of waiting forever."""
+        if self._comm is not None:
+            LIB.ofx_comm_abort(self._comm)
+            self._comm = None
 
     def comm_size(self):
         """(ranks, this rank) of the native RCCL communicator, None without one."""
@@ -874,7 +887,7 @@ class RowSplitSpmm:
 
     def tune(self, out, pipelines=(1, 2, 4), reps: int = 3, force: bool = False,
              budget_s: float | None = None, prune: float = 3.0,
-             first: tuple = ("grid2x4/s2",), log=None) -> dict:
+             first: tuple | None = None, log=None, on_candidate=None) -> dict:
         """Times every exchange on this node with the real step over the bound CSR: all-gather
         (ring / point-to-point) x pipeline depth, the halo exchange and the grid plans if built.
         Keeps the fastest.  Timings are max-reduced over ranks, so all ranks choose the same; every
@@ -882,10 +895,14 @@ class RowSplitSpmm:
         | "grid<R>x<C>[/s<S>]": ms} of the candidates measured.
 
         Order and bounds (so the first 8-GPU run ends in bounded time): the candidates named in
-        `first` (the 2x4 grid with sub-block overlap, DESIGN.md §4's expected best at 8 GPUs), then
-        the rest in ascending model time (_model_ms).  After the first measurement R_X is refitted
-        to it; a candidate whose refitted model time exceeds `prune` x the best measured time is
-        skipped, and once `budget_s` seconds have passed (max over ranks) the rest are skipped.
+        `first` (default: the plain row split + all-gather of the north star, "<comm>/p1", then the
+        2x4 grid with sub-block overlap, DESIGN.md §4's expected best at 8 GPUs), then the rest in
+        ascending model time (_model_ms).  After the first measurement R_X is refitted to it; a
+        candidate whose refitted model time exceeds `prune` x the best measured time is skipped,
+        and once `budget_s` seconds have passed (max over ranks) the rest are skipped.  The plain
+        all-gather is never skipped (the north star's number is always
+        measured, whichever candidate wins).  `on_candidate(name)` is called before each
+        measurement (the bench's per-rank phase log and watchdog).
         Every decision uses max-reduced values, so all ranks take the same path.  The record is in
         `self.tune_report`: per candidate the model time, the measured time and the status.
         One rank has nothing to exchange, so it keeps its setting unless `force` (tests).  With
@@ -964,7 +981,11 @@ class RowSplitSpmm:
         dist.all_reduce(mt, op=dist.ReduceOp.MAX, group=self.group)
         model = {nm: (float(mt[i, 0]), float(mt[i, 1]), model[nm][2]) for i, nm in enumerate(names)}
         prior = {nm: self._model_ms(*model[nm], self.R_X, self.R_HBM) for nm in model}
-        cands.sort(key=lambda c: (c[0] not in first, prior[c[0]], c[0]))
+        always = {f"{base}/p1"}
+        if first is None:
+            first = (f"{base}/p1", "grid2x4/s2")
+        cands.sort(key=lambda c: (c[0] not in first,
+                                  first.index(c[0]) if c[0] in first else 0, prior[c[0]], c[0]))
 
         times = {}
         self.tune_errors = {}
@@ -977,13 +998,16 @@ class RowSplitSpmm:
             best = min(times.values()) if times else float("inf")
             fitted = self._model_ms(*model[name], r_x, self.R_HBM)
             rec["refit_predicted_ms"] = round(fitted, 4)
-            if (budget_s is not None and times
-                    and max_over_ranks(time.perf_counter() - t_start) > budget_s):
-                rec["status"] = "skipped: budget"
-                continue
-            if math.isfinite(best) and fitted > prune * best:
-                rec["status"] = "skipped: model"
-                continue
+            if name not in always:
+                if (budget_s is not None and times
+                        and max_over_ranks(time.perf_counter() - t_start) > budget_s):
+                    rec["status"] = "skipped: budget"
+                    continue
+                if math.isfinite(best) and fitted > prune * best:
+                    rec["status"] = "skipped: model"
+                    continue
+            if on_candidate is not None:
+                on_candidate(name)
             setter()
             ms = measure()
             rec["measured_ms"] = round(ms, 4) if math.isfinite(ms) else None

@@ -14,9 +14,15 @@ add_docstr(
     :math:`out[r, :] = \sum_{j=rp[r]}^{rp[r+1]-1} values[j] \cdot b[col[j], :]`, summed in
     ascending :math:`j` (the order of gather -> multiply -> unsorted_segment_sum).
 
-    Rows with more than ``clamp(65536 / N, 128, 8192)`` nonzeros are summed in chunks of that
-    many nonzeros whose partial sums are then added in order; the result is deterministic and
-    identical on CPU and GPU.
+    Rows with more than ``T = clamp(65536 / N, 128, 512)`` nonzeros (rounded down to a power of
+    two: 512 for N <= 128, 256 at N = 256, 128 from N = 512) are summed in chunks of ``T``
+    nonzeros, the last chunk taking the remainder, and the chunk sums are then added in chunk
+    order; the result is deterministic and identical on CPU and GPU.
+
+    Column indices outside ``[0, a_num_cols)``: a column ``>= a_num_cols`` contributes
+    ``value * 0`` in its place of the order (the gather's zero fill) on every device; a negative
+    column raises on the CPU (the gather's CHECK) and contributes ``value * 0`` on the GPU (the
+    CUDA gather's zero fill of any index outside the table).
 
     Args:
         a_csr_row_ptr (oneflow.Tensor): int32 or int64, shape ``[a_num_rows + 1]``

@@ -249,10 +249,12 @@ def test_baseline_configs_bitexact(device, name):
 
 
 @pytest.mark.parametrize("n,alt_variant", [(16, 10021), (32, 408)])
-def test_plaw1m_chain_bound_config_bitexact(device, n, alt_variant):
-    """1M power-law at N=16 / 32: the big launch whose hub chains outlast its memory traffic runs
-    twice the loads in flight with the (col, val) batch prefetched (chain_bound); the whole output
-    bit for bit against the oracle and against the plain configuration of that width."""
+def test_plaw1m_narrow_widths_bitexact(device, n, alt_variant):
+    """1M power-law (20M nonzeros) at N=16 / 32, the whole output bit for bit against the oracle
+    and against a second configuration of the same width.  The automatic picks: at N=16 the narrow
+    form past kPrefetchNnz (2-lane float2 light rows, 16-lane wave items for the hub chunks and
+    heavy rows), against tuning variant 10021 (one element per lane over 16 lanes, 16 loads in
+    flight); at N=32 the bandwidth configuration, against VEC 4 / LPR 8 forced (variant 408)."""
     cfg = fs.synth.CONFIGS["plaw1m"]
     m, k, nnz = cfg["m"], cfg["k"], cfg["nnz"]
     rp, ci, v = fs.synth.csr(m, k, nnz)
@@ -265,10 +267,11 @@ def test_plaw1m_chain_bound_config_bitexact(device, n, alt_variant):
     assert_bitwise(out, oracle_spmm(rp, ci, v, b), f"plaw1m n={n}")
 
 
-def test_mid_size_n16_chain_config_bitexact(device):
-    """A 15M-nonzero power-law graph at N=16 sits in the mid form's size range, but its hub
-    chains make the prefetching U = 32 configuration faster (chain_beats_mid): the output bit for
-    bit against the oracle, the plain U = 16 configuration and the forced mid form."""
+def test_mid_size_n16_narrow_form_bitexact(device):
+    """A 15M-nonzero power-law graph (750k rows) at N=16: the narrow form past kPrefetchNnz
+    (2-lane float2 light rows, hub chunks and heavy rows as 16-lane wave items); the output bit for
+    bit against the oracle, the one-element bandwidth configuration (tuning variant 10021) and the
+    mid form forced (variant 30002, block items)."""
     m = k = 750_000
     nnz, n = 15_000_000, 16
     rp, ci, v = fs.synth.csr(m, k, nnz)

@@ -130,8 +130,10 @@ def test_bench_eight_rank_rehearsal_pinned_grid2x4_s2():
 
 
 def test_bench_eight_rank_tune_is_ordered_and_bounded():
-    """tune() at 8 ranks: grid2x4/s2 is measured first, every candidate is reported with its model
-    time, and a zero budget stops after the first measurement (the rest 'skipped: budget')."""
+    """tune() at 8 ranks: the north star's plain row split + all-gather ("torch/p1" under gloo,
+    "rccl/p1" on the node) is measured first and always, every candidate is reported with its
+    model time, and a zero budget stops after that first measurement (the rest 'skipped:
+    budget'); the line reports the all-gather's number beside the winner."""
     p = _bench(["--gpus", "8", "--backend", "gloo", "--device", "cpu", "--config", "tiny",
                 "--steps", "1", "--warmup", "0", "--tune-budget", "0"],
                {"OMP_NUM_THREADS": "1"}, drop=_SPAWN_ENV_DROP)
@@ -139,10 +141,46 @@ def test_bench_eight_rank_tune_is_ordered_and_bounded():
     cands = line["extra"]["tune_candidates"]
     assert len(cands) >= 12  # 3 all-gather depths (gloo: one kind), 3 halo, 6 grids
     assert all("predicted_ms" in c for c in cands.values())
+    assert list(cands)[:2] == ["torch/p1", "grid2x4/s2"]  # the measurement order
     measured = [k for k, c in cands.items() if c["status"] == "measured"]
-    assert measured == ["grid2x4/s2"]
-    assert all(c["status"] == "skipped: budget" for k, c in cands.items() if k != "grid2x4/s2")
-    assert line["extra"]["exchange"] == "grid2x4/s2"
+    assert measured == ["torch/p1"]
+    assert all(c["status"] == "skipped: budget" for k, c in cands.items() if k != "torch/p1")
+    assert line["extra"]["exchange"] == "allgather"
+    ag = line["extra"]["rowsplit_allgather_p1"]
+    assert ag["ms"] > 0 and ag["gflops"] > 0
+    # every rank logged its phases
+    for r in range(8):
+        assert f"[rank {r}/8]" in p.stderr and "phase: tune: torch/p1" in p.stderr
+
+
+def test_bench_stalled_rank_names_its_phase_and_fails():
+    """A rank stalled in a phase past its limit (injected: rank 1 sleeps in its first tune
+    candidate) prints the phase, exits 75, and the launcher ends the run non-zero instead of
+    hanging."""
+    import time
+    t0 = time.monotonic()
+    p = _bench(["--gpus", "2", "--backend", "gloo", "--device", "cpu", "--config", "tiny",
+                "--steps", "1", "--warmup", "0", "--phase-timeout-scale", "0.05"],
+               {"OMP_NUM_THREADS": "1", "OFX_BENCH_STALL": "1:tune"}, drop=_SPAWN_ENV_DROP)
+    assert p.returncode != 0
+    # rank 1 sleeps; rank 0 waits for it inside the same candidate's collective, so either
+    # watchdog may fire first (the launcher then stops the other): the phase is named either way
+    assert "STALLED: phase 'tune: torch/p1'" in p.stderr, p.stderr[-3000:]
+    assert p.stdout == ""
+    assert time.monotonic() - t0 < 120
+
+
+def test_bench_spawn_deadline_ends_a_hung_run():
+    """The launcher's own deadline (--deadline) ends a run whose ranks never finish, with
+    timeout(1)'s status 124, whatever the phase limits."""
+    import time
+    t0 = time.monotonic()
+    p = _bench(["--gpus", "2", "--backend", "gloo", "--device", "cpu", "--config", "tiny",
+                "--steps", "1", "--warmup", "0", "--deadline", "15", "--phase-timeout-scale",
+                "1000"], {"OMP_NUM_THREADS": "1", "OFX_BENCH_STALL": "0:inputs"},
+               drop=_SPAWN_ENV_DROP)
+    assert p.returncode == 124, p.stderr[-3000:]
+    assert time.monotonic() - t0 < 90
 
 
 def test_bench_eight_ranks_refuses_a_short_launch():
