@@ -140,6 +140,16 @@ int ofx_spmm_csr_plan(void* stream, int idx_dtype, int val_dtype, int64_t m, int
                       int64_t nnz, const void* row_ptr, int64_t row_begin, int64_t row_end,
                       void* workspace, size_t workspace_bytes, const ofx_spmm_options* opts);
 
+/* The configuration ofx_spmm_csr with these arguments would launch, as text in buf
+ * ("form=<small|mid|narrow|prefetch|bandwidth> kernel=... VEC=.. LPR=.. U=.. ..."): the form
+ * rules of the launch made observable.  Nothing is launched and no pointer is
+ * dereferenced (b and c only enter the width dispatch's alignment checks).  No reference
+ * counterpart (OneFlow logs no kernel configuration).                                        */
+int ofx_spmm_csr_describe(int idx_dtype, int val_dtype, int64_t m, int64_t k, int64_t n,
+                          int64_t nnz, const void* b, int64_t ldb, const void* c, int64_t ldc,
+                          int64_t row_begin, int64_t row_end, const ofx_spmm_options* opts,
+                          char* buf, size_t buf_bytes);
+
 /* Bounds-checked builds only (OFX_DEBUG_BOUNDS, `make -C of-spmm_amd debug`): every global access
  * of the forward kernels is checked against its launch's allocations before it is made, and an
  * access outside all of them is skipped and recorded.  Synchronises the device and copies the

@@ -204,7 +204,7 @@ __device__ __forceinline__ bool sddmm_item(const I* __restrict__ rp, int64_t g, 
     } else {
       const int64_t q = g - nchunks;
       if (q >= nrows - (int64_t)counters[1]) return false;
-      lr = order[q];
+      lr = plan::order_row(order, nrows, (int64_t)counters[3] - (int64_t)counters[2], q);
     }
   }
   const int64_t r = row_begin + lr;

@@ -151,6 +151,32 @@ extern "C" int ofx_spmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t 
                     workspace_bytes, opts);
 }
 
+// The configuration the launch of ofx_spmm_csr with these arguments would take (form, lane layout,
+// loads in flight, flags), written to `buf` as "form=<small|mid|narrow|prefetch|bandwidth> ...";
+// nothing is launched and no pointer is dereferenced (b and c only enter the alignment checks of
+// the width dispatch).  The tests assert each form rule of spmm_launch.h on both sides of its
+// threshold with it.
+extern "C" int ofx_spmm_csr_describe(int idx_dtype, int val_dtype, int64_t m, int64_t k, int64_t n,
+                                     int64_t nnz, const void* b, int64_t ldb, const void* c,
+                                     int64_t ldc, int64_t row_begin, int64_t row_end,
+                                     const ofx_spmm_options* opts, char* buf, size_t buf_bytes) {
+  OFX_REQUIRE(buf != nullptr && buf_bytes > 0, OFX_EINVAL, "spmm_csr_describe: no buffer");
+  buf[0] = 0;
+  int rc = check_common(idx_dtype, val_dtype, m, k, n, nnz);
+  if (rc) return rc;
+  OFX_REQUIRE(0 <= row_begin && row_begin < row_end && row_end <= m && n > 0, OFX_EINVAL,
+              "spmm_csr_describe: empty launch (rows [%lld, %lld), n=%lld)", (long long)row_begin,
+              (long long)row_end, (long long)n);
+  OFX_REQUIRE(ldb >= n && ldc >= n, OFX_EINVAL, "spmm_csr_describe: ldb / ldc < n");
+  const int64_t nrows = row_end - row_begin;
+  const int64_t nnz_est = launch_nnz(m, nrows, nnz);
+  Launch L{nullptr, nullptr, nullptr, nullptr, b, const_cast<void*>(c), ldb, ldc, row_begin, nrows,
+           n, nnz, launch_schedule(nrows, nnz_est, n, resolve_schedule(n, opts)), nullptr, 0,
+           nullptr, OFX_ACT_NONE, k, nullptr, nnz_est, buf, buf_bytes};
+  if (idx_dtype == OFX_DT_INT32) return launch_idx<int32_t>(val_dtype, L);
+  return launch_idx<int64_t>(val_dtype, L);
+}
+
 extern "C" int ofx_spmm_csr_gathered(void* stream, int idx_dtype, int val_dtype, int64_t m,
                                      int64_t k, int64_t n, int64_t nnz, const void* row_ptr,
                                      const void* col_idx, const void* values,

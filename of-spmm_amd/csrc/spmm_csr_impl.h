@@ -36,6 +36,8 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdio>
+#include <cstring>
 #include <type_traits>
 
 #include "ofx_internal.h"
@@ -79,12 +81,15 @@ struct alignas(sizeof(T) * VEC) Pack {
 // paths) stays at the light path's.
 // SH (bandwidth configurations, fp32): n need not be a multiple of VEC; the lane holding a row's
 // last columns takes the VEC-wide window ending at column n - 1 (16-B accesses at 4-B alignment).
+// LR: the hubs' chunk partials are added by the last chunk to finish, inside spmm_main (hub_tail),
+// instead of by the spmm_reduce launch (the mid-size forms, where a launch is a tenth of the call).
 template <int VEC_, int LPR_, int U_ = 8, int WPB_ = 4, bool NT_ = false, bool PF_ = false,
           bool BNT_ = false, bool WH_ = false, bool BI_ = false, bool BUF_ = true, int HL_ = 0,
-          int HU_ = 16, bool SH_ = false>
+          int HU_ = 16, bool SH_ = false, bool LR_ = false>
 struct Cfg {
   static constexpr int VEC = VEC_, LPR = LPR_, U = U_, WPB = WPB_;
   static constexpr bool NT = NT_, PF = PF_, BNT = BNT_, WH = WH_, BI = BI_, BUF = BUF_, SH = SH_;
+  static constexpr bool LR = LR_;
   static constexpr int HL = HL_, HU = HU_;
   // loads in flight per lane of the wave-item form: G * UW * VEC cross-lane moves per batch are
   // unrolled, so UW keeps that at <= 256 (4..32)
@@ -556,6 +561,58 @@ __device__ __forceinline__ void store_partial(A* __restrict__ p, const A (&acc)[
   for (int e = 0; e < VEC; ++e) p[e] = acc[e];
 }
 
+// In-kernel hub reduce (Cfg::LR).  A chunk item, once its partial row is stored, counts itself in
+// at its hub's arrival counter (indexed by the hub's first chunk slot, zeroed by the plan); the last
+// of the hub's nc chunks to arrive adds the hub's partial rows in chunk order from +0 and writes the
+// C row (epilogue included): the bits of spmm_reduce_kernel, without its launch.  It then resets
+// the counter, so a plan built once stays valid for the next launch.  Every lane of the calling
+// group calls this after its column passes; `member` lanes hold columns (VEC x L lanes, the
+// caller's mapping; SH: the last window shifted to end at column n - 1), `lead_lane` is the group's
+// lane 0.  The fences are agent scope: the chunks of one hub run on any XCD.
+template <typename T, int VEC, int L, bool SH>
+__device__ __forceinline__ void hub_tail(unsigned* __restrict__ arrive, int64_t slot0, int64_t nc,
+                                         const typename Num<T>::acc* __restrict__ part,
+                                         T* __restrict__ C, int64_t ldc, int64_t lr, int64_t n,
+                                         int gl, bool member, int lead_lane,
+                                         const T* __restrict__ bias, int act) {
+#pragma clang fp contract(off)
+  using A = typename Num<T>::acc;
+  __threadfence();  // release: this group's partial row, device-wide
+  unsigned old = 0;
+  if (member && gl == 0) old = atomicAdd(arrive + slot0, 1u);
+  old = __shfl(old, lead_lane);
+  if ((int64_t)old != nc - 1) return;
+  __threadfence();  // acquire: the hub's other partial rows
+  if (!member) return;
+  for (int64_t c0 = 0; c0 < n; c0 += (int64_t)L * VEC) {
+    int64_t cc = c0 + (int64_t)gl * VEC;
+    if (cc >= n) continue;
+    if (SH && cc + VEC > n) cc = n - VEC;
+    const A* p = part + slot0 * n + cc;
+    A acc[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc[e] = A(0);
+    constexpr int kPre = 8;  // partial rows in flight (the adds stay in chunk order)
+    int64_t q = 0;
+    for (; q + kPre <= nc; q += kPre) {
+      A x[kPre][VEC];
+#pragma unroll
+      for (int u = 0; u < kPre; ++u)
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) x[u][e] = OFX_LD(p + (q + u) * n + e);
+#pragma unroll
+      for (int u = 0; u < kPre; ++u)
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + x[u][e];
+    }
+    for (; q < nc; ++q)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + OFX_LD(p + q * n + e);
+    store_row<T, VEC, false>(C + lr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
+  }
+  if (gl == 0) OFX_ST(arrive + slot0, 0u);
+}
+
 // Block-engine sizes (compile-time knobs for A/B builds: scripts/ab_build.sh): bytes of products
 // per LDS buffer, nonzeros per batch, B-row loads per lane per batch.
 #ifndef OFX_BE_LDS
@@ -926,7 +983,8 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
                      const unsigned long long* __restrict__ counters,
                      const int64_t* __restrict__ items, const int64_t* __restrict__ order,
                      typename Num<T>::acc* __restrict__ part, const T* __restrict__ bias,
-                     int act, int64_t wave_blocks, int64_t block_base) {
+                     int act, int64_t wave_blocks, int64_t block_base,
+                     unsigned* __restrict__ arrive) {
   using A = typename Num<T>::acc;
   constexpr int VEC = K::VEC, LPR = K::LPR, kWaves = K::WPB;
   const int64_t bid = block_base + (int64_t)blockIdx.x;  // launches of > 2^31 threads are cut
@@ -952,7 +1010,7 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
           wr = OFX_LD(items + (2 * w + 0));
           wc = OFX_LD(items + (2 * w + 1));
         } else {
-          wr = OFX_LD(order + (w - nchunks));
+          wr = plan::order_row(order, nrows, nheavy, w - nchunks);  // a heavy row
         }
         wr = uniform64(wr);
         wc = uniform64(wc);
@@ -978,6 +1036,11 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
               store_row<T, WV, K::NT>(C + wr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
           }
         }
+        if constexpr (K::LR) {
+          if (wc >= 0)
+            hub_tail<T, WV, WL, false>(arrive, w - wc, num_chunks(re - rs, chunk), part, C, ldc,
+                                       wr, n, wgl, lane < WL, 0, bias, act);
+        }
       }
       return;
     }
@@ -997,7 +1060,7 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
         wr = OFX_LD(items + (2 * w + 0));
         wc = OFX_LD(items + (2 * w + 1));
       } else {
-        wr = OFX_LD(order + (w - nchunks));
+        wr = plan::order_row(order, nrows, nheavy, w - nchunks);  // a heavy row
       }
       wr = uniform64(wr);
       wc = uniform64(wc);
@@ -1024,6 +1087,11 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
           else
             store_row<T, VEC, K::NT>(C + wr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
         }
+      }
+      if constexpr (K::LR) {
+        if (wc >= 0 && chain)  // the chain group (wave 0, group 0) holds the partial row
+          hub_tail<T, VEC, LPR, K::SH>(arrive, w - wc, num_chunks(re - rs, chunk), part, C, ldc, wr,
+                                       n, gl, true, gbase, bias, act);
       }
       return;
     }
@@ -1073,7 +1141,7 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
     } else if (g < nchunks + nheavy || !idx) {
       const int64_t q = g - nchunks;
       if (q >= nrows - nhubs) return;
-      lr = OFX_LD(order + q);
+      lr = plan::order_row(order, nrows, nheavy, q);
     } else {
       lr = g - nchunks - nheavy;
       if (lr >= nrows) return;
@@ -1114,6 +1182,11 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
       else
         store_row<T, VEC, K::NT>(C + lr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
     }
+  }
+  if constexpr (K::LR) {
+    if (c >= 0)
+      hub_tail<T, VEC, LPR, K::SH>(arrive, g - c, num_chunks(re - rs, chunk), part, C, ldc, lr, n,
+                                   gl, true, gbase, bias, act);
   }
 }
 
@@ -1228,10 +1301,31 @@ int pick_lpr(int64_t n, int vec) {
   return l;
 }
 
+// ofx_spmm_csr_describe: the configuration a launch takes (kind = "main" for the planned forms'
+// spmm_main_kernel, "small" for spmm_small_kernel), written instead of launching.  The form names
+// follow DESIGN.md §3: small, mid (block items), narrow (wave items of HL lanes), prefetch (PF
+// without block items), bandwidth (the rest).
+template <typename T, typename I, typename K>
+int describe_cfg(const Launch& L, const char* kind) {
+  const char* form = std::strcmp(kind, "small") == 0 ? "small"
+                     : K::BI                         ? "mid"
+                     : (K::WH && K::HL > 0)          ? "narrow"
+                     : K::PF                         ? "prefetch"
+                                                     : "bandwidth";
+  std::snprintf(L.describe, L.describe_bytes,
+                "form=%s kernel=%s VEC=%d LPR=%d U=%d WPB=%d NT=%d PF=%d WH=%d BI=%d BUF=%d SH=%d "
+                "HL=%d HU=%d LR=%d elem=%d idx=%d",
+                form, kind, K::VEC, K::LPR, K::U, K::WPB, (int)K::NT, (int)K::PF, (int)K::WH,
+                (int)K::BI, (int)K::BUF, (int)K::SH, K::HL, K::HU, (int)K::LR, (int)sizeof(T),
+                (int)sizeof(I));
+  return OFX_OK;
+}
+
 #ifdef OFX_DEBUG_BOUNDS
 // OFX_DEBUG_BOUNDS builds: the launch's allocations (dbg_bounds.h), published on its stream before
 // its kernels, and its configuration as the tag recorded with a violation:
-// VEC | LPR << 8 | U << 16 | flags << 24 (NT PF BNT WH BI BUF SH) | HL << 32 | HU << 40 | kind << 48
+// VEC | LPR << 8 | U << 16 | flags << 24 (NT PF BNT WH BI BUF SH LR) | HL << 32 | HU << 40 |
+// kind << 48
 template <typename T, typename I, typename K>
 int debug_publish(const Launch& L, unsigned long long kind) {
   dbg::HostBounds hb;
@@ -1250,7 +1344,7 @@ int debug_publish(const Launch& L, unsigned long long kind) {
   const unsigned long long flags = (unsigned long long)K::NT | (unsigned long long)K::PF << 1 |
                                    (unsigned long long)K::BNT << 2 | (unsigned long long)K::WH << 3 |
                                    (unsigned long long)K::BI << 4 | (unsigned long long)K::BUF << 5 |
-                                   (unsigned long long)K::SH << 6;
+                                   (unsigned long long)K::SH << 6 | (unsigned long long)K::LR << 7;
   const unsigned long long tag = (unsigned long long)K::VEC | (unsigned long long)K::LPR << 8 |
                                  (unsigned long long)K::U << 16 | flags << 24 |
                                  (unsigned long long)K::HL << 32 | (unsigned long long)K::HU << 40 |
@@ -1262,6 +1356,7 @@ int debug_publish(const Launch& L, unsigned long long kind) {
 
 template <typename T, typename I, typename K>
 int launch_cfg(const Launch& L) {
+  if (L.describe != nullptr) return describe_cfg<T, I, K>(L, "main");
   using A = typename Num<T>::acc;
   constexpr int GPW = 64 / K::LPR;
   constexpr int64_t GPB = (int64_t)K::WPB * GPW;  // lane-groups per block
@@ -1317,10 +1412,10 @@ int launch_cfg(const Launch& L) {
                        L.stream, rp, col, val, static_cast<const I*>(L.vperm), B, L.ldb, L.b_rows,
                        C, L.ldc, L.row_begin, L.nrows, L.n, plan ? L.sched.split : INT64_MAX,
                        plan ? L.sched.chunk : INT64_MAX, heavy, counters, items, order, part,
-                       static_cast<const T*>(L.bias), L.act, wave_blocks, b0);
+                       static_cast<const T*>(L.bias), L.act, wave_blocks, b0, wl.arrive);
     OFX_HIP_CHECK(hipGetLastError());
   }
-  if (plan && w.max_hubs > 0)
+  if (plan && w.max_hubs > 0 && !K::LR)  // LR: the main kernel added the hubs (hub_tail)
     return launch_reduce<T>(L.stream, w.max_hubs, L.n, counters, hub, part, C, L.ldc,
                             static_cast<const T*>(L.bias), L.act);
   return OFX_OK;
@@ -1329,6 +1424,7 @@ int launch_cfg(const Launch& L) {
 
 template <typename T, typename I, typename K>
 int launch_small(const Launch& L) {
+  if (L.describe != nullptr) return describe_cfg<T, I, K>(L, "small");
   using SF = SmallForm<T, I, K>;
   // options.heavy_threshold > 0 overrides the light/whole-block cut (tuning; no numeric effect)
   const int64_t light =
@@ -1387,11 +1483,11 @@ template <typename T, typename I, int VEC, bool WH>
 int launch_vec_pf(const Launch& L, int lpr) {
   constexpr int U = VEC * sizeof(T) <= 4 ? 32 : 16;
   switch (lpr) {
-    case 4: return launch_cfg<T, I, Cfg<VEC, 4, U, 4, false, true, false, WH>>(L);
-    case 8: return launch_cfg<T, I, Cfg<VEC, 8, U, 4, false, true, false, WH>>(L);
-    case 16: return launch_cfg<T, I, Cfg<VEC, 16, U, 4, false, true, false, WH>>(L);
-    case 32: return launch_cfg<T, I, Cfg<VEC, 32, U, 4, false, true, false, WH>>(L);
-    case 64: return launch_cfg<T, I, Cfg<VEC, 64, U, 4, false, false, false, false>>(L);
+    case 4: return launch_cfg<T, I, Cfg<VEC, 4, U, 4, false, true, false, WH, false, true, 0, 16, false, true>>(L);
+    case 8: return launch_cfg<T, I, Cfg<VEC, 8, U, 4, false, true, false, WH, false, true, 0, 16, false, true>>(L);
+    case 16: return launch_cfg<T, I, Cfg<VEC, 16, U, 4, false, true, false, WH, false, true, 0, 16, false, true>>(L);
+    case 32: return launch_cfg<T, I, Cfg<VEC, 32, U, 4, false, true, false, WH, false, true, 0, 16, false, true>>(L);
+    case 64: return launch_cfg<T, I, Cfg<VEC, 64, U, 4, false, false, false, false, false, true, 0, 16, false, true>>(L);
     default: return fail(OFX_EINVAL, "spmm_csr: unsupported lanes-per-row %d", lpr);
   }
 }
@@ -1403,11 +1499,11 @@ template <typename T, typename I, int VEC, bool SR>
 int launch_vec_mid(const Launch& L, int lpr) {
   constexpr int U = SR ? (VEC * sizeof(T) <= 4 ? 32 : 16) : (VEC == 1 && sizeof(T) == 4 ? 16 : 8);
   switch (lpr) {
-    case 4: return launch_cfg<T, I, Cfg<VEC, 4, U, 4, false, SR, false, false, true>>(L);
-    case 8: return launch_cfg<T, I, Cfg<VEC, 8, U, 4, false, SR, false, false, true>>(L);
-    case 16: return launch_cfg<T, I, Cfg<VEC, 16, U, 4, false, SR, false, false, true>>(L);
-    case 32: return launch_cfg<T, I, Cfg<VEC, 32, U, 4, false, SR, false, false, true>>(L);
-    case 64: return launch_cfg<T, I, Cfg<VEC, 64, U, 4, false, SR, false, false, true>>(L);
+    case 4: return launch_cfg<T, I, Cfg<VEC, 4, U, 4, false, SR, false, false, true, true, 0, 16, false, true>>(L);
+    case 8: return launch_cfg<T, I, Cfg<VEC, 8, U, 4, false, SR, false, false, true, true, 0, 16, false, true>>(L);
+    case 16: return launch_cfg<T, I, Cfg<VEC, 16, U, 4, false, SR, false, false, true, true, 0, 16, false, true>>(L);
+    case 32: return launch_cfg<T, I, Cfg<VEC, 32, U, 4, false, SR, false, false, true, true, 0, 16, false, true>>(L);
+    case 64: return launch_cfg<T, I, Cfg<VEC, 64, U, 4, false, SR, false, false, true, true, 0, 16, false, true>>(L);
     default: return fail(OFX_EINVAL, "spmm_csr: unsupported lanes-per-row %d", lpr);
   }
 }
@@ -1506,6 +1602,26 @@ int launch_shift(const Launch& L, bool nt) {
   }
 }
 
+// The prefetching form's (mid-size graphs) odd fp32 widths above 16: 16-B lanes with the shifted
+// last window, U = 16 loads in flight and the next (col, val) batch prefetched, instead of one
+// element per lane (N <= 64: up to 64 lanes, one row per wave).  Hubs added in the kernel (LR), as
+// in the rest of the prefetching form.
+template <typename T, typename I>
+int launch_shift_pf(const Launch& L) {
+  switch (pick_lpr(L.n, 4)) {
+    case 8: return launch_cfg<T, I, Cfg<4, 8, 16, 4, false, true, false, false, false, true, 0, 16, true, true>>(L);
+    case 16: return launch_cfg<T, I, Cfg<4, 16, 16, 4, false, true, false, false, false, true, 0, 16, true, true>>(L);
+    case 32: return launch_cfg<T, I, Cfg<4, 32, 16, 4, false, true, false, false, false, true, 0, 16, true, true>>(L);
+    default: return launch_cfg<T, I, Cfg<4, 64, 16, 4, false, false, false, false, false, true, 0, 16, true, true>>(L);
+  }
+}
+
+bool use_shift_pf_form(const Launch& L, int elem_bytes) {
+  return L.sched.variant == 0 && elem_bytes == 4 && L.n > 16 && L.n % 4 != 0 &&
+         use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched) &&
+         ((uintptr_t)L.b % 4) == 0 && ((uintptr_t)L.c % 4) == 0;
+}
+
 bool use_shift_form(const Launch& L, int elem_bytes) {
   return L.sched.variant == 0 && elem_bytes == 4 && L.n > 64 && L.n % 4 != 0 &&
          !use_small_form(L.nrows, L.nnz_est, L.n, L.sched) &&
@@ -1524,7 +1640,7 @@ bool use_shift_form(const Launch& L, int elem_bytes) {
 template <typename T, typename I>
 int launch_narrow(const Launch& L) {
   if (L.nnz_est <= kPrefetchNnz)
-    return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, true, false, true, false, true, 16, 16>>(L);
+    return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, true, false, true, false, true, 16, 16, false, true>>(L);
   return launch_cfg<T, I, Cfg<2, 8, 8, 4, false, true, false, true, false, true, 16, 8>>(L);
 }
 
@@ -1548,6 +1664,9 @@ int launch_typed(const Launch& L) {
     if (use_narrow_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L)) return launch_narrow<T, I>(L);
     if (use_shift_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
       return launch_shift<T, I>(L, (L.b_rows * L.ldb * (int64_t)sizeof(T)) > kNtBytes);
+#ifndef OFX_AB_NO_SHIFT_PF  // A/B builds only (scripts/ab_build.sh)
+    if (use_shift_pf_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L)) return launch_shift_pf<T, I>(L);
+#endif
   }
   // variant = VEC * 100 + LPR forces a configuration (tuning / tests); 0 = auto.
   const int forced_vec = (L.sched.variant > 0 && !form) ? L.sched.variant / 100 : 0;
@@ -1559,10 +1678,11 @@ int launch_typed(const Launch& L) {
   // row (VEC = N / 16: 2-8 B per lane) instead of the widest vector over 4-8 lanes; products bf16
   // N = 8 / 16 / 32 / 64 -8 / -7 / -6 / -13%, Reddit-shaped N = 16 / 32 / 64 -27 / -19 / -6%
   // (profiles/r03y_lanes_*.jsonl; fp32 keeps its layouts, DESIGN.md §3 tuning record)
+  // The prefetching form too (mid-size graphs): arxiv-shaped bf16 N = 16 took 214 us with 8-element
+  // lanes (two active lanes per 4-lane group) against 49 us for fp32 (profiles/r03ah_*.jsonl).
   const bool narrow16 = !forced_vec && sizeof(T) == 2 && L.n <= 64 && L.sched.variant == 0 &&
                         !use_small_form(L.nrows, L.nnz_est, L.n, L.sched) &&
-                        !use_mid_form(L.nrows, L.nnz_est, L.n, L.sched) &&
-                        !use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched);
+                        !use_mid_form(L.nrows, L.nnz_est, L.n, L.sched);
   int cap16 = 1;  // the largest power of two <= N / 16
   while (cap16 * 32 <= L.n) cap16 *= 2;
   const int vec = (!forced_vec && sizeof(T) == 4 && L.n <= 16) ? 1

@@ -24,6 +24,8 @@ struct Launch {
   const void* vperm;  // NULL, or I[nnz]: nonzero j's value is val[vperm[j]] (A^T of a gradient)
   int64_t nnz_est;    // this launch's nonzeros, estimated (launch_nnz): the form choice and the
                       // automatic heavy threshold; `nnz` (the matrix's) bounds the workspace
+  char* describe = nullptr;  // ofx_spmm_csr_describe: write the configuration here, launch nothing
+  size_t describe_bytes = 0;
 };
 
 // Nonzeros of a launch over `nrows` of the matrix's `m` rows: nnz * nrows / m.  row_ptr lives on

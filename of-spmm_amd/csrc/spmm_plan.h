@@ -5,6 +5,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <chrono>
 #include <climits>
 
 #include "ofx_internal.h"
@@ -19,26 +21,39 @@ constexpr int kBlock = 256;
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// ---- work planning (three small launches, no contended atomics) ----------------------------
-// Every row gets a class: hub (len > split: cut into chunks -> partials + spmm_reduce) or one of
-// kBins degree bins (kBins = 2: bin 0 = heavy, len > heavy; bin 1 = the rest; with more bins the
-// thresholds step by 4x).  The main kernel walks ONE work list: the hub chunks first, then the
-// non-hub rows bin by bin (a stable counting sort by degree), so the longest work starts first
-// and the grid ends on short rows.  Two bins measured best on MI355X: the light rows keep index
-// order (sequential row_ptr reads and C writes); more bins cost products-scale 1.2% in random
-// row_ptr/C traffic.  Rows are taken kPlanRows per block.
-//   plan_count  per-block totals of (hubs, hub chunks, rows per bin)
-//   plan_scan   one block: exclusive offsets across blocks; counters[0] = hub chunks,
-//               counters[1] = hubs, counters[2 + b] = start of bin b in `order`
-//   plan_write  hubs[3i..3i+2] = {local row, first chunk slot, chunks},
-//               items[2s..2s+1] = {local row, chunk} for s < counters[0],
-//               order[...] = local row, bins in order, ascending rows inside a bin.
-// The layout is a pure function of row_ptr (deterministic); the partial of chunk s is part[s].
+// ---- work planning (one launch, decoupled look-back) ------------------------------------------
+// Every row gets a class: hub (len > split: cut into chunks -> partials + their reduce) or one of
+// kBins degree bins (kBins = 2: bin 0 = heavy, len > heavy; bin 1 = light, the rest).  The main
+// kernel walks ONE work list: the hub chunks first, then the heavy rows, then the light rows, so
+// the longest work starts first and the grid ends on short rows.  Two bins measured best on
+// MI355X: the light rows keep index order (sequential row_ptr reads and C writes); more bins cost
+// products-scale 1.2% in random row_ptr/C traffic.  Rows are taken kPlanRows per
+// block.  The plan writes
+//   hubs[3i..3i+2] = {local row, first chunk slot, chunks}          (i < counters[1])
+//   items[2s..2s+1] = {local row, chunk}                            (s < counters[0])
+//   order[0 .. nlight) = the light rows, ascending
+//   order[nrows - 1 - h] = heavy row h, h < counters[3] (heavy rows fill the array from its end)
+//   arrive[first slot of each hub] = 0                              (the in-kernel hub reduce)
+// and counters = {hub chunks, hubs, 0, heavy rows}.  Work item q of the non-hub rows is
+// order_row(order, nrows, nheavy, q).  The layout is a pure function of row_ptr (deterministic);
+// the partial of chunk s is part[s].
+//
+// One launch (spmm_plan_kernel): every block counts its rows' classes, then finds the offsets of
+// its hubs / chunks / heavy rows / light rows among all earlier blocks by decoupled look-back
+// (each block publishes its totals, then its inclusive prefix, in a status word tagged with the
+// launch's epoch: the workspace is never zeroed, and a word from an earlier launch or leftover
+// memory carries another epoch), and writes its part of the list.  Because heavy rows fill the
+// order array from its end and light rows from its start, no block needs a grand total.  A block
+// waits only on lower-numbered blocks, which are dispatched first (each XCD dispatches its blocks
+// in order), so the chain always progresses.  This replaced count + scan + write launches
+// (products 11.3 + 9.6 + 14.6 us, arxiv-shaped 4.8 + 5.8 us).
 constexpr int kPlanRowsPerThread = 4;
 constexpr int64_t kPlanRows = (int64_t)kBlock * kPlanRowsPerThread;
 constexpr int kBins = 2;
 constexpr int kPlanVals = 2 + kBins;  // hubs, chunks, bins...
 constexpr int64_t kOwnItems = 8;      // hubs with more chunks get their items written wave-wide
+constexpr int kLookWords = 16;        // per plan block: status, totals[4], inclusive prefix[4]
+constexpr unsigned long long kAgg = 1, kInc = 2;  // status = epoch << 2 | state
 
 template <typename I>
 __device__ __forceinline__ int plan_row(const I* __restrict__ rp, int64_t row_begin, int64_t nrows,
@@ -57,6 +72,12 @@ __device__ __forceinline__ int plan_row(const I* __restrict__ rp, int64_t row_be
   for (int b = 0; b < kBins - 1; ++b, t >>= 2)
     if (len > t) return b;
   return kBins - 1;
+}
+
+// Non-hub work item q (heavy rows first, then light rows) of a plan with `nheavy` heavy rows.
+__device__ __forceinline__ int64_t order_row(const int64_t* __restrict__ order, int64_t nrows,
+                                             int64_t nheavy, int64_t q) {
+  return q < nheavy ? OFX_LDP(order + (nrows - 1 - q)) : OFX_LDP(order + (q - nheavy));
 }
 
 // Block-wide exclusive scan of kPlanVals int64 values (256 threads); returns the block totals.
@@ -119,76 +140,20 @@ __device__ __forceinline__ void plan_thread(const I* __restrict__ rp, int64_t ro
   }
 }
 
-template <typename I>
-__global__ void __launch_bounds__(kBlock)
-    spmm_plan_count_kernel(const I* __restrict__ rp, int64_t row_begin, int64_t nrows,
-                           int64_t split, int64_t chunk, int64_t heavy,
-                           int64_t* __restrict__ block_tot) {
-  int cls[kPlanRowsPerThread];
-  int64_t nc[kPlanRowsPerThread], v[kPlanVals], tot[kPlanVals];
-  const int64_t base = (int64_t)blockIdx.x * kPlanRows + (int64_t)threadIdx.x * kPlanRowsPerThread;
-  plan_thread(rp, row_begin, nrows, base, split, chunk, heavy, cls, nc, v);
-  block_scan_vals(v, tot);
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int i = 0; i < kPlanVals; ++i)
-      OFX_STP(block_tot + (kPlanVals * blockIdx.x + i), tot[i]);
-  }
-}
-
-// One block: each thread owns a run of `per` consecutive plan blocks, sums it, one block-wide
-// scan of the 256 run totals gives the run offsets, then each thread rewrites its run as
-// exclusive offsets.  (A Hillis-Steele block scan per tile of 256 plan blocks took 21 us at
-// products scale: ten tiles x eight barrier steps.)
-__global__ void __launch_bounds__(kBlock)
-    spmm_plan_scan_kernel(int64_t* __restrict__ block_tot, int64_t nblocks,
-                          unsigned long long* __restrict__ counters) {
-  const int64_t per = (nblocks + kBlock - 1) / kBlock;
-  const int64_t b0 = (int64_t)threadIdx.x * per;
-  const int64_t b1 = b0 + per < nblocks ? b0 + per : nblocks;
-  int64_t v[kPlanVals], tot[kPlanVals];
-#pragma unroll
-  for (int i = 0; i < kPlanVals; ++i) v[i] = 0;
-#pragma unroll 8
-  for (int64_t b = b0; b < b1; ++b) {
-#pragma unroll
-    for (int i = 0; i < kPlanVals; ++i) v[i] += OFX_LDP(block_tot + (kPlanVals * b + i));
-  }
-  block_scan_vals(v, tot);  // v: exclusive offset of this thread's run
-#pragma unroll 8
-  for (int64_t b = b0; b < b1; ++b) {
-#pragma unroll
-    for (int i = 0; i < kPlanVals; ++i) {
-      const int64_t x = OFX_LDP(block_tot + (kPlanVals * b + i));
-      OFX_STP(block_tot + (kPlanVals * b + i), v[i]);
-      v[i] += x;
-    }
-  }
-  if (threadIdx.x == 0) {
-    OFX_STP(counters + 0, (unsigned long long)tot[1]);
-    OFX_STP(counters + 1, (unsigned long long)tot[0]);
-    int64_t start = 0;
-    for (int b = 0; b < kBins; ++b) {
-      OFX_STP(counters + (2 + b), (unsigned long long)start);
-      start += tot[2 + b];
-    }
-  }
-}
-
-// Writes one tile's hubs / chunk items / binned order, given this thread's exclusive offsets `v`
-// inside the tile, the tile's offsets `off` across tiles and the bins' start positions.
+// Writes one block's hubs / chunk items / heavy and light rows, given this thread's exclusive
+// offsets `v` inside the block and the block's offsets `off` among all earlier blocks.
 __device__ __forceinline__ void plan_write_rows(const int (&cls)[kPlanRowsPerThread],
                                                 const int64_t (&nc)[kPlanRowsPerThread],
                                                 const int64_t (&v)[kPlanVals], const int64_t* off,
-                                                const unsigned long long* bin_start, int64_t base,
+                                                int64_t base, int64_t nrows,
                                                 int64_t* __restrict__ hubs,
                                                 int64_t* __restrict__ items,
-                                                int64_t* __restrict__ order) {
+                                                int64_t* __restrict__ order,
+                                                unsigned* __restrict__ arrive) {
   int64_t hi = off[0] + v[0];
   int64_t slot = off[1] + v[1];
-  int64_t pos[kBins];
-#pragma unroll
-  for (int b = 0; b < kBins; ++b) pos[b] = (int64_t)bin_start[b] + off[2 + b] + v[2 + b];
+  int64_t heavy_pos = off[2] + v[2];  // heavy row h goes to order[nrows - 1 - h]
+  int64_t light_pos = off[3] + v[3];
   int64_t first[kPlanRowsPerThread];
 #pragma unroll
   for (int q = 0; q < kPlanRowsPerThread; ++q) {
@@ -198,6 +163,9 @@ __device__ __forceinline__ void plan_write_rows(const int (&cls)[kPlanRowsPerThr
       OFX_STP(hubs + (3 * hi + 0), g);
       OFX_STP(hubs + (3 * hi + 1), slot);
       OFX_STP(hubs + (3 * hi + 2), nc[q]);
+      // the hub's arrival count for the in-kernel reduce (indexed by its first chunk slot): zero
+      // here, and the last chunk to arrive resets it, so a plan built once stays valid
+      if (arrive != nullptr) OFX_STP(arrive + slot, 0u);
       if (nc[q] <= kOwnItems) {
         for (int64_t c = 0; c < nc[q]; ++c) {
           OFX_STP(items + (2 * (slot + c) + 0), g);
@@ -206,10 +174,10 @@ __device__ __forceinline__ void plan_write_rows(const int (&cls)[kPlanRowsPerThr
       }
       ++hi;
       slot += nc[q];
+    } else if (cls[q] == 0 && kBins > 1) {
+      OFX_STP(order + (nrows - 1 - heavy_pos++), g);
     } else if (cls[q] >= 0) {
-#pragma unroll
-      for (int b = 0; b < kBins; ++b)
-        if (cls[q] == b) OFX_STP(order + (pos[b]++), g);
+      OFX_STP(order + (light_pos++), g);
     }
   }
   // Hubs with many chunks: the whole wave writes their (row, chunk) items, 64 lanes strided
@@ -231,102 +199,75 @@ __device__ __forceinline__ void plan_write_rows(const int (&cls)[kPlanRowsPerThr
   }
 }
 
-template <typename I>
-__global__ void __launch_bounds__(kBlock)
-    spmm_plan_write_kernel(const I* __restrict__ rp, int64_t row_begin, int64_t nrows,
-                           int64_t split, int64_t chunk, int64_t heavy,
-                           const int64_t* __restrict__ block_off,
-                           const unsigned long long* __restrict__ counters,
-                           int64_t* __restrict__ hubs, int64_t* __restrict__ items,
-                           int64_t* __restrict__ order) {
-  int cls[kPlanRowsPerThread];
-  int64_t nc[kPlanRowsPerThread], v[kPlanVals], tot[kPlanVals];
-  const int64_t base = (int64_t)blockIdx.x * kPlanRows + (int64_t)threadIdx.x * kPlanRowsPerThread;
-  plan_thread(rp, row_begin, nrows, base, split, chunk, heavy, cls, nc, v);
-  block_scan_vals(v, tot);
-  plan_write_rows(cls, nc, v, block_off + kPlanVals * blockIdx.x, counters + 2, base, hubs, items,
-                  order);
+// Status word of plan block b (agent-scope atomics: the look-back crosses XCDs).
+__device__ __forceinline__ unsigned long long look_status(unsigned long long* look, int64_t b) {
+  return __hip_atomic_load(look + b * kLookWords, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void look_publish(unsigned long long* look, int64_t b,
+                                             unsigned long long status) {
+  __hip_atomic_store(look + b * kLookWords, status, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// plan_scan folded into plan_write for launches of at most kFusedPlanBlocks plan blocks (<= 256K
-// rows): every write block sums the per-block totals itself (its exclusive offset and the grand
-// totals, O(blocks) reads per block), so the planner is two launches instead of three.  Block 0
-// publishes the counters.  Same layout as the three-launch form.
-constexpr int64_t kFusedPlanBlocks = 256;
-
 template <typename I>
 __global__ void __launch_bounds__(kBlock)
-    spmm_plan_write_fused_kernel(const I* __restrict__ rp, int64_t row_begin, int64_t nrows,
-                                 int64_t split, int64_t chunk, int64_t heavy,
-                                 const int64_t* __restrict__ block_tot, int64_t nblocks,
-                                 unsigned long long* __restrict__ counters,
-                                 int64_t* __restrict__ hubs, int64_t* __restrict__ items,
-                                 int64_t* __restrict__ order) {
-  __shared__ unsigned long long s_off[kPlanVals], s_tot[kPlanVals], s_bin[kBins];
-  // the per-block totals and this block's row_ptr entries are loaded together (one memory
-  // round trip, not two)
+    spmm_plan_kernel(const I* __restrict__ rp, int64_t row_begin, int64_t nrows, int64_t split,
+                     int64_t chunk, int64_t heavy, unsigned long long* __restrict__ look,
+                     unsigned long long epoch, int64_t nblocks,
+                     unsigned long long* __restrict__ counters, int64_t* __restrict__ hubs,
+                     int64_t* __restrict__ items, int64_t* __restrict__ order,
+                     unsigned* __restrict__ arrive) {
+  __shared__ int64_t s_off[kPlanVals];
   int cls[kPlanRowsPerThread];
-  int64_t nc[kPlanRowsPerThread], v[kPlanVals], tot[kPlanVals], off[kPlanVals];
-  const int64_t base = (int64_t)blockIdx.x * kPlanRows + (int64_t)threadIdx.x * kPlanRowsPerThread;
-  int64_t po[kPlanVals] = {}, pt[kPlanVals] = {};
-  for (int64_t b = threadIdx.x; b < nblocks; b += kBlock) {
-#pragma unroll
-    for (int i = 0; i < kPlanVals; ++i) {
-      const int64_t x = OFX_LDP(block_tot + (kPlanVals * b + i));
-      pt[i] += x;
-      if (b < (int64_t)blockIdx.x) po[i] += x;
-    }
-  }
+  int64_t nc[kPlanRowsPerThread], v[kPlanVals], tot[kPlanVals];
+  const int64_t b = blockIdx.x;
+  const int64_t base = b * kPlanRows + (int64_t)threadIdx.x * kPlanRowsPerThread;
   plan_thread(rp, row_begin, nrows, base, split, chunk, heavy, cls, nc, v);
-  // wave sums of the partial offsets / totals, then one slot per wave (integer sums: any order
-  // gives the same value)
-  __shared__ int64_t w_off[kPlanVals][kBlock / 64], w_tot[kPlanVals][kBlock / 64];
-#pragma unroll
-  for (int i = 0; i < kPlanVals; ++i) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-      po[i] += (int64_t)__shfl_xor((long long)po[i], m);
-      pt[i] += (int64_t)__shfl_xor((long long)pt[i], m);
-    }
-  }
-  if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-    for (int i = 0; i < kPlanVals; ++i) {
-      w_off[i][threadIdx.x >> 6] = po[i];
-      w_tot[i][threadIdx.x >> 6] = pt[i];
-    }
-  }
-  block_scan_vals(v, tot);  // its barriers also publish the wave slots above
+  block_scan_vals(v, tot);
   if (threadIdx.x == 0) {
+    // publish this block's totals (block 0: its inclusive prefix at once), then look back
+    unsigned long long* my = look + b * kLookWords;
 #pragma unroll
     for (int i = 0; i < kPlanVals; ++i) {
-      int64_t a = 0, b = 0;
-      for (int w = 0; w < kBlock / 64; ++w) {
-        a += w_off[i][w];
-        b += w_tot[i][w];
+      my[1 + i] = (unsigned long long)tot[i];
+      if (b == 0) my[1 + kPlanVals + i] = (unsigned long long)tot[i];
+    }
+    look_publish(look, b, epoch << 2 | (b == 0 ? kInc : kAgg));
+    int64_t pre[kPlanVals] = {};
+    for (int64_t p = b - 1; p >= 0; --p) {
+      unsigned long long st;
+      while (((st = look_status(look, p)) >> 2) != epoch) __builtin_amdgcn_s_sleep(1);
+      const unsigned long long* pw = look + p * kLookWords;
+      if ((st & 3) == kInc) {
+#pragma unroll
+        for (int i = 0; i < kPlanVals; ++i) pre[i] += (int64_t)pw[1 + kPlanVals + i];
+        break;
       }
-      s_off[i] = (unsigned long long)a;
-      s_tot[i] = (unsigned long long)b;
+#pragma unroll
+      for (int i = 0; i < kPlanVals; ++i) pre[i] += (int64_t)pw[1 + i];
     }
-    unsigned long long start = 0;
-    for (int b = 0; b < kBins; ++b) {
-      s_bin[b] = start;
-      start += s_tot[2 + b];
+    if (b > 0) {
+#pragma unroll
+      for (int i = 0; i < kPlanVals; ++i) my[1 + kPlanVals + i] = (unsigned long long)(pre[i] + tot[i]);
+      look_publish(look, b, epoch << 2 | kInc);
     }
-    if (blockIdx.x == 0) {
-      OFX_STP(counters + 0, s_tot[1]);
-      OFX_STP(counters + 1, s_tot[0]);
-      for (int b = 0; b < kBins; ++b) OFX_STP(counters + (2 + b), s_bin[b]);
+#pragma unroll
+    for (int i = 0; i < kPlanVals; ++i) s_off[i] = pre[i];
+    if (b == nblocks - 1) {  // the last block knows the grand totals
+      OFX_STP(counters + 0, (unsigned long long)(pre[1] + tot[1]));
+      OFX_STP(counters + 1, (unsigned long long)(pre[0] + tot[0]));
+      OFX_STP(counters + 2, 0ull);
+      OFX_STP(counters + 3, (unsigned long long)(pre[2] + tot[2]));
     }
   }
   __syncthreads();
+  int64_t off[kPlanVals];
 #pragma unroll
-  for (int i = 0; i < kPlanVals; ++i) off[i] = (int64_t)s_off[i];
-  plan_write_rows(cls, nc, v, off, s_bin, base, hubs, items, order);
+  for (int i = 0; i < kPlanVals; ++i) off[i] = s_off[i];
+  plan_write_rows(cls, nc, v, off, base, nrows, hubs, items, order, arrive);
 }
 
 struct WsLayout {
-  size_t counters, block_tot, hubs, items, order, part, total;
+  size_t counters, look, hubs, items, order, arrive, part, total;
   int64_t max_hubs, max_chunks, plan_blocks;
 };
 
@@ -345,14 +286,16 @@ WsLayout ws_layout(int64_t nrows, int64_t nnz, int64_t n, size_t acc_bytes, cons
   size_t off = 0;
   w.counters = off;
   off = align_up(off + (2 + kBins) * sizeof(unsigned long long), 256);
-  w.block_tot = off;
-  off = align_up(off + (size_t)w.plan_blocks * kPlanVals * sizeof(int64_t), 256);
+  w.look = off;
+  off = align_up(off + (size_t)w.plan_blocks * kLookWords * sizeof(unsigned long long), 256);
   w.hubs = off;
   off = align_up(off + (size_t)w.max_hubs * 3 * sizeof(int64_t), 256);
   w.items = off;
   off = align_up(off + (size_t)w.max_chunks * 2 * sizeof(int64_t), 256);
   w.order = off;
   off = align_up(off + (size_t)nrows * sizeof(int64_t), 256);
+  w.arrive = off;  // per chunk slot (only hubs' first slots are used): the in-kernel reduce
+  off = align_up(off + (size_t)w.max_chunks * sizeof(unsigned), 256);
   w.part = off;
   off = align_up(off + (size_t)w.max_chunks * (size_t)n * acc_bytes, 256);
   w.total = off;
@@ -364,6 +307,7 @@ struct WorkList {
   int64_t* hubs;
   int64_t* items;
   int64_t* order;
+  unsigned* arrive;
   void* part;
 };
 
@@ -373,10 +317,21 @@ inline void worklist_of(const WsLayout& w, char* ws, WorkList* wl) {
   wl->hubs = reinterpret_cast<int64_t*>(ws + w.hubs);
   wl->items = reinterpret_cast<int64_t*>(ws + w.items);
   wl->order = reinterpret_cast<int64_t*>(ws + w.order);
+  wl->arrive = reinterpret_cast<unsigned*>(ws + w.arrive);
   wl->part = ws + w.part;
 }
 
-// Launches plan_count / plan_scan / plan_write on `stream` into workspace `ws` laid out as `w`.
+// A launch-unique tag of the look-back status words (62 bits): a per-process random start and a
+// counter.  A status word left by another launch (or uninitialised memory) matches it with
+// probability 2^-62.
+inline unsigned long long next_epoch() {
+  static std::atomic<unsigned long long> counter{
+      splitmix64((unsigned long long)std::chrono::steady_clock::now().time_since_epoch().count() ^
+                 (unsigned long long)(uintptr_t)&counter)};
+  return (splitmix64(counter.fetch_add(1)) >> 2) | 1ull;
+}
+
+// Launches the planner on `stream` into workspace `ws` laid out as `w`: one kernel.
 template <typename I>
 int launch_plan(hipStream_t stream, const I* rp, int64_t row_begin, int64_t nrows, int64_t nnz,
                 const Schedule& sched, const WsLayout& w, char* ws, WorkList* wl) {
@@ -384,24 +339,11 @@ int launch_plan(hipStream_t stream, const I* rp, int64_t row_begin, int64_t nrow
   // 1M power-law config both peak at 4-6x the mean).  Order only, never numerics.
   const int64_t heavy = sched.heavy == 0 ? auto_heavy(nrows, nnz) : sched.heavy;
   worklist_of(w, ws, wl);
-  auto* block_tot = reinterpret_cast<int64_t*>(ws + w.block_tot);
-  const unsigned pgrid = (unsigned)w.plan_blocks;
-  hipLaunchKernelGGL((spmm_plan_count_kernel<I>), dim3(pgrid), dim3(kBlock), 0, stream, rp,
-                     row_begin, nrows, sched.split, sched.chunk, heavy, block_tot);
-  OFX_HIP_CHECK(hipGetLastError());
-  if (w.plan_blocks <= kFusedPlanBlocks) {
-    hipLaunchKernelGGL((spmm_plan_write_fused_kernel<I>), dim3(pgrid), dim3(kBlock), 0, stream, rp,
-                       row_begin, nrows, sched.split, sched.chunk, heavy, block_tot,
-                       w.plan_blocks, wl->counters, wl->hubs, wl->items, wl->order);
-    OFX_HIP_CHECK(hipGetLastError());
-    return OFX_OK;
-  }
-  hipLaunchKernelGGL(spmm_plan_scan_kernel, dim3(1), dim3(kBlock), 0, stream, block_tot,
-                     w.plan_blocks, wl->counters);
-  OFX_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL((spmm_plan_write_kernel<I>), dim3(pgrid), dim3(kBlock), 0, stream, rp,
-                     row_begin, nrows, sched.split, sched.chunk, heavy, block_tot, wl->counters,
-                     wl->hubs, wl->items, wl->order);
+  auto* look = reinterpret_cast<unsigned long long*>(ws + w.look);
+  OFX_REQUIRE(w.plan_blocks < (int64_t)UINT32_MAX, OFX_EINVAL, "spmm_csr: too many rows to plan");
+  hipLaunchKernelGGL((spmm_plan_kernel<I>), dim3((unsigned)w.plan_blocks), dim3(kBlock), 0, stream,
+                     rp, row_begin, nrows, sched.split, sched.chunk, heavy, look, next_epoch(),
+                     w.plan_blocks, wl->counters, wl->hubs, wl->items, wl->order, wl->arrive);
   OFX_HIP_CHECK(hipGetLastError());
   return OFX_OK;
 }

@@ -108,6 +108,27 @@ def spmm_csr_device(row_ptr, col_idx, values, b, m, k, *, out=None, row_begin=0,
     return kern(row_ptr, col_idx, values, b, out, row_begin, row_end)
 
 
+def describe(m: int, k: int, n: int, nnz: int, val_dtype: torch.dtype,
+             idx_dtype: torch.dtype = torch.int32, *, row_begin: int = 0, row_end: int | None = None,
+             ldb: int | None = None, ldc: int | None = None, b_addr: int = 256, c_addr: int = 256,
+             options: Options | None = None) -> dict:
+    """The configuration an ofx_spmm_csr launch with these arguments takes (ofx_spmm_csr_describe):
+    {"form": "small"|"mid"|"narrow"|"prefetch"|"bandwidth", "kernel": ..., "VEC": .., "LPR": ..,
+    "U": .., flags ...}.  Nothing is launched; b_addr / c_addr only set the pointer alignment the
+    width dispatch sees (256: aligned)."""
+    row_end = m if row_end is None else row_end
+    buf = ctypes.create_string_buffer(512)
+    check(LIB.ofx_spmm_csr_describe(dtype_code(idx_dtype), dtype_code(val_dtype), m, k, n, nnz,
+                                    b_addr, ldb or n, c_addr, ldc or n, row_begin, row_end,
+                                    ctypes.byref(options) if options else None, buf, len(buf)),
+          "spmm_csr_describe")
+    out = {}
+    for kv in buf.value.decode().split():
+        key, val = kv.split("=")
+        out[key] = int(val) if val.lstrip("-").isdigit() else val
+    return out
+
+
 def spmm_csr_gathered(row_ptr, col_idx, values, values_perm, b, m, k, *, out=None,
                       options: Options | None = None):
     """out = A @ b where nonzero j's value is values[values_perm[j]] (ofx_spmm_csr_gathered):
@@ -201,5 +222,6 @@ def csr_row_slice(row_ptr, row_begin: int, row_end: int):
 
 
 __all__ = ["make_options", "default_split", "workspace_size", "SpmmCsrKernel", "spmm_csr_device",
+           "describe",
            "spmm_csr_gathered",
            "spmm_csr_cpu", "validate_csr", "csr_row_slice", "INT64_MAX", "_lib"]

@@ -1,0 +1,31 @@
+# round 4, GPU call d (calls b and c of this round together; the pool had no box for either):
+#  1. the round-3 abort's test selection (r03ai) with the parked patch's libraries: bounds-checked
+#     with every test's record checked, then the release library with output capture off (-s);
+#  2. the current tree (the patch + the one-launch planner + the in-kernel hub reduce): the parity
+#     selection under the bounds-checked build, then under the release build;
+#  3. an interleaved A/B of per-call time against the round-3 kernels (HIP graph replay).
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+L=$GRAFT_REPO_ROOT/of-spmm_amd/oneflow_spmm
+PT="python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider"
+SEL="prefetch_form_lane or shifted_window or narrow_16bit or dtype_width or forced_variants or mid_form or small_form or walked or narrow_form or plan_once"
+OFX_DEBUG_BOUNDS_CHECK=1 OFX_SPMM_LIB=$L/libofx_spmm_pf_dbg.so timeout -k 10 240 $PT -k "$SEL" > gpurun_out/r04d_1a.txt 2>&1
+echo "1a patched, bounds-checked r03ai selection: rc=$?"; tail -2 gpurun_out/r04d_1a.txt
+OFX_SPMM_LIB=$L/libofx_spmm_pf.so AMD_LOG_LEVEL=1 timeout -k 10 240 $PT -s -k "$SEL" > gpurun_out/r04d_1b.txt 2>&1
+rc=$?; echo "1b patched release r03ai selection (-s): rc=$rc"; tail -3 gpurun_out/r04d_1b.txt
+[ $rc -le 1 ] || { tail -40 gpurun_out/r04d_1b.txt; exit 1; }
+SEL2="forms or prefetch_form_lane or mid_form or small_form or narrow or plan_once or forced_variants or dtype_width or golden or hub or sddmm or backward or gathered or epilogue or fused or out_of_range or transpose or shifted"
+OFX_DEBUG_BOUNDS_CHECK=1 OFX_SPMM_LIB=$L/libofx_spmm_dbg.so timeout -k 10 360 $PT -k "$SEL2" > gpurun_out/r04d_2a.txt 2>&1
+rc=$?; echo "2a new tree, bounds-checked: rc=$rc"; tail -3 gpurun_out/r04d_2a.txt
+[ $rc -eq 0 ] || { grep -B2 -A12 "Error\|assert" gpurun_out/r04d_2a.txt | head -60; exit 1; }
+timeout -k 10 300 $PT -k "$SEL2" > gpurun_out/r04d_2b.txt 2>&1
+rc=$?; echo "2b new tree, release: rc=$rc"; tail -3 gpurun_out/r04d_2b.txt
+[ $rc -eq 0 ] || { grep -B2 -A12 "Error\|assert" gpurun_out/r04d_2b.txt | head -60; exit 1; }
+SPECS="pubmed:16:0 pubmed:64:0 small20k:16:0 small20k:64:0 arxiv:16:0 arxiv:64:0 arxiv:128:0 g60k:16:0 g60k:64:0 p2m:16:0 p2m:64:0 p5m:16:0 plaw1m:16:0 plaw1m:64:0 products:128:0"
+for lib in prev new prev new; do
+  f=$L/libofx_spmm_prev.so; [ $lib = new ] && f=$L/libofx_spmm.so
+  OFX_SPMM_LIB=$f timeout -k 10 150 python -u scripts/probe_graph.py $SPECS 2>> gpurun_out/r04d_ab.err \
+    | sed "s/^/{\"lib\": \"$lib\", \"r\": /; s/$/}/" >> gpurun_out/r04d_ab.jsonl || { tail -20 gpurun_out/r04d_ab.err; exit 1; }
+done
+echo all done

@@ -28,3 +28,28 @@ def device():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda", 0)
+
+
+@pytest.fixture(autouse=True)
+def _debug_bounds_guard(request):
+    """With OFX_DEBUG_BOUNDS_CHECK=1 and a bounds-checked library (OFX_SPMM_LIB=...libofx_spmm_dbg.so,
+    csrc/dbg_bounds.h), every test fails if any forward launch it made touched memory outside its
+    allocations (the access itself was skipped, so nothing faulted): the site, address, block and
+    launch configuration are in the message."""
+    if os.environ.get("OFX_DEBUG_BOUNDS_CHECK") != "1" or "gpu" not in request.keywords:
+        yield
+        return
+    import ctypes
+    from oneflow_spmm import _lib
+    out = (ctypes.c_uint64 * 8)()
+    _lib.LIB.ofx_debug_bounds_read(out, 1)  # clear
+    yield
+    rc = _lib.LIB.ofx_debug_bounds_read(out, 1)
+    assert rc == _lib.OFX_OK, _lib.last_error()
+    if out[0]:
+        site = int(out[1])
+        raise AssertionError(
+            f"out-of-allocation access ({int(out[0])} in this test): site "
+            f"{['?', 'spmm_csr_impl.h', 'spmm_plan.h'][site // 100000]}:{site % 100000}, address "
+            f"{int(out[2]):#x}, {int(out[3])} B, block {int(out[4])}, thread {int(out[5])}, "
+            f"launch tag {int(out[6]):#x}")

@@ -1,0 +1,147 @@
+"""CPU: every form rule of the forward launch (of-spmm_amd/csrc/spmm_launch.h, launch_typed in
+spmm_csr_impl.h; DESIGN.md §3 "forms") on both sides of its threshold, through
+ofx_spmm_csr_describe (the configuration a launch would take; nothing is launched, so no GPU is
+needed).  The GPU tests (test_gpu_forms.py) then run the same launches and compare the bits."""
+import os
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "of-spmm_amd"))
+
+from oneflow_spmm import ops  # noqa: E402
+
+K_SMALL_ROWS = 32768
+K_SMALL_NNZ = 1 << 17
+K_SMALL_ELEMS = 1 << 23
+K_MID_ELEMS = 1 << 28
+K_PREFETCH_NNZ = 3 << 20
+F32, BF16, F16, F64 = torch.float32, torch.bfloat16, torch.float16, torch.float64
+
+
+def form(m, nnz, n, dt=F32, idx=torch.int32, **kw):
+    return ops.describe(m, kw.pop("k", m), n, nnz, dt, idx, **kw)
+
+
+def test_small_form_bounds():
+    # rows, nonzeros and products (nnz * n) all bound the one-kernel form
+    assert form(K_SMALL_ROWS, K_SMALL_NNZ, 16)["form"] == "small"
+    assert form(K_SMALL_ROWS + 1, K_SMALL_NNZ, 16)["form"] != "small"
+    assert form(K_SMALL_ROWS, K_SMALL_NNZ + 1, 16)["form"] == "mid"
+    assert form(20000, K_SMALL_ELEMS // 128, 128)["form"] == "small"
+    assert form(20000, K_SMALL_ELEMS // 128 + 1, 128)["form"] == "mid"
+    assert form(2708, 10556, 16)["kernel"] == "small"  # Cora-shaped
+
+
+def test_mid_form_bounds():
+    assert form(K_SMALL_ROWS, K_MID_ELEMS // 128, 128)["form"] == "mid"
+    above = form(K_SMALL_ROWS, K_MID_ELEMS // 128 + 1, 128)
+    assert above["form"] == "prefetch" and above["BI"] == 0
+    assert form(K_SMALL_ROWS + 1, 400_000, 64)["form"] == "prefetch"  # rows bound it too
+
+
+@pytest.mark.parametrize("n", [32, 64, 128])
+def test_prefetch_form_bound(n):
+    m = 120_000
+    below, above = form(m, K_PREFETCH_NNZ, n), form(m, K_PREFETCH_NNZ + 1, n)
+    assert below["form"] == "prefetch" and below["PF"] == 1
+    assert above["form"] == "bandwidth" and above["PF"] == 0 and above["U"] == 8
+    # wave items only at 16 < N <= 64
+    assert below["WH"] == (1 if n <= 64 else 0)
+
+
+def test_narrow_form_n16_fp32():
+    m = 169_343
+    below, above = form(m, K_PREFETCH_NNZ, 16), form(m, K_PREFETCH_NNZ + 1, 16)
+    assert below["form"] == above["form"] == "narrow"
+    assert (below["VEC"], below["LPR"], below["U"], below["HL"], below["HU"]) == (4, 4, 4, 16, 16)
+    assert (above["VEC"], above["LPR"], above["U"], above["HL"], above["HU"]) == (2, 8, 8, 16, 8)
+    # fp32 only, N = 16 only, 16-B aligned only
+    assert form(m, K_PREFETCH_NNZ, 16, BF16)["form"] != "narrow"
+    assert form(m, K_PREFETCH_NNZ, 32)["form"] == "prefetch"
+    assert form(m, K_PREFETCH_NNZ, 16, b_addr=260)["form"] != "narrow"
+
+
+def test_shifted_window_bandwidth_only():
+    m, big = 120_000, K_PREFETCH_NNZ + 1
+    sh = form(m, big, 99)
+    assert sh["SH"] == 1 and sh["VEC"] == 4 and sh["LPR"] == 32
+    assert form(m, big, 100)["SH"] == 0
+    assert form(m, big, 63)["SH"] == 0  # 17-63 columns: one element per lane
+    assert form(m, big, 99, b_addr=260)["SH"] == 1  # 16-B accesses at 4-B alignment
+    with pytest.raises(ops._lib.OfxError):  # an fp32 view off 4-B alignment has no lane layout
+        form(m, big, 99, b_addr=258)
+
+
+def test_narrow16_lanes():
+    m, big = 120_000, K_PREFETCH_NNZ + 1
+    for n, vec in ((8, 1), (16, 1), (32, 2), (48, 2), (64, 4), (128, 8)):
+        d = form(m, big, n, BF16)
+        assert d["form"] == "bandwidth" and d["VEC"] == vec, (n, d)
+
+
+def test_bandwidth_narrow_rows_take_eight_lanes():
+    m, big = 120_000, K_PREFETCH_NNZ + 1
+    for n in (1, 2, 3, 4, 7):
+        d = form(m, big, n)
+        assert d["VEC"] == 1 and d["LPR"] == 8, (n, d)
+    assert form(m, big, 16, b_addr=260)["LPR"] == 16
+
+
+def test_cache_hint_and_global_loads():
+    # non-temporal col/val/C streams once B exceeds 1 GiB; global B loads from 4 GiB
+    assert form(2_449_029, 123_718_280, 128)["NT"] == 1
+    assert form(1_000_000, 20_000_000, 64)["NT"] == 0
+    papers = form(111_059_956, 1_615_685_872, 128)
+    assert papers["BUF"] == 0 and papers["form"] == "bandwidth"
+
+
+def test_row_range_uses_its_share_of_nonzeros():
+    # an 8-way S(0) slice of products is planned as the launch it is (launch_nnz): 1/8 of the
+    # nonzeros, still above kPrefetchNnz
+    m, nnz = 2_449_029, 123_718_280
+    d = form(m, nnz, 128, row_begin=0, row_end=m // 8)
+    assert d["form"] == "bandwidth"
+    # a small slice of a mid-size graph drops to the prefetching or mid form
+    d = form(169_343, 1_166_243, 64, row_begin=0, row_end=40_000)
+    assert d["form"] == "prefetch"
+
+
+def test_forced_forms():
+    m, nnz = 169_343, 1_166_243
+    assert form(m, nnz, 64, options=ops.make_options(variant=30000))["form"] == "small"
+    assert form(m, nnz, 64, options=ops.make_options(variant=30001))["form"] == "mid"
+    assert form(m, nnz, 64, options=ops.make_options(variant=30003))["form"] == "bandwidth"
+    w = form(m, nnz, 64, options=ops.make_options(variant=30004))
+    p = form(m, nnz, 64, options=ops.make_options(variant=30005))
+    assert w["form"] == p["form"] == "prefetch" and w["WH"] == 1 and p["WH"] == 0
+    assert form(m, nnz, 64, options=ops.make_options(variant=416)) == \
+        {**form(m, nnz, 64, options=ops.make_options(variant=416)), "VEC": 4, "LPR": 16}
+
+
+def test_prefetch_form_layouts():
+    """The prefetching form's lane layouts (round 4): odd fp32 widths above 16 take 16-B lanes
+    with the shifted last window; 16-bit rows of <= 128 B take N / 16 elements per lane."""
+    m, nnz = 169_343, 1_166_243
+    for n, lpr in ((17, 8), (41, 16), (47, 16), (99, 32)):
+        d = form(m, nnz, n)
+        assert d["form"] == "prefetch" and d["SH"] == 1 and d["VEC"] == 4 and d["LPR"] == lpr, d
+    assert form(m, nnz, 15)["SH"] == 0  # 16 columns or fewer: one element per lane
+    assert form(m, nnz, 17, b_addr=258 + 2)["SH"] == 1
+    for dt in (BF16, F16):
+        for n, vec in ((8, 1), (16, 1), (32, 2), (48, 2), (64, 4), (128, 8)):
+            d = form(m, nnz, n, dt)
+            assert d["form"] == "prefetch" and d["VEC"] == vec, (dt, n, d)
+
+
+def test_in_kernel_hub_reduce_only_in_mid_size_forms():
+    """Cfg::LR (hub partials added by the last chunk inside spmm_main) in the mid, prefetching and
+    narrow-prefetching forms; the bandwidth form keeps the spmm_reduce launch."""
+    assert form(20_000, 400_000, 64)["LR"] == 1                 # mid
+    assert form(169_343, 1_166_243, 64)["LR"] == 1              # prefetching
+    assert form(169_343, 1_166_243, 16)["LR"] == 1              # narrow, <= kPrefetchNnz
+    assert form(1_000_000, 20_000_000, 16)["LR"] == 0           # narrow, past it
+    assert form(2_449_029, 123_718_280, 128)["LR"] == 0         # bandwidth
+    assert form(2708, 10556, 16)["LR"] == 0                     # small form: no plan

@@ -778,3 +778,34 @@ def test_shifted_window_odd_widths(device, idx, n):
     kern(*d, o3, bias=bias.to(device), relu=True)
     torch.cuda.synchronize()
     assert_bitwise(o3, oracle.bias_act(ref, to_oracle(bias), "relu", dtype="f32"), "epilogue")
+
+
+@pytest.mark.parametrize("dtype,n", [("f32", 17), ("f32", 47), ("f32", 99), ("bf16", 16), ("bf16", 48),
+                                     ("f16", 8)])
+def test_prefetch_form_lane_layouts(device, dtype, n):
+    """Mid-size launches (the prefetching form, <= kPrefetchNnz nonzeros): 16-bit rows of <= 128 B
+    take N / 16 elements per lane, odd fp32 widths above 16 the shifted 16-B window (Cfg::SH with
+    the prefetching configuration).  Bit-exact against the oracle, including hub rows, a row range
+    and the one-element-per-lane bandwidth configuration forced."""
+    rng = np.random.default_rng(6100 + n)
+    m, k = 60_000, 60_000
+    deg = rng.integers(0, 30, size=m)
+    deg[11] = 4000
+    deg[777] = 600
+    dt = DTYPES[dtype]
+    rp, ci, v = random_csr(m, k, deg, rng, torch.int32, dt)
+    assert 32_768 < m and ci.numel() <= (3 << 20)
+    b = random_dense(k, n, rng, dt)
+    d = (rp.to(device), ci.to(device), v.to(device), b.to(device))
+    ref = oracle_spmm(rp, ci, v, b)
+    out = fs.spmm(d[0], d[1], d[2], m, k, d[3])
+    torch.cuda.synchronize()
+    assert_bitwise(out, ref, f"{dtype} n={n} auto")
+    kern = ops.SpmmCsrKernel(m, k, n, ci.numel(), torch.int32, dt, device)
+    sub = torch.full((30_000, n), float("nan"), dtype=dt, device=device)
+    kern(*d, sub, row_begin=5_000, row_end=35_000)
+    lpr = min(64, max(4, 1 << (n - 1).bit_length()))
+    o1 = ops.spmm_csr_device(*d, m, k, options=ops.make_options(variant=100 + lpr))
+    torch.cuda.synchronize()
+    assert_bitwise(sub, ref[5_000:35_000], "row range")
+    assert torch.equal(o1.view(torch.uint8), out.view(torch.uint8))
