@@ -96,6 +96,10 @@ typedef struct ofx_spmm_options {
                             * Only for a static graph (the plan-once / compute-many pattern  *
                             * of a bound CSR).  No numeric effect.                           */
   int32_t reserved;        /* 0                                                              */
+  int64_t range_nnz;       /* nonzeros of [row_begin, row_end) when the caller knows them    *
+                            * (row_ptr[row_end] - row_ptr[row_begin]); 0 = estimated as      *
+                            * nnz * rows / m.  Picks the kernel form only (launches of a few *
+                            * rows of a degree-sorted graph); no numeric effect.             */
 } ofx_spmm_options;
 
 /* The default split threshold for dense width n (a fixed function of n; part of the numeric

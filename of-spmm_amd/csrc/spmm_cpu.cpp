@@ -275,12 +275,41 @@ extern "C" int ofx_gather_values_host(int idx_dtype, int val_dtype, int64_t nnz,
   return OFX_OK;
 }
 
+namespace ofx {
+namespace {
+// A negative column of nonzeros [j0, j1): the CPU gather's CHECK_GE(idx, 0)
+// (gather_kernel_util.cpp:80), which the kCPU forward reports as OFX_EINVAL; the gradient ops
+// of the same CPU operator report it the same way.
+int negative_column(int idx_dtype, const void* col_idx, int64_t j0, int64_t j1) {
+  bool neg = false;
+  if (idx_dtype == OFX_DT_INT32) {
+    const int32_t* c = static_cast<const int32_t*>(col_idx);
+#pragma omp parallel for reduction(|| : neg) schedule(static)
+    for (int64_t j = j0; j < j1; ++j) neg = neg || c[j] < 0;
+  } else {
+    const int64_t* c = static_cast<const int64_t*>(col_idx);
+#pragma omp parallel for reduction(|| : neg) schedule(static)
+    for (int64_t j = j0; j < j1; ++j) neg = neg || c[j] < 0;
+  }
+  return neg ? 1 : 0;
+}
+int64_t row_ptr_at(int idx_dtype, const void* row_ptr, int64_t r) {
+  return idx_dtype == OFX_DT_INT32 ? (int64_t) static_cast<const int32_t*>(row_ptr)[r]
+                                   : (int64_t) static_cast<const int64_t*>(row_ptr)[r];
+}
+}  // namespace
+}  // namespace ofx
+
 extern "C" int ofx_csr_transpose_cpu(int idx_dtype, int64_t m, int64_t k, int64_t nnz,
                                      const void* row_ptr, const void* col_idx, void* out_row_ptr,
                                      void* out_col_idx, void* out_perm) {
   OFX_REQUIRE(m >= 0 && k >= 0 && nnz >= 0 && row_ptr && out_row_ptr &&
                   (nnz == 0 || (col_idx && out_col_idx && out_perm)),
               OFX_EINVAL, "csr_transpose_cpu: bad arguments");
+  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "csr_transpose_cpu: bad index dtype %d",
+              idx_dtype);
+  OFX_REQUIRE(nnz == 0 || !negative_column(idx_dtype, col_idx, 0, nnz), OFX_EINVAL,
+              "csr_transpose_cpu: negative column index (gather_kernel_util.cpp:80 CHECK_GE(idx, 0))");
   if (idx_dtype == OFX_DT_INT32)
     cpu_transpose<int32_t>(m, k, nnz, (const int32_t*)row_ptr, (const int32_t*)col_idx,
                            (int32_t*)out_row_ptr, (int32_t*)out_col_idx, (int32_t*)out_perm);
@@ -302,6 +331,10 @@ extern "C" int ofx_sddmm_csr_cpu(int num_threads, int idx_dtype, int val_dtype, 
                   row_begin <= row_end && row_end <= m,
               OFX_EINVAL, "sddmm_csr_cpu: bad sizes");
   if (row_end == row_begin || nnz == 0) return OFX_OK;
+  OFX_REQUIRE(!negative_column(idx_dtype, col_idx, row_ptr_at(idx_dtype, row_ptr, row_begin),
+                               row_ptr_at(idx_dtype, row_ptr, row_end)),
+              OFX_EINVAL,
+              "sddmm_csr_cpu: negative column index (gather_kernel_util.cpp:80 CHECK_GE(idx, 0))");
   const int nt = num_threads > 0 ? num_threads : omp_get_max_threads();
   auto run = [&](auto* ip) {
     using I = std::remove_const_t<std::remove_pointer_t<decltype(ip)>>;

@@ -130,7 +130,7 @@ int spmm_entry(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k,
   OFX_REQUIRE(row_ptr && c, OFX_EINVAL, "spmm_csr: NULL row_ptr or output");
   OFX_REQUIRE(nnz == 0 || (col_idx && values && b), OFX_EINVAL,
               "spmm_csr: NULL col_idx/values/b with nnz=%lld", (long long)nnz);
-  const int64_t nnz_est = launch_nnz(m, nrows, nnz);
+  const int64_t nnz_est = launch_nnz(m, nrows, nnz, opts);
   Launch L{static_cast<hipStream_t>(stream), row_ptr, col_idx, values, b, c, ldb, ldc,
            row_begin, nrows, n, nnz, launch_schedule(nrows, nnz_est, n, resolve_schedule(n, opts)),
            workspace, workspace_bytes,
@@ -169,7 +169,7 @@ extern "C" int ofx_spmm_csr_describe(int idx_dtype, int val_dtype, int64_t m, in
               (long long)row_end, (long long)n);
   OFX_REQUIRE(ldb >= n && ldc >= n, OFX_EINVAL, "spmm_csr_describe: ldb / ldc < n");
   const int64_t nrows = row_end - row_begin;
-  const int64_t nnz_est = launch_nnz(m, nrows, nnz);
+  const int64_t nnz_est = launch_nnz(m, nrows, nnz, opts);
   Launch L{nullptr, nullptr, nullptr, nullptr, b, const_cast<void*>(c), ldb, ldc, row_begin, nrows,
            n, nnz, launch_schedule(nrows, nnz_est, n, resolve_schedule(n, opts)), nullptr, 0,
            nullptr, OFX_ACT_NONE, k, nullptr, nnz_est, buf, buf_bytes};
@@ -202,7 +202,7 @@ extern "C" int ofx_spmm_csr_plan(void* stream, int idx_dtype, int val_dtype, int
               (long long)row_end, (long long)m);
   const int64_t nrows = row_end - row_begin;
   if (nrows == 0 || n == 0) return OFX_OK;  // the launch writes nothing either
-  const int64_t nnz_est = launch_nnz(m, nrows, nnz);  // as the launch estimates it
+  const int64_t nnz_est = launch_nnz(m, nrows, nnz, opts);  // as the launch estimates it
   const Schedule s = launch_schedule(nrows, nnz_est, n, resolve_schedule(n, opts));
   if (use_small_form(nrows, nnz_est, n, s)) return OFX_OK;  // the small form needs no plan
   const plan::WsLayout w = plan::ws_layout(nrows, nnz, n, acc_bytes_of(val_dtype), s);

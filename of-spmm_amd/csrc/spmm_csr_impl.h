@@ -83,6 +83,11 @@ struct alignas(sizeof(T) * VEC) Pack {
 // last columns takes the VEC-wide window ending at column n - 1 (16-B accesses at 4-B alignment).
 // LR: the hubs' chunk partials are added by the last chunk to finish, inside spmm_main (hub_tail),
 // instead of by the spmm_reduce launch (the mid-size forms, where a launch is a tenth of the call).
+#ifndef OFX_AB_NO_LR
+constexpr bool kLR = true;  // the mid-size forms (prefetching, mid, narrow <= kPrefetchNnz): LR
+#else
+constexpr bool kLR = false;  // A/B builds only (scripts/ab_build.sh): the spmm_reduce launch
+#endif
 template <int VEC_, int LPR_, int U_ = 8, int WPB_ = 4, bool NT_ = false, bool PF_ = false,
           bool BNT_ = false, bool WH_ = false, bool BI_ = false, bool BUF_ = true, int HL_ = 0,
           int HU_ = 16, bool SH_ = false, bool LR_ = false>
@@ -554,11 +559,17 @@ __device__ __forceinline__ void store_row(T* __restrict__ p, const typename Num<
   }
 }
 
-template <typename A, int VEC>
+// COH (Cfg::LR): the partial is read back by another work item in the same launch (hub_tail)
+template <typename A, int VEC, bool COH = false>
 __device__ __forceinline__ void store_partial(A* __restrict__ p, const A (&acc)[VEC]) {
-  if (!OFX_DOK(p, sizeof(A) * VEC)) return;  // OFX_DEBUG_BOUNDS builds only
+  if constexpr (COH) {
 #pragma unroll
-  for (int e = 0; e < VEC; ++e) p[e] = acc[e];
+    for (int e = 0; e < VEC; ++e) coh_store(p + e, acc[e]);
+  } else {
+    if (!OFX_DOK(p, sizeof(A) * VEC)) return;  // OFX_DEBUG_BOUNDS builds only
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) p[e] = acc[e];
+  }
 }
 
 // In-kernel hub reduce (Cfg::LR).  A chunk item, once its partial row is stored, counts itself in
@@ -568,7 +579,10 @@ __device__ __forceinline__ void store_partial(A* __restrict__ p, const A (&acc)[
 // the counter, so a plan built once stays valid for the next launch.  Every lane of the calling
 // group calls this after its column passes; `member` lanes hold columns (VEC x L lanes, the
 // caller's mapping; SH: the last window shifted to end at column n - 1), `lead_lane` is the group's
-// lane 0.  The fences are agent scope: the chunks of one hub run on any XCD.
+// lane 0.  The chunks of one hub run on any XCD: partials are stored, counted and read back
+// agent-coherent (store_partial<COH>, coh_load), ordered by waiting for the stores before the count
+// (no agent-scope fence: round 4's first cut had two per chunk item, measured +8 us on a 2M-nonzero
+// N=16 launch, profiles/r04g_ab.jsonl).
 template <typename T, int VEC, int L, bool SH>
 __device__ __forceinline__ void hub_tail(unsigned* __restrict__ arrive, int64_t slot0, int64_t nc,
                                          const typename Num<T>::acc* __restrict__ part,
@@ -577,12 +591,12 @@ __device__ __forceinline__ void hub_tail(unsigned* __restrict__ arrive, int64_t 
                                          const T* __restrict__ bias, int act) {
 #pragma clang fp contract(off)
   using A = typename Num<T>::acc;
-  __threadfence();  // release: this group's partial row, device-wide
+  wait_stores();  // this group's partial row is at the coherence point before it is counted
   unsigned old = 0;
-  if (member && gl == 0) old = atomicAdd(arrive + slot0, 1u);
-  old = __shfl(old, lead_lane);
+  if (member && gl == 0)
+    old = __hip_atomic_fetch_add(arrive + slot0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __shfl(old, lead_lane);  // waits for the count: the loads below issue after it
   if ((int64_t)old != nc - 1) return;
-  __threadfence();  // acquire: the hub's other partial rows
   if (!member) return;
   for (int64_t c0 = 0; c0 < n; c0 += (int64_t)L * VEC) {
     int64_t cc = c0 + (int64_t)gl * VEC;
@@ -599,7 +613,7 @@ __device__ __forceinline__ void hub_tail(unsigned* __restrict__ arrive, int64_t 
 #pragma unroll
       for (int u = 0; u < kPre; ++u)
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) x[u][e] = OFX_LD(p + (q + u) * n + e);
+        for (int e = 0; e < VEC; ++e) x[u][e] = coh_load(p + (q + u) * n + e);
 #pragma unroll
       for (int u = 0; u < kPre; ++u)
 #pragma unroll
@@ -607,10 +621,10 @@ __device__ __forceinline__ void hub_tail(unsigned* __restrict__ arrive, int64_t 
     }
     for (; q < nc; ++q)
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + OFX_LD(p + q * n + e);
+      for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + coh_load(p + q * n + e);
     store_row<T, VEC, false>(C + lr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
   }
-  if (gl == 0) OFX_ST(arrive + slot0, 0u);
+  if (gl == 0) coh_store(arrive + slot0, 0u);
 }
 
 // Block-engine sizes (compile-time knobs for A/B builds: scripts/ab_build.sh): bytes of products
@@ -1031,7 +1045,7 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
                                     j0, j1, lane, wgl, acc);
           if (active && lane < WL) {
             if (wc >= 0)
-              store_partial<A, WV>(part + w * n + cc, acc);
+              store_partial<A, WV, K::LR>(part + w * n + cc, acc);
             else
               store_row<T, WV, K::NT>(C + wr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
           }
@@ -1083,7 +1097,7 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
                                   chain, lds, acc);
         if (chain && active) {
           if (wc >= 0)
-            store_partial<A, VEC>(part + w * n + cc, acc);
+            store_partial<A, VEC, K::LR>(part + w * n + cc, acc);
           else
             store_row<T, VEC, K::NT>(C + wr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
         }
@@ -1178,7 +1192,7 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
                         acc);
     if (active) {
       if (c >= 0)
-        store_partial<A, VEC>(part + g * n + cc, acc);
+        store_partial<A, VEC, K::LR>(part + g * n + cc, acc);
       else
         store_row<T, VEC, K::NT>(C + lr * ldc + cc, acc, bias ? bias + cc : nullptr, act);
     }
@@ -1483,11 +1497,11 @@ template <typename T, typename I, int VEC, bool WH>
 int launch_vec_pf(const Launch& L, int lpr) {
   constexpr int U = VEC * sizeof(T) <= 4 ? 32 : 16;
   switch (lpr) {
-    case 4: return launch_cfg<T, I, Cfg<VEC, 4, U, 4, false, true, false, WH, false, true, 0, 16, false, true>>(L);
-    case 8: return launch_cfg<T, I, Cfg<VEC, 8, U, 4, false, true, false, WH, false, true, 0, 16, false, true>>(L);
-    case 16: return launch_cfg<T, I, Cfg<VEC, 16, U, 4, false, true, false, WH, false, true, 0, 16, false, true>>(L);
-    case 32: return launch_cfg<T, I, Cfg<VEC, 32, U, 4, false, true, false, WH, false, true, 0, 16, false, true>>(L);
-    case 64: return launch_cfg<T, I, Cfg<VEC, 64, U, 4, false, false, false, false, false, true, 0, 16, false, true>>(L);
+    case 4: return launch_cfg<T, I, Cfg<VEC, 4, U, 4, false, true, false, WH, false, true, 0, 16, false, kLR>>(L);
+    case 8: return launch_cfg<T, I, Cfg<VEC, 8, U, 4, false, true, false, WH, false, true, 0, 16, false, kLR>>(L);
+    case 16: return launch_cfg<T, I, Cfg<VEC, 16, U, 4, false, true, false, WH, false, true, 0, 16, false, kLR>>(L);
+    case 32: return launch_cfg<T, I, Cfg<VEC, 32, U, 4, false, true, false, WH, false, true, 0, 16, false, kLR>>(L);
+    case 64: return launch_cfg<T, I, Cfg<VEC, 64, U, 4, false, false, false, false, false, true, 0, 16, false, kLR>>(L);
     default: return fail(OFX_EINVAL, "spmm_csr: unsupported lanes-per-row %d", lpr);
   }
 }
@@ -1499,11 +1513,11 @@ template <typename T, typename I, int VEC, bool SR>
 int launch_vec_mid(const Launch& L, int lpr) {
   constexpr int U = SR ? (VEC * sizeof(T) <= 4 ? 32 : 16) : (VEC == 1 && sizeof(T) == 4 ? 16 : 8);
   switch (lpr) {
-    case 4: return launch_cfg<T, I, Cfg<VEC, 4, U, 4, false, SR, false, false, true, true, 0, 16, false, true>>(L);
-    case 8: return launch_cfg<T, I, Cfg<VEC, 8, U, 4, false, SR, false, false, true, true, 0, 16, false, true>>(L);
-    case 16: return launch_cfg<T, I, Cfg<VEC, 16, U, 4, false, SR, false, false, true, true, 0, 16, false, true>>(L);
-    case 32: return launch_cfg<T, I, Cfg<VEC, 32, U, 4, false, SR, false, false, true, true, 0, 16, false, true>>(L);
-    case 64: return launch_cfg<T, I, Cfg<VEC, 64, U, 4, false, SR, false, false, true, true, 0, 16, false, true>>(L);
+    case 4: return launch_cfg<T, I, Cfg<VEC, 4, U, 4, false, SR, false, false, true, true, 0, 16, false, kLR>>(L);
+    case 8: return launch_cfg<T, I, Cfg<VEC, 8, U, 4, false, SR, false, false, true, true, 0, 16, false, kLR>>(L);
+    case 16: return launch_cfg<T, I, Cfg<VEC, 16, U, 4, false, SR, false, false, true, true, 0, 16, false, kLR>>(L);
+    case 32: return launch_cfg<T, I, Cfg<VEC, 32, U, 4, false, SR, false, false, true, true, 0, 16, false, kLR>>(L);
+    case 64: return launch_cfg<T, I, Cfg<VEC, 64, U, 4, false, SR, false, false, true, true, 0, 16, false, kLR>>(L);
     default: return fail(OFX_EINVAL, "spmm_csr: unsupported lanes-per-row %d", lpr);
   }
 }
@@ -1539,7 +1553,8 @@ template <typename T, typename I, int VEC>
 int launch_vec(const Launch& L, int lpr, bool nt) {
   const int v = L.sched.variant;
   if (!buffer_rows_ok<T>(L)) {
-    OFX_REQUIRE(v == 0 || v == kForceBigVariant || (v > 0 && v < 10000), OFX_EINVAL,
+    OFX_REQUIRE(v == 0 || v == kForceBigVariant || v == kForceGlobalVariant || (v > 0 && v < 10000),
+                OFX_EINVAL,
                 "spmm_csr: variant %d needs B under 4 GiB (k=%lld, ldb=%lld)", v,
                 (long long)L.b_rows, (long long)L.ldb);
     return launch_vec_global<T, I, VEC>(L, lpr, nt);
@@ -1550,6 +1565,7 @@ int launch_vec(const Launch& L, int lpr, bool nt) {
   if (v == kForceMidVariant) return launch_vec_mid<T, I, VEC, false>(L, lpr);
   if (v == kForceWaveVariant) return launch_vec_pf<T, I, VEC, true>(L, lpr);
   if (v == kForcePrefetchVariant) return launch_vec_pf<T, I, VEC, false>(L, lpr);
+  if (v == kForceGlobalVariant) return launch_vec_global<T, I, VEC>(L, lpr, nt);
   // light rows of the mid form: the prefetching small-launch configuration above N = 16 (5-12%
   // faster at N = 64 / 128 on 20k-170k-row power-law graphs), the big-launch one at N <= 16
   // (profiles/r02n_probe_mid.json)
@@ -1609,10 +1625,10 @@ int launch_shift(const Launch& L, bool nt) {
 template <typename T, typename I>
 int launch_shift_pf(const Launch& L) {
   switch (pick_lpr(L.n, 4)) {
-    case 8: return launch_cfg<T, I, Cfg<4, 8, 16, 4, false, true, false, false, false, true, 0, 16, true, true>>(L);
-    case 16: return launch_cfg<T, I, Cfg<4, 16, 16, 4, false, true, false, false, false, true, 0, 16, true, true>>(L);
-    case 32: return launch_cfg<T, I, Cfg<4, 32, 16, 4, false, true, false, false, false, true, 0, 16, true, true>>(L);
-    default: return launch_cfg<T, I, Cfg<4, 64, 16, 4, false, false, false, false, false, true, 0, 16, true, true>>(L);
+    case 8: return launch_cfg<T, I, Cfg<4, 8, 16, 4, false, true, false, false, false, true, 0, 16, true, kLR>>(L);
+    case 16: return launch_cfg<T, I, Cfg<4, 16, 16, 4, false, true, false, false, false, true, 0, 16, true, kLR>>(L);
+    case 32: return launch_cfg<T, I, Cfg<4, 32, 16, 4, false, true, false, false, false, true, 0, 16, true, kLR>>(L);
+    default: return launch_cfg<T, I, Cfg<4, 64, 16, 4, false, false, false, false, false, true, 0, 16, true, kLR>>(L);
   }
 }
 
@@ -1640,7 +1656,7 @@ bool use_shift_form(const Launch& L, int elem_bytes) {
 template <typename T, typename I>
 int launch_narrow(const Launch& L) {
   if (L.nnz_est <= kPrefetchNnz)
-    return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, true, false, true, false, true, 16, 16, false, true>>(L);
+    return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
   return launch_cfg<T, I, Cfg<2, 8, 8, 4, false, true, false, true, false, true, 16, 8>>(L);
 }
 

@@ -34,8 +34,11 @@ struct Launch {
 // share.  The form heuristics use it so that a rank's slice of an S(0) split is treated as the
 // launch it is (with the matrix's nnz an 11M-nonzero graph on 8 ranks took the
 // single-GPU crossovers at 1.4M local nonzeros).  The workspace bounds keep the matrix's nnz.
-inline int64_t launch_nnz(int64_t m, int64_t nrows, int64_t nnz) {
+// A caller that knows the range's count passes it (options.range_nnz, ADVICE r3: an S(0) slice
+// of a degree-sorted or clustered graph can hold far more or fewer than its share).
+inline int64_t launch_nnz(int64_t m, int64_t nrows, int64_t nnz, const ofx_spmm_options* o) {
   if (m <= 0 || nrows >= m) return nnz;
+  if (o != nullptr && o->range_nnz > 0) return o->range_nnz < nnz ? o->range_nnz : nnz;
   return (int64_t)((__int128)nnz * nrows / m);
 }
 
@@ -100,12 +103,16 @@ inline bool use_prefetch_form(int64_t nrows, int64_t nnz, int64_t n, const Sched
 constexpr int kForceBigVariant = 30003;   // tuning: the planned big form, bandwidth configuration
 constexpr int kForceWaveVariant = 30004;  // tuning: the prefetching form with wave items
 constexpr int kForcePrefetchVariant = 30005;  // tuning: the prefetching form without wave items
+// tests: the bandwidth configuration with global B loads (the B >= 4 GiB path, whose out-of-range
+// columns read g_zero_row) at any size
+constexpr int kForceGlobalVariant = 30006;
 
 // Tuning variants that force a form (small / mid / big / wave) but keep the automatic
 // configuration.
 inline bool is_form_variant(int v) {
   return v == kForceSmallVariant || v == kForceMidVariant || v == kForceMidSmallVariant ||
-         v == kForceBigVariant || v == kForceWaveVariant || v == kForcePrefetchVariant;
+         v == kForceBigVariant || v == kForceWaveVariant || v == kForcePrefetchVariant ||
+         v == kForceGlobalVariant;
 }
 
 // The schedule a launch of `nrows` rows runs with: the mid form always plans (binned work list)

@@ -14,6 +14,24 @@
 #include "dbg_bounds.h"
 
 namespace ofx {
+
+// Agent-coherent accesses: relaxed agent-scope atomics (global_load / global_store ... sc1), seen
+// across the XCDs' L2s without an L2 write-back or invalidate.  An agent-scope fence is both
+// (buffer_wbl2 sc1 + buffer_inv sc1: the whole XCD's L2 written back and its lines dropped, for
+// every other wave on it too); the ordering these accesses need comes from s_waitcnt instead.
+template <typename A>
+__device__ __forceinline__ A coh_load(const A* p) {
+  if (!OFX_DOK(p, sizeof(A))) return A(0);  // OFX_DEBUG_BOUNDS builds only
+  return __hip_atomic_load(const_cast<A*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename A>
+__device__ __forceinline__ void coh_store(A* p, A v) {
+  if (!OFX_DOK(p, sizeof(A))) return;
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// This wave's stores have reached their coherence point (gfx9: stores count in vmcnt).
+__device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 namespace plan {
 namespace {  // internal linkage: every HIP translation unit gets its own copy
 
@@ -47,7 +65,10 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // waits only on lower-numbered blocks, which are dispatched first (each XCD dispatches its blocks
 // in order), so the chain always progresses.  This replaced count + scan + write launches
 // (products 11.3 + 9.6 + 14.6 us, arxiv-shaped 4.8 + 5.8 us).
-constexpr int kPlanRowsPerThread = 4;
+#ifndef OFX_PLAN_RPT  // rows per planner thread (compile-time knob for A/B builds)
+#define OFX_PLAN_RPT 4
+#endif
+constexpr int kPlanRowsPerThread = OFX_PLAN_RPT;
 constexpr int64_t kPlanRows = (int64_t)kBlock * kPlanRowsPerThread;
 constexpr int kBins = 2;
 constexpr int kPlanVals = 2 + kBins;  // hubs, chunks, bins...
@@ -199,13 +220,17 @@ __device__ __forceinline__ void plan_write_rows(const int (&cls)[kPlanRowsPerThr
   }
 }
 
-// Status word of plan block b (agent-scope atomics: the look-back crosses XCDs).
+// Status word of plan block b.  The look-back crosses XCDs: every look word is written and read
+// agent-coherent (coh_store / coh_load), and a status is published only once this wave's payload
+// stores are complete (wait_stores).  Acquire / release atomics here cost an L2 write-back and
+// invalidate per access: products' 2,392-block plan took 262 us with them (profiles/r04g_*).
 __device__ __forceinline__ unsigned long long look_status(unsigned long long* look, int64_t b) {
-  return __hip_atomic_load(look + b * kLookWords, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+  return coh_load(look + b * kLookWords);
 }
 __device__ __forceinline__ void look_publish(unsigned long long* look, int64_t b,
                                              unsigned long long status) {
-  __hip_atomic_store(look + b * kLookWords, status, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  wait_stores();
+  coh_store(look + b * kLookWords, status);
 }
 
 template <typename I>
@@ -223,36 +248,56 @@ __global__ void __launch_bounds__(kBlock)
   const int64_t base = b * kPlanRows + (int64_t)threadIdx.x * kPlanRowsPerThread;
   plan_thread(rp, row_begin, nrows, base, split, chunk, heavy, cls, nc, v);
   block_scan_vals(v, tot);
-  if (threadIdx.x == 0) {
-    // publish this block's totals (block 0: its inclusive prefix at once), then look back
+  if (threadIdx.x < 64) {
+    // Wave 0 publishes this block's totals (block 0: its inclusive prefix at once), then looks
+    // back over 64 predecessors per step, one per lane: the nearest one holding its inclusive
+    // prefix ends the walk, the aggregates of those after it are added.  One lane per step (the
+    // round-4 first cut) made the chain ~nblocks / 2 memory round trips long: products' 2,392
+    // plan blocks took ~0.7 ms (profiles/r04e_ab.jsonl); 64 lanes cut it 64-fold.
+    const int lane = threadIdx.x;
     unsigned long long* my = look + b * kLookWords;
+    if (lane == 0) {
 #pragma unroll
-    for (int i = 0; i < kPlanVals; ++i) {
-      my[1 + i] = (unsigned long long)tot[i];
-      if (b == 0) my[1 + kPlanVals + i] = (unsigned long long)tot[i];
+      for (int i = 0; i < kPlanVals; ++i) {
+        coh_store(my + 1 + i, (unsigned long long)tot[i]);
+        if (b == 0) coh_store(my + 1 + kPlanVals + i, (unsigned long long)tot[i]);
+      }
+      look_publish(look, b, epoch << 2 | (b == 0 ? kInc : kAgg));
     }
-    look_publish(look, b, epoch << 2 | (b == 0 ? kInc : kAgg));
     int64_t pre[kPlanVals] = {};
-    for (int64_t p = b - 1; p >= 0; --p) {
-      unsigned long long st;
-      while (((st = look_status(look, p)) >> 2) != epoch) __builtin_amdgcn_s_sleep(1);
-      const unsigned long long* pw = look + p * kLookWords;
-      if ((st & 3) == kInc) {
+    for (int64_t end = b; end > 0; end -= 64) {
+      const int64_t p = end - 1 - lane;  // lane 0: the nearest predecessor
+      unsigned long long st = epoch << 2 | kAgg;
+      if (p >= 0)
+        while (((st = look_status(look, p)) >> 2) != epoch) __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory");  // the payload loads below issue after the status returned
+      const unsigned long long incs = __ballot(p >= 0 && (st & 3) == kInc);
+      const int stop = incs ? __ffsll((long long)incs) - 1 : 64;  // nearest inclusive lane
+      int64_t x[kPlanVals];
+      const unsigned long long* pw = look + (p >= 0 ? p : 0) * kLookWords;
 #pragma unroll
-        for (int i = 0; i < kPlanVals; ++i) pre[i] += (int64_t)pw[1 + kPlanVals + i];
-        break;
+      for (int i = 0; i < kPlanVals; ++i)
+        x[i] = (p < 0 || lane > stop) ? 0
+               : (int64_t)coh_load(pw + (lane == stop ? 1 + kPlanVals + i : 1 + i));
+#pragma unroll
+      for (int w = 1; w < 64; w <<= 1)
+#pragma unroll
+        for (int i = 0; i < kPlanVals; ++i) x[i] += (int64_t)__shfl_xor((long long)x[i], w, 64);
+#pragma unroll
+      for (int i = 0; i < kPlanVals; ++i) pre[i] += x[i];
+      if (incs) break;
+    }
+    if (lane == 0) {
+      if (b > 0) {
+#pragma unroll
+        for (int i = 0; i < kPlanVals; ++i)
+          coh_store(my + 1 + kPlanVals + i, (unsigned long long)(pre[i] + tot[i]));
+        look_publish(look, b, epoch << 2 | kInc);
       }
 #pragma unroll
-      for (int i = 0; i < kPlanVals; ++i) pre[i] += (int64_t)pw[1 + i];
+      for (int i = 0; i < kPlanVals; ++i) s_off[i] = pre[i];
     }
-    if (b > 0) {
-#pragma unroll
-      for (int i = 0; i < kPlanVals; ++i) my[1 + kPlanVals + i] = (unsigned long long)(pre[i] + tot[i]);
-      look_publish(look, b, epoch << 2 | kInc);
-    }
-#pragma unroll
-    for (int i = 0; i < kPlanVals; ++i) s_off[i] = pre[i];
-    if (b == nblocks - 1) {  // the last block knows the grand totals
+    if (lane == 0 && b == nblocks - 1) {  // the last block knows the grand totals
       OFX_STP(counters + 0, (unsigned long long)(pre[1] + tot[1]));
       OFX_STP(counters + 1, (unsigned long long)(pre[0] + tot[0]));
       OFX_STP(counters + 2, 0ull);

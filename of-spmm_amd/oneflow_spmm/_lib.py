@@ -32,7 +32,7 @@ class Options(ctypes.Structure):
     _fields_ = [("split_threshold", ctypes.c_int64), ("chunk", ctypes.c_int64),
                 ("ordered", ctypes.c_int32), ("variant", ctypes.c_int32),
                 ("heavy_threshold", ctypes.c_int64), ("planned", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("reserved", ctypes.c_int32), ("range_nnz", ctypes.c_int64)]
 
 
 class Placement(ctypes.Structure):

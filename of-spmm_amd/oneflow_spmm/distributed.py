@@ -244,8 +244,11 @@ class GridPlan:
         self.kernel = None
         self.events = None
         if dev.type == "cuda":
+            # the row group's own nonzeros pick its kernel form (not its share of nnz)
+            self.grp_nnz = int(row_ptr[self.ghi]) - int(row_ptr[self.glo])
             self.kernel = ops.SpmmCsrKernel(o.m, o.k, w, col_idx.numel(), o.idx_dtype, dt,
-                                            dev, o.options).plan(row_ptr, self.glo, self.ghi)
+                                            dev, o.options).plan(row_ptr, self.glo, self.ghi,
+                                                                 range_nnz=self.grp_nnz)
             self.events = ([torch.cuda.Event() for _ in range(sub)],
                            [torch.cuda.Event() for _ in range(sub)])
 
@@ -303,7 +306,8 @@ class GridPlan:
     def _spmm(self, owner, s):
         rp, ci, v = self.csr
         if self.kernel is not None:
-            self.kernel(rp, ci, v, self.b_cols[s], self.c_grp[s], self.glo, self.ghi, planned=True)
+            self.kernel(rp, ci, v, self.b_cols[s], self.c_grp[s], self.glo, self.ghi, planned=True,
+                        range_nnz=self.grp_nnz)
         else:
             ops.spmm_csr_cpu(rp, ci, v, self.b_cols[s], owner.m, owner.k, out=self.c_grp[s],
                              row_begin=self.glo, row_end=self.ghi, options=owner.options)
@@ -454,7 +458,7 @@ class RowSplitSpmm:
             self.kernel = ops.SpmmCsrKernel(m_kernel, self.k_padded, self.nc, self.nnz_local,
                                             self.idx_dtype, self.dtype, self.device, self.options)
             if self._bound is not None:
-                self.kernel.plan(self._bound[0], *self._rows())
+                self.kernel.plan(self._bound[0], *self._rows(), range_nnz=self._range_nnz())
         if shard is not None:
             self.load_shard(shard)
 
@@ -462,6 +466,11 @@ class RowSplitSpmm:
         """The kernel's row range: local rows of a local CSR, or this rank's rows of the full one."""
         lo, hi = self.row_range
         return (0, hi - lo) if self.local_csr else (lo, hi)
+
+    def _range_nnz(self) -> int:
+        """This rank's nonzeros when its rows are a range of the full CSR (the launch's form
+        choice; a local CSR's launch covers all of it, so the count is exact there already)."""
+        return 0 if self.local_csr else int(self.nnz_local)
 
     def _planned(self, row_ptr) -> bool:
         """Launches over the bound CSR reuse the plan built at bind()."""
@@ -593,7 +602,7 @@ class RowSplitSpmm:
         o = out[:, c * self.nc:(c + 1) * self.nc]
         if self.kernel is not None:
             self.kernel(row_ptr, col_idx, values, self.gathered[c], o, rb, re, stream=stream,
-                        planned=self._planned(row_ptr))
+                        planned=self._planned(row_ptr), range_nnz=self._range_nnz())
         else:
             m_kernel = hi - lo if self.local_csr else self.m
             ops.spmm_csr_cpu(row_ptr, col_idx, values, self.gathered[c], m_kernel, self.k_padded,
@@ -696,7 +705,7 @@ class RowSplitSpmm:
             self.set_halo_pipeline(1, row_ptr=row_ptr, nnz=col_idx.numel())
         self._bound = (row_ptr, cols, values)
         if self.kernel is not None:
-            self.kernel.plan(row_ptr, *self._rows())
+            self.kernel.plan(row_ptr, *self._rows(), range_nnz=self._range_nnz())
 
     def set_halo_pipeline(self, chunks: int, row_ptr=None, nnz=None):
         """(Re)lays out the halo buffers for `chunks` column blocks of N/C, block-major like the
@@ -723,7 +732,9 @@ class RowSplitSpmm:
             rows_local = self.row_range[1] - self.row_range[0]
             self.halo_kernel = ops.SpmmCsrKernel(rows_local if self.local_csr else self.m,
                                                  h.k_compact, nc, nnz, self.idx_dtype, self.dtype,
-                                                 self.device, self.options).plan(row_ptr, *self._rows())
+                                                 self.device, self.options).plan(
+                                                     row_ptr, *self._rows(),
+                                                     range_nnz=self._range_nnz())
         self._load_halo_shard(shard)
 
     def _load_halo_shard(self, b_shard: torch.Tensor):
@@ -770,7 +781,8 @@ class RowSplitSpmm:
         nc = self.halo_nc
         o = out[:, c * nc:(c + 1) * nc]
         if self.halo_kernel is not None:
-            self.halo_kernel(row_ptr, cols["halo"], values, self.compact[c], o, rb, re, planned=True)
+            self.halo_kernel(row_ptr, cols["halo"], values, self.compact[c], o, rb, re, planned=True,
+                             range_nnz=self._range_nnz())
         else:
             m_kernel = hi - lo if self.local_csr else self.m
             ops.spmm_csr_cpu(row_ptr, cols["halo"], values, self.compact[c], m_kernel,

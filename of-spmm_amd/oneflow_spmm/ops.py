@@ -16,11 +16,23 @@ INT64_MAX = (1 << 63) - 1
 
 
 def make_options(split: int = 0, chunk: int = 0, ordered: bool = False, variant: int = 0,
-                 heavy: int = 0, planned: bool = False) -> Options:
+                 heavy: int = 0, planned: bool = False, range_nnz: int = 0) -> Options:
     """heavy: rows longer than this (not split) are scheduled first; 0 = default, <0 = off.
-    planned: the workspace holds ofx_spmm_csr_plan's work list (see SpmmCsrKernel.plan)."""
+    planned: the workspace holds ofx_spmm_csr_plan's work list (see SpmmCsrKernel.plan).
+    range_nnz: the launch's row range holds this many nonzeros (0 = estimated as its share of
+    nnz); picks the kernel form only."""
     return Options(int(split), int(chunk), 1 if ordered else 0, int(variant), int(heavy),
-                   1 if planned else 0, 0)
+                   1 if planned else 0, 0, int(range_nnz))
+
+
+def _with(o: Options | None, **fields) -> Options:
+    """A copy of options `o` (None: the defaults) with `fields` replaced."""
+    c = Options()
+    if o is not None:
+        ctypes.memmove(ctypes.addressof(c), ctypes.addressof(o), ctypes.sizeof(Options))
+    for key, val in fields.items():
+        setattr(c, key, val)
+    return c
 
 
 def default_split(n: int) -> int:
@@ -55,35 +67,36 @@ class SpmmCsrKernel:
         self._planned_for = None
         self._planned_opts = None
 
-    def plan(self, row_ptr, row_begin=0, row_end=None, stream=None):
+    def plan(self, row_ptr, row_begin=0, row_end=None, stream=None, range_nnz: int = 0):
         row_end = self.m if row_end is None else row_end
         s = stream if stream is not None else current_stream_handle(row_ptr)
+        o = _with(self.options, range_nnz=int(range_nnz)) if range_nnz else self.options
         check(LIB.ofx_spmm_csr_plan(s, self.idx_dt, self.val_dt, self.m, self.k, self.n, self.nnz,
                                     row_ptr.data_ptr(), row_begin, row_end,
                                     self.workspace.data_ptr(), self.ws_bytes,
-                                    ctypes.byref(self.options) if self.options else None),
+                                    ctypes.byref(o) if o else None),
               "spmm_csr_plan")
-        o = self.options or Options()
-        self._planned_opts = Options(o.split_threshold, o.chunk, o.ordered, o.variant,
-                                     o.heavy_threshold, 1, 0)
-        self._planned_for = (row_ptr.data_ptr(), row_ptr.numel(), row_begin, row_end)
+        self._planned_opts = _with(o, planned=1)
+        self._planned_for = (row_ptr.data_ptr(), row_ptr.numel(), row_begin, row_end, int(range_nnz))
         return self
 
-    def launch_options(self, row_ptr, row_begin, row_end, planned: bool):
+    def launch_options(self, row_ptr, row_begin, row_end, planned: bool, range_nnz: int = 0):
         """The options struct of one launch (the planned form after a matching plan())."""
         if not planned:
-            return self.options
-        if self._planned_for != (row_ptr.data_ptr(), row_ptr.numel(), row_begin, row_end):
-            raise RuntimeError("SpmmCsrKernel: planned launch without a plan() of this row_ptr "
-                               "and row range")
+            return _with(self.options, range_nnz=int(range_nnz)) if range_nnz else self.options
+        if self._planned_for != (row_ptr.data_ptr(), row_ptr.numel(), row_begin, row_end,
+                                 int(range_nnz)):
+            raise RuntimeError("SpmmCsrKernel: planned launch without a plan() of this row_ptr, "
+                               "row range and range_nnz")
         return self._planned_opts
 
     def __call__(self, row_ptr, col_idx, values, b, out, row_begin=0, row_end=None, stream=None,
-                 bias=None, relu=False, planned: bool = False):
-        """bias / relu: the fused epilogue (ofx_spmm_csr_fused); none = the plain op."""
+                 bias=None, relu=False, planned: bool = False, range_nnz: int = 0):
+        """bias / relu: the fused epilogue (ofx_spmm_csr_fused); none = the plain op.
+        range_nnz: nonzeros of [row_begin, row_end) if known (the form choice; 0 = estimated)."""
         row_end = self.m if row_end is None else row_end
         s = stream if stream is not None else current_stream_handle(b)
-        opts = self.launch_options(row_ptr, row_begin, row_end, planned)
+        opts = self.launch_options(row_ptr, row_begin, row_end, planned, range_nnz)
         check(LIB.ofx_spmm_csr_fused(s, self.idx_dt, self.val_dt, self.m, self.k, self.n, self.nnz,
                                      row_ptr.data_ptr(), col_idx.data_ptr() if col_idx.numel() else None,
                                      values.data_ptr() if values.numel() else None,

@@ -160,6 +160,23 @@ def main():
         np.savez_compressed(path, row_ptr=rp, col_idx=c, values=v, b=b, bias=bias, m=m, k=k,
                             expected_relu_f64=relu, absum=absum)
         manifest["files"][f"{name}.npz"] = hashlib.sha256(open(path, "rb").read()).hexdigest()
+
+    # N = 256 (the Reddit configuration's width): at N = 256 the split is 256
+    # nonzeros, so the 900- and 600-nonzero rows are hubs of 3 and 2 chunks, the 256-nonzero row
+    # is one chunk exactly and the 257-nonzero row is just over.  Separate RNG: the fixtures above
+    # are unchanged.
+    nrng = np.random.default_rng(20261017)
+    m, k, n = 120, 1000, 256
+    deg = nrng.integers(0, 40, size=m)
+    deg[[0, 5, 60, 61, 119]] = [0, 900, 256, 257, 600]
+    for name, exact in (("n256_f32", False), ("n256_exact", True)):
+        rp, c, v = make_csr(m, k, deg, nrng, exact=exact)
+        b = dense(k, n, nrng, exact=exact)
+        e64, absum, e32 = expected(rp, c, v, b, m, k)
+        path = os.path.join(HERE, f"{name}.npz")
+        np.savez_compressed(path, row_ptr=rp, col_idx=c, values=v, b=b, m=m, k=k,
+                            expected_f64=e64, absum=absum, expected_t32=e32)
+        manifest["files"][f"{name}.npz"] = hashlib.sha256(open(path, "rb").read()).hexdigest()
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
     print("wrote", len(manifest["files"]), "fixtures")

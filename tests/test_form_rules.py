@@ -109,6 +109,26 @@ def test_row_range_uses_its_share_of_nonzeros():
     assert d["form"] == "prefetch"
 
 
+def test_row_range_with_its_known_nonzeros():
+    """options.range_nnz: a caller that knows the range's count overrides the
+    proportional estimate, e.g. the first eighth of a degree-sorted products graph holding most of
+    its nonzeros takes the bandwidth form, a sparse tail slice the prefetching one; the count is
+    clamped to the matrix's nnz and 0 keeps the estimate."""
+    m, nnz = 2_449_029, 123_718_280
+    rng = dict(row_begin=0, row_end=m // 8)
+    est = form(m, nnz, 128, **rng)
+    assert form(m, nnz, 128, options=ops.make_options(range_nnz=0), **rng) == est
+    assert form(m, nnz, 128, options=ops.make_options(range_nnz=2_000_000), **rng)["form"] == "prefetch"
+    arxiv = dict(row_begin=0, row_end=30_000)  # estimated 206k nonzeros: the mid form
+    assert form(169_343, 1_166_243, 64, **arxiv)["form"] == "mid"
+    assert form(169_343, 1_166_243, 64, options=ops.make_options(range_nnz=100_000),
+                **arxiv)["form"] == "small"
+    assert form(169_343, 1_166_243, 64, options=ops.make_options(range_nnz=10**12),
+                **arxiv)["form"] == "mid"  # clamped to the matrix's 1.17M
+    # a launch over every row ignores it (nnz is exact there)
+    assert form(m, nnz, 128, options=ops.make_options(range_nnz=5))["form"] == "bandwidth"
+
+
 def test_forced_forms():
     m, nnz = 169_343, 1_166_243
     assert form(m, nnz, 64, options=ops.make_options(variant=30000))["form"] == "small"

@@ -72,6 +72,28 @@ def test_oracle_chunked_schedule_by_hand():
     np.testing.assert_array_equal(got[r], acc)
 
 
+def test_oracle_default_schedule_at_n256_by_hand():
+    """N = 256: the default split is 256 nonzeros; the 900-nonzero row is 3 chunks (256, 256, 388),
+    the 257-nonzero row 1 chunk (floor(257 / 256) chunks, the last taking the remainder: the
+    whole row from +0), the 600-nonzero row 2 chunks (256, 344)."""
+    z = np.load(os.path.join(GOLD, "n256_f32.npz"))
+    rp, c, v, b = z["row_ptr"], z["col_idx"], z["values"], z["b"]
+    got = oracle.spmm(rp, c, v, b, nthreads=2)
+    for r, want_chunks in ((5, 3), (61, 1), (119, 2), (60, 1)):
+        j0, j1 = int(rp[r]), int(rp[r + 1])
+        nc = max(1, (j1 - j0) // 256) if j1 - j0 > 256 else 1
+        assert nc == want_chunks
+        acc = np.zeros(256, dtype=np.float32)
+        for q in range(nc):
+            a = j0 + q * 256
+            e = j1 if q == nc - 1 else a + 256
+            part = np.zeros(256, dtype=np.float32)
+            for j in range(a, e):
+                part = (part + (v[j] * b[c[j]]).astype(np.float32)).astype(np.float32)
+            acc = (acc + part).astype(np.float32) if nc > 1 else part
+        np.testing.assert_array_equal(got[r], acc)
+
+
 def test_balanced_range_fixture():
     part = json.load(open(os.path.join(GOLD, "partition.json")))
     for key, ranges in part["balanced"].items():

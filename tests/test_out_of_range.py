@@ -92,6 +92,18 @@ def test_negative_column_raises_on_cpu():
                                   oracle_spmm(rp, ci2, v, b2).view(np.uint32))
 
 
+def test_cpu_gradient_ops_raise_on_a_negative_column():
+    """The kCPU transpose and SDDMM report a negative column as the kCPU forward does (the CPU
+    gather's CHECK_GE, gather_kernel_util.cpp:80), instead of zero-filling it."""
+    rng = np.random.default_rng(17)
+    m, k, n, rp, ci, v, b = _problem(rng, n=8)
+    ci[33] = -2
+    with pytest.raises(fs.OfxError, match="negative column"):
+        fs.csr_transpose(rp, ci, k)
+    with pytest.raises(fs.OfxError, match="negative column"):
+        fs.sddmm(rp, ci, random_dense(m, n, rng), b)
+
+
 def test_cpu_transpose_and_sddmm_with_out_of_range_columns():
     rng = np.random.default_rng(11)
     m, k, n, rp, ci, v, b = _problem(rng, n=24)
@@ -115,7 +127,8 @@ def test_cpu_transpose_and_sddmm_with_out_of_range_columns():
 
 
 # ---- HIP ----------------------------------------------------------------------------------------
-FORMS = [0, 30000, 30001, 30002, 30003, 30004]
+# auto, small, mid (two), bandwidth, prefetching with / without wave items, global B loads
+FORMS = [0, 30000, 30001, 30002, 30003, 30004, 30005, 30006]
 
 
 @pytest.mark.gpu
@@ -170,3 +183,31 @@ def test_gpu_transpose_and_sddmm_with_out_of_range_columns(device):
         got = fs.sddmm(rp.to(device), ci.to(device), aa.to(device), bb.to(device))
         ref = oracle.sddmm(rp.numpy(), ci.numpy(), aa.numpy(), bb.numpy())
         np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,n", [("f32", 16), ("f32", 99), ("bf16", 32)])
+def test_gpu_zero_fill_mid_size_automatic_forms(device, dtype, n):
+    """out-of-range columns in launches of more than 32,768 rows and more than 3M
+    nonzeros, where only the automatic choice reaches the N = 16 narrow form (16-lane wave items),
+    the shifted window (odd widths), the 16-bit lane layouts and the by-index light rows; and the
+    same graph below 3M nonzeros (the prefetching form, its in-kernel hub reduce)."""
+    dt = DTYPES[dtype]
+    for nnz in (3_300_000, 2_900_000):
+        m = k = 100_000
+        rp, ci, v = fs.synth.csr(m, k, nnz, val_dtype=dt)
+        rng = np.random.default_rng(nnz + n)
+        ci = ci.clone()
+        bad = rng.choice(ci.numel(), size=2000, replace=False)
+        ci[bad[:1000]] = k
+        ci[bad[1000:]] = k + 777
+        hub = int(torch.argmax(rp[1:] - rp[:-1]))  # the longest row: a split hub
+        ci[int(rp[hub]) + np.arange(0, 2048, 97)] = k
+        b = random_dense(k, n, rng, dt)
+        ci2, b2 = _appended(ci, b, k)
+        ref = oracle_spmm(rp, ci2, v, b2)
+        d = [t.to(device) for t in (rp, ci, v, b)]
+        out = fs.spmm(*d[:3], m, k, d[3])
+        torch.cuda.synchronize()
+        assert_bitwise(out, ref, f"{dtype} n={n} nnz={nnz} auto "
+                                 f"({ops.describe(m, k, n, nnz, dt)['form']})")
