@@ -1666,6 +1666,28 @@ bool use_narrow_form(const Launch& L, int elem_bytes) {
          !use_mid_form(L.nrows, L.nnz_est, L.n, L.sched);
 }
 
+// Narrow rows of mid-size launches (round 4): 16-bit rows of 8 or 16 columns and fp32 rows of 8
+// in the prefetching form take the narrow form's shape -- four lanes per light row (8 B per lane),
+// hub chunks and heavy rows as 16-lane one-element wave items, hubs added in the kernel -- instead
+// of one element per lane over 8-16 lanes.  Tuning entries 10050-10063 on three mid-size graphs
+// (profiles/r04k_variants.jsonl; arxiv-shaped / 60k x 1.5M / 169k x 2M): bf16 N = 16 86 / 77 / 94
+// -> 50 / 45 / 58 us and N = 8 99 / 82 / 105 -> 50 / 45 / 55 (U = 8, entry 51), fp32 N = 8 74 /
+// 66 / 74 -> 46 / 43 / 53 (U = 4, entry 63).  Same bits: only who adds changes.
+template <typename T, typename I>
+int launch_narrow_pf(const Launch& L) {
+  if constexpr (sizeof(T) == 2)
+    return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
+  else
+    return launch_cfg<T, I, Cfg<2, 4, 4, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
+}
+
+bool use_narrow_pf_form(const Launch& L, int elem_bytes) {
+  if (L.sched.variant != 0 || !use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched)) return false;
+  if (elem_bytes == 2) return (L.n == 8 || L.n == 16) && pick_vec(2, L, 0, 4) == 4;
+  if (elem_bytes == 4) return L.n == 8 && pick_vec(4, L, 0, 2) == 2;
+  return false;
+}
+
 }  // namespace
 
 template <typename T, typename I>
@@ -1675,6 +1697,10 @@ int launch_typed(const Launch& L) {
     OFX_REQUIRE(buffer_rows_ok<T>(L), OFX_EINVAL,
                 "spmm_csr: tuning variant %d needs B under 4 GiB", L.sched.variant);
     return launch_tuned<T, I>(L, L.sched.variant - 10000);
+  }
+  if constexpr (sizeof(T) <= 4) {
+    if (use_narrow_pf_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
+      return launch_narrow_pf<T, I>(L);
   }
   if constexpr (sizeof(T) == 4) {
     if (use_narrow_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L)) return launch_narrow<T, I>(L);

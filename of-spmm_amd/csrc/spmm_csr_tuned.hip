@@ -10,6 +10,42 @@ namespace ofx {
 // same bits (the accumulation order does not depend on the launch shape).
 template <typename T, typename I>
 int launch_tuned(const Launch& L, int id) {
+  // rows of VEC-element lanes: n, the strides and both pointers a multiple of VEC elements
+  auto rows_of = [&](int vec) {
+    const uintptr_t a = (uintptr_t)vec * sizeof(T);
+    return L.n % vec == 0 && L.ldb % vec == 0 && L.ldc % vec == 0 && ((uintptr_t)L.b % a) == 0 &&
+           ((uintptr_t)L.c % a) == 0;
+  };
+  // Round 4: narrow rows of mid-size launches (the prefetching form's share of the narrow form:
+  // VEC x LPR light-row layouts with HL-lane one-element wave items, hubs added in the kernel).
+  // 16-bit N = 16 / 8 and fp32 N = 8 (profiles/r04i_sweep.jsonl: 73-98 us against fp32 N = 16's
+  // 47 us in the narrow form on the arxiv-shaped graph).
+  if constexpr (sizeof(T) == 2 && std::is_same<I, int32_t>::value) {
+    constexpr bool P = true, W = true;
+    switch (id) {
+      case 50: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
+      case 51: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
+      case 52: if (rows_of(2)) return launch_cfg<T, I, Cfg<2, 8, 4, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
+      case 53: if (rows_of(2)) return launch_cfg<T, I, Cfg<2, 8, 8, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
+      case 54: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, P, false, W, false, true, 16, 8, false, kLR>>(L); break;
+      case 55: if (rows_of(2)) return launch_cfg<T, I, Cfg<2, 4, 4, 4, false, P, false, W, false, true, 8, 16, false, kLR>>(L); break;
+      case 56: if (rows_of(2)) return launch_cfg<T, I, Cfg<2, 4, 8, 4, false, P, false, W, false, true, 8, 16, false, kLR>>(L); break;
+      case 57: return launch_cfg<T, I, Cfg<1, 8, 8, 4, false, P, false, W, false, true, 8, 16, false, kLR>>(L);
+      case 58: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, false, false, true, 0, 16, false, kLR>>(L); break;
+      case 59: if (rows_of(8)) return launch_cfg<T, I, Cfg<8, 4, 4, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
+      default: break;
+    }
+  }
+  if constexpr (std::is_same<T, float>::value && std::is_same<I, int32_t>::value) {
+    constexpr bool P = true, W = true;
+    switch (id) {
+      case 60: if (rows_of(2)) return launch_cfg<T, I, Cfg<2, 4, 4, 4, false, P, false, W, false, true, 8, 16, false, kLR>>(L); break;
+      case 61: if (rows_of(2)) return launch_cfg<T, I, Cfg<2, 4, 8, 4, false, P, false, W, false, true, 8, 16, false, kLR>>(L); break;
+      case 62: return launch_cfg<T, I, Cfg<1, 8, 8, 4, false, P, false, W, false, true, 8, 16, false, kLR>>(L);
+      case 63: if (rows_of(2)) return launch_cfg<T, I, Cfg<2, 4, 4, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
+      default: break;
+    }
+  }
   if constexpr (std::is_same<T, float>::value && std::is_same<I, int32_t>::value) {
     OFX_REQUIRE(L.n % 4 == 0 && L.ldb % 4 == 0 && L.ldc % 4 == 0 && ((uintptr_t)L.b % 16) == 0 &&
                     ((uintptr_t)L.c % 16) == 0,

@@ -45,7 +45,7 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // kernel walks ONE work list: the hub chunks first, then the heavy rows, then the light rows, so
 // the longest work starts first and the grid ends on short rows.  Two bins measured best on
 // MI355X: the light rows keep index order (sequential row_ptr reads and C writes); more bins cost
-// products-scale 1.2% in random row_ptr/C traffic.  Rows are taken kPlanRows per
+// products-scale 1.2% in random row_ptr/C traffic.  Rows are taken 256 * plan_rpt per
 // block.  The plan writes
 //   hubs[3i..3i+2] = {local row, first chunk slot, chunks}          (i < counters[1])
 //   items[2s..2s+1] = {local row, chunk}                            (s < counters[0])
@@ -65,11 +65,13 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // waits only on lower-numbered blocks, which are dispatched first (each XCD dispatches its blocks
 // in order), so the chain always progresses.  This replaced count + scan + write launches
 // (products 11.3 + 9.6 + 14.6 us, arxiv-shaped 4.8 + 5.8 us).
-#ifndef OFX_PLAN_RPT  // rows per planner thread (compile-time knob for A/B builds)
-#define OFX_PLAN_RPT 4
-#endif
-constexpr int kPlanRowsPerThread = OFX_PLAN_RPT;
-constexpr int64_t kPlanRows = (int64_t)kBlock * kPlanRowsPerThread;
+// Rows per planner thread: 4 up to kPlanRptRows rows, 16 above.  Fewer plan blocks shorten the
+// look-back (products: 2,392 blocks of 1,024 rows -> 598 of 4,096); more rows per block lengthen
+// each block's count-and-write, which a launch of few blocks feels (graph replay, same box,
+// profiles/r04i_ab.jsonl, rows per thread 4 / 8 / 16: products 8477 / 8440 / 8413 us, 1M
+// power-law N=16 359 / 353 / 352; 20k rows 29.1 / 30.6 / 33.4, 60k x 1.5M 42.7 / 44.3 / 47.5).
+constexpr int64_t kPlanRptRows = int64_t(1) << 18;
+inline int plan_rpt(int64_t nrows) { return nrows <= kPlanRptRows ? 4 : 16; }
 constexpr int kBins = 2;
 constexpr int kPlanVals = 2 + kBins;  // hubs, chunks, bins...
 constexpr int64_t kOwnItems = 8;      // hubs with more chunks get their items written wave-wide
@@ -139,17 +141,16 @@ __device__ __forceinline__ void block_scan_vals(int64_t (&v)[kPlanVals], int64_t
   __syncthreads();
 }
 
-template <typename I>
+template <int RPT, typename I>
 __device__ __forceinline__ void plan_thread(const I* __restrict__ rp, int64_t row_begin,
                                             int64_t nrows, int64_t base, int64_t split,
                                             int64_t chunk, int64_t heavy,
-                                            int (&cls)[kPlanRowsPerThread],
-                                            int64_t (&nc)[kPlanRowsPerThread],
+                                            int (&cls)[RPT], int64_t (&nc)[RPT],
                                             int64_t (&v)[kPlanVals]) {
 #pragma unroll
   for (int i = 0; i < kPlanVals; ++i) v[i] = 0;
 #pragma unroll
-  for (int q = 0; q < kPlanRowsPerThread; ++q) {
+  for (int q = 0; q < RPT; ++q) {
     cls[q] = plan_row(rp, row_begin, nrows, base + q, split, chunk, heavy, nc[q]);
     if (cls[q] == -1) {
       v[0] += 1;
@@ -163,8 +164,8 @@ __device__ __forceinline__ void plan_thread(const I* __restrict__ rp, int64_t ro
 
 // Writes one block's hubs / chunk items / heavy and light rows, given this thread's exclusive
 // offsets `v` inside the block and the block's offsets `off` among all earlier blocks.
-__device__ __forceinline__ void plan_write_rows(const int (&cls)[kPlanRowsPerThread],
-                                                const int64_t (&nc)[kPlanRowsPerThread],
+template <int RPT>
+__device__ __forceinline__ void plan_write_rows(const int (&cls)[RPT], const int64_t (&nc)[RPT],
                                                 const int64_t (&v)[kPlanVals], const int64_t* off,
                                                 int64_t base, int64_t nrows,
                                                 int64_t* __restrict__ hubs,
@@ -175,9 +176,9 @@ __device__ __forceinline__ void plan_write_rows(const int (&cls)[kPlanRowsPerThr
   int64_t slot = off[1] + v[1];
   int64_t heavy_pos = off[2] + v[2];  // heavy row h goes to order[nrows - 1 - h]
   int64_t light_pos = off[3] + v[3];
-  int64_t first[kPlanRowsPerThread];
+  int64_t first[RPT];
 #pragma unroll
-  for (int q = 0; q < kPlanRowsPerThread; ++q) {
+  for (int q = 0; q < RPT; ++q) {
     const int64_t g = base + q;
     first[q] = slot;
     if (cls[q] == -1) {
@@ -204,7 +205,7 @@ __device__ __forceinline__ void plan_write_rows(const int (&cls)[kPlanRowsPerThr
   // Hubs with many chunks: the whole wave writes their (row, chunk) items, 64 lanes strided
   // (one thread looping over a 900-chunk hub held the Reddit-shaped plan at 38 us).
 #pragma unroll
-  for (int q = 0; q < kPlanRowsPerThread; ++q) {
+  for (int q = 0; q < RPT; ++q) {
     unsigned long long big = __ballot(cls[q] == -1 && nc[q] > kOwnItems);
     while (big) {
       const int src = __ffsll((long long)big) - 1;
@@ -233,7 +234,7 @@ __device__ __forceinline__ void look_publish(unsigned long long* look, int64_t b
   coh_store(look + b * kLookWords, status);
 }
 
-template <typename I>
+template <int RPT, typename I>
 __global__ void __launch_bounds__(kBlock)
     spmm_plan_kernel(const I* __restrict__ rp, int64_t row_begin, int64_t nrows, int64_t split,
                      int64_t chunk, int64_t heavy, unsigned long long* __restrict__ look,
@@ -242,11 +243,11 @@ __global__ void __launch_bounds__(kBlock)
                      int64_t* __restrict__ items, int64_t* __restrict__ order,
                      unsigned* __restrict__ arrive) {
   __shared__ int64_t s_off[kPlanVals];
-  int cls[kPlanRowsPerThread];
-  int64_t nc[kPlanRowsPerThread], v[kPlanVals], tot[kPlanVals];
+  int cls[RPT];
+  int64_t nc[RPT], v[kPlanVals], tot[kPlanVals];
   const int64_t b = blockIdx.x;
-  const int64_t base = b * kPlanRows + (int64_t)threadIdx.x * kPlanRowsPerThread;
-  plan_thread(rp, row_begin, nrows, base, split, chunk, heavy, cls, nc, v);
+  const int64_t base = (b * kBlock + (int64_t)threadIdx.x) * RPT;
+  plan_thread<RPT>(rp, row_begin, nrows, base, split, chunk, heavy, cls, nc, v);
   block_scan_vals(v, tot);
   if (threadIdx.x < 64) {
     // Wave 0 publishes this block's totals (block 0: its inclusive prefix at once), then looks
@@ -327,7 +328,8 @@ WsLayout ws_layout(int64_t nrows, int64_t nnz, int64_t n, size_t acc_bytes, cons
   if (!bin && !hub) return w;  // identity work list: no plan, no workspace
   w.max_hubs = s.split == INT64_MAX ? 0 : nnz / (s.split + 1) + 1;
   w.max_chunks = s.split == INT64_MAX ? 0 : nnz / s.chunk + 1;
-  w.plan_blocks = (nrows + kPlanRows - 1) / kPlanRows;
+  const int64_t rows_per_block = (int64_t)kBlock * plan_rpt(nrows);
+  w.plan_blocks = (nrows + rows_per_block - 1) / rows_per_block;
   size_t off = 0;
   w.counters = off;
   off = align_up(off + (2 + kBins) * sizeof(unsigned long long), 256);
@@ -386,9 +388,15 @@ int launch_plan(hipStream_t stream, const I* rp, int64_t row_begin, int64_t nrow
   worklist_of(w, ws, wl);
   auto* look = reinterpret_cast<unsigned long long*>(ws + w.look);
   OFX_REQUIRE(w.plan_blocks < (int64_t)UINT32_MAX, OFX_EINVAL, "spmm_csr: too many rows to plan");
-  hipLaunchKernelGGL((spmm_plan_kernel<I>), dim3((unsigned)w.plan_blocks), dim3(kBlock), 0, stream,
-                     rp, row_begin, nrows, sched.split, sched.chunk, heavy, look, next_epoch(),
-                     w.plan_blocks, wl->counters, wl->hubs, wl->items, wl->order, wl->arrive);
+  const unsigned long long epoch = next_epoch();
+  if (plan_rpt(nrows) == 4)
+    hipLaunchKernelGGL((spmm_plan_kernel<4, I>), dim3((unsigned)w.plan_blocks), dim3(kBlock), 0,
+                       stream, rp, row_begin, nrows, sched.split, sched.chunk, heavy, look, epoch,
+                       w.plan_blocks, wl->counters, wl->hubs, wl->items, wl->order, wl->arrive);
+  else
+    hipLaunchKernelGGL((spmm_plan_kernel<16, I>), dim3((unsigned)w.plan_blocks), dim3(kBlock), 0,
+                       stream, rp, row_begin, nrows, sched.split, sched.chunk, heavy, look, epoch,
+                       w.plan_blocks, wl->counters, wl->hubs, wl->items, wl->order, wl->arrive);
   OFX_HIP_CHECK(hipGetLastError());
   return OFX_OK;
 }

@@ -18,4 +18,12 @@ tail -c 300 gpurun_out/r04f_rank_local_reddit_g4.json; echo
 bash scripts/profile.sh r04f_plaw1m --config plaw1m --steps 10 --warmup 3 --no-cpu-baseline || exit 1
 bash scripts/profile.sh r04f_reddit --config reddit --steps 10 --warmup 3 --no-cpu-baseline || exit 1
 cat gpurun_out/prof_r04f_plaw1m/trace_bench.json gpurun_out/prof_r04f_reddit/trace_bench.json
+# the 8-rank products rehearsal (gloo, ranks sharing this GPU): tune() must
+# report the plain row split + all-gather (torch/p1 here, rccl/p1 on the node) as measured
+T0=$SECONDS
+timeout -k 10 900 python -u bench.py --gpus 8 --backend gloo --steps 3 --warmup 1 --tune-budget 150 \
+  --deadline 850 > gpurun_out/r04f_rehearsal8_products.json 2> gpurun_out/r04f_rehearsal8_products.err \
+  || { tail -40 gpurun_out/r04f_rehearsal8_products.err; exit 1; }
+echo "rehearsal wall seconds: $((SECONDS - T0))" | tee -a gpurun_out/r04f_rehearsal8_products.err
+grep "tune\]" gpurun_out/r04f_rehearsal8_products.err | head -20
 echo all done

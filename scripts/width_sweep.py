@@ -69,14 +69,18 @@ def main():
             for var in [int(x) for x in args.variants.split(",")]:
                 if var:
                     vec, lpr = var // 100, var % 100
-                    if n % vec or vec * b.element_size() > 16 or vec * lpr > 4 * max(n, 1) + 64:
+                    if var < 10000 and (n % vec or vec * b.element_size() > 16 or
+                                        vec * lpr > 4 * max(n, 1) + 64):
                         continue
                     opts = ops.make_options(variant=var)
 
                     def call():
                         ops.spmm_csr_device(d_rp, d_ci, d_v, b, m, k, out=o2, options=opts)
                     o2 = torch.empty_like(out)
-                    call()
+                    try:  # tuning-table entries (10000 + id) refuse the dtypes / widths they lack
+                        call()
+                    except fs.OfxError:
+                        continue
                     torch.cuda.synchronize()
                     same = bool(torch.equal(o2.view(torch.uint8), out.view(torch.uint8)))
                 else:

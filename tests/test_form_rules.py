@@ -58,8 +58,9 @@ def test_narrow_form_n16_fp32():
     assert below["form"] == above["form"] == "narrow"
     assert (below["VEC"], below["LPR"], below["U"], below["HL"], below["HU"]) == (4, 4, 4, 16, 16)
     assert (above["VEC"], above["LPR"], above["U"], above["HL"], above["HU"]) == (2, 8, 8, 16, 8)
-    # fp32 only, N = 16 only, 16-B aligned only
-    assert form(m, K_PREFETCH_NNZ, 16, BF16)["form"] != "narrow"
+    # above kPrefetchNnz fp32 only (16-bit N = 16 below it: test_narrow_rows_of_mid_size_launches),
+    # N = 16 only, 16-B aligned only
+    assert form(m, K_PREFETCH_NNZ + 1, 16, BF16)["form"] != "narrow"
     assert form(m, K_PREFETCH_NNZ, 32)["form"] == "prefetch"
     assert form(m, K_PREFETCH_NNZ, 16, b_addr=260)["form"] != "narrow"
 
@@ -151,9 +152,28 @@ def test_prefetch_form_layouts():
     assert form(m, nnz, 15)["SH"] == 0  # 16 columns or fewer: one element per lane
     assert form(m, nnz, 17, b_addr=258 + 2)["SH"] == 1
     for dt in (BF16, F16):
-        for n, vec in ((8, 1), (16, 1), (32, 2), (48, 2), (64, 4), (128, 8)):
+        for n, vec in ((32, 2), (48, 2), (64, 4), (128, 8)):
             d = form(m, nnz, n, dt)
             assert d["form"] == "prefetch" and d["VEC"] == vec, (dt, n, d)
+
+
+def test_narrow_rows_of_mid_size_launches():
+    """Round 4: 16-bit N = 8 / 16 and fp32 N = 8 in the prefetching form's size range take the
+    narrow shape (4 lanes per light row, 8 B per lane; 16-lane wave items; hubs added in the
+    kernel); unaligned views and the sizes either side keep their forms."""
+    m, nnz = 169_343, 1_166_243
+    for dt in (BF16, F16):
+        for n in (8, 16):
+            d = form(m, nnz, n, dt)
+            assert (d["form"], d["VEC"], d["LPR"], d["U"], d["HL"], d["LR"]) == \
+                ("narrow", 4, 4, 8, 16, 1), (dt, n, d)
+        assert form(m, nnz, 16, dt, b_addr=258)["form"] == "prefetch"  # 2-B aligned B
+        assert form(m, K_PREFETCH_NNZ + 1, 16, dt)["form"] == "bandwidth"
+        assert form(20_000, 400_000, 16, dt)["form"] == "mid"
+    d = form(m, nnz, 8)
+    assert (d["form"], d["VEC"], d["LPR"], d["U"], d["HL"]) == ("narrow", 2, 4, 4, 16), d
+    assert form(m, nnz, 8, b_addr=260)["form"] == "prefetch"  # 4-B aligned B: one element per lane
+    assert form(m, nnz, 4)["form"] == "prefetch"
 
 
 def test_in_kernel_hub_reduce_only_in_mid_size_forms():

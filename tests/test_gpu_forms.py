@@ -41,7 +41,8 @@ def test_prefetch_form_threshold(device, side, dtype, n, idx):
     v = v32.to(dt)
     nnz = ci.numel()
     d_form = ops.describe(M, M, n, nnz, dt, idx)
-    assert d_form["form"] == ("prefetch" if side == "below" else
+    narrow_below = (dtype, n) in (("f32", 8), ("bf16", 8), ("bf16", 16), ("f16", 8), ("f16", 16))
+    assert d_form["form"] == (("narrow" if narrow_below else "prefetch") if side == "below" else
                               ("narrow" if (dtype, n) == ("f32", 16) else "bandwidth")), d_form
     rng = np.random.default_rng(7000 + n)
     b = random_dense(M, n, rng, dt)
