@@ -33,6 +33,13 @@ int launch_tuned(const Launch& L, int id) {
       case 57: return launch_cfg<T, I, Cfg<1, 8, 8, 4, false, P, false, W, false, true, 8, 16, false, kLR>>(L);
       case 58: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, false, false, true, 0, 16, false, kLR>>(L); break;
       case 59: if (rows_of(8)) return launch_cfg<T, I, Cfg<8, 4, 4, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
+      // odd 16-bit widths (no vector layout): one element per lane in 16 / 32-lane groups with
+      // several column passes, instead of one 64-lane row per wave
+      case 64: return launch_cfg<T, I, Cfg<1, 16, 32, 4, false, P, false, W, false, true, 0, 16, false, kLR>>(L);
+      case 65: return launch_cfg<T, I, Cfg<1, 32, 32, 4, false, P, false, W, false, true, 0, 16, false, kLR>>(L);
+      case 66: return launch_cfg<T, I, Cfg<1, 16, 32, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L);
+      case 67: return launch_cfg<T, I, Cfg<1, 16, 16, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L);
+      case 68: return launch_cfg<T, I, Cfg<1, 32, 16, 4, false, P, false, W, false, true, 32, 16, false, kLR>>(L);
       default: break;
     }
   }
