@@ -1681,6 +1681,24 @@ int launch_narrow_pf(const Launch& L) {
     return launch_cfg<T, I, Cfg<2, 4, 4, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
 }
 
+// Odd 16-bit widths of mid-size launches (round 4): no vector layout applies (an element is 2 B,
+// a window would be unaligned), so lanes hold one element each; the automatic layout gave a row
+// 64 lanes (one row per wave).  16-lane groups with ceil(N / 16) column passes and 16-lane wave
+// items (U = 16) up to N = 48, 32-lane groups with two passes above: tuning entries 10064-10068
+// (profiles/r04j_odd16.jsonl), arxiv-shaped bf16 N = 17 / 41 / 47 / 63 152 / 264 / 261 / 264 ->
+// 91 / 127 / 128 / 155 us, 60k x 1.5M 88 / 136 / 135 / 136 -> 78 / 116 / 117 / 117.
+template <typename T, typename I>
+int launch_odd16_pf(const Launch& L) {
+  if (L.n <= 48)
+    return launch_cfg<T, I, Cfg<1, 16, 16, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
+  return launch_cfg<T, I, Cfg<1, 32, 16, 4, false, true, false, true, false, true, 32, 16, false, kLR>>(L);
+}
+
+bool use_odd16_pf_form(const Launch& L, int elem_bytes) {
+  return L.sched.variant == 0 && elem_bytes == 2 && L.n > 16 && L.n <= 64 &&
+         pick_vec(2, L, 0) == 1 && use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched);
+}
+
 bool use_narrow_pf_form(const Launch& L, int elem_bytes) {
   if (L.sched.variant != 0 || !use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched)) return false;
   if (elem_bytes == 2) return (L.n == 8 || L.n == 16) && pick_vec(2, L, 0, 4) == 4;
@@ -1701,6 +1719,10 @@ int launch_typed(const Launch& L) {
   if constexpr (sizeof(T) <= 4) {
     if (use_narrow_pf_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
       return launch_narrow_pf<T, I>(L);
+  }
+  if constexpr (sizeof(T) == 2) {
+    if (use_odd16_pf_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
+      return launch_odd16_pf<T, I>(L);
   }
   if constexpr (sizeof(T) == 4) {
     if (use_narrow_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L)) return launch_narrow<T, I>(L);

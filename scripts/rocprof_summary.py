@@ -29,8 +29,16 @@ def main(src, tag, dst="profiles", alg_bytes=None):
         for r in csv.DictReader(open(f)):
             pmc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
     pmc_avg = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in pmc.items()}
-    main_k = max(stats, key=lambda s: s["pct"])["kernel"]
-    c = pmc_avg.get(main_k, {})
+    main_s = max(stats, key=lambda s: s["pct"])
+    main_k = main_s["kernel"]
+    # a launch of more than 2^32 threads goes out in pieces (papers-scale: 3 dispatches of
+    # spmm_main per op call); the planner runs once per call, so pieces = main / plan dispatches,
+    # and per-launch figures are the per-dispatch averages times that
+    plan_calls = [s["calls"] for s in stats if s["kernel"].startswith("spmm_plan_kernel")]
+    pieces = 1
+    if plan_calls and plan_calls[0] and main_s["calls"] % plan_calls[0] == 0:
+        pieces = main_s["calls"] // plan_calls[0]
+    c = {n: v * pieces for n, v in pmc_avg.get(main_k, {}).items()}
     traffic = {}
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         # gfx950: FETCH_SIZE tallies 128-B requests of wide streaming reads at 64 B (x2 correction,
@@ -47,13 +55,14 @@ def main(src, tag, dst="profiles", alg_bytes=None):
     if alg_bytes:
         # the gather model's bytes per launch against the measured beyond-L2 bytes,
         # and the dominant kernel's rate / fraction of the 8 TB/s HBM spec at its average duration
-        avg_us = max(stats, key=lambda s: s["pct"])["avg_us"]
+        avg_us = main_s["avg_us"] * pieces
         traffic["algorithmic_bytes_per_launch"] = float(alg_bytes)
         if "beyond_l2_bytes_per_launch" in traffic:
             traffic["beyond_l2_over_algorithmic"] = traffic["beyond_l2_bytes_per_launch"] / float(alg_bytes)
-        traffic["dominant_kernel_avg_us"] = avg_us
+        traffic["dominant_kernel_avg_us"] = avg_us  # per launch (all its dispatches)
         traffic["achieved_gbs_gather_model"] = float(alg_bytes) / (avg_us * 1e-6) / 1e9
         traffic["frac_of_8tbs"] = traffic["achieved_gbs_gather_model"] / 8000.0
+    traffic["dispatches_per_launch"] = pieces
     out = {"tag": tag, "dominant_kernel": main_k, "kernels": stats, "pmc_avg_per_dispatch": pmc_avg,
            "traffic": traffic}
     os.makedirs(dst, exist_ok=True)

@@ -185,3 +185,22 @@ def test_in_kernel_hub_reduce_only_in_mid_size_forms():
     assert form(1_000_000, 20_000_000, 16)["LR"] == 0           # narrow, past it
     assert form(2_449_029, 123_718_280, 128)["LR"] == 0         # bandwidth
     assert form(2708, 10556, 16)["LR"] == 0                     # small form: no plan
+
+
+def test_odd_16bit_widths_of_mid_size_launches():
+    """Round 4: odd 16-bit widths 17-64 in the prefetching form's size range take one-element lanes
+    in 16-lane groups (several column passes) up to N = 48 and 32-lane groups above, with wave
+    items of the same width, instead of one 64-lane row per wave; past kPrefetchNnz and for even
+    (vector) widths the layouts are unchanged."""
+    m, nnz = 169_343, 1_166_243
+    for dt in (BF16, F16):
+        for n, lpr in ((17, 16), (41, 16), (47, 16), (48, 16), (49, 32), (63, 32)):
+            if n % 2 == 0:
+                continue
+            d = form(m, nnz, n, dt)
+            assert (d["form"], d["VEC"], d["LPR"], d["U"], d["HL"], d["LR"]) == \
+                ("narrow", 1, lpr, 16, lpr, 1), (dt, n, d)
+        assert form(m, nnz, 48, dt)["VEC"] == 2                 # even: a vector layout
+        assert form(m, nnz, 48, dt, b_addr=258)["LPR"] == 16    # an unaligned view: one-element lanes
+        assert form(m, nnz, 65, dt)["LPR"] == 64                # past 64 columns: unchanged
+        assert form(m, K_PREFETCH_NNZ + 1, 41, dt)["form"] == "bandwidth"
