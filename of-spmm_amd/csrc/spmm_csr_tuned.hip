@@ -50,6 +50,17 @@ int launch_tuned(const Launch& L, int id) {
       case 61: if (rows_of(2)) return launch_cfg<T, I, Cfg<2, 4, 8, 4, false, P, false, W, false, true, 8, 16, false, kLR>>(L); break;
       case 62: return launch_cfg<T, I, Cfg<1, 8, 8, 4, false, P, false, W, false, true, 8, 16, false, kLR>>(L);
       case 63: if (rows_of(2)) return launch_cfg<T, I, Cfg<2, 4, 4, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
+      // fp32 N = 17-32 of mid-size launches (round 4: N = 17 took 113 us against 49 at N = 16 in
+      // the shifted-window prefetching configuration): one-element 16 / 32-lane groups with column
+      // passes, and the shifted window with 16-lane wave items
+      case 69: return launch_cfg<T, I, Cfg<1, 16, 16, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L);
+      case 70: return launch_cfg<T, I, Cfg<1, 32, 16, 4, false, P, false, W, false, true, 32, 16, false, kLR>>(L);
+      case 71: if (((uintptr_t)L.b % 4) == 0 && ((uintptr_t)L.c % 4) == 0 && L.n >= 4)
+                 return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L);
+               break;
+      case 72: if (((uintptr_t)L.b % 4) == 0 && ((uintptr_t)L.c % 4) == 0 && L.n >= 4)
+                 return launch_cfg<T, I, Cfg<4, 8, 4, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L);
+               break;
       default: break;
     }
   }
