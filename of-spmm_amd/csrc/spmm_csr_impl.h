@@ -1632,6 +1632,22 @@ int launch_shift_pf(const Launch& L) {
   }
 }
 
+// fp32 rows of 17-32 columns in the prefetching form: the shifted 16-B window (any N, 4-B
+// alignment) over 8 lanes with U = 8 and the hub chunks / heavy rows as 16-lane one-element wave
+// items (tuning entry 10071; profiles/r04s_f32mid.jsonl): arxiv-shaped N = 17 / 24 / 25 / 32
+// 112 / 88 / 120 / 89 -> 76 / 76 / 77 / 75 us, 60k x 1.5M 106 / 82 / 110 / 82 -> 71 / 72 / 73 /
+// 71 us.  From 33 columns the automatic layouts stay (as fast or faster there).
+template <typename T, typename I>
+int launch_shift_wh_pf(const Launch& L) {
+  return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, true, false, true, false, true, 16, 16, true, kLR>>(L);
+}
+
+bool use_shift_wh_pf_form(const Launch& L, int elem_bytes) {
+  return L.sched.variant == 0 && elem_bytes == 4 && L.n > 16 && L.n <= 32 &&
+         use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched) && ((uintptr_t)L.b % 4) == 0 &&
+         ((uintptr_t)L.c % 4) == 0;
+}
+
 bool use_shift_pf_form(const Launch& L, int elem_bytes) {
   return L.sched.variant == 0 && elem_bytes == 4 && L.n > 16 && L.n % 4 != 0 &&
          use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched) &&
@@ -1726,6 +1742,8 @@ int launch_typed(const Launch& L) {
   }
   if constexpr (sizeof(T) == 4) {
     if (use_narrow_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L)) return launch_narrow<T, I>(L);
+    if (use_shift_wh_pf_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
+      return launch_shift_wh_pf<T, I>(L);
     if (use_shift_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
       return launch_shift<T, I>(L, (L.b_rows * L.ldb * (int64_t)sizeof(T)) > kNtBytes);
 #ifndef OFX_AB_NO_SHIFT_PF  // A/B builds only (scripts/ab_build.sh)

@@ -40,6 +40,14 @@ int launch_tuned(const Launch& L, int id) {
       case 66: return launch_cfg<T, I, Cfg<1, 16, 32, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L);
       case 67: return launch_cfg<T, I, Cfg<1, 16, 16, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L);
       case 68: return launch_cfg<T, I, Cfg<1, 32, 16, 4, false, P, false, W, false, true, 32, 16, false, kLR>>(L);
+      // 16-bit rows of 24-32 columns (round 4: bf16 N = 32 took 220 us on the arxiv-shaped graph,
+      // the 2-element lanes' wave items unrolled to 259 VGPRs): 8 / 16-B lanes with 16-lane
+      // one-element wave items
+      case 73: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
+      case 74: if (rows_of(8)) return launch_cfg<T, I, Cfg<8, 4, 8, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
+      case 75: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 8, 4, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
+      case 76: if (rows_of(8)) return launch_cfg<T, I, Cfg<8, 4, 4, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
+      case 77: if (rows_of(2)) return launch_cfg<T, I, Cfg<2, 16, 8, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
       default: break;
     }
   }

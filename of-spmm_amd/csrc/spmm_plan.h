@@ -77,6 +77,10 @@ constexpr int kPlanVals = 2 + kBins;  // hubs, chunks, bins...
 constexpr int64_t kOwnItems = 8;      // hubs with more chunks get their items written wave-wide
 constexpr int kLookWords = 16;        // per plan block: status, totals[4], inclusive prefix[4]
 constexpr unsigned long long kAgg = 1, kInc = 2;  // status = epoch << 2 | state
+// Polls of one status word before the look-back gives up (seconds; a wait in a correct launch is
+// microseconds): a planner bug then leaves the block's part of the list unwritten, which the
+// parity tests see, instead of hanging the GPU.
+constexpr int kSpinLimit = 1 << 22;
 
 template <typename I>
 __device__ __forceinline__ int plan_row(const I* __restrict__ rp, int64_t row_begin, int64_t nrows,
@@ -243,6 +247,7 @@ __global__ void __launch_bounds__(kBlock)
                      int64_t* __restrict__ items, int64_t* __restrict__ order,
                      unsigned* __restrict__ arrive) {
   __shared__ int64_t s_off[kPlanVals];
+  __shared__ int s_fail;
   int cls[RPT];
   int64_t nc[RPT], v[kPlanVals], tot[kPlanVals];
   const int64_t b = blockIdx.x;
@@ -266,12 +271,20 @@ __global__ void __launch_bounds__(kBlock)
       look_publish(look, b, epoch << 2 | (b == 0 ? kInc : kAgg));
     }
     int64_t pre[kPlanVals] = {};
+    bool failed = false;
     for (int64_t end = b; end > 0; end -= 64) {
       const int64_t p = end - 1 - lane;  // lane 0: the nearest predecessor
       unsigned long long st = epoch << 2 | kAgg;
-      if (p >= 0)
-        while (((st = look_status(look, p)) >> 2) != epoch) __builtin_amdgcn_s_sleep(1);
+      if (p >= 0) {
+        int spins = 0;  // bounded: a predecessor that never publishes cannot hang the launch
+        while (((st = look_status(look, p)) >> 2) != epoch && ++spins < kSpinLimit)
+          __builtin_amdgcn_s_sleep(1);
+      }
       asm volatile("" ::: "memory");  // the payload loads below issue after the status returned
+      if (__ballot(p >= 0 && (st >> 2) != epoch)) {
+        failed = true;  // no prefix: this block writes nothing and publishes no prefix
+        break;
+      }
       const unsigned long long incs = __ballot(p >= 0 && (st & 3) == kInc);
       const int stop = incs ? __ffsll((long long)incs) - 1 : 64;  // nearest inclusive lane
       int64_t x[kPlanVals];
@@ -289,7 +302,8 @@ __global__ void __launch_bounds__(kBlock)
       if (incs) break;
     }
     if (lane == 0) {
-      if (b > 0) {
+      s_fail = failed ? 1 : 0;
+      if (b > 0 && !failed) {
 #pragma unroll
         for (int i = 0; i < kPlanVals; ++i)
           coh_store(my + 1 + kPlanVals + i, (unsigned long long)(pre[i] + tot[i]));
@@ -298,7 +312,7 @@ __global__ void __launch_bounds__(kBlock)
 #pragma unroll
       for (int i = 0; i < kPlanVals; ++i) s_off[i] = pre[i];
     }
-    if (lane == 0 && b == nblocks - 1) {  // the last block knows the grand totals
+    if (lane == 0 && b == nblocks - 1 && !failed) {  // the last block knows the grand totals
       OFX_STP(counters + 0, (unsigned long long)(pre[1] + tot[1]));
       OFX_STP(counters + 1, (unsigned long long)(pre[0] + tot[0]));
       OFX_STP(counters + 2, 0ull);
@@ -306,6 +320,7 @@ __global__ void __launch_bounds__(kBlock)
     }
   }
   __syncthreads();
+  if (s_fail) return;  // uniform across the block
   int64_t off[kPlanVals];
 #pragma unroll
   for (int i = 0; i < kPlanVals; ++i) off[i] = s_off[i];

@@ -53,7 +53,7 @@ class SpmmCsrKernel:
 
     plan(row_ptr, row_begin, row_end) builds the work list once (ofx_spmm_csr_plan) for a static
     graph; launches with planned=True on that same row_ptr tensor and row range then skip the
-    three planning kernels.  The caller promises row_ptr's contents have not changed (a bound
+    planning kernel.  The caller promises row_ptr's contents have not changed (a bound
     CSR); the tensor identity and range are checked here."""
 
     def __init__(self, m: int, k: int, n: int, nnz: int, idx_dtype: torch.dtype,

@@ -46,7 +46,8 @@ def test_mid_form_bounds():
 def test_prefetch_form_bound(n):
     m = 120_000
     below, above = form(m, K_PREFETCH_NNZ, n), form(m, K_PREFETCH_NNZ + 1, n)
-    assert below["form"] == "prefetch" and below["PF"] == 1
+    # 17-32 fp32 columns: the shifted window with 16-lane wave items ("narrow", round 4)
+    assert below["form"] == ("narrow" if n <= 32 else "prefetch") and below["PF"] == 1
     assert above["form"] == "bandwidth" and above["PF"] == 0 and above["U"] == 8
     # wave items only at 16 < N <= 64
     assert below["WH"] == (1 if n <= 64 else 0)
@@ -61,7 +62,8 @@ def test_narrow_form_n16_fp32():
     # above kPrefetchNnz fp32 only (16-bit N = 16 below it: test_narrow_rows_of_mid_size_launches),
     # N = 16 only, 16-B aligned only
     assert form(m, K_PREFETCH_NNZ + 1, 16, BF16)["form"] != "narrow"
-    assert form(m, K_PREFETCH_NNZ, 32)["form"] == "prefetch"
+    assert form(m, K_PREFETCH_NNZ, 33)["form"] == "prefetch"
+    assert form(m, K_PREFETCH_NNZ + 1, 32)["form"] == "bandwidth"
     assert form(m, K_PREFETCH_NNZ, 16, b_addr=260)["form"] != "narrow"
 
 
@@ -146,9 +148,15 @@ def test_prefetch_form_layouts():
     """The prefetching form's lane layouts (round 4): odd fp32 widths above 16 take 16-B lanes
     with the shifted last window; 16-bit rows of <= 128 B take N / 16 elements per lane."""
     m, nnz = 169_343, 1_166_243
-    for n, lpr in ((17, 8), (41, 16), (47, 16), (99, 32)):
+    for n, lpr in ((41, 16), (47, 16), (99, 32)):
         d = form(m, nnz, n)
         assert d["form"] == "prefetch" and d["SH"] == 1 and d["VEC"] == 4 and d["LPR"] == lpr, d
+    # 17-32 columns: the shifted window with 16-lane wave items (round 4)
+    for n in (17, 24, 25, 32):
+        d = form(m, nnz, n)
+        assert (d["form"], d["SH"], d["VEC"], d["LPR"], d["U"], d["HL"], d["LR"]) == \
+            ("narrow", 1, 4, 8, 8, 16, 1), (n, d)
+    assert form(m, nnz, 33)["HL"] == 0
     assert form(m, nnz, 15)["SH"] == 0  # 16 columns or fewer: one element per lane
     assert form(m, nnz, 17, b_addr=258 + 2)["SH"] == 1
     for dt in (BF16, F16):
@@ -204,3 +212,4 @@ def test_odd_16bit_widths_of_mid_size_launches():
         assert form(m, nnz, 48, dt, b_addr=258)["LPR"] == 16    # an unaligned view: one-element lanes
         assert form(m, nnz, 65, dt)["LPR"] == 64                # past 64 columns: unchanged
         assert form(m, K_PREFETCH_NNZ + 1, 41, dt)["form"] == "bandwidth"
+
