@@ -1689,12 +1689,22 @@ bool use_narrow_form(const Launch& L, int elem_bytes) {
 // (profiles/r04k_variants.jsonl; arxiv-shaped / 60k x 1.5M / 169k x 2M): bf16 N = 16 86 / 77 / 94
 // -> 50 / 45 / 58 us and N = 8 99 / 82 / 105 -> 50 / 45 / 55 (U = 8, entry 51), fp32 N = 8 74 /
 // 66 / 74 -> 46 / 43 / 53 (U = 4, entry 63).  Same bits: only who adds changes.
+// 16-bit rows of 17-32 columns (even widths) the same way: 8-B lanes over 8 lanes (4-B over 16 for
+// views only 4-B aligned), U = 8, 16-lane wave items; their automatic layouts (2-element lanes)
+// unrolled the wave items to 259 VGPRs.  Entries 10073 / 10077 (profiles/r04u_16bit_mid.jsonl):
+// arxiv-shaped bf16 N = 20 / 24 / 28 / 32 148 / 148 / 148 / 221 -> 83 / 82 / 83 / 83 us, 60k x
+// 1.5M 87 / 87 / 88 / 159 -> 76 / 77 / 78 / 78 us, f16 N = 32 218 -> 82 us.
 template <typename T, typename I>
 int launch_narrow_pf(const Launch& L) {
-  if constexpr (sizeof(T) == 2)
-    return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
-  else
+  if constexpr (sizeof(T) == 2) {
+    if (L.n <= 16)
+      return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
+    if (pick_vec(2, L, 0, 4) == 4)
+      return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
+    return launch_cfg<T, I, Cfg<2, 16, 8, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
+  } else {
     return launch_cfg<T, I, Cfg<2, 4, 4, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
+  }
 }
 
 // Odd 16-bit widths of mid-size launches (round 4): no vector layout applies (an element is 2 B,
@@ -1717,7 +1727,9 @@ bool use_odd16_pf_form(const Launch& L, int elem_bytes) {
 
 bool use_narrow_pf_form(const Launch& L, int elem_bytes) {
   if (L.sched.variant != 0 || !use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched)) return false;
-  if (elem_bytes == 2) return (L.n == 8 || L.n == 16) && pick_vec(2, L, 0, 4) == 4;
+  if (elem_bytes == 2)
+    return ((L.n == 8 || L.n == 16) && pick_vec(2, L, 0, 4) == 4) ||
+           (L.n > 16 && L.n <= 32 && pick_vec(2, L, 0, 4) >= 2);
   if (elem_bytes == 4) return L.n == 8 && pick_vec(4, L, 0, 2) == 2;
   return false;
 }

@@ -48,6 +48,9 @@ int launch_tuned(const Launch& L, int id) {
       case 75: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 8, 4, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
       case 76: if (rows_of(8)) return launch_cfg<T, I, Cfg<8, 4, 4, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
       case 77: if (rows_of(2)) return launch_cfg<T, I, Cfg<2, 16, 8, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
+      // 16-bit rows of 33-64 columns: 16 / 8-B lanes with 16-lane wave items
+      case 78: if (rows_of(8)) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
+      case 79: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
       default: break;
     }
   }
@@ -69,6 +72,9 @@ int launch_tuned(const Launch& L, int id) {
       case 72: if (((uintptr_t)L.b % 4) == 0 && ((uintptr_t)L.c % 4) == 0 && L.n >= 4)
                  return launch_cfg<T, I, Cfg<4, 8, 4, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L);
                break;
+      // fp32 rows of 33-64 columns: 16-B lanes with 16-lane wave items
+      case 80: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
+      case 81: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 16, 4, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
       default: break;
     }
   }

@@ -160,7 +160,7 @@ def test_prefetch_form_layouts():
     assert form(m, nnz, 15)["SH"] == 0  # 16 columns or fewer: one element per lane
     assert form(m, nnz, 17, b_addr=258 + 2)["SH"] == 1
     for dt in (BF16, F16):
-        for n, vec in ((32, 2), (48, 2), (64, 4), (128, 8)):
+        for n, vec in ((48, 2), (64, 4), (128, 8)):  # 32: the narrow shape (below)
             d = form(m, nnz, n, dt)
             assert d["form"] == "prefetch" and d["VEC"] == vec, (dt, n, d)
 
@@ -176,6 +176,15 @@ def test_narrow_rows_of_mid_size_launches():
             assert (d["form"], d["VEC"], d["LPR"], d["U"], d["HL"], d["LR"]) == \
                 ("narrow", 4, 4, 8, 16, 1), (dt, n, d)
         assert form(m, nnz, 16, dt, b_addr=258)["form"] == "prefetch"  # 2-B aligned B
+        # 17-32 even columns: 8-B lanes over 8 lanes, or 4-B lanes over 16 for a 4-B aligned view
+        for n in (20, 24, 32):
+            d = form(m, nnz, n, dt)
+            assert (d["form"], d["VEC"], d["LPR"], d["U"], d["HL"]) == ("narrow", 4, 8, 8, 16), (n, d)
+        d = form(m, nnz, 32, dt, b_addr=260)
+        assert (d["form"], d["VEC"], d["LPR"], d["U"], d["HL"]) == ("narrow", 2, 16, 8, 16), d
+        d = form(m, nnz, 18, dt)
+        assert (d["form"], d["VEC"], d["LPR"]) == ("narrow", 2, 16), d
+        assert form(m, nnz, 34, dt)["HL"] == 0                           # past 32: unchanged
         assert form(m, K_PREFETCH_NNZ + 1, 16, dt)["form"] == "bandwidth"
         assert form(20_000, 400_000, 16, dt)["form"] == "mid"
     d = form(m, nnz, 8)

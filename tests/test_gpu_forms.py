@@ -3,7 +3,8 @@ medium).  Launches of more than 32,768 rows with nonzeros just below and just ab
 the prefetching form (U = 32 / 16 loads in flight, the next (col, val) batch prefetched, wave items
 at 16 < N <= 64) and the bandwidth form (U = 8) respectively (tests/test_form_rules.py asserts the
 rule itself on the CPU).  Each launch is bit-exact against the oracle and against the automatic
-pick: fp32 N = 1 / 8 / 25 / 64 / 128, bf16 and f16 N = 8 / 16 / 64, bf16 N = 41, f16 N = 63 (odd
+pick: fp32 N = 1 / 8 / 25 / 64 / 128, bf16 and f16 N = 8 / 16 / 64, bf16 N = 32, f16 N = 24,
+bf16 N = 41, f16 N = 63 (odd
 widths: one-element lanes in 16 / 32-lane groups), int32 and int64; a row range, a
 plan built once, the fused epilogue, and variants 30004 / 30005 (the prefetching form with and
 without wave items) forced."""
@@ -24,8 +25,8 @@ K_PREFETCH_NNZ = 3 << 20
 M = 100_000
 SIDES = {"below": K_PREFETCH_NNZ - 5_000, "above": K_PREFETCH_NNZ + 5_000}
 CASES = [("f32", 1), ("f32", 8), ("f32", 25), ("f32", 64), ("f32", 128), ("bf16", 8),
-         ("bf16", 16), ("bf16", 41), ("bf16", 64), ("f16", 8), ("f16", 16), ("f16", 63),
-         ("f16", 64)]
+         ("bf16", 16), ("bf16", 32), ("bf16", 41), ("bf16", 64), ("f16", 8), ("f16", 16),
+         ("f16", 24), ("f16", 63), ("f16", 64)]
 
 
 @functools.lru_cache(maxsize=4)
@@ -43,8 +44,8 @@ def test_prefetch_form_threshold(device, side, dtype, n, idx):
     v = v32.to(dt)
     nnz = ci.numel()
     d_form = ops.describe(M, M, n, nnz, dt, idx)
-    narrow_below = (dtype, n) in (("f32", 8), ("f32", 25), ("bf16", 8), ("bf16", 16), ("f16", 8),
-                                  ("f16", 16), ("bf16", 41), ("f16", 63))
+    narrow_below = (dtype, n) in (("f32", 8), ("f32", 25), ("bf16", 8), ("bf16", 16), ("bf16", 32),
+                                  ("f16", 8), ("f16", 16), ("f16", 24), ("bf16", 41), ("f16", 63))
     assert d_form["form"] == (("narrow" if narrow_below else "prefetch") if side == "below" else
                               ("narrow" if (dtype, n) == ("f32", 16) else "bandwidth")), d_form
     rng = np.random.default_rng(7000 + n)
