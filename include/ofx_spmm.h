@@ -135,7 +135,7 @@ int ofx_spmm_csr_gathered(void* stream, int idx_dtype, int val_dtype, int64_t m,
                           void* workspace, size_t workspace_bytes, const ofx_spmm_options* opts);
 
 /* Plans rows [row_begin, row_end) into `workspace` (the hub chunks and degree-binned work list
- * every ofx_spmm_csr launch otherwise builds first: three small kernels over row_ptr), so that
+ * every ofx_spmm_csr launch otherwise builds first: one small kernel over row_ptr), so that
  * launches with opts->planned != 0 on the same row_ptr, range, shapes and options skip it.
  * Asynchronous on `stream`; the same workspace size as ofx_spmm_csr.  A problem that needs no
  * plan (workspace size 0) is a no-op.  No reference counterpart (OneFlow re-plans per call); the
