@@ -1774,9 +1774,10 @@ int launch_typed(const Launch& L) {
   // (profiles/r03y_lanes_*.jsonl; fp32 keeps its layouts, DESIGN.md §3 tuning record)
   // The prefetching form too (mid-size graphs): arxiv-shaped bf16 N = 16 took 214 us with 8-element
   // lanes (two active lanes per 4-lane group) against 49 us for fp32 (profiles/r03ah_*.jsonl).
-  const bool narrow16 = !forced_vec && sizeof(T) == 2 && L.n <= 64 && L.sched.variant == 0 &&
-                        !use_small_form(L.nrows, L.nnz_est, L.n, L.sched) &&
-                        !use_mid_form(L.nrows, L.nnz_est, L.n, L.sched);
+  // The small and mid forms too (round 4, profiles/r04y_small16.jsonl, interleaved A/B): PubMed-
+  // shaped bf16 / f16 N = 8-32 33 -> 23 us, N = 64 36 -> 29; 20k rows x 400k N = 8-64 -4..-30%;
+  // Cora-shaped (host-bound) -1..-8%.
+  const bool narrow16 = !forced_vec && sizeof(T) == 2 && L.n <= 64 && L.sched.variant == 0;
   int cap16 = 1;  // the largest power of two <= N / 16
   while (cap16 * 32 <= L.n) cap16 *= 2;
   const int vec = (!forced_vec && sizeof(T) == 4 && L.n <= 16) ? 1

@@ -222,3 +222,15 @@ def test_odd_16bit_widths_of_mid_size_launches():
         assert form(m, nnz, 65, dt)["LPR"] == 64                # past 64 columns: unchanged
         assert form(m, K_PREFETCH_NNZ + 1, 41, dt)["form"] == "bandwidth"
 
+
+
+def test_narrow16_lanes_in_small_and_mid_forms():
+    """Round 4: 16-bit rows of <= 64 columns take N / 16 elements per lane in the small and mid
+    forms too (profiles/r04y_small16.jsonl: PubMed-shaped bf16 N = 8-32 33 -> 23 us)."""
+    for dt in (BF16, F16):
+        for n, vec in ((8, 1), (16, 1), (32, 2), (64, 4)):
+            small = form(19_717, 88_648, n, dt)
+            assert small["form"] == "small" and small["VEC"] == vec, (dt, n, small)
+            mid = form(20_000, 400_000, n, dt)
+            assert mid["form"] == "mid" and mid["VEC"] == vec, (dt, n, mid)
+        assert form(19_717, 88_648, 128, dt)["VEC"] == 8  # past 64 columns: the widest vector
