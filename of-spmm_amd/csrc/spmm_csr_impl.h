@@ -1671,8 +1671,10 @@ bool use_shift_form(const Launch& L, int elem_bytes) {
 // 396 -> 402 us).  profiles/r03n_graph.jsonl.  Same bits: only who adds changes.
 template <typename T, typename I>
 int launch_narrow(const Launch& L) {
+  // round 4: U = 8 with the in-kernel reduce (entry 10082, profiles/r04ac_n16_u.jsonl: 60k x
+  // 1.5M 42.8 -> 41.3 us, 2M nonzeros 50.9 -> 45.7, arxiv-shaped 45.4 -> 45.1)
   if (L.nnz_est <= kPrefetchNnz)
-    return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
+    return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
   return launch_cfg<T, I, Cfg<2, 8, 8, 4, false, true, false, true, false, true, 16, 8>>(L);
 }
 

@@ -75,6 +75,11 @@ int launch_tuned(const Launch& L, int id) {
       // fp32 rows of 33-64 columns: 16-B lanes with 16-lane wave items
       case 80: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
       case 81: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 16, 4, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
+      // fp32 N = 16 narrow form of mid-size launches with the in-kernel reduce (the automatic
+      // pick is U = 4, HU = 16): U = 8, HU = 8 / 32
+      case 82: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
+      case 83: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, P, false, W, false, true, 16, 8, false, kLR>>(L); break;
+      case 84: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, P, false, W, false, true, 16, 32, false, kLR>>(L); break;
       default: break;
     }
   }

@@ -57,7 +57,7 @@ def test_narrow_form_n16_fp32():
     m = 169_343
     below, above = form(m, K_PREFETCH_NNZ, 16), form(m, K_PREFETCH_NNZ + 1, 16)
     assert below["form"] == above["form"] == "narrow"
-    assert (below["VEC"], below["LPR"], below["U"], below["HL"], below["HU"]) == (4, 4, 4, 16, 16)
+    assert (below["VEC"], below["LPR"], below["U"], below["HL"], below["HU"]) == (4, 4, 8, 16, 16)
     assert (above["VEC"], above["LPR"], above["U"], above["HL"], above["HU"]) == (2, 8, 8, 16, 8)
     # above kPrefetchNnz fp32 only (16-bit N = 16 below it: test_narrow_rows_of_mid_size_launches),
     # N = 16 only, 16-B aligned only
