@@ -58,6 +58,12 @@ extern "C" {
 #define OFX_EUNSUPPORTED 4 /* dtype / layout combination not registered (OpKernelNotFound)     */
 #define OFX_ECOMM 5        /* RCCL error                                                       */
 #define OFX_EWORKSPACE 6   /* workspace smaller than ofx_spmm_csr_workspace_size()             */
+#define OFX_EPLAN 7        /* an EARLIER asynchronous launch wrote nothing: its device-side     *
+                            * work-list plan gave up, or it found no valid plan in its workspace *
+                            * (reported once, at the next launching call or sync; see            *
+                            * ofx_device_error_check)                                            */
+#define OFX_EINTERNAL 8    /* an unexpected C++ exception inside the library, caught at the     *
+                            * boundary (no exception ever crosses this C-ABI)                    */
 
 /* ---- OneFlow DataType codes (oneflow/core/common/data_type.proto:4-26) ------------------- */
 #define OFX_DT_FLOAT 2
@@ -69,8 +75,25 @@ extern "C" {
 
 /* Message describing the last failure on the calling thread ("" if none). */
 const char* ofx_last_error(void);
-/* Library version string, e.g. "ofx-spmm 0.1.0 gfx950". */
+/* Library version string, e.g. "ofx-spmm 0.2.0 gfx950". */
 const char* ofx_version(void);
+
+/* Device-side loud failures.  A kernel that cannot produce its output writes none of it and raises
+ * a device-error word (host-mapped memory); the library reports it as OFX_EPLAN, once, at the
+ * next launching entry (ofx_spmm_csr*, ofx_sddmm_csr), at ofx_stream_sync / ofx_event_sync /
+ * ofx_device_synchronize / ofx_graph_launch, or here (after the caller's own synchronisation,
+ * e.g. torch.cuda.synchronize()).  Mirrors the reference's fatal kernel CHECKs
+ * (oneflow/user/kernels/matrix_vector_product_kernel.cpp:98-105) as a status code.            */
+int ofx_device_error_check(void);
+
+/* Test hooks (no effect unless set).  OFX_DEBUG_PLAN_SPIN_LIMIT: polls of a predecessor's status
+ * word before the planner's look-back gives up (default 2^22; 0 = every block but the first gives
+ * up at once).  OFX_DEBUG_THROW_IN_COMPUTE: the op kernels' Compute throws (1 std::runtime_error,
+ * 2 std::bad_alloc, 3 a non-std exception; 0 off), to test the boundary's exception guard.
+ * value < 0 restores the default.                                                            */
+#define OFX_DEBUG_PLAN_SPIN_LIMIT 1
+#define OFX_DEBUG_THROW_IN_COMPUTE 2
+int ofx_debug_set(int knob, int64_t value);
 
 /* ---- SpMM schedule options --------------------------------------------------------------
  * Accumulation-order contract (identical in the CPU kernel, the HIP kernel and the oracle):
@@ -82,6 +105,12 @@ const char* ofx_version(void);
  * ofx_spmm_default_split(n); split_threshold == INT64_MAX (or `ordered` != 0) never splits,
  * which is exactly the reference composition's order.                                      */
 typedef struct ofx_spmm_options {
+  uint32_t struct_size;    /* sizeof(ofx_spmm_options) as the CALLER was compiled: the library *
+                            * reads only the fields inside it and takes the defaults for the   *
+                            * rest (a caller built against an older header keeps working); a   *
+                            * size below OFX_SPMM_OPTIONS_MIN_SIZE (e.g. 0: not set) is refused *
+                            * with OFX_EINVAL.  Initialise with OFX_SPMM_OPTIONS_INIT.          */
+  int32_t reserved0;       /* 0                                                              */
   int64_t split_threshold; /* 0 = default                                                    */
   int64_t chunk;           /* 0 = same as split_threshold                                    */
   int32_t ordered;         /* != 0: never split (reference order, slower on hub rows)       */
@@ -101,6 +130,9 @@ typedef struct ofx_spmm_options {
                             * nnz * rows / m.  Picks the kernel form only (launches of a few *
                             * rows of a degree-sorted graph); no numeric effect.             */
 } ofx_spmm_options;
+/* The first versioned layout ended at `reserved` (48 bytes); range_nnz came after it.         */
+#define OFX_SPMM_OPTIONS_MIN_SIZE 48u
+#define OFX_SPMM_OPTIONS_INIT {(uint32_t)sizeof(ofx_spmm_options), 0, 0, 0, 0, 0, 0, 0, 0, 0}
 
 /* The default split threshold for dense width n (a fixed function of n; part of the numeric
  * contract).  Written out in DESIGN.md §3 and restated by oracle/oracle.py.                */
@@ -393,14 +425,17 @@ int ofx_synth_dense_host(int val_dtype, int64_t r_begin, int64_t r_end, int64_t 
 /* A tensor as the functional layer sees it: dtype code, device (-1 = CPU, >=0 HIP ordinal),
  * rank-1/2 shape, row stride (elements) for rank-2, data pointer.                          */
 typedef struct ofx_tensor_desc {
+  uint32_t struct_size; /* sizeof(ofx_tensor_desc) as the caller was compiled (checked, as in   *
+                         * ofx_spmm_options; OFX_TENSOR_DESC_INIT)                              */
   int32_t dtype;
   int32_t device;
   int32_t ndim;
-  int32_t reserved;
   int64_t shape[2];
   int64_t stride[2];
   void* data;
 } ofx_tensor_desc;
+#define OFX_TENSOR_DESC_MIN_SIZE 56u
+#define OFX_TENSOR_DESC_INIT {(uint32_t)sizeof(ofx_tensor_desc), 0, 0, 0, {0, 0}, {0, 0}, 0}
 /* Shape/dtype inference of op "spmm_csr" (oneflow/user/ops/spmm_op.cpp mirror). Fills
  * out->dtype/ndim/shape; returns OFX_EINVAL with the op's error message on mismatch.      */
 int ofx_functional_spmm_csr_infer(const ofx_tensor_desc* row_ptr, const ofx_tensor_desc* col_idx,
@@ -499,13 +534,16 @@ int ofx_process_ctx_init(int64_t rank, int64_t world, ofx_kv_push_fn push, ofx_k
 #define OFX_DEV_CPU 1
 #define OFX_DEV_HIP 4
 typedef struct ofx_placement {
+  uint32_t struct_size; /* sizeof(ofx_placement) as the caller was compiled (checked, as in     *
+                         * ofx_spmm_options; OFX_PLACEMENT_INIT)                                */
   int32_t device_type;
-  int32_t reserved;
   int64_t parallel_num;
   int64_t parallel_id;
   const int64_t* machine_ids;
   const int64_t* device_ids;
 } ofx_placement;
+#define OFX_PLACEMENT_MIN_SIZE 40u
+#define OFX_PLACEMENT_INIT {(uint32_t)sizeof(ofx_placement), 0, 0, 0, 0, 0}
 /* Whether ccl::AllGather and a ccl::CommunicationContext are registered for a device type
  * (REGISTER_COLLECTIVE_COMMUNICATION, collective_communication/include/all_gather.h:24-38). */
 int ofx_ccl_registered(int device_type, int* all_gather, int* communication_context);

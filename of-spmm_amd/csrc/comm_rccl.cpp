@@ -93,23 +93,27 @@ int comm_wait(ncclComm_t c, ncclResult_t r, const char* what) {
 }  // namespace
 
 extern "C" int ofx_comm_get_unique_id(void* uid_out) {
-  OFX_REQUIRE(uid_out, OFX_EINVAL, "comm_get_unique_id: NULL");
-  ncclUniqueId id;
-  OFX_NCCL_CHECK(ncclGetUniqueId(&id));
-  std::memset(uid_out, 0, OFX_UNIQUE_ID_BYTES);
-  std::memcpy(uid_out, &id, sizeof(id));
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(uid_out, OFX_EINVAL, "comm_get_unique_id: NULL");
+    ncclUniqueId id;
+    OFX_NCCL_CHECK(ncclGetUniqueId(&id));
+    std::memset(uid_out, 0, OFX_UNIQUE_ID_BYTES);
+    std::memcpy(uid_out, &id, sizeof(id));
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_comm_init_rank(void** comm, int nranks, const void* uid, int rank) {
-  OFX_REQUIRE(comm && uid && nranks > 0 && rank >= 0 && rank < nranks, OFX_EINVAL,
-              "comm_init_rank: bad arguments (nranks=%d rank=%d)", nranks, rank);
-  ncclUniqueId id;
-  std::memcpy(&id, uid, sizeof(id));
-  ncclComm_t c;
-  OFX_NCCL_CHECK(ncclCommInitRank(&c, nranks, id, rank));
-  *comm = c;
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(comm && uid && nranks > 0 && rank >= 0 && rank < nranks, OFX_EINVAL,
+                "comm_init_rank: bad arguments (nranks=%d rank=%d)", nranks, rank);
+    ncclUniqueId id;
+    std::memcpy(&id, uid, sizeof(id));
+    ncclComm_t c;
+    OFX_NCCL_CHECK(ncclCommInitRank(&c, nranks, id, rank));
+    *comm = c;
+    return OFX_OK;
+  });
 }
 
 // ofx_comm_init_rank with a deadline: a non-blocking communicator
@@ -121,77 +125,87 @@ extern "C" int ofx_comm_init_rank(void** comm, int nranks, const void* uid, int 
 // (oneflow/core/job/eager_nccl_comm_manager.cpp:57-80) blocks without a bound.
 extern "C" int ofx_comm_init_rank_deadline(void** comm, int nranks, const void* uid, int rank,
                                            double timeout_s) {
-  OFX_REQUIRE(comm && uid && nranks > 0 && rank >= 0 && rank < nranks && timeout_s > 0, OFX_EINVAL,
-              "comm_init_rank_deadline: bad arguments (nranks=%d rank=%d timeout=%g)", nranks, rank,
-              timeout_s);
-  g_call_timeout_s = timeout_s;
-  ncclUniqueId id;
-  std::memcpy(&id, uid, sizeof(id));
-  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-  cfg.blocking = 0;
-  ncclComm_t c = nullptr;
-  const ncclResult_t r = ncclCommInitRankConfig(&c, nranks, id, rank, &cfg);
-  if (r != ncclSuccess && r != ncclInProgress) {
-    if (c != nullptr) ncclCommAbort(c);
-    return ofx::fail(OFX_ECOMM, "comm_init_rank_deadline: ncclCommInitRankConfig failed: %s",
-                     ncclGetErrorString(r));
-  }
-  const auto t0 = std::chrono::steady_clock::now();
-  ncclResult_t st = r;
-  while (st == ncclInProgress) {
-    const ncclResult_t q = ncclCommGetAsyncError(c, &st);
-    if (q != ncclSuccess) st = q;
-    if (st != ncclInProgress) break;
-    if (seconds_since(t0) > timeout_s) {
-      ncclCommAbort(c);
-      return ofx::fail(OFX_ECOMM,
-                       "comm_init_rank_deadline: rank %d of %d: communicator not set up after %.0f s "
-                       "(a peer did not join); aborted", rank, nranks, timeout_s);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(comm && uid && nranks > 0 && rank >= 0 && rank < nranks && timeout_s > 0, OFX_EINVAL,
+                "comm_init_rank_deadline: bad arguments (nranks=%d rank=%d timeout=%g)", nranks, rank,
+                timeout_s);
+    g_call_timeout_s = timeout_s;
+    ncclUniqueId id;
+    std::memcpy(&id, uid, sizeof(id));
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclComm_t c = nullptr;
+    const ncclResult_t r = ncclCommInitRankConfig(&c, nranks, id, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) {
+      if (c != nullptr) ncclCommAbort(c);
+      return ofx::fail(OFX_ECOMM, "comm_init_rank_deadline: ncclCommInitRankConfig failed: %s",
+                       ncclGetErrorString(r));
     }
-    std::this_thread::sleep_for(std::chrono::milliseconds(1));
-  }
-  if (st != ncclSuccess) {
-    ncclCommAbort(c);
-    return ofx::fail(OFX_ECOMM, "comm_init_rank_deadline: rank %d of %d: %s", rank, nranks,
-                     ncclGetErrorString(st));
-  }
-  *comm = c;
-  return OFX_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    ncclResult_t st = r;
+    while (st == ncclInProgress) {
+      const ncclResult_t q = ncclCommGetAsyncError(c, &st);
+      if (q != ncclSuccess) st = q;
+      if (st != ncclInProgress) break;
+      if (seconds_since(t0) > timeout_s) {
+        ncclCommAbort(c);
+        return ofx::fail(OFX_ECOMM,
+                         "comm_init_rank_deadline: rank %d of %d: communicator not set up after %.0f s "
+                         "(a peer did not join); aborted", rank, nranks, timeout_s);
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    if (st != ncclSuccess) {
+      ncclCommAbort(c);
+      return ofx::fail(OFX_ECOMM, "comm_init_rank_deadline: rank %d of %d: %s", rank, nranks,
+                       ncclGetErrorString(st));
+    }
+    *comm = c;
+    return OFX_OK;
+  });
 }
 
 // Aborts a communicator (ncclCommAbort): its pending operations are dropped and peers blocked on
 // it fail.  Called by a rank's phase watchdog before it exits (bench.py).
 extern "C" int ofx_comm_abort(void* comm) {
-  if (comm) OFX_NCCL_CHECK(ncclCommAbort(static_cast<ncclComm_t>(comm)));
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    if (comm) OFX_NCCL_CHECK(ncclCommAbort(static_cast<ncclComm_t>(comm)));
+    return OFX_OK;
+  });
 }
 
 // Finalize (flushes the communicator's operations; a non-blocking communicator may report
 // ncclInProgress, waited for with the call deadline), then destroy.
 extern "C" int ofx_comm_destroy(void* comm) {
-  if (comm == nullptr) return OFX_OK;
-  ncclComm_t c = static_cast<ncclComm_t>(comm);
-  OFX_NCCL_CALL(c, ncclCommFinalize(c));
-  OFX_NCCL_CHECK(ncclCommDestroy(c));
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    if (comm == nullptr) return OFX_OK;
+    ncclComm_t c = static_cast<ncclComm_t>(comm);
+    OFX_NCCL_CALL(c, ncclCommFinalize(c));
+    OFX_NCCL_CHECK(ncclCommDestroy(c));
+    return OFX_OK;
+  });
 }
 
 // Ranks and this rank's index in a communicator (what bench.py reports as the RCCL comm size).
 extern "C" int ofx_comm_count(void* comm, int* nranks, int* rank) {
-  OFX_REQUIRE(comm && nranks && rank, OFX_EINVAL, "comm_count: NULL argument");
-  OFX_NCCL_CHECK(ncclCommCount(static_cast<ncclComm_t>(comm), nranks));
-  OFX_NCCL_CHECK(ncclCommUserRank(static_cast<ncclComm_t>(comm), rank));
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(comm && nranks && rank, OFX_EINVAL, "comm_count: NULL argument");
+    OFX_NCCL_CHECK(ncclCommCount(static_cast<ncclComm_t>(comm), nranks));
+    OFX_NCCL_CHECK(ncclCommUserRank(static_cast<ncclComm_t>(comm), rank));
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_allgather(void* stream, const void* in, void* out, size_t count, int dtype,
                              void* comm) {
-  ncclDataType_t t;
-  OFX_REQUIRE(nccl_dtype(dtype, &t), OFX_EUNSUPPORTED, "allgather: unsupported dtype %d", dtype);
-  OFX_REQUIRE(comm && (count == 0 || (in && out)), OFX_EINVAL, "allgather: NULL argument");
-  ncclComm_t c = static_cast<ncclComm_t>(comm);
-  OFX_NCCL_CALL(c, ncclAllGather(in, out, count, t, c, static_cast<hipStream_t>(stream)));
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    ncclDataType_t t;
+    OFX_REQUIRE(nccl_dtype(dtype, &t), OFX_EUNSUPPORTED, "allgather: unsupported dtype %d", dtype);
+    OFX_REQUIRE(comm && (count == 0 || (in && out)), OFX_EINVAL, "allgather: NULL argument");
+    ncclComm_t c = static_cast<ncclComm_t>(comm);
+    OFX_NCCL_CALL(c, ncclAllGather(in, out, count, t, c, static_cast<hipStream_t>(stream)));
+    return OFX_OK;
+  });
 }
 
 // All-gather as grouped point-to-point transfers: every rank sends its slot to every peer and
@@ -199,24 +213,26 @@ extern "C" int ofx_allgather(void* stream, const void* in, void* out, size_t cou
 // instead of RCCL's ring/tree schedule.  `buf` holds nranks slots of `count` elements; this
 // rank's slot (rank * count) is the send buffer (in place).  Same bytes as ofx_allgather.
 extern "C" int ofx_allgather_p2p(void* stream, void* buf, size_t count, int dtype, void* comm) {
-  ncclDataType_t t;
-  OFX_REQUIRE(nccl_dtype(dtype, &t), OFX_EUNSUPPORTED, "allgather_p2p: unsupported dtype %d", dtype);
-  OFX_REQUIRE(comm && (count == 0 || buf), OFX_EINVAL, "allgather_p2p: NULL argument");
-  ncclComm_t c = static_cast<ncclComm_t>(comm);
-  int nranks = 0, rank = 0;
-  OFX_NCCL_CHECK(ncclCommCount(c, &nranks));
-  OFX_NCCL_CHECK(ncclCommUserRank(c, &rank));
-  const size_t esz = (size_t)ofx::dtype_size(dtype);
-  char* base = static_cast<char*>(buf);
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  OFX_NCCL_CHECK(ncclGroupStart());
-  for (int d = 1; d < nranks; ++d) {  // peers in a rotated order so links are loaded evenly
-    const int to = (rank + d) % nranks, from = (rank - d + nranks) % nranks;
-    OFX_NCCL_GROUPED(ncclSend(base + (size_t)rank * count * esz, count, t, to, c, s));
-    OFX_NCCL_GROUPED(ncclRecv(base + (size_t)from * count * esz, count, t, from, c, s));
-  }
-  OFX_NCCL_CALL(c, ncclGroupEnd());
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    ncclDataType_t t;
+    OFX_REQUIRE(nccl_dtype(dtype, &t), OFX_EUNSUPPORTED, "allgather_p2p: unsupported dtype %d", dtype);
+    OFX_REQUIRE(comm && (count == 0 || buf), OFX_EINVAL, "allgather_p2p: NULL argument");
+    ncclComm_t c = static_cast<ncclComm_t>(comm);
+    int nranks = 0, rank = 0;
+    OFX_NCCL_CHECK(ncclCommCount(c, &nranks));
+    OFX_NCCL_CHECK(ncclCommUserRank(c, &rank));
+    const size_t esz = (size_t)ofx::dtype_size(dtype);
+    char* base = static_cast<char*>(buf);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    OFX_NCCL_CHECK(ncclGroupStart());
+    for (int d = 1; d < nranks; ++d) {  // peers in a rotated order so links are loaded evenly
+      const int to = (rank + d) % nranks, from = (rank - d + nranks) % nranks;
+      OFX_NCCL_GROUPED(ncclSend(base + (size_t)rank * count * esz, count, t, to, c, s));
+      OFX_NCCL_GROUPED(ncclRecv(base + (size_t)from * count * esz, count, t, from, c, s));
+    }
+    OFX_NCCL_CALL(c, ncclGroupEnd());
+    return OFX_OK;
+  });
 }
 
 // Halo exchange of B rows: grouped point-to-point send/recv with
@@ -228,30 +244,32 @@ extern "C" int ofx_exchange_rows(void* stream, void* comm, int dtype, int64_t n,
                                  const void* send_buf, const int64_t* send_counts,
                                  const int64_t* send_offsets, void* recv_buf,
                                  const int64_t* recv_counts, const int64_t* recv_offsets) {
-  ncclDataType_t t;
-  OFX_REQUIRE(nccl_dtype(dtype, &t), OFX_EUNSUPPORTED, "exchange_rows: unsupported dtype %d", dtype);
-  OFX_REQUIRE(comm && send_counts && send_offsets && recv_counts && recv_offsets && n >= 0,
-              OFX_EINVAL, "exchange_rows: NULL argument");
-  ncclComm_t c = static_cast<ncclComm_t>(comm);
-  int nranks = 0, rank = 0;
-  OFX_NCCL_CHECK(ncclCommCount(c, &nranks));
-  OFX_NCCL_CHECK(ncclCommUserRank(c, &rank));
-  const size_t row_bytes = (size_t)n * (size_t)ofx::dtype_size(dtype);
-  const char* sb = static_cast<const char*>(send_buf);
-  char* rb = static_cast<char*>(recv_buf);
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  OFX_NCCL_CHECK(ncclGroupStart());
-  for (int d = 1; d < nranks; ++d) {
-    const int to = (rank + d) % nranks, from = (rank - d + nranks) % nranks;
-    if (send_counts[to] > 0)
-      OFX_NCCL_GROUPED(ncclSend(sb + (size_t)send_offsets[to] * row_bytes,
-                                (size_t)(send_counts[to] * n), t, to, c, s));
-    if (recv_counts[from] > 0)
-      OFX_NCCL_GROUPED(ncclRecv(rb + (size_t)recv_offsets[from] * row_bytes,
-                                (size_t)(recv_counts[from] * n), t, from, c, s));
-  }
-  OFX_NCCL_CALL(c, ncclGroupEnd());
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    ncclDataType_t t;
+    OFX_REQUIRE(nccl_dtype(dtype, &t), OFX_EUNSUPPORTED, "exchange_rows: unsupported dtype %d", dtype);
+    OFX_REQUIRE(comm && send_counts && send_offsets && recv_counts && recv_offsets && n >= 0,
+                OFX_EINVAL, "exchange_rows: NULL argument");
+    ncclComm_t c = static_cast<ncclComm_t>(comm);
+    int nranks = 0, rank = 0;
+    OFX_NCCL_CHECK(ncclCommCount(c, &nranks));
+    OFX_NCCL_CHECK(ncclCommUserRank(c, &rank));
+    const size_t row_bytes = (size_t)n * (size_t)ofx::dtype_size(dtype);
+    const char* sb = static_cast<const char*>(send_buf);
+    char* rb = static_cast<char*>(recv_buf);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    OFX_NCCL_CHECK(ncclGroupStart());
+    for (int d = 1; d < nranks; ++d) {
+      const int to = (rank + d) % nranks, from = (rank - d + nranks) % nranks;
+      if (send_counts[to] > 0)
+        OFX_NCCL_GROUPED(ncclSend(sb + (size_t)send_offsets[to] * row_bytes,
+                                  (size_t)(send_counts[to] * n), t, to, c, s));
+      if (recv_counts[from] > 0)
+        OFX_NCCL_GROUPED(ncclRecv(rb + (size_t)recv_offsets[from] * row_bytes,
+                                  (size_t)(recv_counts[from] * n), t, from, c, s));
+    }
+    OFX_NCCL_CALL(c, ncclGroupEnd());
+    return OFX_OK;
+  });
 }
 
 // One step of the row-split operator on this rank (SURVEY.md §8b "ofx_spmm_rowsplit"): the
@@ -264,22 +282,24 @@ extern "C" int ofx_spmm_rowsplit(void* stream, void* comm, int idx_dtype, int va
                                  const void* row_ptr, const void* col_idx, const void* values,
                                  void* b_gathered, void* c, int64_t ldc, void* workspace,
                                  size_t workspace_bytes, const ofx_spmm_options* opts) {
-  OFX_REQUIRE(comm && k_padded >= 0 && n >= 0, OFX_EINVAL, "spmm_rowsplit: bad arguments");
-  int nranks = 0, rank = 0;
-  ncclComm_t cm = static_cast<ncclComm_t>(comm);
-  OFX_NCCL_CHECK(ncclCommCount(cm, &nranks));
-  OFX_NCCL_CHECK(ncclCommUserRank(cm, &rank));
-  OFX_REQUIRE(k_padded % nranks == 0, OFX_EINVAL,
-              "spmm_rowsplit: k_padded=%lld is not a multiple of %d ranks", (long long)k_padded,
-              nranks);
-  const int64_t pad = k_padded / nranks;
-  const size_t esz = (size_t)ofx::dtype_size(val_dtype);
-  if (pad * n > 0) {
-    char* slot = static_cast<char*>(b_gathered) + (size_t)(rank * pad * n) * esz;
-    const int rc = ofx_allgather(stream, slot, b_gathered, (size_t)(pad * n), val_dtype, comm);
-    if (rc) return rc;
-  }
-  return ofx_spmm_csr(stream, idx_dtype, val_dtype, m_local, k_padded, n, nnz_local, row_ptr,
-                      col_idx, values, b_gathered, n, c, ldc, 0, m_local, workspace,
-                      workspace_bytes, opts);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(comm && k_padded >= 0 && n >= 0, OFX_EINVAL, "spmm_rowsplit: bad arguments");
+    int nranks = 0, rank = 0;
+    ncclComm_t cm = static_cast<ncclComm_t>(comm);
+    OFX_NCCL_CHECK(ncclCommCount(cm, &nranks));
+    OFX_NCCL_CHECK(ncclCommUserRank(cm, &rank));
+    OFX_REQUIRE(k_padded % nranks == 0, OFX_EINVAL,
+                "spmm_rowsplit: k_padded=%lld is not a multiple of %d ranks", (long long)k_padded,
+                nranks);
+    const int64_t pad = k_padded / nranks;
+    const size_t esz = (size_t)ofx::dtype_size(val_dtype);
+    if (pad * n > 0) {
+      char* slot = static_cast<char*>(b_gathered) + (size_t)(rank * pad * n) * esz;
+      const int rc = ofx_allgather(stream, slot, b_gathered, (size_t)(pad * n), val_dtype, comm);
+      if (rc) return rc;
+    }
+    return ofx_spmm_csr(stream, idx_dtype, val_dtype, m_local, k_padded, n, nnz_local, row_ptr,
+                        col_idx, values, b_gathered, n, c, ldc, 0, m_local, workspace,
+                        workspace_bytes, opts);
+  });
 }

@@ -212,14 +212,16 @@ using namespace ofx;
 
 extern "C" int ofx_coo_to_csr_workspace_size(int idx_dtype, int64_t m, int64_t k, int64_t nnz,
                                              size_t* bytes) {
-  OFX_REQUIRE(bytes && m >= 0 && k >= 0 && nnz >= 0 && nnz <= INT32_MAX, OFX_EINVAL,
-              "coo_to_csr: bad sizes (nnz must be < 2^31)");
-  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "coo_to_csr: bad index dtype %d",
-              idx_dtype);
-  BuildWs w;
-  const int rc = build_ws(m, k, nnz, &w);
-  *bytes = w.total;
-  return rc;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(bytes && m >= 0 && k >= 0 && nnz >= 0 && nnz <= INT32_MAX, OFX_EINVAL,
+                "coo_to_csr: bad sizes (nnz must be < 2^31)");
+    OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "coo_to_csr: bad index dtype %d",
+                idx_dtype);
+    BuildWs w;
+    const int rc = build_ws(m, k, nnz, &w);
+    *bytes = w.total;
+    return rc;
+  });
 }
 
 extern "C" int ofx_coo_to_csr(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k,
@@ -227,23 +229,25 @@ extern "C" int ofx_coo_to_csr(void* stream, int idx_dtype, int val_dtype, int64_
                               int merge_duplicates, void* out_row_ptr, void* out_col_idx,
                               void* out_values, void* out_nnz, void* bad_flag, void* workspace,
                               size_t workspace_bytes) {
-  OFX_REQUIRE(m >= 0 && k >= 0 && nnz >= 0 && nnz <= INT32_MAX, OFX_EINVAL,
-              "coo_to_csr: bad sizes (nnz must be < 2^31)");
-  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "coo_to_csr: bad index dtype %d",
-              idx_dtype);
-  OFX_REQUIRE(out_row_ptr && out_nnz && (nnz == 0 || (row && col && out_col_idx)), OFX_EINVAL,
-              "coo_to_csr: NULL pointer");
-  OFX_REQUIRE((values == nullptr) == (out_values == nullptr), OFX_EINVAL,
-              "coo_to_csr: values and out_values must both be given or both be NULL");
-  const int vdt = values ? val_dtype : OFX_DT_FLOAT;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  if (idx_dtype == OFX_DT_INT32)
-    return build_typed<int32_t>(vdt, s, m, k, nnz, (const int32_t*)row, (const int32_t*)col, values,
-                                merge_duplicates, (int32_t*)out_row_ptr, (int32_t*)out_col_idx,
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(m >= 0 && k >= 0 && nnz >= 0 && nnz <= INT32_MAX, OFX_EINVAL,
+                "coo_to_csr: bad sizes (nnz must be < 2^31)");
+    OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "coo_to_csr: bad index dtype %d",
+                idx_dtype);
+    OFX_REQUIRE(out_row_ptr && out_nnz && (nnz == 0 || (row && col && out_col_idx)), OFX_EINVAL,
+                "coo_to_csr: NULL pointer");
+    OFX_REQUIRE((values == nullptr) == (out_values == nullptr), OFX_EINVAL,
+                "coo_to_csr: values and out_values must both be given or both be NULL");
+    const int vdt = values ? val_dtype : OFX_DT_FLOAT;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (idx_dtype == OFX_DT_INT32)
+      return build_typed<int32_t>(vdt, s, m, k, nnz, (const int32_t*)row, (const int32_t*)col, values,
+                                  merge_duplicates, (int32_t*)out_row_ptr, (int32_t*)out_col_idx,
+                                  out_values, (int64_t*)out_nnz, (unsigned int*)bad_flag,
+                                  (char*)workspace, workspace_bytes);
+    return build_typed<int64_t>(vdt, s, m, k, nnz, (const int64_t*)row, (const int64_t*)col, values,
+                                merge_duplicates, (int64_t*)out_row_ptr, (int64_t*)out_col_idx,
                                 out_values, (int64_t*)out_nnz, (unsigned int*)bad_flag,
                                 (char*)workspace, workspace_bytes);
-  return build_typed<int64_t>(vdt, s, m, k, nnz, (const int64_t*)row, (const int64_t*)col, values,
-                              merge_duplicates, (int64_t*)out_row_ptr, (int64_t*)out_col_idx,
-                              out_values, (int64_t*)out_nnz, (unsigned int*)bad_flag,
-                              (char*)workspace, workspace_bytes);
+  });
 }

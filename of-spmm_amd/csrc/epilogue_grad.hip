@@ -124,34 +124,38 @@ using namespace ofx;
 
 extern "C" int ofx_relu_bias_grad_workspace_size(int val_dtype, int64_t m, int64_t n,
                                                  size_t* bytes) {
-  OFX_REQUIRE(bytes != nullptr, OFX_EINVAL, "relu_bias_grad_workspace_size: bytes is NULL");
-  OFX_REQUIRE(is_value_dtype(val_dtype), OFX_EUNSUPPORTED, "relu_bias_grad: bad dtype %d",
-              val_dtype);
-  OFX_REQUIRE(m >= 0 && n >= 0, OFX_EINVAL, "relu_bias_grad: negative size");
-  *bytes = (size_t)nchunks_of(m) * (size_t)n * (val_dtype == OFX_DT_DOUBLE ? 8 : 4);
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(bytes != nullptr, OFX_EINVAL, "relu_bias_grad_workspace_size: bytes is NULL");
+    OFX_REQUIRE(is_value_dtype(val_dtype), OFX_EUNSUPPORTED, "relu_bias_grad: bad dtype %d",
+                val_dtype);
+    OFX_REQUIRE(m >= 0 && n >= 0, OFX_EINVAL, "relu_bias_grad: negative size");
+    *bytes = (size_t)nchunks_of(m) * (size_t)n * (val_dtype == OFX_DT_DOUBLE ? 8 : 4);
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_relu_bias_grad(void* stream, int val_dtype, int64_t m, int64_t n, const void* y,
                                   int64_t ldy, const void* dy, int64_t lddy, void* dx,
                                   int64_t lddx, void* d_bias, int relu, void* workspace,
                                   size_t workspace_bytes) {
-  OFX_REQUIRE(is_value_dtype(val_dtype), OFX_EUNSUPPORTED, "relu_bias_grad: bad dtype %d",
-              val_dtype);
-  OFX_REQUIRE(m >= 0 && n >= 0, OFX_EINVAL, "relu_bias_grad: negative size");
-  if (n == 0) return OFX_OK;
-  OFX_REQUIRE(m == 0 || (dy && (!relu || y) && lddy >= n && (!relu || ldy >= n)), OFX_EINVAL,
-              "relu_bias_grad: NULL input or leading dimension < n");
-  OFX_REQUIRE(dx == nullptr || lddx >= n, OFX_EINVAL, "relu_bias_grad: lddx < n");
-  size_t need = 0;
-  ofx_relu_bias_grad_workspace_size(val_dtype, m, n, &need);
-  OFX_REQUIRE(d_bias == nullptr || (workspace && workspace_bytes >= need) || need == 0,
-              OFX_EWORKSPACE, "relu_bias_grad: workspace of %zu bytes < %zu", workspace_bytes, need);
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  switch (val_dtype) {
-    case OFX_DT_FLOAT: return launch<float>(s, m, n, y, ldy, dy, lddy, dx, lddx, d_bias, relu, workspace);
-    case OFX_DT_DOUBLE: return launch<double>(s, m, n, y, ldy, dy, lddy, dx, lddx, d_bias, relu, workspace);
-    case OFX_DT_BFLOAT16: return launch<bf16>(s, m, n, y, ldy, dy, lddy, dx, lddx, d_bias, relu, workspace);
-    default: return launch<f16>(s, m, n, y, ldy, dy, lddy, dx, lddx, d_bias, relu, workspace);
-  }
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(is_value_dtype(val_dtype), OFX_EUNSUPPORTED, "relu_bias_grad: bad dtype %d",
+                val_dtype);
+    OFX_REQUIRE(m >= 0 && n >= 0, OFX_EINVAL, "relu_bias_grad: negative size");
+    if (n == 0) return OFX_OK;
+    OFX_REQUIRE(m == 0 || (dy && (!relu || y) && lddy >= n && (!relu || ldy >= n)), OFX_EINVAL,
+                "relu_bias_grad: NULL input or leading dimension < n");
+    OFX_REQUIRE(dx == nullptr || lddx >= n, OFX_EINVAL, "relu_bias_grad: lddx < n");
+    size_t need = 0;
+    ofx_relu_bias_grad_workspace_size(val_dtype, m, n, &need);
+    OFX_REQUIRE(d_bias == nullptr || (workspace && workspace_bytes >= need) || need == 0,
+                OFX_EWORKSPACE, "relu_bias_grad: workspace of %zu bytes < %zu", workspace_bytes, need);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (val_dtype) {
+      case OFX_DT_FLOAT: return launch<float>(s, m, n, y, ldy, dy, lddy, dx, lddx, d_bias, relu, workspace);
+      case OFX_DT_DOUBLE: return launch<double>(s, m, n, y, ldy, dy, lddy, dx, lddx, d_bias, relu, workspace);
+      case OFX_DT_BFLOAT16: return launch<bf16>(s, m, n, y, ldy, dy, lddy, dx, lddx, d_bias, relu, workspace);
+      default: return launch<f16>(s, m, n, y, ldy, dy, lddy, dx, lddx, d_bias, relu, workspace);
+    }
+  });
 }

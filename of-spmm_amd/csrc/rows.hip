@@ -77,19 +77,21 @@ using namespace ofx;
 extern "C" int ofx_gather_rows(void* stream, int idx_dtype, int64_t count, int64_t row_bytes,
                                const void* idx, const void* src, int64_t src_stride_bytes,
                                void* dst, int64_t dst_stride_bytes) {
-  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "gather_rows: bad index dtype %d",
-              idx_dtype);
-  OFX_REQUIRE(count >= 0 && row_bytes >= 0 && src_stride_bytes >= row_bytes &&
-                  dst_stride_bytes >= row_bytes,
-              OFX_EINVAL, "gather_rows: bad sizes");
-  if (count == 0 || row_bytes == 0) return OFX_OK;
-  OFX_REQUIRE(src && dst, OFX_EINVAL, "gather_rows: NULL pointer");
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  if (idx_dtype == OFX_DT_INT32)
-    return dispatch(s, static_cast<const int32_t*>(idx), count, row_bytes, src, src_stride_bytes,
-                    dst, dst_stride_bytes);
-  return dispatch(s, static_cast<const int64_t*>(idx), count, row_bytes, src, src_stride_bytes, dst,
-                  dst_stride_bytes);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "gather_rows: bad index dtype %d",
+                idx_dtype);
+    OFX_REQUIRE(count >= 0 && row_bytes >= 0 && src_stride_bytes >= row_bytes &&
+                    dst_stride_bytes >= row_bytes,
+                OFX_EINVAL, "gather_rows: bad sizes");
+    if (count == 0 || row_bytes == 0) return OFX_OK;
+    OFX_REQUIRE(src && dst, OFX_EINVAL, "gather_rows: NULL pointer");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (idx_dtype == OFX_DT_INT32)
+      return dispatch(s, static_cast<const int32_t*>(idx), count, row_bytes, src, src_stride_bytes,
+                      dst, dst_stride_bytes);
+    return dispatch(s, static_cast<const int64_t*>(idx), count, row_bytes, src, src_stride_bytes, dst,
+                    dst_stride_bytes);
+  });
 }
 
 // ---- 3-level strided block copy (grid exchange pack / unpack) ---------------
@@ -150,24 +152,26 @@ extern "C" int ofx_copy_blocks(void* stream, int64_t nouter, int64_t ninner, int
                                int64_t row_bytes, const void* src, int64_t src_outer,
                                int64_t src_inner, int64_t src_row, void* dst, int64_t dst_outer,
                                int64_t dst_inner, int64_t dst_row) {
-  OFX_REQUIRE(nouter >= 0 && ninner >= 0 && rows >= 0 && row_bytes >= 0, OFX_EINVAL,
-              "copy_blocks: negative size");
-  if (nouter == 0 || ninner == 0 || rows == 0 || row_bytes == 0) return OFX_OK;
-  OFX_REQUIRE(src && dst, OFX_EINVAL, "copy_blocks: NULL pointer");
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  auto aligned = [&](int64_t a) {
-    return row_bytes % a == 0 && src_outer % a == 0 && src_inner % a == 0 && src_row % a == 0 &&
-           dst_outer % a == 0 && dst_inner % a == 0 && dst_row % a == 0 &&
-           (uintptr_t)src % a == 0 && (uintptr_t)dst % a == 0;
-  };
-  if (aligned(16))
-    return launch_blocks<uint4>(s, nouter, ninner, rows, row_bytes, src, src_outer, src_inner,
-                                src_row, dst, dst_outer, dst_inner, dst_row);
-  if (aligned(4))
-    return launch_blocks<uint32_t>(s, nouter, ninner, rows, row_bytes, src, src_outer, src_inner,
-                                   src_row, dst, dst_outer, dst_inner, dst_row);
-  return launch_blocks<unsigned char>(s, nouter, ninner, rows, row_bytes, src, src_outer,
-                                      src_inner, src_row, dst, dst_outer, dst_inner, dst_row);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(nouter >= 0 && ninner >= 0 && rows >= 0 && row_bytes >= 0, OFX_EINVAL,
+                "copy_blocks: negative size");
+    if (nouter == 0 || ninner == 0 || rows == 0 || row_bytes == 0) return OFX_OK;
+    OFX_REQUIRE(src && dst, OFX_EINVAL, "copy_blocks: NULL pointer");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    auto aligned = [&](int64_t a) {
+      return row_bytes % a == 0 && src_outer % a == 0 && src_inner % a == 0 && src_row % a == 0 &&
+             dst_outer % a == 0 && dst_inner % a == 0 && dst_row % a == 0 &&
+             (uintptr_t)src % a == 0 && (uintptr_t)dst % a == 0;
+    };
+    if (aligned(16))
+      return launch_blocks<uint4>(s, nouter, ninner, rows, row_bytes, src, src_outer, src_inner,
+                                  src_row, dst, dst_outer, dst_inner, dst_row);
+    if (aligned(4))
+      return launch_blocks<uint32_t>(s, nouter, ninner, rows, row_bytes, src, src_outer, src_inner,
+                                     src_row, dst, dst_outer, dst_inner, dst_row);
+    return launch_blocks<unsigned char>(s, nouter, ninner, rows, row_bytes, src, src_outer,
+                                        src_inner, src_row, dst, dst_outer, dst_inner, dst_row);
+  });
 }
 
 // ---- padded-owner column remap (row split) -----------------------------------
@@ -194,21 +198,23 @@ __global__ void padded_remap_kernel(const I* __restrict__ in, I* __restrict__ ou
 
 extern "C" int ofx_padded_owner_remap(void* stream, int idx_dtype, int64_t nnz, int64_t k,
                                       int64_t world, const void* col_in, void* col_out) {
-  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "padded_owner_remap: bad index dtype");
-  OFX_REQUIRE(nnz >= 0 && k >= 0 && world > 0, OFX_EINVAL, "padded_owner_remap: bad sizes");
-  if (nnz == 0) return OFX_OK;
-  OFX_REQUIRE(col_in && col_out, OFX_EINVAL, "padded_owner_remap: NULL pointer");
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const int64_t base = k / world, extra = k % world;
-  const unsigned grid = (unsigned)std::min<int64_t>((nnz + kBlock - 1) / kBlock, 65536);
-  if (idx_dtype == OFX_DT_INT32)
-    hipLaunchKernelGGL(padded_remap_kernel<int32_t>, dim3(grid), dim3(kBlock), 0, s,
-                       static_cast<const int32_t*>(col_in), static_cast<int32_t*>(col_out), nnz,
-                       base, extra);
-  else
-    hipLaunchKernelGGL(padded_remap_kernel<int64_t>, dim3(grid), dim3(kBlock), 0, s,
-                       static_cast<const int64_t*>(col_in), static_cast<int64_t*>(col_out), nnz,
-                       base, extra);
-  OFX_HIP_CHECK(hipGetLastError());
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "padded_owner_remap: bad index dtype");
+    OFX_REQUIRE(nnz >= 0 && k >= 0 && world > 0, OFX_EINVAL, "padded_owner_remap: bad sizes");
+    if (nnz == 0) return OFX_OK;
+    OFX_REQUIRE(col_in && col_out, OFX_EINVAL, "padded_owner_remap: NULL pointer");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t base = k / world, extra = k % world;
+    const unsigned grid = (unsigned)std::min<int64_t>((nnz + kBlock - 1) / kBlock, 65536);
+    if (idx_dtype == OFX_DT_INT32)
+      hipLaunchKernelGGL(padded_remap_kernel<int32_t>, dim3(grid), dim3(kBlock), 0, s,
+                         static_cast<const int32_t*>(col_in), static_cast<int32_t*>(col_out), nnz,
+                         base, extra);
+    else
+      hipLaunchKernelGGL(padded_remap_kernel<int64_t>, dim3(grid), dim3(kBlock), 0, s,
+                         static_cast<const int64_t*>(col_in), static_cast<int64_t*>(col_out), nnz,
+                         base, extra);
+    OFX_HIP_CHECK(hipGetLastError());
+    return OFX_OK;
+  });
 }

@@ -220,6 +220,16 @@ __device__ __forceinline__ bool sddmm_item(const I* __restrict__ rp, int64_t g, 
   return j0 < j1;
 }
 
+// A work list from a failed, superseded or never-built plan: the launch writes nothing and reports
+// it (spmm_plan.h plan_valid; the host's next entry returns OFX_EPLAN).
+__device__ __forceinline__ bool sddmm_plan_invalid(const unsigned long long* __restrict__ counters,
+                                                   int64_t block_base, unsigned* err) {
+  if (counters == nullptr || plan::plan_valid(counters)) return false;
+  if (block_base + blockIdx.x == 0 && threadIdx.x == 0)
+    plan::raise_device_error(err, plan::kErrPlanInvalid);
+  return true;
+}
+
 // Grid pieces: a launch holds fewer than 2^32 threads (papers-scale row counts would not).
 constexpr int64_t kLaunchBlocks = ((int64_t)1 << 31) / kBlock;
 
@@ -229,10 +239,11 @@ __global__ void __launch_bounds__(kBlock)
                  int64_t ldc, const T* __restrict__ B, int64_t ldb, int64_t kb,
                  T* __restrict__ out, int64_t row_begin, int64_t nrows, int64_t n, int64_t chunk,
                  const unsigned long long* __restrict__ counters, const int64_t* __restrict__ items,
-                 const int64_t* __restrict__ order, int64_t block_base) {
+                 const int64_t* __restrict__ order, int64_t block_base, unsigned* err) {
 #pragma clang fp contract(off)
   using A = typename Num<T>::acc;
   constexpr int GPW = 64 / LG;
+  if (sddmm_plan_invalid(counters, block_base, err)) return;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int gl = lane & (LG - 1);
@@ -308,10 +319,11 @@ __global__ void __launch_bounds__(kBlock)
                       int64_t chunk, int tiles,
                       const unsigned long long* __restrict__ counters,
                       const int64_t* __restrict__ items, const int64_t* __restrict__ order,
-                      int64_t block_base) {
+                      int64_t block_base, unsigned* err) {
 #pragma clang fp contract(off)
   using A = typename Num<T>::acc;
   constexpr int L = kWideLeaves / 64, U = 2;
+  if (sddmm_plan_invalid(counters, block_base, err)) return;
   const int lane = threadIdx.x & 63;
   const int64_t g = (block_base + (int64_t)blockIdx.x) * (kBlock / 64) +
                     __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -442,7 +454,8 @@ int sddmm_cfg(const SddmmArgs& a) {
                        static_cast<const I*>(a.rp), static_cast<const I*>(a.col),
                        static_cast<const T*>(a.dC), a.ldc, static_cast<const T*>(a.B), a.ldb, a.k,
                        static_cast<T*>(a.out), a.row_begin, a.nrows, a.n,
-                       w.total > 0 ? sched.chunk : INT64_MAX, wl.counters, wl.items, wl.order, b0);
+                       w.total > 0 ? sched.chunk : INT64_MAX, wl.counters, wl.items, wl.order, b0,
+                       w.total > 0 ? device_error_words() : nullptr);
     OFX_HIP_CHECK(hipGetLastError());
   }
   return OFX_OK;
@@ -484,7 +497,7 @@ int sddmm_aligned(const SddmmArgs& a) {
                        static_cast<const T*>(a.dC), a.ldc, static_cast<const T*>(a.B), a.ldb, a.k,
                        static_cast<T*>(a.out), a.row_begin, a.nrows, a.n,
                        w.total > 0 ? sched.chunk : INT64_MAX, (int)tiles, wl.counters, wl.items,
-                       wl.order, b0);
+                       wl.order, b0, w.total > 0 ? device_error_words() : nullptr);
     OFX_HIP_CHECK(hipGetLastError());
   }
   return OFX_OK;
@@ -516,74 +529,82 @@ using namespace ofx;
 
 extern "C" int ofx_csr_transpose_workspace_size(int idx_dtype, int64_t m, int64_t k, int64_t nnz,
                                                 size_t* bytes) {
-  OFX_REQUIRE(bytes && m >= 0 && k >= 0 && nnz >= 0, OFX_EINVAL, "csr_transpose: bad arguments");
-  OFX_REQUIRE(nnz <= INT32_MAX, OFX_EINVAL, "csr_transpose: nnz > 2^31-1 is not supported");
-  size_t cub = 0;
-  if (idx_dtype == OFX_DT_INT32) return transpose_ws<int32_t>(nnz, k, bytes, &cub);
-  if (idx_dtype == OFX_DT_INT64) return transpose_ws<int64_t>(nnz, k, bytes, &cub);
-  return fail(OFX_EUNSUPPORTED, "csr_transpose: index dtype %d is not int32/int64", idx_dtype);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(bytes && m >= 0 && k >= 0 && nnz >= 0, OFX_EINVAL, "csr_transpose: bad arguments");
+    OFX_REQUIRE(nnz <= INT32_MAX, OFX_EINVAL, "csr_transpose: nnz > 2^31-1 is not supported");
+    size_t cub = 0;
+    if (idx_dtype == OFX_DT_INT32) return transpose_ws<int32_t>(nnz, k, bytes, &cub);
+    if (idx_dtype == OFX_DT_INT64) return transpose_ws<int64_t>(nnz, k, bytes, &cub);
+    return fail(OFX_EUNSUPPORTED, "csr_transpose: index dtype %d is not int32/int64", idx_dtype);
+  });
 }
 
 extern "C" int ofx_csr_transpose(void* stream, int idx_dtype, int64_t m, int64_t k, int64_t nnz,
                                  const void* row_ptr, const void* col_idx, void* out_row_ptr,
                                  void* out_col_idx, void* out_perm, void* workspace,
                                  size_t workspace_bytes) {
-  OFX_REQUIRE(m >= 0 && k >= 0 && nnz >= 0 && row_ptr && out_row_ptr &&
-                  (nnz == 0 || (col_idx && out_col_idx && out_perm)),
-              OFX_EINVAL, "csr_transpose: bad arguments");
-  OFX_REQUIRE(nnz <= INT32_MAX, OFX_EINVAL, "csr_transpose: nnz > 2^31-1 is not supported");
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  if (idx_dtype == OFX_DT_INT32)
-    return transpose<int32_t>(s, m, k, nnz, (const int32_t*)row_ptr, (const int32_t*)col_idx,
-                              (int32_t*)out_row_ptr, (int32_t*)out_col_idx, (int32_t*)out_perm,
-                              workspace, workspace_bytes);
-  if (idx_dtype == OFX_DT_INT64)
-    return transpose<int64_t>(s, m, k, nnz, (const int64_t*)row_ptr, (const int64_t*)col_idx,
-                              (int64_t*)out_row_ptr, (int64_t*)out_col_idx, (int64_t*)out_perm,
-                              workspace, workspace_bytes);
-  return fail(OFX_EUNSUPPORTED, "csr_transpose: index dtype %d is not int32/int64", idx_dtype);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(m >= 0 && k >= 0 && nnz >= 0 && row_ptr && out_row_ptr &&
+                    (nnz == 0 || (col_idx && out_col_idx && out_perm)),
+                OFX_EINVAL, "csr_transpose: bad arguments");
+    OFX_REQUIRE(nnz <= INT32_MAX, OFX_EINVAL, "csr_transpose: nnz > 2^31-1 is not supported");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (idx_dtype == OFX_DT_INT32)
+      return transpose<int32_t>(s, m, k, nnz, (const int32_t*)row_ptr, (const int32_t*)col_idx,
+                                (int32_t*)out_row_ptr, (int32_t*)out_col_idx, (int32_t*)out_perm,
+                                workspace, workspace_bytes);
+    if (idx_dtype == OFX_DT_INT64)
+      return transpose<int64_t>(s, m, k, nnz, (const int64_t*)row_ptr, (const int64_t*)col_idx,
+                                (int64_t*)out_row_ptr, (int64_t*)out_col_idx, (int64_t*)out_perm,
+                                workspace, workspace_bytes);
+    return fail(OFX_EUNSUPPORTED, "csr_transpose: index dtype %d is not int32/int64", idx_dtype);
+  });
 }
 
 extern "C" int ofx_gather_values(void* stream, int idx_dtype, int val_dtype, int64_t nnz,
                                  const void* perm, const void* src, void* dst) {
-  if (nnz == 0) return OFX_OK;
-  OFX_REQUIRE(perm && src && dst, OFX_EINVAL, "gather_values: NULL pointer");
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const unsigned g = (unsigned)std::min<int64_t>((nnz + kBlock - 1) / kBlock, 65536);
-  auto go = [&](auto* ip) -> int {
-    using I = std::remove_const_t<std::remove_pointer_t<decltype(ip)>>;
-    switch (dtype_size(val_dtype)) {
-      case 2:
-        hipLaunchKernelGGL((gather_values_kernel<uint16_t, I>), dim3(g), dim3(kBlock), 0, s,
-                           (const I*)perm, (const uint16_t*)src, nnz, (uint16_t*)dst);
-        break;
-      case 4:
-        hipLaunchKernelGGL((gather_values_kernel<uint32_t, I>), dim3(g), dim3(kBlock), 0, s,
-                           (const I*)perm, (const uint32_t*)src, nnz, (uint32_t*)dst);
-        break;
-      case 8:
-        hipLaunchKernelGGL((gather_values_kernel<uint64_t, I>), dim3(g), dim3(kBlock), 0, s,
-                           (const I*)perm, (const uint64_t*)src, nnz, (uint64_t*)dst);
-        break;
-      default: return fail(OFX_EUNSUPPORTED, "gather_values: bad value dtype %d", val_dtype);
-    }
-    OFX_HIP_CHECK(hipGetLastError());
-    return OFX_OK;
-  };
-  OFX_REQUIRE(is_value_dtype(val_dtype) || is_index_dtype(val_dtype), OFX_EUNSUPPORTED,
-              "gather_values: bad value dtype %d", val_dtype);
-  if (idx_dtype == OFX_DT_INT32) return go((const int32_t*)nullptr);
-  if (idx_dtype == OFX_DT_INT64) return go((const int64_t*)nullptr);
-  return fail(OFX_EUNSUPPORTED, "gather_values: bad index dtype %d", idx_dtype);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    if (nnz == 0) return OFX_OK;
+    OFX_REQUIRE(perm && src && dst, OFX_EINVAL, "gather_values: NULL pointer");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const unsigned g = (unsigned)std::min<int64_t>((nnz + kBlock - 1) / kBlock, 65536);
+    auto go = [&](auto* ip) -> int {
+      using I = std::remove_const_t<std::remove_pointer_t<decltype(ip)>>;
+      switch (dtype_size(val_dtype)) {
+        case 2:
+          hipLaunchKernelGGL((gather_values_kernel<uint16_t, I>), dim3(g), dim3(kBlock), 0, s,
+                             (const I*)perm, (const uint16_t*)src, nnz, (uint16_t*)dst);
+          break;
+        case 4:
+          hipLaunchKernelGGL((gather_values_kernel<uint32_t, I>), dim3(g), dim3(kBlock), 0, s,
+                             (const I*)perm, (const uint32_t*)src, nnz, (uint32_t*)dst);
+          break;
+        case 8:
+          hipLaunchKernelGGL((gather_values_kernel<uint64_t, I>), dim3(g), dim3(kBlock), 0, s,
+                             (const I*)perm, (const uint64_t*)src, nnz, (uint64_t*)dst);
+          break;
+        default: return fail(OFX_EUNSUPPORTED, "gather_values: bad value dtype %d", val_dtype);
+      }
+      OFX_HIP_CHECK(hipGetLastError());
+      return OFX_OK;
+    };
+    OFX_REQUIRE(is_value_dtype(val_dtype) || is_index_dtype(val_dtype), OFX_EUNSUPPORTED,
+                "gather_values: bad value dtype %d", val_dtype);
+    if (idx_dtype == OFX_DT_INT32) return go((const int32_t*)nullptr);
+    if (idx_dtype == OFX_DT_INT64) return go((const int64_t*)nullptr);
+    return fail(OFX_EUNSUPPORTED, "gather_values: bad index dtype %d", idx_dtype);
+  });
 }
 
 extern "C" int ofx_sddmm_csr_workspace_size(int idx_dtype, int val_dtype, int64_t m, int64_t n,
                                             int64_t nnz, size_t* bytes) {
-  OFX_REQUIRE(bytes && m >= 0 && n >= 0 && nnz >= 0, OFX_EINVAL, "sddmm_csr: bad arguments");
-  OFX_REQUIRE(is_index_dtype(idx_dtype) && is_value_dtype(val_dtype), OFX_EUNSUPPORTED,
-              "sddmm_csr: unsupported dtypes (%d, %d)", idx_dtype, val_dtype);
-  *bytes = plan::ws_layout(m, nnz, 0, 0, sddmm_schedule(n)).total;
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(bytes && m >= 0 && n >= 0 && nnz >= 0, OFX_EINVAL, "sddmm_csr: bad arguments");
+    OFX_REQUIRE(is_index_dtype(idx_dtype) && is_value_dtype(val_dtype), OFX_EUNSUPPORTED,
+                "sddmm_csr: unsupported dtypes (%d, %d)", idx_dtype, val_dtype);
+    *bytes = plan::ws_layout(m, nnz, 0, 0, sddmm_schedule(n)).total;
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_sddmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k,
@@ -591,19 +612,22 @@ extern "C" int ofx_sddmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t
                              const void* a, int64_t lda, const void* b, int64_t ldb, void* out,
                              int64_t row_begin, int64_t row_end, void* workspace,
                              size_t workspace_bytes) {
-  OFX_REQUIRE(is_index_dtype(idx_dtype) && is_value_dtype(val_dtype), OFX_EUNSUPPORTED,
-              "sddmm_csr: unsupported dtypes (%d, %d)", idx_dtype, val_dtype);
-  OFX_REQUIRE(m >= 0 && k >= 0 && n >= 0 && nnz >= 0 && lda >= n && ldb >= n, OFX_EINVAL,
-              "sddmm_csr: bad sizes");
-  OFX_REQUIRE(0 <= row_begin && row_begin <= row_end && row_end <= m, OFX_EINVAL,
-              "sddmm_csr: row range [%lld, %lld) outside [0, %lld)", (long long)row_begin,
-              (long long)row_end, (long long)m);
-  if (row_end == row_begin || nnz == 0) return OFX_OK;
-  OFX_REQUIRE(row_ptr && col_idx && out && (n == 0 || (a && b)), OFX_EINVAL,
-              "sddmm_csr: NULL pointer");
-  if (n == 0) return fail(OFX_EINVAL, "sddmm_csr: n == 0 (use a zero fill)");
-  SddmmArgs args{static_cast<hipStream_t>(stream), row_ptr, col_idx, a, b, out, lda, ldb,
-                 row_begin, row_end - row_begin, n, nnz, k, workspace, workspace_bytes};
-  if (idx_dtype == OFX_DT_INT32) return sddmm_idx<int32_t>(val_dtype, args);
-  return sddmm_idx<int64_t>(val_dtype, args);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_TAKE_DEVICE_ERROR("sddmm_csr");  // an earlier launch's loud failure (spmm_plan.h)
+    OFX_REQUIRE(is_index_dtype(idx_dtype) && is_value_dtype(val_dtype), OFX_EUNSUPPORTED,
+                "sddmm_csr: unsupported dtypes (%d, %d)", idx_dtype, val_dtype);
+    OFX_REQUIRE(m >= 0 && k >= 0 && n >= 0 && nnz >= 0 && lda >= n && ldb >= n, OFX_EINVAL,
+                "sddmm_csr: bad sizes");
+    OFX_REQUIRE(0 <= row_begin && row_begin <= row_end && row_end <= m, OFX_EINVAL,
+                "sddmm_csr: row range [%lld, %lld) outside [0, %lld)", (long long)row_begin,
+                (long long)row_end, (long long)m);
+    if (row_end == row_begin || nnz == 0) return OFX_OK;
+    OFX_REQUIRE(row_ptr && col_idx && out && (n == 0 || (a && b)), OFX_EINVAL,
+                "sddmm_csr: NULL pointer");
+    if (n == 0) return fail(OFX_EINVAL, "sddmm_csr: n == 0 (use a zero fill)");
+    SddmmArgs args{static_cast<hipStream_t>(stream), row_ptr, col_idx, a, b, out, lda, ldb,
+                   row_begin, row_end - row_begin, n, nnz, k, workspace, workspace_bytes};
+    if (idx_dtype == OFX_DT_INT32) return sddmm_idx<int32_t>(val_dtype, args);
+    return sddmm_idx<int64_t>(val_dtype, args);
+  });
 }

@@ -115,6 +115,7 @@ int spmm_cpu_entry(int num_threads, int idx_dtype, int val_dtype, int64_t m, int
                    int64_t nnz, const void* row_ptr, const void* col_idx, const void* values,
                    const void* b, int64_t ldb, void* c, int64_t ldc, int64_t row_begin,
                    int64_t row_end, const void* bias, int act, const ofx_spmm_options* opts) {
+  OFX_READ_OPTIONS(opts, "spmm_csr_cpu");
   OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED,
               "spmm_csr_cpu: index dtype %d is not int32/int64", idx_dtype);
   OFX_REQUIRE(is_value_dtype(val_dtype), OFX_EUNSUPPORTED,
@@ -145,8 +146,10 @@ extern "C" int ofx_spmm_csr_cpu(int num_threads, int idx_dtype, int val_dtype, i
                                 const void* col_idx, const void* values, const void* b,
                                 int64_t ldb, void* c, int64_t ldc, int64_t row_begin,
                                 int64_t row_end, const ofx_spmm_options* opts) {
-  return spmm_cpu_entry(num_threads, idx_dtype, val_dtype, m, k, n, nnz, row_ptr, col_idx, values,
-                        b, ldb, c, ldc, row_begin, row_end, nullptr, OFX_ACT_NONE, opts);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    return spmm_cpu_entry(num_threads, idx_dtype, val_dtype, m, k, n, nnz, row_ptr, col_idx, values,
+                          b, ldb, c, ldc, row_begin, row_end, nullptr, OFX_ACT_NONE, opts);
+  });
 }
 
 extern "C" int ofx_spmm_csr_fused_cpu(int num_threads, int idx_dtype, int val_dtype, int64_t m,
@@ -155,43 +158,49 @@ extern "C" int ofx_spmm_csr_fused_cpu(int num_threads, int idx_dtype, int val_dt
                                       int64_t ldb, void* c, int64_t ldc, int64_t row_begin,
                                       int64_t row_end, const void* bias, int activation,
                                       const ofx_spmm_options* opts) {
-  return spmm_cpu_entry(num_threads, idx_dtype, val_dtype, m, k, n, nnz, row_ptr, col_idx, values,
-                        b, ldb, c, ldc, row_begin, row_end, bias, activation, opts);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    return spmm_cpu_entry(num_threads, idx_dtype, val_dtype, m, k, n, nnz, row_ptr, col_idx, values,
+                          b, ldb, c, ldc, row_begin, row_end, bias, activation, opts);
+  });
 }
 
 // ---- BalancedSplitter (oneflow/core/common/balanced_splitter.cpp:20-40) -------------------
 extern "C" int ofx_balanced_range(int64_t total, int64_t parts, int64_t idx, int64_t* begin,
                                   int64_t* end) {
-  OFX_REQUIRE(total >= 0 && parts > 0 && idx >= 0 && idx < parts && begin && end, OFX_EINVAL,
-              "balanced_range: bad arguments (total=%lld parts=%lld idx=%lld)", (long long)total,
-              (long long)parts, (long long)idx);
-  const int64_t base = total / parts, extra = total % parts;
-  // The first `extra` parts hold base+1 elements.
-  const int64_t lo = idx < extra ? idx * (base + 1) : extra * (base + 1) + (idx - extra) * base;
-  *begin = lo;
-  *end = lo + base + (idx < extra ? 1 : 0);
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(total >= 0 && parts > 0 && idx >= 0 && idx < parts && begin && end, OFX_EINVAL,
+                "balanced_range: bad arguments (total=%lld parts=%lld idx=%lld)", (long long)total,
+                (long long)parts, (long long)idx);
+    const int64_t base = total / parts, extra = total % parts;
+    // The first `extra` parts hold base+1 elements.
+    const int64_t lo = idx < extra ? idx * (base + 1) : extra * (base + 1) + (idx - extra) * base;
+    *begin = lo;
+    *end = lo + base + (idx < extra ? 1 : 0);
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_csr_row_slice_host(int idx_dtype, const void* row_ptr, int64_t row_begin,
                                       int64_t row_end, void* out_row_ptr, int64_t* nnz_begin,
                                       int64_t* nnz_end) {
-  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "csr_row_slice_host: bad dtype");
-  OFX_REQUIRE(row_ptr && 0 <= row_begin && row_begin <= row_end, OFX_EINVAL,
-              "csr_row_slice_host: bad arguments");
-  auto run = [&](auto* rp, auto* out) {
-    const int64_t base = (int64_t)rp[row_begin];
-    if (out)
-      for (int64_t i = 0; i <= row_end - row_begin; ++i)
-        out[i] = (std::remove_pointer_t<decltype(out)>)((int64_t)rp[row_begin + i] - base);
-    if (nnz_begin) *nnz_begin = base;
-    if (nnz_end) *nnz_end = (int64_t)rp[row_end];
-  };
-  if (idx_dtype == OFX_DT_INT32)
-    run(static_cast<const int32_t*>(row_ptr), static_cast<int32_t*>(out_row_ptr));
-  else
-    run(static_cast<const int64_t*>(row_ptr), static_cast<int64_t*>(out_row_ptr));
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "csr_row_slice_host: bad dtype");
+    OFX_REQUIRE(row_ptr && 0 <= row_begin && row_begin <= row_end, OFX_EINVAL,
+                "csr_row_slice_host: bad arguments");
+    auto run = [&](auto* rp, auto* out) {
+      const int64_t base = (int64_t)rp[row_begin];
+      if (out)
+        for (int64_t i = 0; i <= row_end - row_begin; ++i)
+          out[i] = (std::remove_pointer_t<decltype(out)>)((int64_t)rp[row_begin + i] - base);
+      if (nnz_begin) *nnz_begin = base;
+      if (nnz_end) *nnz_end = (int64_t)rp[row_end];
+    };
+    if (idx_dtype == OFX_DT_INT32)
+      run(static_cast<const int32_t*>(row_ptr), static_cast<int32_t*>(out_row_ptr));
+    else
+      run(static_cast<const int64_t*>(row_ptr), static_cast<int64_t*>(out_row_ptr));
+    return OFX_OK;
+  });
 }
 
 // ---- backward building blocks on the host (DeviceType::kCPU; same bits as the HIP kernels) ---
@@ -256,23 +265,25 @@ void cpu_sddmm(int nthreads, int64_t k, int64_t n, const I* rp, const I* col, co
 
 extern "C" int ofx_gather_values_host(int idx_dtype, int val_dtype, int64_t nnz, const void* perm,
                                       const void* src, void* dst) {
-  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "gather_values: bad index dtype %d",
-              idx_dtype);
-  const int vs = dtype_size(val_dtype);
-  OFX_REQUIRE(vs == 2 || vs == 4 || vs == 8, OFX_EUNSUPPORTED, "gather_values: bad value dtype %d",
-              val_dtype);
-  OFX_REQUIRE(nnz >= 0 && (nnz == 0 || (perm && src && dst)), OFX_EINVAL,
-              "gather_values: NULL argument");
-  const char* s = static_cast<const char*>(src);
-  char* d = static_cast<char*>(dst);
-  for (int64_t t = 0; t < nnz; ++t) {
-    const int64_t j = idx_dtype == OFX_DT_INT32 ? (int64_t) static_cast<const int32_t*>(perm)[t]
-                                                : static_cast<const int64_t*>(perm)[t];
-    OFX_REQUIRE(j >= 0 && j < nnz, OFX_EINVAL, "gather_values: perm[%lld] = %lld outside [0, %lld)",
-                (long long)t, (long long)j, (long long)nnz);
-    memcpy(d + (size_t)t * vs, s + (size_t)j * vs, (size_t)vs);
-  }
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "gather_values: bad index dtype %d",
+                idx_dtype);
+    const int vs = dtype_size(val_dtype);
+    OFX_REQUIRE(vs == 2 || vs == 4 || vs == 8, OFX_EUNSUPPORTED, "gather_values: bad value dtype %d",
+                val_dtype);
+    OFX_REQUIRE(nnz >= 0 && (nnz == 0 || (perm && src && dst)), OFX_EINVAL,
+                "gather_values: NULL argument");
+    const char* s = static_cast<const char*>(src);
+    char* d = static_cast<char*>(dst);
+    for (int64_t t = 0; t < nnz; ++t) {
+      const int64_t j = idx_dtype == OFX_DT_INT32 ? (int64_t) static_cast<const int32_t*>(perm)[t]
+                                                  : static_cast<const int64_t*>(perm)[t];
+      OFX_REQUIRE(j >= 0 && j < nnz, OFX_EINVAL, "gather_values: perm[%lld] = %lld outside [0, %lld)",
+                  (long long)t, (long long)j, (long long)nnz);
+      memcpy(d + (size_t)t * vs, s + (size_t)j * vs, (size_t)vs);
+    }
+    return OFX_OK;
+  });
 }
 
 namespace ofx {
@@ -303,61 +314,65 @@ int64_t row_ptr_at(int idx_dtype, const void* row_ptr, int64_t r) {
 extern "C" int ofx_csr_transpose_cpu(int idx_dtype, int64_t m, int64_t k, int64_t nnz,
                                      const void* row_ptr, const void* col_idx, void* out_row_ptr,
                                      void* out_col_idx, void* out_perm) {
-  OFX_REQUIRE(m >= 0 && k >= 0 && nnz >= 0 && row_ptr && out_row_ptr &&
-                  (nnz == 0 || (col_idx && out_col_idx && out_perm)),
-              OFX_EINVAL, "csr_transpose_cpu: bad arguments");
-  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "csr_transpose_cpu: bad index dtype %d",
-              idx_dtype);
-  OFX_REQUIRE(nnz == 0 || !negative_column(idx_dtype, col_idx, 0, nnz), OFX_EINVAL,
-              "csr_transpose_cpu: negative column index (gather_kernel_util.cpp:80 CHECK_GE(idx, 0))");
-  if (idx_dtype == OFX_DT_INT32)
-    cpu_transpose<int32_t>(m, k, nnz, (const int32_t*)row_ptr, (const int32_t*)col_idx,
-                           (int32_t*)out_row_ptr, (int32_t*)out_col_idx, (int32_t*)out_perm);
-  else if (idx_dtype == OFX_DT_INT64)
-    cpu_transpose<int64_t>(m, k, nnz, (const int64_t*)row_ptr, (const int64_t*)col_idx,
-                           (int64_t*)out_row_ptr, (int64_t*)out_col_idx, (int64_t*)out_perm);
-  else
-    return fail(OFX_EUNSUPPORTED, "csr_transpose_cpu: bad index dtype %d", idx_dtype);
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(m >= 0 && k >= 0 && nnz >= 0 && row_ptr && out_row_ptr &&
+                    (nnz == 0 || (col_idx && out_col_idx && out_perm)),
+                OFX_EINVAL, "csr_transpose_cpu: bad arguments");
+    OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "csr_transpose_cpu: bad index dtype %d",
+                idx_dtype);
+    OFX_REQUIRE(nnz == 0 || !negative_column(idx_dtype, col_idx, 0, nnz), OFX_EINVAL,
+                "csr_transpose_cpu: negative column index (gather_kernel_util.cpp:80 CHECK_GE(idx, 0))");
+    if (idx_dtype == OFX_DT_INT32)
+      cpu_transpose<int32_t>(m, k, nnz, (const int32_t*)row_ptr, (const int32_t*)col_idx,
+                             (int32_t*)out_row_ptr, (int32_t*)out_col_idx, (int32_t*)out_perm);
+    else if (idx_dtype == OFX_DT_INT64)
+      cpu_transpose<int64_t>(m, k, nnz, (const int64_t*)row_ptr, (const int64_t*)col_idx,
+                             (int64_t*)out_row_ptr, (int64_t*)out_col_idx, (int64_t*)out_perm);
+    else
+      return fail(OFX_EUNSUPPORTED, "csr_transpose_cpu: bad index dtype %d", idx_dtype);
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_sddmm_csr_cpu(int num_threads, int idx_dtype, int val_dtype, int64_t m,
                                  int64_t k, int64_t n, int64_t nnz, const void* row_ptr,
                                  const void* col_idx, const void* a, int64_t lda, const void* b,
                                  int64_t ldb, void* out, int64_t row_begin, int64_t row_end) {
-  OFX_REQUIRE(is_index_dtype(idx_dtype) && is_value_dtype(val_dtype), OFX_EUNSUPPORTED,
-              "sddmm_csr_cpu: unsupported dtypes (%d, %d)", idx_dtype, val_dtype);
-  OFX_REQUIRE(m >= 0 && k >= 0 && n > 0 && nnz >= 0 && lda >= n && ldb >= n && 0 <= row_begin &&
-                  row_begin <= row_end && row_end <= m,
-              OFX_EINVAL, "sddmm_csr_cpu: bad sizes");
-  if (row_end == row_begin || nnz == 0) return OFX_OK;
-  OFX_REQUIRE(!negative_column(idx_dtype, col_idx, row_ptr_at(idx_dtype, row_ptr, row_begin),
-                               row_ptr_at(idx_dtype, row_ptr, row_end)),
-              OFX_EINVAL,
-              "sddmm_csr_cpu: negative column index (gather_kernel_util.cpp:80 CHECK_GE(idx, 0))");
-  const int nt = num_threads > 0 ? num_threads : omp_get_max_threads();
-  auto run = [&](auto* ip) {
-    using I = std::remove_const_t<std::remove_pointer_t<decltype(ip)>>;
-    const I* rp = (const I*)row_ptr;
-    const I* ci = (const I*)col_idx;
-    switch (val_dtype) {
-      case OFX_DT_FLOAT:
-        cpu_sddmm<float, I>(nt, k, n, rp, ci, (const float*)a, lda, (const float*)b, ldb, (float*)out, row_begin, row_end);
-        break;
-      case OFX_DT_DOUBLE:
-        cpu_sddmm<double, I>(nt, k, n, rp, ci, (const double*)a, lda, (const double*)b, ldb, (double*)out, row_begin, row_end);
-        break;
-      case OFX_DT_BFLOAT16:
-        cpu_sddmm<bf16, I>(nt, k, n, rp, ci, (const bf16*)a, lda, (const bf16*)b, ldb, (bf16*)out, row_begin, row_end);
-        break;
-      default:
-        cpu_sddmm<f16, I>(nt, k, n, rp, ci, (const f16*)a, lda, (const f16*)b, ldb, (f16*)out, row_begin, row_end);
-        break;
-    }
-  };
-  if (idx_dtype == OFX_DT_INT32) run((const int32_t*)nullptr);
-  else run((const int64_t*)nullptr);
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(is_index_dtype(idx_dtype) && is_value_dtype(val_dtype), OFX_EUNSUPPORTED,
+                "sddmm_csr_cpu: unsupported dtypes (%d, %d)", idx_dtype, val_dtype);
+    OFX_REQUIRE(m >= 0 && k >= 0 && n > 0 && nnz >= 0 && lda >= n && ldb >= n && 0 <= row_begin &&
+                    row_begin <= row_end && row_end <= m,
+                OFX_EINVAL, "sddmm_csr_cpu: bad sizes");
+    if (row_end == row_begin || nnz == 0) return OFX_OK;
+    OFX_REQUIRE(!negative_column(idx_dtype, col_idx, row_ptr_at(idx_dtype, row_ptr, row_begin),
+                                 row_ptr_at(idx_dtype, row_ptr, row_end)),
+                OFX_EINVAL,
+                "sddmm_csr_cpu: negative column index (gather_kernel_util.cpp:80 CHECK_GE(idx, 0))");
+    const int nt = num_threads > 0 ? num_threads : omp_get_max_threads();
+    auto run = [&](auto* ip) {
+      using I = std::remove_const_t<std::remove_pointer_t<decltype(ip)>>;
+      const I* rp = (const I*)row_ptr;
+      const I* ci = (const I*)col_idx;
+      switch (val_dtype) {
+        case OFX_DT_FLOAT:
+          cpu_sddmm<float, I>(nt, k, n, rp, ci, (const float*)a, lda, (const float*)b, ldb, (float*)out, row_begin, row_end);
+          break;
+        case OFX_DT_DOUBLE:
+          cpu_sddmm<double, I>(nt, k, n, rp, ci, (const double*)a, lda, (const double*)b, ldb, (double*)out, row_begin, row_end);
+          break;
+        case OFX_DT_BFLOAT16:
+          cpu_sddmm<bf16, I>(nt, k, n, rp, ci, (const bf16*)a, lda, (const bf16*)b, ldb, (bf16*)out, row_begin, row_end);
+          break;
+        default:
+          cpu_sddmm<f16, I>(nt, k, n, rp, ci, (const f16*)a, lda, (const f16*)b, ldb, (f16*)out, row_begin, row_end);
+          break;
+      }
+    };
+    if (idx_dtype == OFX_DT_INT32) run((const int32_t*)nullptr);
+    else run((const int64_t*)nullptr);
+    return OFX_OK;
+  });
 }
 
 // ---- COO -> CSR on the host (same output as csr_build.hip) ------------------------------------
@@ -402,44 +417,46 @@ extern "C" int ofx_coo_to_csr_cpu(int idx_dtype, int val_dtype, int64_t m, int64
                                   const void* row, const void* col, const void* values,
                                   int merge_duplicates, void* out_row_ptr, void* out_col_idx,
                                   void* out_values, int64_t* out_nnz) {
-  OFX_REQUIRE(m >= 0 && k >= 0 && nnz >= 0 && out_row_ptr && out_nnz &&
-                  (nnz == 0 || (row && col && out_col_idx)),
-              OFX_EINVAL, "coo_to_csr_cpu: bad arguments");
-  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "coo_to_csr_cpu: bad index dtype");
-  OFX_REQUIRE((values == nullptr) == (out_values == nullptr), OFX_EINVAL,
-              "coo_to_csr_cpu: values and out_values must both be given or both be NULL");
-  auto run = [&](auto* ip) -> int {
-    using I = std::remove_const_t<std::remove_pointer_t<decltype(ip)>>;
-    const I* r = (const I*)row;
-    const I* c = (const I*)col;
-    for (int64_t i = 0; i < nnz; ++i)
-      OFX_REQUIRE(r[i] >= 0 && r[i] < m && c[i] >= 0 && c[i] < k, OFX_EINVAL,
-                  "coo_to_csr_cpu: entry %lld (%lld, %lld) outside %lld x %lld", (long long)i,
-                  (long long)r[i], (long long)c[i], (long long)m, (long long)k);
-    const int vdt = values ? val_dtype : OFX_DT_FLOAT;
-    switch (vdt) {
-      case OFX_DT_FLOAT:
-        *out_nnz = cpu_coo_to_csr<float, I>(m, k, nnz, r, c, (const float*)values, merge_duplicates,
-                                            (I*)out_row_ptr, (I*)out_col_idx, (float*)out_values);
-        break;
-      case OFX_DT_DOUBLE:
-        *out_nnz = cpu_coo_to_csr<double, I>(m, k, nnz, r, c, (const double*)values, merge_duplicates,
-                                             (I*)out_row_ptr, (I*)out_col_idx, (double*)out_values);
-        break;
-      case OFX_DT_BFLOAT16:
-        *out_nnz = cpu_coo_to_csr<bf16, I>(m, k, nnz, r, c, (const bf16*)values, merge_duplicates,
-                                           (I*)out_row_ptr, (I*)out_col_idx, (bf16*)out_values);
-        break;
-      case OFX_DT_FLOAT16:
-        *out_nnz = cpu_coo_to_csr<f16, I>(m, k, nnz, r, c, (const f16*)values, merge_duplicates,
-                                          (I*)out_row_ptr, (I*)out_col_idx, (f16*)out_values);
-        break;
-      default: return fail(OFX_EUNSUPPORTED, "coo_to_csr_cpu: bad value dtype %d", vdt);
-    }
-    return OFX_OK;
-  };
-  if (idx_dtype == OFX_DT_INT32) return run((const int32_t*)nullptr);
-  return run((const int64_t*)nullptr);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(m >= 0 && k >= 0 && nnz >= 0 && out_row_ptr && out_nnz &&
+                    (nnz == 0 || (row && col && out_col_idx)),
+                OFX_EINVAL, "coo_to_csr_cpu: bad arguments");
+    OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "coo_to_csr_cpu: bad index dtype");
+    OFX_REQUIRE((values == nullptr) == (out_values == nullptr), OFX_EINVAL,
+                "coo_to_csr_cpu: values and out_values must both be given or both be NULL");
+    auto run = [&](auto* ip) -> int {
+      using I = std::remove_const_t<std::remove_pointer_t<decltype(ip)>>;
+      const I* r = (const I*)row;
+      const I* c = (const I*)col;
+      for (int64_t i = 0; i < nnz; ++i)
+        OFX_REQUIRE(r[i] >= 0 && r[i] < m && c[i] >= 0 && c[i] < k, OFX_EINVAL,
+                    "coo_to_csr_cpu: entry %lld (%lld, %lld) outside %lld x %lld", (long long)i,
+                    (long long)r[i], (long long)c[i], (long long)m, (long long)k);
+      const int vdt = values ? val_dtype : OFX_DT_FLOAT;
+      switch (vdt) {
+        case OFX_DT_FLOAT:
+          *out_nnz = cpu_coo_to_csr<float, I>(m, k, nnz, r, c, (const float*)values, merge_duplicates,
+                                              (I*)out_row_ptr, (I*)out_col_idx, (float*)out_values);
+          break;
+        case OFX_DT_DOUBLE:
+          *out_nnz = cpu_coo_to_csr<double, I>(m, k, nnz, r, c, (const double*)values, merge_duplicates,
+                                               (I*)out_row_ptr, (I*)out_col_idx, (double*)out_values);
+          break;
+        case OFX_DT_BFLOAT16:
+          *out_nnz = cpu_coo_to_csr<bf16, I>(m, k, nnz, r, c, (const bf16*)values, merge_duplicates,
+                                             (I*)out_row_ptr, (I*)out_col_idx, (bf16*)out_values);
+          break;
+        case OFX_DT_FLOAT16:
+          *out_nnz = cpu_coo_to_csr<f16, I>(m, k, nnz, r, c, (const f16*)values, merge_duplicates,
+                                            (I*)out_row_ptr, (I*)out_col_idx, (f16*)out_values);
+          break;
+        default: return fail(OFX_EUNSUPPORTED, "coo_to_csr_cpu: bad value dtype %d", vdt);
+      }
+      return OFX_OK;
+    };
+    if (idx_dtype == OFX_DT_INT32) return run((const int32_t*)nullptr);
+    return run((const int64_t*)nullptr);
+  });
 }
 
 // ---- fused-epilogue backward on the host (csrc/epilogue_grad.hip states the order) -----------
@@ -491,22 +508,24 @@ int relu_bias_grad_cpu(int num_threads, int64_t m, int64_t n, const T* y, int64_
 extern "C" int ofx_relu_bias_grad_cpu(int num_threads, int val_dtype, int64_t m, int64_t n,
                                       const void* y, int64_t ldy, const void* dy, int64_t lddy,
                                       void* dx, int64_t lddx, void* d_bias, int relu) {
-  OFX_REQUIRE(is_value_dtype(val_dtype), OFX_EUNSUPPORTED, "relu_bias_grad: bad dtype %d",
-              val_dtype);
-  OFX_REQUIRE(m >= 0 && n >= 0, OFX_EINVAL, "relu_bias_grad: negative size");
-  if (n == 0) return OFX_OK;
-  OFX_REQUIRE(m == 0 || (dy && (!relu || y) && lddy >= n && (!relu || ldy >= n)), OFX_EINVAL,
-              "relu_bias_grad: NULL input or leading dimension < n");
-  OFX_REQUIRE(dx == nullptr || lddx >= n, OFX_EINVAL, "relu_bias_grad: lddx < n");
-#define OFX_RBG(T)                                                                               \
-  return relu_bias_grad_cpu<T>(num_threads, m, n, static_cast<const T*>(y), ldy,                 \
-                               static_cast<const T*>(dy), lddy, static_cast<T*>(dx), lddx,       \
-                               static_cast<T*>(d_bias), relu)
-  switch (val_dtype) {
-    case OFX_DT_FLOAT: OFX_RBG(float);
-    case OFX_DT_DOUBLE: OFX_RBG(double);
-    case OFX_DT_BFLOAT16: OFX_RBG(bf16);
-    default: OFX_RBG(f16);
-  }
-#undef OFX_RBG
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(is_value_dtype(val_dtype), OFX_EUNSUPPORTED, "relu_bias_grad: bad dtype %d",
+                val_dtype);
+    OFX_REQUIRE(m >= 0 && n >= 0, OFX_EINVAL, "relu_bias_grad: negative size");
+    if (n == 0) return OFX_OK;
+    OFX_REQUIRE(m == 0 || (dy && (!relu || y) && lddy >= n && (!relu || ldy >= n)), OFX_EINVAL,
+                "relu_bias_grad: NULL input or leading dimension < n");
+    OFX_REQUIRE(dx == nullptr || lddx >= n, OFX_EINVAL, "relu_bias_grad: lddx < n");
+  #define OFX_RBG(T)                                                                               \
+    return relu_bias_grad_cpu<T>(num_threads, m, n, static_cast<const T*>(y), ldy,                 \
+                                 static_cast<const T*>(dy), lddy, static_cast<T*>(dx), lddx,       \
+                                 static_cast<T*>(d_bias), relu)
+    switch (val_dtype) {
+      case OFX_DT_FLOAT: OFX_RBG(float);
+      case OFX_DT_DOUBLE: OFX_RBG(double);
+      case OFX_DT_BFLOAT16: OFX_RBG(bf16);
+      default: OFX_RBG(f16);
+    }
+  #undef OFX_RBG
+  });
 }

@@ -998,10 +998,15 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
                      const int64_t* __restrict__ items, const int64_t* __restrict__ order,
                      typename Num<T>::acc* __restrict__ part, const T* __restrict__ bias,
                      int act, int64_t wave_blocks, int64_t block_base,
-                     unsigned* __restrict__ arrive) {
+                     unsigned* __restrict__ arrive, unsigned* err) {
   using A = typename Num<T>::acc;
   constexpr int VEC = K::VEC, LPR = K::LPR, kWaves = K::WPB;
   const int64_t bid = block_base + (int64_t)blockIdx.x;  // launches of > 2^31 threads are cut
+  // a plan that failed, was superseded or never built: write nothing, loudly (spmm_plan.h)
+  if (counters != nullptr && !plan::plan_valid(counters)) {
+    if (bid == 0 && threadIdx.x == 0) plan::raise_device_error(err, plan::kErrPlanInvalid);
+    return;
+  }
   constexpr int GPW = 64 / LPR;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1223,6 +1228,7 @@ __global__ void __launch_bounds__(kBlock)
   using A = typename Num<T>::acc;
   using P = Pack<A, VEC>;
   constexpr int kPre = 16;  // partial rows in flight per lane (the adds stay in chunk order)
+  if (!plan::plan_valid(counters)) return;  // spmm_main reported it and wrote nothing either
   const int64_t nhubs = (int64_t)OFX_LD(counters + 1);
   const int gl = threadIdx.x % L;
   const int64_t groups = (int64_t)gridDim.x * (kBlock / L);
@@ -1326,12 +1332,16 @@ int describe_cfg(const Launch& L, const char* kind) {
                      : (K::WH && K::HL > 0)          ? "narrow"
                      : K::PF                         ? "prefetch"
                                                      : "bandwidth";
+  // the workspace this launch lays out (<= ofx_spmm_csr_workspace_size over the matrix's m)
+  const size_t ws = std::strcmp(kind, "small") == 0
+                        ? 0
+                        : ws_layout(L.nrows, L.nnz, L.n, sizeof(typename Num<T>::acc), L.sched).total;
   std::snprintf(L.describe, L.describe_bytes,
                 "form=%s kernel=%s VEC=%d LPR=%d U=%d WPB=%d NT=%d PF=%d WH=%d BI=%d BUF=%d SH=%d "
-                "HL=%d HU=%d LR=%d elem=%d idx=%d",
+                "HL=%d HU=%d LR=%d elem=%d idx=%d ws=%zu",
                 form, kind, K::VEC, K::LPR, K::U, K::WPB, (int)K::NT, (int)K::PF, (int)K::WH,
                 (int)K::BI, (int)K::BUF, (int)K::SH, K::HL, K::HU, (int)K::LR, (int)sizeof(T),
-                (int)sizeof(I));
+                (int)sizeof(I), ws);
   return OFX_OK;
 }
 
@@ -1426,7 +1436,8 @@ int launch_cfg(const Launch& L) {
                        L.stream, rp, col, val, static_cast<const I*>(L.vperm), B, L.ldb, L.b_rows,
                        C, L.ldc, L.row_begin, L.nrows, L.n, plan ? L.sched.split : INT64_MAX,
                        plan ? L.sched.chunk : INT64_MAX, heavy, counters, items, order, part,
-                       static_cast<const T*>(L.bias), L.act, wave_blocks, b0, wl.arrive);
+                       static_cast<const T*>(L.bias), L.act, wave_blocks, b0, wl.arrive,
+                       plan ? device_error_words() : nullptr);
     OFX_HIP_CHECK(hipGetLastError());
   }
   if (plan && w.max_hubs > 0 && !K::LR)  // LR: the main kernel added the hubs (hub_tail)

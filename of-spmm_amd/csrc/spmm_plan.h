@@ -52,15 +52,28 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 //   order[0 .. nlight) = the light rows, ascending
 //   order[nrows - 1 - h] = heavy row h, h < counters[3] (heavy rows fill the array from its end)
 //   arrive[first slot of each hub] = 0                              (the in-kernel hub reduce)
-// and counters = {hub chunks, hubs, 0, heavy rows}.  Work item q of the non-hub rows is
-// order_row(order, nrows, nheavy, q).  The layout is a pure function of row_ptr (deterministic);
-// the partial of chunk s is part[s].
+// and counters = {hub chunks, hubs, 0, heavy rows, epoch, host tag, ok tag, fail tag}.  Work item q
+// of the non-hub rows is order_row(order, nrows, nheavy, q).  The layout is a pure function of
+// row_ptr (deterministic); the partial of chunk s is part[s].
 //
 // One launch (spmm_plan_kernel): every block counts its rows' classes, then finds the offsets of
 // its hubs / chunks / heavy rows / light rows among all earlier blocks by decoupled look-back
 // (each block publishes its totals, then its inclusive prefix, in a status word tagged with the
-// launch's epoch: the workspace is never zeroed, and a word from an earlier launch or leftover
-// memory carries another epoch), and writes its part of the list.  Because heavy rows fill the
+// launch's tag: the workspace is never zeroed, and a word from an earlier launch or leftover
+// memory carries another tag), and writes its part of the list.
+//
+// The launch's tag (a host-chosen epoch is frozen into a captured hipGraph, so every
+// replay would take the previous replay's status words as its own) mixes a device-side epoch word
+// (counters[kEpoch]: read by every block at entry, advanced by the last block once its look-back
+// is done, by which time every block has read it) with the host's per-call tag: replays of one
+// capture get distinct tags, and so do calls from different processes on one buffer.  The last
+// block also records the plan as valid (counters[kOk] = the tag, with the host tag beside it);
+// a block whose look-back gives up records the tag as failed (counters[kFail]), refuses the tag a
+// replay of the same capture would take next (counters[kPoison]: a block of this launch that had
+// not started yet may publish under it), and sets the library's device-error word.  Every consumer of the work list (spmm_main, spmm_reduce, SDDMM)
+// checks plan_valid() at entry and writes nothing for a failed, stale or never-built plan; the
+// host reports the error word at its next entry (ofx_device_error_check).
+// Because heavy rows fill the
 // order array from its end and light rows from its start, no block needs a grand total.  A block
 // waits only on lower-numbered blocks, which are dispatched first (each XCD dispatches its blocks
 // in order), so the chain always progresses.  This replaced count + scan + write launches
@@ -76,11 +89,38 @@ constexpr int kBins = 2;
 constexpr int kPlanVals = 2 + kBins;  // hubs, chunks, bins...
 constexpr int64_t kOwnItems = 8;      // hubs with more chunks get their items written wave-wide
 constexpr int kLookWords = 16;        // per plan block: status, totals[4], inclusive prefix[4]
-constexpr unsigned long long kAgg = 1, kInc = 2;  // status = epoch << 2 | state
+constexpr unsigned long long kAgg = 1, kInc = 2;  // status = tag << 2 | state
+// counters[]: the list's sizes, then the validity words (above)
+constexpr int kEpoch = 4, kHostTag = 5, kOk = 6, kFail = 7, kPoison = 8, kCounterWords = 9;
 // Polls of one status word before the look-back gives up (seconds; a wait in a correct launch is
-// microseconds): a planner bug then leaves the block's part of the list unwritten, which the
-// parity tests see, instead of hanging the GPU.
+// microseconds): a planner bug or a stalled predecessor then fails the plan loudly (plan_valid,
+// the device-error word) instead of hanging the GPU.  Tests lower it (ofx_debug_set); 0 makes
+// every block but the first give up without polling.
 constexpr int kSpinLimit = 1 << 22;
+
+// The tag of a plan launch from the device epoch word and the host's per-call tag: 62 bits, odd
+// (never 0, the "no valid plan" value of counters[kOk]).
+__host__ __device__ __forceinline__ unsigned long long plan_tag(unsigned long long epoch,
+                                                               unsigned long long host_tag) {
+  return (splitmix64(epoch * 0x9e3779b97f4a7c15ull + splitmix64(host_tag)) >> 2) | 1ull;
+}
+
+// Whether `counters` describe a plan that completed (every block wrote its part of the list) and
+// has not been superseded by a failed or half-built one.  Uniform across the grid.
+__device__ __forceinline__ bool plan_valid(const unsigned long long* __restrict__ counters) {
+  const unsigned long long e = OFX_LDP(counters + kEpoch), h = OFX_LDP(counters + kHostTag);
+  const unsigned long long ok = OFX_LDP(counters + kOk), fl = OFX_LDP(counters + kFail);
+  const unsigned long long poison = OFX_LDP(counters + kPoison);
+  return ok != 0 && ok == plan_tag(e - 1, h) && fl != ok && poison != ok;
+}
+
+// The library's device-error words (host-mapped, ofx_device_error_check reads them): a plain
+// system-scope vector store, never an atomic read-modify-write on host memory.
+constexpr int kErrPlanFailed = 0, kErrPlanInvalid = 1;
+__device__ __forceinline__ void raise_device_error(unsigned* err, int which) {
+  if (err != nullptr)
+    __hip_atomic_store(err + which, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 template <typename I>
 __device__ __forceinline__ int plan_row(const I* __restrict__ rp, int64_t row_begin, int64_t nrows,
@@ -242,10 +282,10 @@ template <int RPT, typename I>
 __global__ void __launch_bounds__(kBlock)
     spmm_plan_kernel(const I* __restrict__ rp, int64_t row_begin, int64_t nrows, int64_t split,
                      int64_t chunk, int64_t heavy, unsigned long long* __restrict__ look,
-                     unsigned long long epoch, int64_t nblocks,
+                     unsigned long long host_tag, int64_t nblocks,
                      unsigned long long* __restrict__ counters, int64_t* __restrict__ hubs,
                      int64_t* __restrict__ items, int64_t* __restrict__ order,
-                     unsigned* __restrict__ arrive) {
+                     unsigned* __restrict__ arrive, int spin_limit, unsigned* err) {
   __shared__ int64_t s_off[kPlanVals];
   __shared__ int s_fail;
   int cls[RPT];
@@ -255,6 +295,10 @@ __global__ void __launch_bounds__(kBlock)
   plan_thread<RPT>(rp, row_begin, nrows, base, split, chunk, heavy, cls, nc, v);
   block_scan_vals(v, tot);
   if (threadIdx.x < 64) {
+    // this launch's tag (see the top of the file): wave 0 reads the epoch word before it
+    // publishes anything, and the last block advances it only after every block has published
+    const unsigned long long dev_epoch = coh_load(counters + kEpoch);
+    const unsigned long long epoch = plan_tag(dev_epoch, host_tag);
     // Wave 0 publishes this block's totals (block 0: its inclusive prefix at once), then looks
     // back over 64 predecessors per step, one per lane: the nearest one holding its inclusive
     // prefix ends the walk, the aggregates of those after it are added.  One lane per step (the
@@ -271,13 +315,13 @@ __global__ void __launch_bounds__(kBlock)
       look_publish(look, b, epoch << 2 | (b == 0 ? kInc : kAgg));
     }
     int64_t pre[kPlanVals] = {};
-    bool failed = false;
-    for (int64_t end = b; end > 0; end -= 64) {
+    bool failed = spin_limit == 0 && b > 0;  // test knob: give up without polling
+    for (int64_t end = failed ? 0 : b; end > 0; end -= 64) {
       const int64_t p = end - 1 - lane;  // lane 0: the nearest predecessor
       unsigned long long st = epoch << 2 | kAgg;
       if (p >= 0) {
         int spins = 0;  // bounded: a predecessor that never publishes cannot hang the launch
-        while (((st = look_status(look, p)) >> 2) != epoch && ++spins < kSpinLimit)
+        while (((st = look_status(look, p)) >> 2) != epoch && ++spins < spin_limit)
           __builtin_amdgcn_s_sleep(1);
       }
       asm volatile("" ::: "memory");  // the payload loads below issue after the status returned
@@ -312,11 +356,27 @@ __global__ void __launch_bounds__(kBlock)
 #pragma unroll
       for (int i = 0; i < kPlanVals; ++i) s_off[i] = pre[i];
     }
-    if (lane == 0 && b == nblocks - 1 && !failed) {  // the last block knows the grand totals
-      OFX_STP(counters + 0, (unsigned long long)(pre[1] + tot[1]));
-      OFX_STP(counters + 1, (unsigned long long)(pre[0] + tot[0]));
-      OFX_STP(counters + 2, 0ull);
-      OFX_STP(counters + 3, (unsigned long long)(pre[2] + tot[2]));
+    if (lane == 0 && failed) {
+      // Loud failure: the consumers see counters[kFail] == the tag and write nothing, and the
+      // host reports the error word at its next entry.  A predecessor that had not published may
+      // not even have started; it can read the advanced epoch word and publish under the NEXT
+      // launch's tag (a replay of the same capture), so that tag is refused too (kPoison).
+      coh_store(counters + kFail, epoch);
+      coh_store(counters + kPoison, plan_tag(dev_epoch + 1, host_tag));
+      raise_device_error(err, kErrPlanFailed);
+    }
+    if (lane == 0 && b == nblocks - 1) {  // the last block knows the grand totals
+      if (!failed) {
+        OFX_STP(counters + 0, (unsigned long long)(pre[1] + tot[1]));
+        OFX_STP(counters + 1, (unsigned long long)(pre[0] + tot[0]));
+        OFX_STP(counters + 2, 0ull);
+        OFX_STP(counters + 3, (unsigned long long)(pre[2] + tot[2]));
+        OFX_STP(counters + kHostTag, host_tag);
+      }
+      OFX_STP(counters + kOk, failed ? 0ull : epoch);
+      // a successful look-back means every block has published, so every block has read the
+      // epoch word: the next launch on this workspace gets the next tag
+      OFX_STP(counters + kEpoch, dev_epoch + 1);
     }
   }
   __syncthreads();
@@ -345,11 +405,15 @@ WsLayout ws_layout(int64_t nrows, int64_t nnz, int64_t n, size_t acc_bytes, cons
   w.max_chunks = s.split == INT64_MAX ? 0 : nnz / s.chunk + 1;
   const int64_t rows_per_block = (int64_t)kBlock * plan_rpt(nrows);
   w.plan_blocks = (nrows + rows_per_block - 1) / rows_per_block;
+  // The look region is sized for the smallest rows-per-thread (the most blocks), not this
+  // launch's: the size is then monotone in nrows, so the workspace query over the matrix's m
+  // bounds every row range of it (m = 2^18 + 1 planned 65 blocks, rows [1, m) 256).
+  const int64_t look_blocks = (nrows + (int64_t)kBlock * 4 - 1) / ((int64_t)kBlock * 4);
   size_t off = 0;
   w.counters = off;
-  off = align_up(off + (2 + kBins) * sizeof(unsigned long long), 256);
+  off = align_up(off + kCounterWords * sizeof(unsigned long long), 256);
   w.look = off;
-  off = align_up(off + (size_t)w.plan_blocks * kLookWords * sizeof(unsigned long long), 256);
+  off = align_up(off + (size_t)look_blocks * kLookWords * sizeof(unsigned long long), 256);
   w.hubs = off;
   off = align_up(off + (size_t)w.max_hubs * 3 * sizeof(int64_t), 256);
   w.items = off;
@@ -383,10 +447,10 @@ inline void worklist_of(const WsLayout& w, char* ws, WorkList* wl) {
   wl->part = ws + w.part;
 }
 
-// A launch-unique tag of the look-back status words (62 bits): a per-process random start and a
-// counter.  A status word left by another launch (or uninitialised memory) matches it with
-// probability 2^-62.
-inline unsigned long long next_epoch() {
+// The host's per-call part of a plan's tag (a per-process random start and a counter; the device
+// epoch word makes the tag launch-unique within one capture, see the top of the file).  A status
+// word left by another launch (or uninitialised memory) matches a tag with probability 2^-62.
+inline unsigned long long next_host_tag() {
   static std::atomic<unsigned long long> counter{
       splitmix64((unsigned long long)std::chrono::steady_clock::now().time_since_epoch().count() ^
                  (unsigned long long)(uintptr_t)&counter)};
@@ -403,15 +467,19 @@ int launch_plan(hipStream_t stream, const I* rp, int64_t row_begin, int64_t nrow
   worklist_of(w, ws, wl);
   auto* look = reinterpret_cast<unsigned long long*>(ws + w.look);
   OFX_REQUIRE(w.plan_blocks < (int64_t)UINT32_MAX, OFX_EINVAL, "spmm_csr: too many rows to plan");
-  const unsigned long long epoch = next_epoch();
+  const unsigned long long host_tag = next_host_tag();
+  const int spin = debug_knob(OFX_DEBUG_PLAN_SPIN_LIMIT, kSpinLimit);
+  unsigned* err = device_error_words();
   if (plan_rpt(nrows) == 4)
     hipLaunchKernelGGL((spmm_plan_kernel<4, I>), dim3((unsigned)w.plan_blocks), dim3(kBlock), 0,
-                       stream, rp, row_begin, nrows, sched.split, sched.chunk, heavy, look, epoch,
-                       w.plan_blocks, wl->counters, wl->hubs, wl->items, wl->order, wl->arrive);
+                       stream, rp, row_begin, nrows, sched.split, sched.chunk, heavy, look, host_tag,
+                       w.plan_blocks, wl->counters, wl->hubs, wl->items, wl->order, wl->arrive,
+                       spin, err);
   else
     hipLaunchKernelGGL((spmm_plan_kernel<16, I>), dim3((unsigned)w.plan_blocks), dim3(kBlock), 0,
-                       stream, rp, row_begin, nrows, sched.split, sched.chunk, heavy, look, epoch,
-                       w.plan_blocks, wl->counters, wl->hubs, wl->items, wl->order, wl->arrive);
+                       stream, rp, row_begin, nrows, sched.split, sched.chunk, heavy, look, host_tag,
+                       w.plan_blocks, wl->counters, wl->hubs, wl->items, wl->order, wl->arrive,
+                       spin, err);
   OFX_HIP_CHECK(hipGetLastError());
   return OFX_OK;
 }

@@ -125,89 +125,97 @@ using namespace ofx;
 
 extern "C" int ofx_synth_row_ptr(int64_t m, int64_t k, int64_t nnz, double gamma, uint64_t seed,
                                  int64_t* row_ptr_out) {
-  OFX_REQUIRE(m >= 0 && k >= 0 && nnz >= 0 && row_ptr_out && gamma > 1.0, OFX_EINVAL,
-              "synth_row_ptr: bad arguments");
-  OFX_REQUIRE(m == 0 || (double)nnz <= (double)m * (double)k, OFX_EINVAL,
-              "synth_row_ptr: nnz=%lld exceeds m*k", (long long)nnz);
-  row_ptr_out[0] = 0;
-  if (m == 0) return OFX_OK;
-  std::vector<double> w(m);
-  double W = 0.0;
-  for (int64_t i = 0; i < m; ++i) {
-    w[i] = weight(i, gamma);
-    W += w[i];
-  }
-  std::vector<int64_t> d(m);
-  int64_t total = 0;
-  for (int64_t i = 0; i < m; ++i) {
-    int64_t di = (int64_t)std::floor((double)nnz * w[i] / W);
-    if (di > k) di = k;
-    d[i] = di;
-    total += di;
-  }
-  int64_t rem = nnz - total;
-  while (rem > 0) {
-    for (int64_t i = 0; i < m && rem > 0; ++i)
-      if (d[i] < k) {
-        ++d[i];
-        --rem;
-      }
-  }
-  while (rem < 0) {  // floor() never overshoots, kept for completeness
-    for (int64_t i = m - 1; i >= 0 && rem < 0; --i)
-      if (d[i] > 0) {
-        --d[i];
-        ++rem;
-      }
-  }
-  const std::vector<int64_t> perm = permutation(m, seed);
-  std::vector<int64_t> deg(m);
-  for (int64_t i = 0; i < m; ++i) deg[perm[i]] = d[i];
-  for (int64_t r = 0; r < m; ++r) row_ptr_out[r + 1] = row_ptr_out[r] + deg[r];
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(m >= 0 && k >= 0 && nnz >= 0 && row_ptr_out && gamma > 1.0, OFX_EINVAL,
+                "synth_row_ptr: bad arguments");
+    OFX_REQUIRE(m == 0 || (double)nnz <= (double)m * (double)k, OFX_EINVAL,
+                "synth_row_ptr: nnz=%lld exceeds m*k", (long long)nnz);
+    row_ptr_out[0] = 0;
+    if (m == 0) return OFX_OK;
+    std::vector<double> w(m);
+    double W = 0.0;
+    for (int64_t i = 0; i < m; ++i) {
+      w[i] = weight(i, gamma);
+      W += w[i];
+    }
+    std::vector<int64_t> d(m);
+    int64_t total = 0;
+    for (int64_t i = 0; i < m; ++i) {
+      int64_t di = (int64_t)std::floor((double)nnz * w[i] / W);
+      if (di > k) di = k;
+      d[i] = di;
+      total += di;
+    }
+    int64_t rem = nnz - total;
+    while (rem > 0) {
+      for (int64_t i = 0; i < m && rem > 0; ++i)
+        if (d[i] < k) {
+          ++d[i];
+          --rem;
+        }
+    }
+    while (rem < 0) {  // floor() never overshoots, kept for completeness
+      for (int64_t i = m - 1; i >= 0 && rem < 0; --i)
+        if (d[i] > 0) {
+          --d[i];
+          ++rem;
+        }
+    }
+    const std::vector<int64_t> perm = permutation(m, seed);
+    std::vector<int64_t> deg(m);
+    for (int64_t i = 0; i < m; ++i) deg[perm[i]] = d[i];
+    for (int64_t r = 0; r < m; ++r) row_ptr_out[r + 1] = row_ptr_out[r] + deg[r];
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_synth_columns(int64_t m, int64_t k, double gamma, uint64_t seed,
                                  const int64_t* row_ptr, int64_t row_begin, int64_t row_end,
                                  int idx_dtype, void* col_out, int num_threads) {
-  OFX_REQUIRE(row_ptr && 0 <= row_begin && row_begin <= row_end && row_end <= m && k >= 0,
-              OFX_EINVAL, "synth_columns: bad arguments");
-  OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "synth_columns: bad index dtype");
-  if (row_end == row_begin || row_ptr[row_end] == row_ptr[row_begin]) return OFX_OK;
-  OFX_REQUIRE(col_out && k > 0, OFX_EINVAL, "synth_columns: NULL output or k == 0");
-  const int nt = num_threads > 0 ? num_threads : omp_get_max_threads();
-  if (idx_dtype == OFX_DT_INT32)
-    fill_columns<int32_t>(k, gamma, seed, row_ptr, row_begin, row_end,
-                          static_cast<int32_t*>(col_out), nt);
-  else
-    fill_columns<int64_t>(k, gamma, seed, row_ptr, row_begin, row_end,
-                          static_cast<int64_t*>(col_out), nt);
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(row_ptr && 0 <= row_begin && row_begin <= row_end && row_end <= m && k >= 0,
+                OFX_EINVAL, "synth_columns: bad arguments");
+    OFX_REQUIRE(is_index_dtype(idx_dtype), OFX_EUNSUPPORTED, "synth_columns: bad index dtype");
+    if (row_end == row_begin || row_ptr[row_end] == row_ptr[row_begin]) return OFX_OK;
+    OFX_REQUIRE(col_out && k > 0, OFX_EINVAL, "synth_columns: NULL output or k == 0");
+    const int nt = num_threads > 0 ? num_threads : omp_get_max_threads();
+    if (idx_dtype == OFX_DT_INT32)
+      fill_columns<int32_t>(k, gamma, seed, row_ptr, row_begin, row_end,
+                            static_cast<int32_t*>(col_out), nt);
+    else
+      fill_columns<int64_t>(k, gamma, seed, row_ptr, row_begin, row_end,
+                            static_cast<int64_t*>(col_out), nt);
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_synth_values_host(int val_dtype, int64_t j_begin, int64_t j_end, uint64_t seed,
                                      int exact, void* out) {
-  OFX_REQUIRE(j_begin <= j_end && (out || j_begin == j_end), OFX_EINVAL,
-              "synth_values_host: bad arguments");
-  switch (val_dtype) {
-    case OFX_DT_FLOAT: fill_values(j_begin, j_end, seed, exact, static_cast<float*>(out)); break;
-    case OFX_DT_DOUBLE: fill_values(j_begin, j_end, seed, exact, static_cast<double*>(out)); break;
-    case OFX_DT_BFLOAT16: fill_values(j_begin, j_end, seed, exact, static_cast<bf16*>(out)); break;
-    case OFX_DT_FLOAT16: fill_values(j_begin, j_end, seed, exact, static_cast<f16*>(out)); break;
-    default: return fail(OFX_EUNSUPPORTED, "synth_values_host: bad dtype %d", val_dtype);
-  }
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(j_begin <= j_end && (out || j_begin == j_end), OFX_EINVAL,
+                "synth_values_host: bad arguments");
+    switch (val_dtype) {
+      case OFX_DT_FLOAT: fill_values(j_begin, j_end, seed, exact, static_cast<float*>(out)); break;
+      case OFX_DT_DOUBLE: fill_values(j_begin, j_end, seed, exact, static_cast<double*>(out)); break;
+      case OFX_DT_BFLOAT16: fill_values(j_begin, j_end, seed, exact, static_cast<bf16*>(out)); break;
+      case OFX_DT_FLOAT16: fill_values(j_begin, j_end, seed, exact, static_cast<f16*>(out)); break;
+      default: return fail(OFX_EUNSUPPORTED, "synth_values_host: bad dtype %d", val_dtype);
+    }
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_synth_dense_host(int val_dtype, int64_t r_begin, int64_t r_end, int64_t n,
                                     int64_t ld, uint64_t seed, int exact, void* out) {
-  OFX_REQUIRE(r_begin <= r_end && ld >= n && n >= 0, OFX_EINVAL, "synth_dense_host: bad shape");
-  switch (val_dtype) {
-    case OFX_DT_FLOAT: fill_dense(r_begin, r_end, n, ld, seed, exact, static_cast<float*>(out)); break;
-    case OFX_DT_DOUBLE: fill_dense(r_begin, r_end, n, ld, seed, exact, static_cast<double*>(out)); break;
-    case OFX_DT_BFLOAT16: fill_dense(r_begin, r_end, n, ld, seed, exact, static_cast<bf16*>(out)); break;
-    case OFX_DT_FLOAT16: fill_dense(r_begin, r_end, n, ld, seed, exact, static_cast<f16*>(out)); break;
-    default: return fail(OFX_EUNSUPPORTED, "synth_dense_host: bad dtype %d", val_dtype);
-  }
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(r_begin <= r_end && ld >= n && n >= 0, OFX_EINVAL, "synth_dense_host: bad shape");
+    switch (val_dtype) {
+      case OFX_DT_FLOAT: fill_dense(r_begin, r_end, n, ld, seed, exact, static_cast<float*>(out)); break;
+      case OFX_DT_DOUBLE: fill_dense(r_begin, r_end, n, ld, seed, exact, static_cast<double*>(out)); break;
+      case OFX_DT_BFLOAT16: fill_dense(r_begin, r_end, n, ld, seed, exact, static_cast<bf16*>(out)); break;
+      case OFX_DT_FLOAT16: fill_dense(r_begin, r_end, n, ld, seed, exact, static_cast<f16*>(out)); break;
+      default: return fail(OFX_EUNSUPPORTED, "synth_dense_host: bad dtype %d", val_dtype);
+    }
+    return OFX_OK;
+  });
 }

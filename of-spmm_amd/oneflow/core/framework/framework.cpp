@@ -3,7 +3,21 @@
 
 #include "ofx_spmm.h"
 
+#include <new>
+#include <stdexcept>
+
+#include "ofx_internal.h"
+
 namespace oneflow {
+
+void TestHookCompute(const char* op_name) {
+  switch (ofx::debug_knob(OFX_DEBUG_THROW_IN_COMPUTE, 0)) {
+    case 1: throw std::runtime_error(std::string(op_name) + ": injected by OFX_DEBUG_THROW_IN_COMPUTE");
+    case 2: throw std::bad_alloc();
+    case 3: throw 42;  // not derived from std::exception
+    default: break;
+  }
+}
 
 const char* DataType_Name(DataType dt) {
   switch (dt) {

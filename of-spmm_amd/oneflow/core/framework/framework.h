@@ -172,6 +172,11 @@ struct KernelCheckError {
     }                                                                                        \
   } while (0)
 
+// Test hook of this stand-in (no OneFlow counterpart; INTEGRATION.md: define it empty in a
+// OneFlow tree): the op kernels' Compute throws when ofx_debug_set(OFX_DEBUG_THROW_IN_COMPUTE)
+// asks it to, so the tests can show that no exception crosses the C-ABI (ofx::guarded).
+void TestHookCompute(const char* op_name);
+
 template <typename T>
 struct GetDataType;
 template <>

@@ -46,6 +46,10 @@ DeviceType DeviceOf(int32_t code) {
 
 Maybe<void> MakeParallelDesc(const ofx_placement* pl, ParallelDesc* pd) {
   CHECK_OR_RETURN(pl != nullptr) << Error::RuntimeError() << "NULL placement";
+  CHECK_OR_RETURN(pl->struct_size >= OFX_PLACEMENT_MIN_SIZE)
+      << Error::RuntimeError() << "ofx_placement.struct_size = " << pl->struct_size
+      << " is below the first versioned layout (" << OFX_PLACEMENT_MIN_SIZE
+      << " bytes): initialise it with OFX_PLACEMENT_INIT";
   CHECK_OR_RETURN(pl->parallel_num >= 1 && pl->parallel_id >= 0 &&
                   pl->parallel_id < pl->parallel_num)
       << Error::RuntimeError() << "placement: parallel_id " << pl->parallel_id << " of "
@@ -68,6 +72,10 @@ Shape ShapeOf(const ofx_tensor_desc* d) {
 
 Maybe<void> CheckContiguous(const ofx_tensor_desc* t, const char* name) {
   CHECK_OR_RETURN(t != nullptr) << Error::RuntimeError() << "NULL " << name;
+  CHECK_OR_RETURN(t->struct_size >= OFX_TENSOR_DESC_MIN_SIZE)
+      << Error::RuntimeError() << name << ": ofx_tensor_desc.struct_size = " << t->struct_size
+      << " is below the first versioned layout (" << OFX_TENSOR_DESC_MIN_SIZE
+      << " bytes): initialise it with OFX_TENSOR_DESC_INIT";
   CHECK_OR_RETURN(t->ndim >= 1 && t->ndim <= 2) << Error::RuntimeError() << name << " must be 1-D or 2-D";
   if (t->ndim == 2 && t->shape[0] > 1)
     CHECK_OR_RETURN(t->stride[0] == t->shape[1] && (t->shape[1] <= 1 || t->stride[1] == 1))
@@ -308,6 +316,7 @@ class SpmmJob {
              ofx_tensor_desc* d_b, ofx_tensor_desc* d_o) const {
     auto vec = [&](ofx_tensor_desc* d, int dt, int64_t len, const void* p) {
       std::memset(d, 0, sizeof(*d));
+      d->struct_size = sizeof(*d);
       d->dtype = dt;
       d->device = device_;
       d->ndim = 1;
@@ -317,6 +326,7 @@ class SpmmJob {
     };
     auto mat = [&](ofx_tensor_desc* d, int64_t r, const void* p) {
       std::memset(d, 0, sizeof(*d));
+      d->struct_size = sizeof(*d);
       d->dtype = val_dtype_;
       d->device = device_;
       d->ndim = 2;
@@ -356,171 +366,197 @@ using namespace oneflow;
 
 extern "C" int ofx_process_ctx_init(int64_t rank, int64_t world, ofx_kv_push_fn push,
                                     ofx_kv_pull_fn pull, ofx_sendrecv_fn sendrecv, void* user) {
-  OFX_REQUIRE(world >= 1 && rank >= 0 && rank < world, OFX_EINVAL,
-              "process_ctx_init: rank %lld of %lld", (long long)rank, (long long)world);
-  ctrl::Install(rank, world, push, pull, sendrecv, user);
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(world >= 1 && rank >= 0 && rank < world, OFX_EINVAL,
+                "process_ctx_init: rank %lld of %lld", (long long)rank, (long long)world);
+    ctrl::Install(rank, world, push, pull, sendrecv, user);
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_ccl_registered(int device_type, int* all_gather, int* communication_context) {
-  OFX_REQUIRE(all_gather && communication_context, OFX_EINVAL, "ccl_registered: NULL argument");
-  *all_gather = ccl::IsAllGatherRegistered(DeviceOf(device_type)) ? 1 : 0;
-  *communication_context = ccl::IsCommunicationContextRegistered(DeviceOf(device_type)) ? 1 : 0;
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(all_gather && communication_context, OFX_EINVAL, "ccl_registered: NULL argument");
+    *all_gather = ccl::IsAllGatherRegistered(DeviceOf(device_type)) ? 1 : 0;
+    *communication_context = ccl::IsCommunicationContextRegistered(DeviceOf(device_type)) ? 1 : 0;
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_boxing_check_ccl_s2b(const ofx_placement* pl, int ndim,
                                         const int64_t* logical_shape, const char* in_sbp,
                                         const char* out_sbp) {
-  OFX_REQUIRE(ndim >= 0 && ndim <= 8 && (ndim == 0 || logical_shape) && in_sbp && out_sbp,
-              OFX_EINVAL, "boxing_check_ccl_s2b: bad arguments");
-  ParallelDesc pd;
-  int rc = ToStatus(MakeParallelDesc(pl, &pd));
-  if (rc) return rc;
-  const Shape logical(std::vector<int64_t>(logical_shape, logical_shape + ndim));
-  return ToStatus(CheckCclS2B({{in_sbp}, pd}, {{out_sbp}, pd}, logical));
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(ndim >= 0 && ndim <= 8 && (ndim == 0 || logical_shape) && in_sbp && out_sbp,
+                OFX_EINVAL, "boxing_check_ccl_s2b: bad arguments");
+    ParallelDesc pd;
+    int rc = ToStatus(MakeParallelDesc(pl, &pd));
+    if (rc) return rc;
+    const Shape logical(std::vector<int64_t>(logical_shape, logical_shape + ndim));
+    return ToStatus(CheckCclS2B({{in_sbp}, pd}, {{out_sbp}, pd}, logical));
+  });
 }
 
 extern "C" int ofx_boxing_ccl_s2b(void* stream, const ofx_placement* pl, const ofx_tensor_desc* in,
                                   ofx_tensor_desc* out, int64_t logical_dim0) {
-  ParallelDesc pd;
-  int rc = ToStatus(MakeParallelDesc(pl, &pd));
-  if (rc) return rc;
-  rc = ToStatus(CheckContiguous(in, "in"));
-  if (rc) return rc;
-  rc = ToStatus(CheckContiguous(out, "out"));
-  if (rc) return rc;
-  Shape logical = ShapeOf(in);
-  logical.Set(0, logical_dim0);
-  user_op::Tensor t_in(ShapeOf(in), (DataType)in->dtype, in->data);
-  user_op::Tensor t_out(ShapeOf(out), (DataType)out->dtype, out->data);
-  StreamPair sp(stream, in->device);
-  return ToStatus(CclS2B(sp.of(pd.device_type()), t_in, &t_out, {{"S(0)"}, pd}, {{"B"}, pd}, logical,
-                         pl->parallel_id),
-                  OFX_ECOMM);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    ParallelDesc pd;
+    int rc = ToStatus(MakeParallelDesc(pl, &pd));
+    if (rc) return rc;
+    rc = ToStatus(CheckContiguous(in, "in"));
+    if (rc) return rc;
+    rc = ToStatus(CheckContiguous(out, "out"));
+    if (rc) return rc;
+    Shape logical = ShapeOf(in);
+    logical.Set(0, logical_dim0);
+    user_op::Tensor t_in(ShapeOf(in), (DataType)in->dtype, in->data);
+    user_op::Tensor t_out(ShapeOf(out), (DataType)out->dtype, out->data);
+    StreamPair sp(stream, in->device);
+    return ToStatus(CclS2B(sp.of(pd.device_type()), t_in, &t_out, {{"S(0)"}, pd}, {{"B"}, pd}, logical,
+                           pl->parallel_id),
+                    OFX_ECOMM);
+  });
 }
 
 extern "C" int ofx_nccl_logical_all_gather(void* stream, const ofx_placement* pl,
                                            const ofx_tensor_desc* in, ofx_tensor_desc* out,
                                            const char* stream_name) {
-  ParallelDesc pd;
-  int rc = ToStatus(MakeParallelDesc(pl, &pd));
-  if (rc) return rc;
-  rc = ToStatus(CheckContiguous(in, "in"));
-  if (rc) return rc;
-  rc = ToStatus(CheckContiguous(out, "out"));
-  if (rc) return rc;
-  const std::string op_name = "_nccl_logical_all_gather";
-  const user_op::OpRegistryResult* op = user_op::UserOpRegistryMgr::Get().GetOpRegistryResult(op_name);
-  OFX_REQUIRE(op, OFX_EINVAL, "%s is not registered", op_name.c_str());
-  Shape logical = ShapeOf(in);
-  logical.Set(0, ShapeOf(out).At(0));
-  user_op::InferNdSbpFnContext sctx(*pd.hierarchy(), {},
-                                    {{"src_reduced_nd_sbp", {"S(0)"}}, {"dst_reduced_nd_sbp", {"B"}}});
-  rc = ToStatus(op->nd_sbp_infer(&sctx));
-  if (rc) return rc;
-  user_op::KernelRegContext reg_ctx;
-  reg_ctx.device_type_ = pd.device_type();
-  reg_ctx.dtypes[{"in", 0}] = reg_ctx.dtypes[{"out", 0}] = (DataType)in->dtype;
-  const user_op::OpKernelRegistryResult* reg = nullptr;
-  rc = ToStatus(user_op::UserOpRegistryMgr::Get().GetOpKernelRegistryResult(op_name, reg_ctx, &reg));
-  if (rc) return rc;
-  std::unique_ptr<user_op::OpKernel> kernel(reg->create_fn());
-  const ParallelContext pc(pl->parallel_id, pd.parallel_num());
-  user_op::KernelInitContext ictx(pc, pd, pd.device_type(), stream_name ? stream_name : "");
-  user_op::Tensor t_in(ShapeOf(in), (DataType)in->dtype, in->data);
-  user_op::Tensor t_out(ShapeOf(out), (DataType)out->dtype, out->data);
-  std::map<std::pair<std::string, int32_t>, user_op::Tensor*> tensors = {{{"in", 0}, &t_in},
-                                                                         {{"out", 0}, &t_out}};
-  StreamPair sp(stream, in->device);
-  user_op::KernelComputeContext ctx(sp.of(pd.device_type()), tensors, {}, pd.device_type());
-  ctx.set_parallel_ctx(pc);
-  try {
-    std::shared_ptr<user_op::OpKernelState> state = kernel->CreateOpKernelState(&ictx);
-    kernel->Compute(&ctx, state.get(), nullptr);
-  } catch (const KernelCheckError& e) {
-    return ofx::fail(OFX_ECOMM, "%s", e.msg.c_str());
-  }
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    ParallelDesc pd;
+    int rc = ToStatus(MakeParallelDesc(pl, &pd));
+    if (rc) return rc;
+    rc = ToStatus(CheckContiguous(in, "in"));
+    if (rc) return rc;
+    rc = ToStatus(CheckContiguous(out, "out"));
+    if (rc) return rc;
+    const std::string op_name = "_nccl_logical_all_gather";
+    const user_op::OpRegistryResult* op = user_op::UserOpRegistryMgr::Get().GetOpRegistryResult(op_name);
+    OFX_REQUIRE(op, OFX_EINVAL, "%s is not registered", op_name.c_str());
+    Shape logical = ShapeOf(in);
+    logical.Set(0, ShapeOf(out).At(0));
+    user_op::InferNdSbpFnContext sctx(*pd.hierarchy(), {},
+                                      {{"src_reduced_nd_sbp", {"S(0)"}}, {"dst_reduced_nd_sbp", {"B"}}});
+    rc = ToStatus(op->nd_sbp_infer(&sctx));
+    if (rc) return rc;
+    user_op::KernelRegContext reg_ctx;
+    reg_ctx.device_type_ = pd.device_type();
+    reg_ctx.dtypes[{"in", 0}] = reg_ctx.dtypes[{"out", 0}] = (DataType)in->dtype;
+    const user_op::OpKernelRegistryResult* reg = nullptr;
+    rc = ToStatus(user_op::UserOpRegistryMgr::Get().GetOpKernelRegistryResult(op_name, reg_ctx, &reg));
+    if (rc) return rc;
+    std::unique_ptr<user_op::OpKernel> kernel(reg->create_fn());
+    const ParallelContext pc(pl->parallel_id, pd.parallel_num());
+    user_op::KernelInitContext ictx(pc, pd, pd.device_type(), stream_name ? stream_name : "");
+    user_op::Tensor t_in(ShapeOf(in), (DataType)in->dtype, in->data);
+    user_op::Tensor t_out(ShapeOf(out), (DataType)out->dtype, out->data);
+    std::map<std::pair<std::string, int32_t>, user_op::Tensor*> tensors = {{{"in", 0}, &t_in},
+                                                                           {{"out", 0}, &t_out}};
+    StreamPair sp(stream, in->device);
+    user_op::KernelComputeContext ctx(sp.of(pd.device_type()), tensors, {}, pd.device_type());
+    ctx.set_parallel_ctx(pc);
+    try {
+      std::shared_ptr<user_op::OpKernelState> state = kernel->CreateOpKernelState(&ictx);
+      kernel->Compute(&ctx, state.get(), nullptr);
+    } catch (const KernelCheckError& e) {
+      return ofx::fail(OFX_ECOMM, "%s", e.msg.c_str());
+    }
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_insert_nccl_logical_op(const char* src_sbp, const char* dst_sbp, int ndim,
                                           const int64_t* logical_shape, int64_t parallel_num,
                                           char* op_type, size_t len) {
-  OFX_REQUIRE(src_sbp && dst_sbp && op_type && len > 0 && ndim >= 0 && ndim <= 8 &&
-                  (ndim == 0 || logical_shape) && parallel_num >= 1,
-              OFX_EINVAL, "insert_nccl_logical_op: bad arguments");
-  const Shape logical(std::vector<int64_t>(logical_shape, logical_shape + ndim));
-  snprintf(op_type, len, "%s", NcclLogicalOpType1D(src_sbp, dst_sbp, logical, parallel_num).c_str());
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(src_sbp && dst_sbp && op_type && len > 0 && ndim >= 0 && ndim <= 8 &&
+                    (ndim == 0 || logical_shape) && parallel_num >= 1,
+                OFX_EINVAL, "insert_nccl_logical_op: bad arguments");
+    const Shape logical(std::vector<int64_t>(logical_shape, logical_shape + ndim));
+    snprintf(op_type, len, "%s", NcclLogicalOpType1D(src_sbp, dst_sbp, logical, parallel_num).c_str());
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_rccl_comm_key(const ofx_placement* pl, const char* stream_name, int64_t machine,
                                  int64_t device, char* key, size_t len, int* rank) {
-  ParallelDesc pd;
-  int rc = ToStatus(MakeParallelDesc(pl, &pd));
-  if (rc) return rc;
-  OFX_REQUIRE(key && len > 0 && rank, OFX_EINVAL, "rccl_comm_key: NULL argument");
-  DeviceSet set;
-  for (int64_t p = 0; p < pd.parallel_num(); ++p)
-    set.emplace(pd.MachineId4ParallelId(p), pd.DeviceId4ParallelId(p));
-  const std::vector<std::pair<int64_t, int64_t>> vec(set.begin(), set.end());
-  snprintf(key, len, "%s",
-           EagerRcclCommMgr::UniqueIdKey(vec, stream_name ? stream_name
-                                                          : EagerRcclCommMgr::kDefaultStreamName)
-               .c_str());
-  *rank = EagerRcclCommMgr::RankInSet(vec, machine, device);
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    ParallelDesc pd;
+    int rc = ToStatus(MakeParallelDesc(pl, &pd));
+    if (rc) return rc;
+    OFX_REQUIRE(key && len > 0 && rank, OFX_EINVAL, "rccl_comm_key: NULL argument");
+    DeviceSet set;
+    for (int64_t p = 0; p < pd.parallel_num(); ++p)
+      set.emplace(pd.MachineId4ParallelId(p), pd.DeviceId4ParallelId(p));
+    const std::vector<std::pair<int64_t, int64_t>> vec(set.begin(), set.end());
+    snprintf(key, len, "%s",
+             EagerRcclCommMgr::UniqueIdKey(vec, stream_name ? stream_name
+                                                            : EagerRcclCommMgr::kDefaultStreamName)
+                 .c_str());
+    *rank = EagerRcclCommMgr::RankInSet(vec, machine, device);
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_spmm_job_create(const ofx_placement* pl, int idx_dtype, int val_dtype, int64_t m,
                                    int64_t k, int64_t n, int64_t nnz, const char* stream_name,
                                    void** job) {
-  OFX_REQUIRE(job, OFX_EINVAL, "spmm_job_create: NULL job");
-  OFX_REQUIRE(ofx::is_index_dtype(idx_dtype) && ofx::is_value_dtype(val_dtype), OFX_EUNSUPPORTED,
-              "spmm_job_create: dtypes %d / %d", idx_dtype, val_dtype);
-  OFX_REQUIRE(m >= 0 && k >= 0 && n >= 0 && nnz >= 0, OFX_EINVAL, "spmm_job_create: bad shape");
-  ParallelDesc pd;
-  int rc = ToStatus(MakeParallelDesc(pl, &pd));
-  if (rc) return rc;
-  std::unique_ptr<SpmmJob> j(new SpmmJob());
-  rc = ToStatus(j->Compile(pd, pl->parallel_id, idx_dtype, val_dtype, m, k, n, nnz,
-                           stream_name && *stream_name ? stream_name
-                                                       : EagerRcclCommMgr::kDefaultStreamName));
-  if (rc) return rc;
-  *job = j.release();
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(job, OFX_EINVAL, "spmm_job_create: NULL job");
+    OFX_REQUIRE(ofx::is_index_dtype(idx_dtype) && ofx::is_value_dtype(val_dtype), OFX_EUNSUPPORTED,
+                "spmm_job_create: dtypes %d / %d", idx_dtype, val_dtype);
+    OFX_REQUIRE(m >= 0 && k >= 0 && n >= 0 && nnz >= 0, OFX_EINVAL, "spmm_job_create: bad shape");
+    ParallelDesc pd;
+    int rc = ToStatus(MakeParallelDesc(pl, &pd));
+    if (rc) return rc;
+    std::unique_ptr<SpmmJob> j(new SpmmJob());
+    rc = ToStatus(j->Compile(pd, pl->parallel_id, idx_dtype, val_dtype, m, k, n, nnz,
+                             stream_name && *stream_name ? stream_name
+                                                         : EagerRcclCommMgr::kDefaultStreamName));
+    if (rc) return rc;
+    *job = j.release();
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_spmm_job_describe(void* job, char* buf, size_t len, size_t* tmp_bytes) {
-  OFX_REQUIRE(job && buf && len > 0, OFX_EINVAL, "spmm_job_describe: NULL argument");
-  const SpmmJob* j = static_cast<SpmmJob*>(job);
-  snprintf(buf, len, "%s", j->plan().c_str());
-  if (tmp_bytes) *tmp_bytes = j->tmp_bytes();
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(job && buf && len > 0, OFX_EINVAL, "spmm_job_describe: NULL argument");
+    const SpmmJob* j = static_cast<SpmmJob*>(job);
+    snprintf(buf, len, "%s", j->plan().c_str());
+    if (tmp_bytes) *tmp_bytes = j->tmp_bytes();
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_spmm_job_run(void* job, void* stream, const void* row_ptr, const void* col_idx,
                                 const void* values, const void* b_shard, void* out, void* tmp,
                                 size_t tmp_bytes) {
-  OFX_REQUIRE(job, OFX_EINVAL, "spmm_job_run: NULL job");
-  return static_cast<SpmmJob*>(job)->Run(stream, row_ptr, col_idx, values, b_shard, out, tmp,
-                                         tmp_bytes);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(job, OFX_EINVAL, "spmm_job_run: NULL job");
+    return static_cast<SpmmJob*>(job)->Run(stream, row_ptr, col_idx, values, b_shard, out, tmp,
+                                           tmp_bytes);
+  });
 }
 
 extern "C" int ofx_spmm_job_destroy(void* job) {
-  delete static_cast<SpmmJob*>(job);
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    delete static_cast<SpmmJob*>(job);
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_spmm_job_set_graph(void* job, int enable) {
-  OFX_REQUIRE(job, OFX_EINVAL, "spmm_job_set_graph: NULL job");
-  return static_cast<SpmmJob*>(job)->set_graph(enable != 0);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(job, OFX_EINVAL, "spmm_job_set_graph: NULL job");
+    return static_cast<SpmmJob*>(job)->set_graph(enable != 0);
+  });
 }
 
 extern "C" int ofx_spmm_job_graph_stats(void* job, int64_t* captures, int64_t* replays,
                                         int64_t* updates) {
-  OFX_REQUIRE(job, OFX_EINVAL, "spmm_job_graph_stats: NULL job");
-  static_cast<const SpmmJob*>(job)->graph_stats(captures, replays, updates);
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(job, OFX_EINVAL, "spmm_job_graph_stats: NULL job");
+    static_cast<const SpmmJob*>(job)->graph_stats(captures, replays, updates);
+    return OFX_OK;
+  });
 }

@@ -34,10 +34,23 @@ int ToStatus(const Maybe<void>& m) {
   return ofx::fail(OFX_EINVAL, "%s: %s", m.kind().c_str(), m.message().c_str());
 }
 
+// A versioned descriptor (include/ofx_spmm.h): struct_size at least the first layout's.
+Maybe<void> CheckDesc(const ofx_tensor_desc* d, const char* name) {
+  CHECK_OR_RETURN(d == nullptr || d->struct_size >= OFX_TENSOR_DESC_MIN_SIZE)
+      << Error::RuntimeError() << name << ": ofx_tensor_desc.struct_size = "
+      << (d ? d->struct_size : 0) << " is below the first versioned layout ("
+      << OFX_TENSOR_DESC_MIN_SIZE << " bytes): initialise it with OFX_TENSOR_DESC_INIT";
+  return Maybe<void>::Ok();
+}
+
 Maybe<void> CheckArgs(const ofx_tensor_desc* row_ptr, const ofx_tensor_desc* col_idx,
                       const ofx_tensor_desc* values, const ofx_tensor_desc* b) {
   CHECK_OR_RETURN(row_ptr && col_idx && values && b)
       << Error::RuntimeError() << "spmm_csr: NULL tensor argument";
+  JUST(CheckDesc(row_ptr, "a_csr_row_ptr"));
+  JUST(CheckDesc(col_idx, "a_csr_col_idx"));
+  JUST(CheckDesc(values, "a_csr_values"));
+  JUST(CheckDesc(b, "b"));
   CHECK_OR_RETURN(row_ptr->ndim >= 1 && row_ptr->ndim <= 2 && col_idx->ndim >= 1 &&
                   col_idx->ndim <= 2 && values->ndim >= 1 && values->ndim <= 2 && b->ndim >= 1 &&
                   b->ndim <= 2)
@@ -175,6 +188,8 @@ int RunSpmmCsr(void* stream, const ofx_tensor_desc* row_ptr, const ofx_tensor_de
     return OFX_OK;
   }
   OFX_REQUIRE(out, OFX_EINVAL, "spmm_csr: out is NULL");
+  rc = ToStatus(CheckDesc(out, "out"));
+  if (rc) return rc;
   const int64_t phys_rows = od.shape().At(0);
   OFX_REQUIRE(out->ndim == 2 && out->shape[0] == phys_rows && out->shape[1] == od.shape().At(1) &&
                   out->dtype == (int32_t)od.data_type() && out->device == b->device,
@@ -228,17 +243,21 @@ extern "C" int ofx_functional_spmm_csr_infer(const ofx_tensor_desc* row_ptr,
                                              const ofx_tensor_desc* values, int64_t a_num_rows,
                                              int64_t a_num_cols, const ofx_tensor_desc* b,
                                              ofx_tensor_desc* out) {
-  user_op::TensorDesc lod, od;
-  int rc = ToStatus(Infer(row_ptr, col_idx, values, a_num_rows, a_num_cols, b, -1, Placement(),
-                          &lod, &od));
-  if (rc) return rc;
-  if (out) {
-    out->dtype = od.data_type();
-    out->ndim = (int32_t)od.shape().NumAxes();
-    for (int i = 0; i < out->ndim; ++i) out->shape[i] = od.shape().At(i);
-    out->device = b->device;
-  }
-  return OFX_OK;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    user_op::TensorDesc lod, od;
+    int rc = ToStatus(Infer(row_ptr, col_idx, values, a_num_rows, a_num_cols, b, -1, Placement(),
+                            &lod, &od));
+    if (rc) return rc;
+    rc = ToStatus(CheckDesc(out, "out"));
+    if (rc) return rc;
+    if (out) {
+      out->dtype = od.data_type();
+      out->ndim = (int32_t)od.shape().NumAxes();
+      for (int i = 0; i < out->ndim; ++i) out->shape[i] = od.shape().At(i);
+      out->device = b->device;
+    }
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_functional_spmm_csr_tmp_size(const ofx_tensor_desc* row_ptr,
@@ -246,9 +265,11 @@ extern "C" int ofx_functional_spmm_csr_tmp_size(const ofx_tensor_desc* row_ptr,
                                                 const ofx_tensor_desc* values, int64_t a_num_rows,
                                                 int64_t a_num_cols, const ofx_tensor_desc* b,
                                                 size_t* bytes) {
-  OFX_REQUIRE(bytes, OFX_EINVAL, "spmm_csr_tmp_size: bytes is NULL");
-  return RunSpmmCsr(nullptr, row_ptr, col_idx, values, a_num_rows, a_num_cols, b, -1, nullptr,
-                    nullptr, 0, Placement(), 0, bytes);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(bytes, OFX_EINVAL, "spmm_csr_tmp_size: bytes is NULL");
+    return RunSpmmCsr(nullptr, row_ptr, col_idx, values, a_num_rows, a_num_cols, b, -1, nullptr,
+                      nullptr, 0, Placement(), 0, bytes);
+  });
 }
 
 extern "C" int ofx_functional_spmm_csr_global(
@@ -257,11 +278,13 @@ extern "C" int ofx_functional_spmm_csr_global(
     const ofx_tensor_desc* b, int64_t b_logical_cols, ofx_tensor_desc* out, void* tmp,
     size_t tmp_bytes, int hierarchy_ndim, const int64_t* hierarchy, const int32_t* out_split_axes,
     int64_t parallel_id, int num_threads, size_t* tmp_size_out) {
-  Placement pl;
-  int rc = ToStatus(MakePlacement(hierarchy_ndim, hierarchy, out_split_axes, parallel_id, &pl));
-  if (rc) return rc;
-  return RunSpmmCsr(stream, row_ptr, col_idx, values, a_num_rows, a_num_cols, b, b_logical_cols,
-                    out, tmp, tmp_bytes, pl, num_threads, tmp_size_out);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    Placement pl;
+    int rc = ToStatus(MakePlacement(hierarchy_ndim, hierarchy, out_split_axes, parallel_id, &pl));
+    if (rc) return rc;
+    return RunSpmmCsr(stream, row_ptr, col_idx, values, a_num_rows, a_num_cols, b, b_logical_cols,
+                      out, tmp, tmp_bytes, pl, num_threads, tmp_size_out);
+  });
 }
 
 extern "C" int ofx_functional_spmm_csr_ex(void* stream, const ofx_tensor_desc* row_ptr,
@@ -271,14 +294,16 @@ extern "C" int ofx_functional_spmm_csr_ex(void* stream, const ofx_tensor_desc* r
                                           ofx_tensor_desc* out, void* tmp, size_t tmp_bytes,
                                           int64_t parallel_id, int64_t parallel_num,
                                           int out_split_axis, int num_threads) {
-  OFX_REQUIRE(out_split_axis != 1 || parallel_num == 1, OFX_EINVAL,
-              "spmm_csr_ex: a column split needs the logical width: use "
-              "ofx_functional_spmm_csr_global");
-  const int64_t h = parallel_num;
-  const int32_t ax = out_split_axis;
-  return ofx_functional_spmm_csr_global(stream, row_ptr, col_idx, values, a_num_rows, a_num_cols,
-                                        b, -1, out, tmp, tmp_bytes, 1, &h, &ax, parallel_id,
-                                        num_threads, nullptr);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(out_split_axis != 1 || parallel_num == 1, OFX_EINVAL,
+                "spmm_csr_ex: a column split needs the logical width: use "
+                "ofx_functional_spmm_csr_global");
+    const int64_t h = parallel_num;
+    const int32_t ax = out_split_axis;
+    return ofx_functional_spmm_csr_global(stream, row_ptr, col_idx, values, a_num_rows, a_num_cols,
+                                          b, -1, out, tmp, tmp_bytes, 1, &h, &ax, parallel_id,
+                                          num_threads, nullptr);
+  });
 }
 
 extern "C" int ofx_functional_spmm_csr(void* stream, const ofx_tensor_desc* row_ptr,
@@ -286,57 +311,63 @@ extern "C" int ofx_functional_spmm_csr(void* stream, const ofx_tensor_desc* row_
                                        const ofx_tensor_desc* values, int64_t a_num_rows,
                                        int64_t a_num_cols, const ofx_tensor_desc* b,
                                        ofx_tensor_desc* out, void* tmp, size_t tmp_bytes) {
-  return RunSpmmCsr(stream, row_ptr, col_idx, values, a_num_rows, a_num_cols, b, -1, out, tmp,
-                    tmp_bytes, Placement(), 0, nullptr);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    return RunSpmmCsr(stream, row_ptr, col_idx, values, a_num_rows, a_num_cols, b, -1, out, tmp,
+                      tmp_bytes, Placement(), 0, nullptr);
+  });
 }
 
 // SBP signatures of a registered op, for the tests: "arg:sbp,arg:sbp;...|no_grad:..." into buf.
 // `optional_inputs`: comma-separated optional inputs the op instance has (e.g. "bias").
 extern "C" int ofx_op_sbp_signatures(const char* op_name, const char* optional_inputs, char* buf,
                                      size_t len) {
-  OFX_REQUIRE(op_name && buf && len > 0, OFX_EINVAL, "op_sbp_signatures: NULL argument");
-  const user_op::OpRegistryResult* op = user_op::UserOpRegistryMgr::Get().GetOpRegistryResult(op_name);
-  OFX_REQUIRE(op, OFX_EINVAL, "op %s is not registered", op_name);
-  std::vector<std::string> present;
-  if (optional_inputs) {
-    std::string all(optional_inputs), cur;
-    for (char ch : all + ",") {
-      if (ch == ',') {
-        if (!cur.empty()) present.push_back(cur);
-        cur.clear();
-      } else {
-        cur += ch;
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(op_name && buf && len > 0, OFX_EINVAL, "op_sbp_signatures: NULL argument");
+    const user_op::OpRegistryResult* op = user_op::UserOpRegistryMgr::Get().GetOpRegistryResult(op_name);
+    OFX_REQUIRE(op, OFX_EINVAL, "op %s is not registered", op_name);
+    std::vector<std::string> present;
+    if (optional_inputs) {
+      std::string all(optional_inputs), cur;
+      for (char ch : all + ",") {
+        if (ch == ',') {
+          if (!cur.empty()) present.push_back(cur);
+          cur.clear();
+        } else {
+          cur += ch;
+        }
       }
     }
-  }
-  user_op::SbpContext ctx{user_op::UserOpConfView(present)};
-  int rc = ToStatus(op->get_sbp(&ctx));
-  if (rc) return rc;
-  std::string s;
-  for (const auto& sig : ctx.signatures()) {
-    if (!s.empty()) s += ";";
-    for (size_t i = 0; i < sig.size(); ++i) s += (i ? "," : "") + sig[i].first + ":" + sig[i].second;
-  }
-  // input-arg modifiers: which inputs have requires_grad disabled
-  std::map<std::string, user_op::InputArgModifier> mods;
-  user_op::GetInputArgModifier get = [&](const std::string& n, int32_t) { return &mods[n]; };
-  if (op->input_modify) {
-    rc = ToStatus(op->input_modify(get, user_op::UserOpConfWrapper()));
+    user_op::SbpContext ctx{user_op::UserOpConfView(present)};
+    int rc = ToStatus(op->get_sbp(&ctx));
     if (rc) return rc;
-  }
-  s += "|no_grad:";
-  bool first = true;
-  for (const auto& kv : mods)
-    if (!kv.second.requires_grad) {
-      s += (first ? "" : ",") + kv.first;
-      first = false;
+    std::string s;
+    for (const auto& sig : ctx.signatures()) {
+      if (!s.empty()) s += ";";
+      for (size_t i = 0; i < sig.size(); ++i) s += (i ? "," : "") + sig[i].first + ":" + sig[i].second;
     }
-  snprintf(buf, len, "%s", s.c_str());
-  return OFX_OK;
+    // input-arg modifiers: which inputs have requires_grad disabled
+    std::map<std::string, user_op::InputArgModifier> mods;
+    user_op::GetInputArgModifier get = [&](const std::string& n, int32_t) { return &mods[n]; };
+    if (op->input_modify) {
+      rc = ToStatus(op->input_modify(get, user_op::UserOpConfWrapper()));
+      if (rc) return rc;
+    }
+    s += "|no_grad:";
+    bool first = true;
+    for (const auto& kv : mods)
+      if (!kv.second.requires_grad) {
+        s += (first ? "" : ",") + kv.first;
+        first = false;
+      }
+    snprintf(buf, len, "%s", s.c_str());
+    return OFX_OK;
+  });
 }
 
 extern "C" int ofx_op_spmm_csr_sbp_signatures(char* buf, size_t len) {
-  return ofx_op_sbp_signatures("spmm_csr", nullptr, buf, len);
+  return ::ofx::guarded(__func__, [&]() -> int {
+    return ofx_op_sbp_signatures("spmm_csr", nullptr, buf, len);
+  });
 }
 
 // ---- gradient functors: functional::SddmmCsr / functional::CsrTranspose ----------------------
@@ -361,6 +392,7 @@ Maybe<void> RunUserOp(const std::string& op_name, const std::vector<Arg>& ins,
   DescMap in;
   for (const Arg& a : ins) {
     CHECK_OR_RETURN(a.d != nullptr) << Error::RuntimeError() << op_name << ": NULL input " << a.name;
+    JUST(CheckDesc(a.d, a.name));
     CHECK_OR_RETURN(a.d->ndim >= 1 && a.d->ndim <= 2)
         << Error::RuntimeError() << op_name << ": " << a.name << " must be 1-D or 2-D";
     CHECK_EQ_OR_RETURN(a.d->device, device)
@@ -394,6 +426,7 @@ Maybe<void> RunUserOp(const std::string& op_name, const std::vector<Arg>& ins,
   for (const Arg& a : ins) add(a);
   for (const Arg& o : outs) {
     CHECK_OR_RETURN(o.d != nullptr) << Error::RuntimeError() << op_name << ": NULL output " << o.name;
+    JUST(CheckDesc(o.d, o.name));
     const user_op::TensorDesc& want = ictx.OutputTensorDesc(o.name, 0);
     CHECK_OR_RETURN(ShapeOf(o.d) == want.shape() && (DataType)o.d->dtype == want.data_type() &&
                     o.d->device == device)
@@ -425,10 +458,12 @@ extern "C" int ofx_functional_sddmm_csr(void* stream, const ofx_tensor_desc* row
                                         const ofx_tensor_desc* b, int64_t a_num_rows,
                                         int64_t a_num_cols, ofx_tensor_desc* out, void* tmp,
                                         size_t tmp_bytes, size_t* tmp_size_out) {
-  return ToStatus(RunUserOp("sddmm_csr",
-                            {{"a_csr_row_ptr", row_ptr}, {"a_csr_col_idx", col_idx}, {"a", a}, {"b", b}},
-                            {{"out", out}}, {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols}},
-                            stream, tmp, tmp_bytes, tmp_size_out));
+  return ::ofx::guarded(__func__, [&]() -> int {
+    return ToStatus(RunUserOp("sddmm_csr",
+                              {{"a_csr_row_ptr", row_ptr}, {"a_csr_col_idx", col_idx}, {"a", a}, {"b", b}},
+                              {{"out", out}}, {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols}},
+                              stream, tmp, tmp_bytes, tmp_size_out));
+  });
 }
 
 extern "C" int ofx_functional_csr_transpose(void* stream, const ofx_tensor_desc* row_ptr,
@@ -436,10 +471,12 @@ extern "C" int ofx_functional_csr_transpose(void* stream, const ofx_tensor_desc*
                                             int64_t a_num_cols, ofx_tensor_desc* out_row_ptr,
                                             ofx_tensor_desc* out_col_idx, ofx_tensor_desc* out_perm,
                                             void* tmp, size_t tmp_bytes, size_t* tmp_size_out) {
-  return ToStatus(RunUserOp("csr_transpose", {{"a_csr_row_ptr", row_ptr}, {"a_csr_col_idx", col_idx}},
-                            {{"out_row_ptr", out_row_ptr}, {"out_col_idx", out_col_idx}, {"out_perm", out_perm}},
-                            {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols}}, stream, tmp,
-                            tmp_bytes, tmp_size_out));
+  return ::ofx::guarded(__func__, [&]() -> int {
+    return ToStatus(RunUserOp("csr_transpose", {{"a_csr_row_ptr", row_ptr}, {"a_csr_col_idx", col_idx}},
+                              {{"out_row_ptr", out_row_ptr}, {"out_col_idx", out_col_idx}, {"out_perm", out_perm}},
+                              {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols}}, stream, tmp,
+                              tmp_bytes, tmp_size_out));
+  });
 }
 
 // functional::SpmmCsrGathered: the d(b) gradient of spmm_csr with learnable values, A^T's
@@ -452,11 +489,13 @@ extern "C" int ofx_functional_spmm_csr_gathered(void* stream, const ofx_tensor_d
                                                 int64_t a_num_cols, ofx_tensor_desc* out,
                                                 void* tmp, size_t tmp_bytes,
                                                 size_t* tmp_size_out) {
-  return ToStatus(RunUserOp("spmm_csr_gathered",
-                            {{"a_csr_row_ptr", row_ptr}, {"a_csr_col_idx", col_idx},
-                             {"a_csr_values", values}, {"values_perm", values_perm}, {"b", b}},
-                            {{"out", out}}, {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols}},
-                            stream, tmp, tmp_bytes, tmp_size_out));
+  return ::ofx::guarded(__func__, [&]() -> int {
+    return ToStatus(RunUserOp("spmm_csr_gathered",
+                              {{"a_csr_row_ptr", row_ptr}, {"a_csr_col_idx", col_idx},
+                               {"a_csr_values", values}, {"values_perm", values_perm}, {"b", b}},
+                              {{"out", out}}, {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols}},
+                              stream, tmp, tmp_bytes, tmp_size_out));
+  });
 }
 
 // functional::FusedSpmmCsr: relu?(A @ b + bias?) through op
@@ -468,11 +507,13 @@ extern "C" int ofx_functional_fused_spmm_csr(void* stream, const ofx_tensor_desc
                                              int64_t a_num_rows, int64_t a_num_cols, int relu,
                                              ofx_tensor_desc* out, void* tmp, size_t tmp_bytes,
                                              size_t* tmp_size_out) {
-  std::vector<Arg> ins = {{"a_csr_row_ptr", row_ptr}, {"a_csr_col_idx", col_idx},
-                          {"a_csr_values", values}, {"b", b}};
-  if (bias != nullptr) ins.push_back({"bias", bias});
-  return ToStatus(RunUserOp("fused_spmm_csr", ins, {{"out", out}},
-                            {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols},
-                             {"relu", relu ? 1 : 0}},
-                            stream, tmp, tmp_bytes, tmp_size_out));
+  return ::ofx::guarded(__func__, [&]() -> int {
+    std::vector<Arg> ins = {{"a_csr_row_ptr", row_ptr}, {"a_csr_col_idx", col_idx},
+                            {"a_csr_values", values}, {"b", b}};
+    if (bias != nullptr) ins.push_back({"bias", bias});
+    return ToStatus(RunUserOp("fused_spmm_csr", ins, {{"out", out}},
+                              {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols},
+                               {"relu", relu ? 1 : 0}},
+                              stream, tmp, tmp_bytes, tmp_size_out));
+  });
 }

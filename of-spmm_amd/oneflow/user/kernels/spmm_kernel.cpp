@@ -54,7 +54,7 @@ std::shared_ptr<user_op::OpKernelCache> CreateSpmmCsrOpKernelCache(user_op::Kern
 // Options of a launch: the contract's schedule for the logical width (no cache: local op, the
 // physical width is the logical one).
 ofx_spmm_options OptionsOf(const SpmmCsrOpKernelCache* cache) {
-  ofx_spmm_options o{};
+  ofx_spmm_options o = OFX_SPMM_OPTIONS_INIT;
   if (cache != nullptr) o.split_threshold = ofx_spmm_default_split(cache->logical_n());
   return o;
 }
@@ -66,6 +66,7 @@ int DtCode(DataType dt) { return static_cast<int>(dt); }
 template <DeviceType device_type>
 void ComputeSpmmCsr(user_op::KernelComputeContext* ctx, const user_op::OpKernelCache* cache,
                     const user_op::Tensor* bias, bool relu, const char* op_name) {
+  TestHookCompute(op_name);
   const user_op::Tensor* row_ptr = ctx->Tensor4ArgNameAndIndex("a_csr_row_ptr", 0);
   const user_op::Tensor* col_idx = ctx->Tensor4ArgNameAndIndex("a_csr_col_idx", 0);
   const user_op::Tensor* values = ctx->Tensor4ArgNameAndIndex("a_csr_values", 0);
@@ -240,7 +241,7 @@ size_t InferSpmmCsrTmpSize(user_op::InferSizeContext* ctx) {
   const user_op::TensorDesc& col_idx = ctx->InputTensorDesc("a_csr_col_idx", 0);
   const user_op::TensorDesc& b = ctx->InputTensorDesc("b", 0);
   const user_op::TensorDesc* out_logical = ctx->LogicalTensorDesc4ArgNameAndIndex("out", 0);
-  ofx_spmm_options o{};
+  ofx_spmm_options o = OFX_SPMM_OPTIONS_INIT;
   if (out_logical != nullptr) o.split_threshold = ofx_spmm_default_split(out_logical->shape().At(1));
   size_t bytes = 0;
   const int rc = ofx_spmm_csr_workspace_size(

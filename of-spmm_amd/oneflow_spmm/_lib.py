@@ -15,7 +15,10 @@ LIB_PATH = os.environ.get("OFX_SPMM_LIB") or os.path.join(_HERE, "libofx_spmm.so
 # OneFlow DataType codes (oneflow/core/common/data_type.proto:4-26)
 DT_FLOAT, DT_DOUBLE, DT_INT32, DT_INT64, DT_FLOAT16, DT_BFLOAT16 = 2, 3, 5, 6, 9, 11
 
-OFX_OK, OFX_EINVAL, OFX_EDEVICE, OFX_ENOMEM, OFX_EUNSUPPORTED, OFX_ECOMM, OFX_EWORKSPACE = range(7)
+(OFX_OK, OFX_EINVAL, OFX_EDEVICE, OFX_ENOMEM, OFX_EUNSUPPORTED, OFX_ECOMM, OFX_EWORKSPACE, OFX_EPLAN,
+ OFX_EINTERNAL) = range(9)
+# test knobs of ofx_debug_set (include/ofx_spmm.h)
+DEBUG_PLAN_SPIN_LIMIT, DEBUG_THROW_IN_COMPUTE = 1, 2
 MEMCPY_H2D, MEMCPY_D2H, MEMCPY_D2D, MEMCPY_DEFAULT = 1, 2, 3, 4
 UNIQUE_ID_BYTES = 128
 
@@ -28,15 +31,27 @@ class OfxError(RuntimeError):
         self.code = code
 
 
-class Options(ctypes.Structure):
-    _fields_ = [("split_threshold", ctypes.c_int64), ("chunk", ctypes.c_int64),
+class _Versioned(ctypes.Structure):
+    """A versioned C-ABI struct: struct_size (its first field) is set to this layout's size, as
+    the OFX_*_INIT initialisers of include/ofx_spmm.h do."""
+
+    def __init__(self, *args, **kw):
+        super().__init__(ctypes.sizeof(type(self)), *args, **kw)
+
+
+class Options(_Versioned):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("reserved0", ctypes.c_int32),
+                ("split_threshold", ctypes.c_int64), ("chunk", ctypes.c_int64),
                 ("ordered", ctypes.c_int32), ("variant", ctypes.c_int32),
                 ("heavy_threshold", ctypes.c_int64), ("planned", ctypes.c_int32),
                 ("reserved", ctypes.c_int32), ("range_nnz", ctypes.c_int64)]
 
+    def __init__(self, *args, **kw):  # positional fields start after struct_size / reserved0
+        super().__init__(0, *args, **kw)
 
-class Placement(ctypes.Structure):
-    _fields_ = [("device_type", ctypes.c_int32), ("reserved", ctypes.c_int32),
+
+class Placement(_Versioned):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("device_type", ctypes.c_int32),
                 ("parallel_num", ctypes.c_int64), ("parallel_id", ctypes.c_int64),
                 ("machine_ids", ctypes.POINTER(ctypes.c_int64)),
                 ("device_ids", ctypes.POINTER(ctypes.c_int64))]
@@ -52,10 +67,11 @@ SENDRECV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, c
 DEV_CPU, DEV_HIP = 1, 4
 
 
-class TensorDesc(ctypes.Structure):
-    _fields_ = [("dtype", ctypes.c_int32), ("device", ctypes.c_int32), ("ndim", ctypes.c_int32),
-                ("reserved", ctypes.c_int32), ("shape", ctypes.c_int64 * 2),
-                ("stride", ctypes.c_int64 * 2), ("data", ctypes.c_void_p)]
+class TensorDesc(_Versioned):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("dtype", ctypes.c_int32),
+                ("device", ctypes.c_int32), ("ndim", ctypes.c_int32),
+                ("shape", ctypes.c_int64 * 2), ("stride", ctypes.c_int64 * 2),
+                ("data", ctypes.c_void_p)]
 
 
 def _load():
@@ -71,6 +87,8 @@ def _load():
     ppl = ctypes.POINTER(Placement)
     sigs = {
         "ofx_last_error": ([], ctypes.c_char_p),
+        "ofx_device_error_check": ([], i32),
+        "ofx_debug_set": ([i32, i64], i32),
         "ofx_version": ([], ctypes.c_char_p),
         "ofx_spmm_default_split": ([i64], i64),
         "ofx_spmm_csr_workspace_size": ([i32, i32, i64, i64, i64, i64, popt, ctypes.POINTER(sz)], i32),

@@ -12,6 +12,17 @@ for p in (ROOT, os.path.join(ROOT, "of-spmm_amd")):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
     config.addinivalue_line("markers", "slow: full BASELINE-size problems")
+    # GPU calls (scripts/gpu_run.sh): a fatal signal's thread dump also goes to a file that
+    # survives pytest's output capture (the r03ai abort's messages were lost)
+    path = os.environ.get("OFX_FAULTHANDLER_FILE")
+    if path:
+        import faulthandler
+        global _FAULT_FILE
+        _FAULT_FILE = open(path, "a")
+        faulthandler.enable(file=_FAULT_FILE, all_threads=True)
+
+
+_FAULT_FILE = None
 
 
 def gpu_available() -> bool:

@@ -100,7 +100,7 @@ void check_spmm_f64(int idx_dt, int64_t m, int64_t k, int64_t n, int64_t max_deg
   for (auto& x : val) x = next_f32();
   for (auto& x : b) x = next_f32();
   const int64_t ldb = n + 3, ldc = n + 1;
-  ofx_spmm_options o{};
+  ofx_spmm_options o = OFX_SPMM_OPTIONS_INIT;
   o.split_threshold = 16;
   o.chunk = 8;
   const int64_t r0 = m > 2 ? 1 : 0, r1 = m;

@@ -1,0 +1,140 @@
+"""The C-ABI boundary's guarantees (CPU):
+
+- no C++ exception crosses `extern "C"`: a kernel Compute that throws something other than the
+  op's KernelCheckError returns OFX_EINTERNAL / OFX_ENOMEM with what() in ofx_last_error()
+  instead of std::terminate -> abort (the r03ai SIGABRT candidate);
+- versioned structs: a caller's ofx_spmm_options / ofx_tensor_desc / ofx_placement is read up to
+  its struct_size, older (smaller) layouts keep working with defaults for the newer fields, and an
+  unset or pre-versioning layout is refused rather than misread;
+- the workspace query over the matrix's m bounds the workspace of every row range of it.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import oneflow_spmm as fs
+from oneflow_spmm import _lib, ops
+from oneflow_spmm._lib import LIB
+from tests.helpers import oracle_spmm, random_csr, random_dense, assert_bitwise
+
+
+def small_problem(seed=0, m=40, k=30, n=8):
+    rng = np.random.default_rng(seed)
+    deg = rng.integers(0, 9, size=m)
+    rp, ci, v = random_csr(m, k, deg, rng)
+    return rp, ci, v, random_dense(k, n, rng), m, k
+
+
+@pytest.fixture
+def throw_knob():
+    yield
+    assert LIB.ofx_debug_set(_lib.DEBUG_THROW_IN_COMPUTE, -1) == _lib.OFX_OK
+
+
+@pytest.mark.parametrize("kind,code,text", [
+    (1, _lib.OFX_EINTERNAL, "injected by OFX_DEBUG_THROW_IN_COMPUTE"),
+    (2, _lib.OFX_ENOMEM, "out of host memory"),
+    (3, _lib.OFX_EINTERNAL, "non-standard C++ exception"),
+])
+def test_exception_in_compute_becomes_a_status(throw_knob, kind, code, text):
+    rp, ci, v, b, m, k = small_problem()
+    ref = oracle_spmm(rp, ci, v, b)
+    assert LIB.ofx_debug_set(_lib.DEBUG_THROW_IN_COMPUTE, kind) == _lib.OFX_OK
+    for call in (lambda: fs.spmm(rp, ci, v, m, k, b),
+                 lambda: fs._C.fused_spmm_csr(rp, ci, v, m, k, b, relu=True)):
+        with pytest.raises(_lib.OfxError) as ei:
+            call()
+        assert ei.value.code == code, str(ei.value)
+        assert text in str(ei.value) and "ofx_functional_" in str(ei.value)
+    # the process survived and the next call is ordinary
+    assert LIB.ofx_debug_set(_lib.DEBUG_THROW_IN_COMPUTE, -1) == _lib.OFX_OK
+    assert_bitwise(fs.spmm(rp, ci, v, m, k, b), ref, "after the injected exceptions")
+
+
+def test_debug_set_rejects_unknown_knobs():
+    assert LIB.ofx_debug_set(0, 1) == _lib.OFX_EINVAL
+    assert LIB.ofx_debug_set(99, 1) == _lib.OFX_EINVAL
+
+
+def test_device_error_check_without_launches_is_ok():
+    assert LIB.ofx_device_error_check() == _lib.OFX_OK
+
+
+# ---- versioned structs -------------------------------------------------------------------------
+def test_options_struct_size_is_checked():
+    rp, ci, v, b, m, k = small_problem(1)
+    ref = oracle_spmm(rp, ci, v, b)
+    o = ops.make_options()
+    assert o.struct_size == ctypes.sizeof(_lib.Options) == 56
+    assert_bitwise(ops.spmm_csr_cpu(rp, ci, v, b, m, k, options=o), ref, "current layout")
+    o.struct_size = 0  # not initialised (or a caller from before the versioned layout)
+    with pytest.raises(_lib.OfxError) as ei:
+        ops.spmm_csr_cpu(rp, ci, v, b, m, k, options=o)
+    assert ei.value.code == _lib.OFX_EINVAL and "OFX_SPMM_OPTIONS_INIT" in str(ei.value)
+    o.struct_size = 47
+    with pytest.raises(_lib.OfxError):
+        ops.spmm_csr_cpu(rp, ci, v, b, m, k, options=o)
+
+
+def test_options_older_layout_takes_defaults_for_newer_fields():
+    """A caller compiled against the first versioned layout (48 bytes, no range_nnz) passes a
+    48-byte struct: range_nnz is never read (it is outside the caller's memory) and defaults to
+    0.  The form of a row-range launch shows it: range_nnz = 50 picks the small form, the
+    estimate from nnz does not."""
+    m, k, n, nnz = 1_000_000, 1_000_000, 64, 20_000_000
+    rows = dict(row_begin=0, row_end=20_000)
+    base = ops.describe(m, k, n, nnz, torch.float32, **rows)
+    new = ops.make_options(range_nnz=50)
+    assert ops.describe(m, k, n, nnz, torch.float32, options=new, **rows)["form"] == "small"
+    assert base["form"] != "small"
+    # the same bytes, declared 48 long, and the 8 bytes past them poisoned in a bigger buffer
+    buf = (ctypes.c_uint8 * 64)(*([0xAB] * 64))
+    ctypes.memmove(buf, ctypes.addressof(new), 48)
+    old = _lib.Options.from_buffer(buf)
+    old.struct_size = 48
+    got = ops.describe(m, k, n, nnz, torch.float32, options=old, **rows)
+    assert got == base, (got, base)
+    # a newer caller's larger struct: the known fields are read, the rest ignored
+    buf2 = (ctypes.c_uint8 * 80)()
+    ctypes.memmove(buf2, ctypes.addressof(new), ctypes.sizeof(new))
+    newer = _lib.Options.from_buffer(buf2)
+    newer.struct_size = 80
+    assert ops.describe(m, k, n, nnz, torch.float32, options=newer, **rows)["form"] == "small"
+
+
+def test_tensor_desc_and_placement_struct_size_are_checked():
+    rp, ci, v, b, m, k = small_problem(2)
+    d = [fs._C.desc(t) for t in (rp, ci, v, b)]
+    out = _lib.TensorDesc()
+    rc = LIB.ofx_functional_spmm_csr_infer(ctypes.byref(d[0]), ctypes.byref(d[1]), ctypes.byref(d[2]),
+                                           m, k, ctypes.byref(d[3]), ctypes.byref(out))
+    assert rc == _lib.OFX_OK and out.shape[0] == m
+    d[1].struct_size = 0
+    rc = LIB.ofx_functional_spmm_csr_infer(ctypes.byref(d[0]), ctypes.byref(d[1]), ctypes.byref(d[2]),
+                                           m, k, ctypes.byref(d[3]), ctypes.byref(out))
+    assert rc == _lib.OFX_EINVAL and "OFX_TENSOR_DESC_INIT" in _lib.last_error()
+    pl = _lib.Placement()
+    pl.device_type, pl.parallel_num, pl.parallel_id = _lib.DEV_CPU, 2, 0
+    shape = (ctypes.c_int64 * 2)(10, 4)
+    assert LIB.ofx_boxing_check_ccl_s2b(ctypes.byref(pl), 2, shape, b"S(0)", b"B") == _lib.OFX_OK
+    pl.struct_size = 8
+    assert LIB.ofx_boxing_check_ccl_s2b(ctypes.byref(pl), 2, shape, b"S(0)", b"B") == _lib.OFX_EINVAL
+    assert "OFX_PLACEMENT_INIT" in _lib.last_error()
+
+
+# ---- workspace bound over row ranges --------------------------------------------
+@pytest.mark.parametrize("m", [(1 << 18) + 1, (1 << 18) + 700, 3 << 18, 1 << 20])
+def test_workspace_query_bounds_every_row_range(m):
+    """The planner's rows per thread switch from 16 to 4 below 2^18 rows, so a launch over fewer
+    rows lays out more look-back blocks; the look region is sized for the most blocks, so the
+    query over the matrix's m (what OneFlow's tmp-size function asks) bounds every row range."""
+    k, n, nnz = m, 64, 16 * m
+    whole = ops.workspace_size(torch.int32, torch.float32, m, k, n, nnz)
+    assert whole > 0
+    for lo, hi in [(1, m), (0, 1 << 18), (5, (1 << 18) + 3), (m // 3, m), (0, m - 1), (m - 40000, m)]:
+        if hi <= lo or hi > m:
+            continue
+        d = ops.describe(m, k, n, nnz, torch.float32, row_begin=lo, row_end=hi)
+        assert d["ws"] <= whole, (m, lo, hi, d["ws"], whole)

@@ -1,0 +1,213 @@
+"""GPU: the work-list planner fails loudly and never hands out a stale plan (VERDICT r4 item 2,
+ADVICE r4 high + mediums).
+
+- A look-back that gives up (test knob OFX_DEBUG_PLAN_SPIN_LIMIT: 0 = every block but the first
+  gives up at once, 1 = one poll) makes every consumer of the work list write nothing, and the
+  host reports OFX_EPLAN at the next entry / ofx_device_error_check.  The output buffer keeps its
+  sentinel bits: no result from a partial or earlier plan ever appears.
+- options.planned over a workspace that holds no valid plan is refused the same way.
+- A launch captured in a hipGraph re-plans on every replay under a fresh tag (the device epoch
+  word): rewriting row_ptr / col_idx in place between replays gives the new graph's bits.
+- The workspace query over the matrix's m bounds a row range whose planner lays out more blocks.
+The reference fails loudly on kernel errors (oneflow/user/kernels/matrix_vector_product_kernel.cpp:
+98-105); these are the C-ABI's status-code form of that."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import oneflow_spmm as fs
+from oneflow_spmm import _lib, ops
+from oneflow_spmm._lib import LIB
+from tests.helpers import assert_bitwise, oracle_spmm, power_law_degrees, random_csr, random_dense
+
+pytestmark = pytest.mark.gpu
+
+SENTINEL = 0x7FC0DEAD  # a NaN payload no kernel writes
+
+
+@pytest.fixture(autouse=True)
+def _reset_knobs():
+    LIB.ofx_device_error_check()
+    yield
+    LIB.ofx_debug_set(_lib.DEBUG_PLAN_SPIN_LIMIT, -1)
+    torch.cuda.synchronize()
+    LIB.ofx_device_error_check()
+
+
+def sentinel_out(rows, n, device):
+    return torch.full((rows, n), SENTINEL, dtype=torch.int32, device=device).view(torch.float32)
+
+
+def untouched(out):
+    return bool((out.view(torch.int32) == SENTINEL).all().item())
+
+
+def hub_graph(m, k, rng, hubs=((11, 4000), (777, 600))):
+    deg = rng.integers(0, 30, size=m)
+    for r, d in hubs:
+        deg[r] = d
+    return deg
+
+
+@pytest.mark.parametrize("variant", [0, 30001, 30003, 30004])
+def test_forced_look_back_failure_writes_nothing_and_is_reported(device, variant):
+    """Knob 0: the plan of a 60k-row launch (59 planner blocks) fails in every block but the
+    first; whichever form consumes it (prefetching / mid / bandwidth + reduce / wave items)
+    writes nothing and the error surfaces once."""
+    rng = np.random.default_rng(500 + variant)
+    m, k, n = 60_000, 60_000, 64
+    rp, ci, v = random_csr(m, k, hub_graph(m, k, rng), rng)
+    b = random_dense(k, n, rng)
+    d = [t.to(device) for t in (rp, ci, v, b)]
+    opts = ops.make_options(variant=variant) if variant else None
+    kern = ops.SpmmCsrKernel(m, k, n, ci.numel(), torch.int32, torch.float32, device, opts)
+    out = sentinel_out(m, n, device)
+    assert LIB.ofx_debug_set(_lib.DEBUG_PLAN_SPIN_LIMIT, 0) == _lib.OFX_OK
+    kern(*d, out)  # asynchronous: accepted
+    torch.cuda.synchronize()
+    assert untouched(out), "a failed plan's launch wrote output"
+    assert LIB.ofx_device_error_check() == _lib.OFX_EPLAN
+    assert "gave up" in _lib.last_error()
+    assert LIB.ofx_device_error_check() == _lib.OFX_OK  # reported once
+    # reported at the next launching call too (and that call launches nothing)
+    kern(*d, out)
+    torch.cuda.synchronize()
+    LIB.ofx_debug_set(_lib.DEBUG_PLAN_SPIN_LIMIT, -1)
+    with pytest.raises(_lib.OfxError) as ei:
+        kern(*d, out)
+    assert ei.value.code == _lib.OFX_EPLAN
+    torch.cuda.synchronize()
+    assert untouched(out)
+    kern(*d, out)  # the default limit: an ordinary launch
+    torch.cuda.synchronize()
+    assert LIB.ofx_device_error_check() == _lib.OFX_OK
+    assert_bitwise(out, oracle_spmm(rp, ci, v, b), f"variant {variant} after recovery")
+
+
+def test_failed_plan_never_returns_a_stale_plan(device):
+    """A workspace holding a valid plan of graph A, then a failing plan of graph B (same shapes):
+    the launch over B must not run A's work list.  Before round 5 it did, silently."""
+    rng = np.random.default_rng(510)
+    m, k, n = 60_000, 60_000, 32
+    rp_a, ci_a, v_a = random_csr(m, k, hub_graph(m, k, rng), rng)
+    deg_b = rng.permutation(np.diff(rp_a.numpy()))  # the hubs move; the same nnz (workspace)
+    rp_b, ci_b, v_b = random_csr(m, k, deg_b, rng)
+    b = random_dense(k, n, rng).to(device)
+    kern = ops.SpmmCsrKernel(m, k, n, ci_a.numel(), torch.int32, torch.float32, device)
+    out = torch.empty((m, n), device=device)
+    kern(rp_a.to(device), ci_a.to(device), v_a.to(device), b, out)
+    torch.cuda.synchronize()
+    assert_bitwise(out, oracle_spmm(rp_a, ci_a, v_a, b.cpu()), "graph A")
+    out_b = sentinel_out(m, n, device)
+    LIB.ofx_debug_set(_lib.DEBUG_PLAN_SPIN_LIMIT, 0)
+    kern(rp_b.to(device), ci_b.to(device), v_b.to(device), b, out_b)
+    torch.cuda.synchronize()
+    assert untouched(out_b), "graph B's launch ran on a stale plan"
+    assert LIB.ofx_device_error_check() == _lib.OFX_EPLAN
+
+
+def test_one_poll_look_back_is_exact_or_loud(device):
+    """Knob 1 (a single poll per predecessor) on a 250k-row launch (245 planner blocks): each run
+    either completes bit-exact or writes nothing and reports; never a partial list."""
+    rng = np.random.default_rng(520)
+    m, k, n = 250_000, 250_000, 16
+    rp, ci, v = random_csr(m, k, power_law_degrees(m, 2_500_000, k, rng), rng)
+    b = random_dense(k, n, rng)
+    d = [t.to(device) for t in (rp, ci, v, b)]
+    ref = oracle_spmm(rp, ci, v, b)
+    kern = ops.SpmmCsrKernel(m, k, n, ci.numel(), torch.int32, torch.float32, device)
+    LIB.ofx_debug_set(_lib.DEBUG_PLAN_SPIN_LIMIT, 1)
+    outcomes = []
+    for _ in range(4):
+        out = sentinel_out(m, n, device)
+        kern(*d, out)
+        torch.cuda.synchronize()
+        rc = LIB.ofx_device_error_check()
+        if rc == _lib.OFX_EPLAN:
+            assert untouched(out)
+            outcomes.append("loud")
+        else:
+            assert rc == _lib.OFX_OK
+            assert_bitwise(out, ref, "one-poll plan that completed")
+            outcomes.append("exact")
+    print("one-poll outcomes:", outcomes)
+
+
+def test_planned_launch_over_an_unplanned_workspace_is_refused(device):
+    rng = np.random.default_rng(530)
+    m, k, n = 60_000, 60_000, 64
+    rp, ci, v = random_csr(m, k, hub_graph(m, k, rng), rng)
+    b = random_dense(k, n, rng)
+    d = [t.to(device) for t in (rp, ci, v, b)]
+    kern = ops.SpmmCsrKernel(m, k, n, ci.numel(), torch.int32, torch.float32, device)
+    for fill in (0, 0xA5):
+        kern.workspace.fill_(fill)  # never planned: zeros, then garbage
+        out = sentinel_out(m, n, device)
+        o = ops.make_options(planned=True)
+        _lib.check(LIB.ofx_spmm_csr(fs._C.current_stream_handle(d[3]), _lib.DT_INT32, _lib.DT_FLOAT,
+                                    m, k, n, ci.numel(), d[0].data_ptr(), d[1].data_ptr(),
+                                    d[2].data_ptr(), d[3].data_ptr(), n, out.data_ptr(), n, 0, m,
+                                    kern.workspace.data_ptr(), kern.ws_bytes, ctypes.byref(o)))
+        torch.cuda.synchronize()
+        assert untouched(out), f"planned launch over a workspace filled with {fill:#x} wrote output"
+        assert LIB.ofx_device_error_check() == _lib.OFX_EPLAN
+        assert "no valid work-list plan" in _lib.last_error()
+    # plan() then the planned launch: accepted and exact
+    kern.plan(d[0])
+    out = torch.empty((m, n), device=device)
+    kern(*d, out, planned=True)
+    torch.cuda.synchronize()
+    assert LIB.ofx_device_error_check() == _lib.OFX_OK
+    assert_bitwise(out, oracle_spmm(rp, ci, v, b), "planned after plan()")
+
+
+def test_graph_replay_replans_after_row_ptr_is_rewritten(device):
+    """a non-planned launch captured into a hipGraph carried one host epoch for
+    every replay, so a replay took the previous replay's status words.  Rewriting row_ptr /
+    col_idx / values in place (same addresses and nnz, different structure) between replays must
+    give the new structure's bits."""
+    rng = np.random.default_rng(540)
+    m, k, n = 20_000, 20_000, 64
+    deg_a = power_law_degrees(m, 400_000, k, rng)
+    deg_b = rng.permutation(deg_a)  # the hubs move; nnz is unchanged
+    graphs = [random_csr(m, k, dg, rng) for dg in (deg_a, deg_b, deg_a)]
+    b = random_dense(k, n, rng)
+    rp, ci, v = (t.clone().to(device) for t in graphs[0])
+    db = b.to(device)
+    out = torch.empty((m, n), device=device)
+    kern = ops.SpmmCsrKernel(m, k, n, ci.numel(), torch.int32, torch.float32, device)
+    s = torch.cuda.Stream(device)
+    s.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(s):
+        kern(rp, ci, v, db, out)  # warm (outside capture)
+    torch.cuda.current_stream(device).wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        kern(rp, ci, v, db, out)
+    for i, (grp, gci, gv) in enumerate(graphs[1:] + graphs[:1]):
+        rp.copy_(grp.to(device))
+        ci.copy_(gci.to(device))
+        v.copy_(gv.to(device))
+        out.fill_(float("nan"))
+        g.replay()
+        torch.cuda.synchronize()
+        assert LIB.ofx_device_error_check() == _lib.OFX_OK
+        assert_bitwise(out, oracle_spmm(grp, gci, gv, b), f"replay {i} after rewriting the CSR")
+
+
+def test_row_range_within_the_matrix_workspace(device):
+    """m = 2^18 + 1, rows [1, m) lays out 256 planner blocks where m lays out 65; the
+    workspace sized by the query over m must be enough."""
+    rng = np.random.default_rng(550)
+    m = (1 << 18) + 1
+    k, n = m, 16
+    rp, ci, v = random_csr(m, k, power_law_degrees(m, 2_000_000, k, rng), rng)
+    b = random_dense(k, n, rng)
+    d = [t.to(device) for t in (rp, ci, v, b)]
+    kern = ops.SpmmCsrKernel(m, k, n, ci.numel(), torch.int32, torch.float32, device)
+    out = torch.empty((m - 1, n), device=device)
+    kern(*d, out, row_begin=1, row_end=m)
+    torch.cuda.synchronize()
+    assert_bitwise(out, oracle_spmm(rp, ci, v, b)[1:], "rows [1, m)")
