@@ -45,7 +45,9 @@ int read_options(const ofx_spmm_options* in, ofx_spmm_options* out, const char* 
   std::memset(out, 0, sizeof(*out));
   out->struct_size = sizeof(*out);
   if (in == nullptr) return OFX_OK;  // every field at its default
-  const uint32_t size = in->struct_size;
+  // the caller's object may be shorter than this header's struct: its first 4 bytes only, as bytes
+  uint32_t size = 0;
+  std::memcpy(&size, in, sizeof(size));
   if (size < OFX_SPMM_OPTIONS_MIN_SIZE)
     return fail(OFX_EINVAL,
                 "%s: ofx_spmm_options.struct_size = %u is below the first versioned layout (%u "

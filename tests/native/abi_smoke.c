@@ -59,6 +59,46 @@ int main(void) {
                           NULL) == OFX_EINVAL); /* ldb < n */
   EXPECT(ofx_spmm_default_split(128) == 512);
 
+  /* versioned options (include/ofx_spmm.h): a caller compiled against the first versioned layout
+   * (48 bytes, before range_nnz) is read with range_nnz at its default; the round-3 layout, which
+   * had no struct_size field (its first 4 bytes are the low half of split_threshold), is refused
+   * instead of misread */
+  struct options_v1 {
+    uint32_t struct_size;
+    int32_t reserved0;
+    int64_t split_threshold, chunk;
+    int32_t ordered, variant;
+    int64_t heavy_threshold;
+    int32_t planned, reserved;
+  } v1;
+  struct options_round3 {
+    int64_t split_threshold, chunk;
+    int32_t ordered, variant;
+    int64_t heavy_threshold;
+    int32_t planned, reserved;
+  } r3;
+  EXPECT(sizeof(v1) == OFX_SPMM_OPTIONS_MIN_SIZE && sizeof(ofx_spmm_options) > sizeof(v1));
+  memset(&v1, 0, sizeof(v1));
+  v1.struct_size = sizeof(v1);
+  v1.split_threshold = 1; /* every row of 2 nonzeros splits: same bits (exact inputs) */
+  memset(c, 0xff, sizeof(c));
+  EXPECT(ofx_spmm_csr_cpu(1, OFX_DT_INT32, OFX_DT_FLOAT, 2, 3, 2, 3, rp, col, val, b, 2, c, 2, 0, 2,
+                          (const ofx_spmm_options*)&v1) == OFX_OK);
+  EXPECT(c[0] == 3.f && c[1] == 2.f && c[2] == 0.f && c[3] == 3.f);
+  memset(&r3, 0, sizeof(r3));
+  EXPECT(ofx_spmm_csr_cpu(1, OFX_DT_INT32, OFX_DT_FLOAT, 2, 3, 2, 3, rp, col, val, b, 2, c, 2, 0, 2,
+                          (const ofx_spmm_options*)&r3) == OFX_EINVAL);
+  r3.split_threshold = 16;
+  EXPECT(ofx_spmm_csr_cpu(1, OFX_DT_INT32, OFX_DT_FLOAT, 2, 3, 2, 3, rp, col, val, b, 2, c, 2, 0, 2,
+                          (const ofx_spmm_options*)&r3) == OFX_EINVAL);
+  EXPECT(strstr(ofx_last_error(), "OFX_SPMM_OPTIONS_INIT") != NULL);
+  {
+    ofx_spmm_options cur = OFX_SPMM_OPTIONS_INIT;
+    EXPECT(cur.struct_size == sizeof(ofx_spmm_options));
+    EXPECT(ofx_spmm_csr_cpu(1, OFX_DT_INT32, OFX_DT_FLOAT, 2, 3, 2, 3, rp, col, val, b, 2, c, 2, 0,
+                            2, &cur) == OFX_OK);
+  }
+
   printf("%s %d failures\n", fails ? "FAIL" : "OK", fails);
   return fails ? 1 : 0;
 }
