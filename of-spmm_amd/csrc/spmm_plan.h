@@ -19,10 +19,18 @@ namespace ofx {
 // across the XCDs' L2s without an L2 write-back or invalidate.  An agent-scope fence is both
 // (buffer_wbl2 sc1 + buffer_inv sc1: the whole XCD's L2 written back and its lines dropped, for
 // every other wave on it too); the ordering these accesses need comes from s_waitcnt instead.
+// tests/test_isa_ordering.py pins this order in the ISA of every hand-off (the planner's status
+// words, the in-kernel hub reduce): sc1 payload stores, s_waitcnt vmcnt(0), then the signal; sc1
+// loads issued after the consumed signal.  OFX_AB_UNORDERED_HANDOFF (A/B builds only: `make
+// asm-ab-handoff`) removes both halves, to show that the test rejects such a build.
 template <typename A>
 __device__ __forceinline__ A coh_load(const A* p) {
   if (!OFX_DOK(p, sizeof(A))) return A(0);  // OFX_DEBUG_BOUNDS builds only
+#ifdef OFX_AB_UNORDERED_HANDOFF
+  return *(volatile const A*)p;
+#else
   return __hip_atomic_load(const_cast<A*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
 }
 template <typename A>
 __device__ __forceinline__ void coh_store(A* p, A v) {
@@ -30,7 +38,11 @@ __device__ __forceinline__ void coh_store(A* p, A v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // This wave's stores have reached their coherence point (gfx9: stores count in vmcnt).
+#ifdef OFX_AB_UNORDERED_HANDOFF
+__device__ __forceinline__ void wait_stores() { asm volatile("" ::: "memory"); }
+#else
 __device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+#endif
 
 namespace plan {
 namespace {  // internal linkage: every HIP translation unit gets its own copy
@@ -52,7 +64,7 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 //   order[0 .. nlight) = the light rows, ascending
 //   order[nrows - 1 - h] = heavy row h, h < counters[3] (heavy rows fill the array from its end)
 //   arrive[first slot of each hub] = 0                              (the in-kernel hub reduce)
-// and counters = {hub chunks, hubs, 0, heavy rows, epoch, host tag, ok tag, fail tag}.  Work item q
+// and counters = {hub chunks, hubs, 0, heavy rows, epoch, host tag, ok / fail / poison tags}.  Item q
 // of the non-hub rows is order_row(order, nrows, nheavy, q).  The layout is a pure function of
 // row_ptr (deterministic); the partial of chunk s is part[s].
 //
@@ -70,11 +82,13 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // block also records the plan as valid (counters[kOk] = the tag, with the host tag beside it);
 // a block whose look-back gives up records the tag as failed (counters[kFail]), refuses the tag a
 // replay of the same capture would take next (counters[kPoison]: a block of this launch that had
-// not started yet may publish under it), and sets the library's device-error word.  Every consumer of the work list (spmm_main, spmm_reduce, SDDMM)
-// checks plan_valid() at entry and writes nothing for a failed, stale or never-built plan; the
-// host reports the error word at its next entry (ofx_device_error_check).
-// Because heavy rows fill the
-// order array from its end and light rows from its start, no block needs a grand total.  A block
+// not started yet may publish under it), and sets the library's device-error word.  Every
+// consumer of the work list (spmm_main, spmm_reduce, SDDMM) checks plan_valid() at entry and
+// writes nothing for a failed, stale or never-built plan; the host reports the error word at its
+// next entry (ofx_device_error_check).
+//
+// Because heavy rows fill the order array from its end and light rows from its start, no block
+// needs a grand total.  A block
 // waits only on lower-numbered blocks, which are dispatched first (each XCD dispatches its blocks
 // in order), so the chain always progresses.  This replaced count + scan + write launches
 // (products 11.3 + 9.6 + 14.6 us, arxiv-shaped 4.8 + 5.8 us).
