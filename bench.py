@@ -196,7 +196,13 @@ def main():
                     help="multiplies every per-rank phase limit (N>1: a rank stalled in a phase "
                          "past its limit names it and exits 75)")
     ap.add_argument("--stall-test", default=os.environ.get("OFX_BENCH_STALL", ""),
-                    help="tests only: 'rank:phase' makes that rank sleep in that phase")
+                    help="tests only: 'rank:phase' makes that rank sleep in that phase; "
+                         "'rank:exchange' makes it never join its first exchange of B")
+    ap.add_argument("--exchange-deadline", type=float,
+                    default=float(os.environ.get("OFX_EXCHANGE_DEADLINE", "120")),
+                    help="N>1, set-up / tune / warmup: seconds an exchange of B may take to "
+                         "complete before the rank aborts its communicator and exits 76 naming it "
+                         "(0 = off; the timed steps never wait: exchanges stay asynchronous)")
     ap.add_argument("--tune-budget", type=float, default=120.0,
                     help="seconds of exchange-candidate timing at setup (N>1); the candidates run "
                          "in order of their modelled time, the rest are skipped")
@@ -229,6 +235,8 @@ def main():
             torch.cuda.synchronize()
     rowsplit = world > 1 or args.force_rowsplit
     watch = PhaseWatch(rank, world, args.phase_timeout_scale) if rowsplit else None
+    global _WATCH
+    _WATCH = watch
     stall_rank, _, stall_phase = args.stall_test.partition(":")
 
     def enter_phase(name, limit_s):
@@ -298,6 +306,12 @@ def main():
             log(f"[bench] native RCCL communicator unavailable ({e}); using torch.distributed")
             rs = RowSplitSpmm(m, k, n, nnz_local, dt, torch.int32, device, comm="torch")
         watch.on_abort.append(rs.abort)
+        # set-up, tune and warmup await every exchange (a peer that never joins ends this rank
+        # with the exchange named); the timed steps do not
+        rs.set_exchange_deadline(args.exchange_deadline)
+        if stall_phase == "exchange" and int(stall_rank) == rank:
+            # tests only: this rank never joins its first exchange of B (its peers' deadline fires)
+            rs.gather_block = lambda *a, **kw: time.sleep(1e6)
         enter_phase("bind (shards, remap, plans, halo and grid layouts)", 900)
         klo, khi = rs.k_range
         rs.load_shard(synth.dense(klo, khi, n, dt, device=device))
@@ -346,6 +360,8 @@ def main():
     if rowsplit:
         dist.barrier()
     sync()
+    if rowsplit:
+        rs.set_exchange_deadline(0)  # asynchronous exchanges in the timed region
     enter_phase("timed steps", 600)
     ev_start, ev_end = Mark(on_gpu), Mark(on_gpu)
     t_start = time.perf_counter()
@@ -622,5 +638,25 @@ def main():
             watch.phase("done")
 
 
+_WATCH = None
+EXIT_EXCHANGE = 76
+
+
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except Exception as e:  # noqa: BLE001
+        if type(e).__name__ != "ExchangeTimeout":
+            raise
+        # an exchange of B did not complete (the RCCL path aborted its communicator already): name
+        # the phase and the exchange, run the abort hooks, exit -- never re-exec a GPU process
+        w = _WATCH
+        where = f"phase '{w.name}'" if w is not None else "setup"
+        print(f"[rank {os.environ.get('RANK', '0')}/{os.environ.get('WORLD_SIZE', '1')}] EXCHANGE "
+              f"STALLED in {where}: {e}; exiting {EXIT_EXCHANGE}", file=sys.stderr, flush=True)
+        for f in (w.on_abort if w is not None else []):
+            try:
+                f()
+            except Exception as ee:  # noqa: BLE001 -- exiting anyway
+                print(f"abort hook failed: {ee!r}", file=sys.stderr, flush=True)
+        os._exit(EXIT_EXCHANGE)

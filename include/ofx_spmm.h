@@ -90,9 +90,11 @@ int ofx_device_error_check(void);
  * word before the planner's look-back gives up (default 2^22; 0 = every block but the first gives
  * up at once).  OFX_DEBUG_THROW_IN_COMPUTE: the op kernels' Compute throws (1 std::runtime_error,
  * 2 std::bad_alloc, 3 a non-std exception; 0 off), to test the boundary's exception guard.
+ * OFX_DEBUG_EXCHANGE_STALL: the device deadline of ofx_comm_set_timeouts expires (test).
  * value < 0 restores the default.                                                            */
 #define OFX_DEBUG_PLAN_SPIN_LIMIT 1
 #define OFX_DEBUG_THROW_IN_COMPUTE 2
+#define OFX_DEBUG_EXCHANGE_STALL 3 /* != 0: an exchange's device completion is never seen      */
 int ofx_debug_set(int knob, int64_t value);
 
 /* ---- SpMM schedule options --------------------------------------------------------------
@@ -355,10 +357,18 @@ int ofx_comm_init_rank(void** comm, int nranks, const void* uid, int rank);
  * unbounded EagerNcclCommMgr::CreateNcclComm (eager_nccl_comm_manager.cpp:57-80).           */
 int ofx_comm_init_rank_deadline(void** comm, int nranks, const void* uid, int rank,
                                 double timeout_s);
+/* This communicator's deadlines: call_timeout_s bounds a call left in progress (<= 0 keeps it);
+ * device_timeout_s > 0 makes every exchange on it (all-gathers, send/recv groups) wait for its
+ * completion on the device for at most that long, then abort the communicator and return
+ * OFX_ECOMM naming the exchange (a peer that never joins otherwise leaves the stream stuck with
+ * no host call to time out); 0 keeps exchanges asynchronous.  Not waited for during a capture.  */
+int ofx_comm_set_timeouts(void* comm, double call_timeout_s, double device_timeout_s);
 /* ncclCommAbort: drops the communicator's pending operations so that peers waiting on this rank
- * fail too (a rank's watchdog calls it before exiting). */
+ * fail too (a rank's watchdog calls it before exiting).  The handle stays valid: every later call
+ * on it returns OFX_ECOMM; ofx_comm_destroy frees it. */
 int ofx_comm_abort(void* comm);
-/* ncclCommFinalize (waited for) + ncclCommDestroy. */
+/* ncclCommFinalize (waited for) + ncclCommDestroy; an aborted communicator's handle is only freed,
+ * and one whose finalize fails is aborted rather than leaked. */
 int ofx_comm_destroy(void* comm);
 /* ncclCommCount / ncclCommUserRank of a communicator. */
 int ofx_comm_count(void* comm, int* nranks, int* rank);

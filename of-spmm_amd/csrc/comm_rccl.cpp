@@ -10,8 +10,12 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <chrono>
+#include <memory>
 #include <cstring>
+#include <mutex>
+#include <string>
 #include <thread>
 
 #include "ofx_internal.h"
@@ -33,6 +37,13 @@
     const int ofx_rc_ = comm_wait((comm), (expr), #expr);                                      \
     if (ofx_rc_ != OFX_OK) return ofx_rc_;                                                     \
   } while (0)
+// The communicator behind a handle, or OFX_ECOMM if it was aborted (its NCCL object is gone).
+#define OFX_LIVE_COMM(h, fn)                                                                   \
+  OfxComm* ofx_cm_ = static_cast<OfxComm*>(h);                                                 \
+  OFX_REQUIRE(ofx_cm_ != nullptr, OFX_EINVAL, "%s: NULL communicator", fn);                     \
+  OFX_REQUIRE(!ofx_cm_->aborted.load(), OFX_ECOMM, "%s: the communicator was aborted (%s)", fn, \
+              ofx_cm_->why.c_str());                                                           \
+  ncclComm_t c = ofx_cm_->nccl
 // Between ncclGroupStart and ncclGroupEnd a call only records its operation: ncclInProgress
 // there is not waited for (the group's ncclGroupEnd is, through OFX_NCCL_CALL).
 #define OFX_NCCL_GROUPED(expr)                                                                 \
@@ -58,36 +69,110 @@ bool nccl_dtype(int dt, ncclDataType_t* out) {
   }
 }
 
-// Seconds a call on a non-blocking communicator may stay in progress (ofx_comm_init_rank_deadline
-// sets it; the reference's blocking NCCL calls have no bound).
-double g_call_timeout_s = 300.0;
-
 double seconds_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// The handle behind `void* comm`: the NCCL communicator with its own deadlines and an
+// aborted flag.  An abort (a deadline expiring, or ofx_comm_abort from a watchdog) frees the NCCL
+// object at once and leaves the handle alive: every later call returns OFX_ECOMM naming why, and
+// ofx_comm_destroy only frees the handle, so nothing touches the freed communicator.  `mu`
+// serialises an abort against a poll of the same communicator from another thread.
+struct OfxComm {
+  ncclComm_t nccl = nullptr;
+  double call_timeout_s = 300.0;  // a call left ncclInProgress (non-blocking communicators)
+  double device_timeout_s = 0.0;  // the exchange's completion on the device; 0 = not waited for
+  std::mutex mu;
+  std::atomic<bool> aborted{false};
+  std::string why;
+
+  // ncclCommAbort once; the caller holds no lock
+  void abort(const std::string& reason) {
+    std::lock_guard<std::mutex> lock(mu);
+    if (aborted.load()) return;
+    why = reason;
+    aborted.store(true);
+    (void)ncclCommAbort(nccl);
+    nccl = nullptr;
+  }
+};
+
 // Completes a call that returned ncclInProgress (non-blocking communicator): polls the
-// communicator's state until it leaves ncclInProgress, or aborts it after g_call_timeout_s so
-// that peers blocked on this rank fail as well instead of hanging.
-int comm_wait(ncclComm_t c, ncclResult_t r, const char* what) {
+// communicator's state until it leaves ncclInProgress, or aborts it after the communicator's call
+// timeout so that peers blocked on this rank fail as well instead of hanging.
+int comm_wait(OfxComm* cm, ncclResult_t r, const char* what) {
   if (r == ncclSuccess) return OFX_OK;
   if (r != ncclInProgress)
     return ofx::fail(OFX_ECOMM, "%s failed: %s", what, ncclGetErrorString(r));
   const auto t0 = std::chrono::steady_clock::now();
   ncclResult_t st = ncclInProgress;
   while (true) {
-    const ncclResult_t q = ncclCommGetAsyncError(c, &st);
-    if (q != ncclSuccess)
-      return ofx::fail(OFX_ECOMM, "%s: ncclCommGetAsyncError failed: %s", what, ncclGetErrorString(q));
+    {
+      std::lock_guard<std::mutex> lock(cm->mu);
+      if (cm->aborted.load())
+        return ofx::fail(OFX_ECOMM, "%s: the communicator was aborted meanwhile (%s)", what,
+                         cm->why.c_str());
+      const ncclResult_t q = ncclCommGetAsyncError(cm->nccl, &st);
+      if (q != ncclSuccess)
+        return ofx::fail(OFX_ECOMM, "%s: ncclCommGetAsyncError failed: %s", what,
+                         ncclGetErrorString(q));
+    }
     if (st != ncclInProgress) break;
-    if (seconds_since(t0) > g_call_timeout_s) {
-      ncclCommAbort(c);
-      return ofx::fail(OFX_ECOMM, "%s: still in progress after %.0f s; communicator aborted", what,
-                       g_call_timeout_s);
+    if (seconds_since(t0) > cm->call_timeout_s) {
+      char why[256];
+      snprintf(why, sizeof(why), "%s still in progress after %.0f s", what, cm->call_timeout_s);
+      cm->abort(why);
+      return ofx::fail(OFX_ECOMM, "%s; communicator aborted", why);
     }
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
   if (st != ncclSuccess) return ofx::fail(OFX_ECOMM, "%s failed: %s", what, ncclGetErrorString(st));
+  return OFX_OK;
+}
+
+// The optional device-side deadline of an exchange: the host call enqueues the
+// collective and returns at once, so a peer that never joins leaves the stream stuck with no host
+// call to time out.  With device_timeout_s > 0 the exchange's completion is awaited here (an event
+// on the stream, queried until done); past the deadline the communicator is aborted (its kernels
+// are dropped, the peers' calls fail) and OFX_ECOMM names the exchange.  Skipped while the stream
+// is being captured (a graph replay is waited for by its launcher).  The test knob
+// OFX_DEBUG_EXCHANGE_STALL treats the exchange as never completing.
+int device_deadline(OfxComm* cm, hipStream_t s, const char* what) {
+  if (cm->device_timeout_s <= 0) return OFX_OK;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  OFX_HIP_CHECK(hipStreamIsCapturing(s, &cap));
+  if (cap != hipStreamCaptureStatusNone) return OFX_OK;
+  hipEvent_t ev;
+  OFX_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  hipError_t e = hipEventRecord(ev, s);
+  const bool stall = ofx::debug_knob(OFX_DEBUG_EXCHANGE_STALL, 0) != 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  while (e == hipSuccess) {
+    e = hipEventQuery(ev);
+    if (e == hipSuccess && !stall) break;
+    if (e == hipErrorNotReady || (e == hipSuccess && stall)) {
+      e = hipSuccess;
+      if (cm->aborted.load()) {  // a watchdog aborted the communicator meanwhile
+        (void)hipEventDestroy(ev);
+        return ofx::fail(OFX_ECOMM, "%s: the communicator was aborted meanwhile (%s)", what,
+                         cm->why.c_str());
+      }
+      if (seconds_since(t0) > cm->device_timeout_s) {
+        (void)hipEventDestroy(ev);
+        char why[256];
+        snprintf(why, sizeof(why), "%s did not complete on the device within %.1f s", what,
+                 cm->device_timeout_s);
+        cm->abort(why);
+        return ofx::fail(OFX_ECOMM, "%s; communicator aborted", why);
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+  }
+  (void)hipEventDestroy(ev);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return ofx::fail(OFX_EDEVICE, "%s: waiting for the exchange: %s", what, hipGetErrorString(e));
+  }
   return OFX_OK;
 }
 }  // namespace
@@ -111,7 +196,9 @@ extern "C" int ofx_comm_init_rank(void** comm, int nranks, const void* uid, int 
     std::memcpy(&id, uid, sizeof(id));
     ncclComm_t c;
     OFX_NCCL_CHECK(ncclCommInitRank(&c, nranks, id, rank));
-    *comm = c;
+    OfxComm* cm = new OfxComm();
+    cm->nccl = c;
+    *comm = cm;
     return OFX_OK;
   });
 }
@@ -121,15 +208,15 @@ extern "C" int ofx_comm_init_rank(void** comm, int nranks, const void* uid, int 
 // ncclCommGetAsyncError; a rank whose peers have not all joined within `timeout_s` seconds aborts
 // the communicator (ncclCommAbort) and returns OFX_ECOMM naming the wait, instead of blocking
 // forever inside ncclCommInitRank.  Every later call on the communicator is bounded the same way
-// (OFX_NCCL_CALL).  The reference's EagerNcclCommMgr::CreateNcclComm
-// (oneflow/core/job/eager_nccl_comm_manager.cpp:57-80) blocks without a bound.
+// (OFX_NCCL_CALL, this communicator's own timeout: ofx_comm_set_timeouts).  The reference's
+// EagerNcclCommMgr::CreateNcclComm (oneflow/core/job/eager_nccl_comm_manager.cpp:57-80) blocks
+// without a bound.
 extern "C" int ofx_comm_init_rank_deadline(void** comm, int nranks, const void* uid, int rank,
                                            double timeout_s) {
   return ::ofx::guarded(__func__, [&]() -> int {
     OFX_REQUIRE(comm && uid && nranks > 0 && rank >= 0 && rank < nranks && timeout_s > 0, OFX_EINVAL,
                 "comm_init_rank_deadline: bad arguments (nranks=%d rank=%d timeout=%g)", nranks, rank,
                 timeout_s);
-    g_call_timeout_s = timeout_s;
     ncclUniqueId id;
     std::memcpy(&id, uid, sizeof(id));
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
@@ -160,28 +247,54 @@ extern "C" int ofx_comm_init_rank_deadline(void** comm, int nranks, const void* 
       return ofx::fail(OFX_ECOMM, "comm_init_rank_deadline: rank %d of %d: %s", rank, nranks,
                        ncclGetErrorString(st));
     }
-    *comm = c;
+    OfxComm* cm = new OfxComm();
+    cm->nccl = c;
+    cm->call_timeout_s = timeout_s;
+    *comm = cm;
+    return OFX_OK;
+  });
+}
+
+// This communicator's deadlines (per communicator, not one process-wide value):
+// call_timeout_s bounds a call left in progress (non-blocking communicators; <= 0 keeps the
+// current one), device_timeout_s > 0 awaits every exchange's completion on the device for at most
+// that long (0 = off: the exchanges stay asynchronous, as a timed step needs).
+extern "C" int ofx_comm_set_timeouts(void* comm, double call_timeout_s, double device_timeout_s) {
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_LIVE_COMM(comm, "comm_set_timeouts");
+    (void)c;
+    OFX_REQUIRE(device_timeout_s >= 0, OFX_EINVAL, "comm_set_timeouts: negative device timeout");
+    if (call_timeout_s > 0) ofx_cm_->call_timeout_s = call_timeout_s;
+    ofx_cm_->device_timeout_s = device_timeout_s;
     return OFX_OK;
   });
 }
 
 // Aborts a communicator (ncclCommAbort): its pending operations are dropped and peers blocked on
-// it fail.  Called by a rank's phase watchdog before it exits (bench.py).
+// it fail.  Called by a rank's phase watchdog before it exits (bench.py).  The handle stays valid
+// (every call on it returns OFX_ECOMM); ofx_comm_destroy frees it.
 extern "C" int ofx_comm_abort(void* comm) {
   return ::ofx::guarded(__func__, [&]() -> int {
-    if (comm) OFX_NCCL_CHECK(ncclCommAbort(static_cast<ncclComm_t>(comm)));
+    if (comm) static_cast<OfxComm*>(comm)->abort("ofx_comm_abort");
     return OFX_OK;
   });
 }
 
-// Finalize (flushes the communicator's operations; a non-blocking communicator may report
-// ncclInProgress, waited for with the call deadline), then destroy.
+// Frees a handle.  A live communicator is finalized first (flushes its operations; a non-blocking
+// one may report ncclInProgress, waited for with its call timeout), then destroyed; if finalizing
+// fails it is aborted instead, so it is never leaked.  An aborted one only has its handle freed.
 extern "C" int ofx_comm_destroy(void* comm) {
   return ::ofx::guarded(__func__, [&]() -> int {
     if (comm == nullptr) return OFX_OK;
-    ncclComm_t c = static_cast<ncclComm_t>(comm);
-    OFX_NCCL_CALL(c, ncclCommFinalize(c));
-    OFX_NCCL_CHECK(ncclCommDestroy(c));
+    std::unique_ptr<OfxComm> cm(static_cast<OfxComm*>(comm));
+    if (cm->aborted.load()) return OFX_OK;
+    const int rc = comm_wait(cm.get(), ncclCommFinalize(cm->nccl), "ncclCommFinalize");
+    if (cm->aborted.load()) return rc;  // the finalize timed out: comm_wait aborted it
+    if (rc != OFX_OK) {
+      cm->abort("finalize failed");
+      return rc;
+    }
+    OFX_NCCL_CHECK(ncclCommDestroy(cm->nccl));
     return OFX_OK;
   });
 }
@@ -189,9 +302,10 @@ extern "C" int ofx_comm_destroy(void* comm) {
 // Ranks and this rank's index in a communicator (what bench.py reports as the RCCL comm size).
 extern "C" int ofx_comm_count(void* comm, int* nranks, int* rank) {
   return ::ofx::guarded(__func__, [&]() -> int {
-    OFX_REQUIRE(comm && nranks && rank, OFX_EINVAL, "comm_count: NULL argument");
-    OFX_NCCL_CHECK(ncclCommCount(static_cast<ncclComm_t>(comm), nranks));
-    OFX_NCCL_CHECK(ncclCommUserRank(static_cast<ncclComm_t>(comm), rank));
+    OFX_REQUIRE(nranks && rank, OFX_EINVAL, "comm_count: NULL argument");
+    OFX_LIVE_COMM(comm, "comm_count");
+    OFX_NCCL_CHECK(ncclCommCount(c, nranks));
+    OFX_NCCL_CHECK(ncclCommUserRank(c, rank));
     return OFX_OK;
   });
 }
@@ -201,10 +315,11 @@ extern "C" int ofx_allgather(void* stream, const void* in, void* out, size_t cou
   return ::ofx::guarded(__func__, [&]() -> int {
     ncclDataType_t t;
     OFX_REQUIRE(nccl_dtype(dtype, &t), OFX_EUNSUPPORTED, "allgather: unsupported dtype %d", dtype);
-    OFX_REQUIRE(comm && (count == 0 || (in && out)), OFX_EINVAL, "allgather: NULL argument");
-    ncclComm_t c = static_cast<ncclComm_t>(comm);
-    OFX_NCCL_CALL(c, ncclAllGather(in, out, count, t, c, static_cast<hipStream_t>(stream)));
-    return OFX_OK;
+    OFX_REQUIRE(count == 0 || (in && out), OFX_EINVAL, "allgather: NULL argument");
+    OFX_LIVE_COMM(comm, "allgather");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    OFX_NCCL_CALL(ofx_cm_, ncclAllGather(in, out, count, t, c, s));
+    return device_deadline(ofx_cm_, s, "allgather");
   });
 }
 
@@ -216,8 +331,8 @@ extern "C" int ofx_allgather_p2p(void* stream, void* buf, size_t count, int dtyp
   return ::ofx::guarded(__func__, [&]() -> int {
     ncclDataType_t t;
     OFX_REQUIRE(nccl_dtype(dtype, &t), OFX_EUNSUPPORTED, "allgather_p2p: unsupported dtype %d", dtype);
-    OFX_REQUIRE(comm && (count == 0 || buf), OFX_EINVAL, "allgather_p2p: NULL argument");
-    ncclComm_t c = static_cast<ncclComm_t>(comm);
+    OFX_REQUIRE(count == 0 || buf, OFX_EINVAL, "allgather_p2p: NULL argument");
+    OFX_LIVE_COMM(comm, "allgather_p2p");
     int nranks = 0, rank = 0;
     OFX_NCCL_CHECK(ncclCommCount(c, &nranks));
     OFX_NCCL_CHECK(ncclCommUserRank(c, &rank));
@@ -230,8 +345,8 @@ extern "C" int ofx_allgather_p2p(void* stream, void* buf, size_t count, int dtyp
       OFX_NCCL_GROUPED(ncclSend(base + (size_t)rank * count * esz, count, t, to, c, s));
       OFX_NCCL_GROUPED(ncclRecv(base + (size_t)from * count * esz, count, t, from, c, s));
     }
-    OFX_NCCL_CALL(c, ncclGroupEnd());
-    return OFX_OK;
+    OFX_NCCL_CALL(ofx_cm_, ncclGroupEnd());
+    return device_deadline(ofx_cm_, s, "allgather_p2p");
   });
 }
 
@@ -247,9 +362,9 @@ extern "C" int ofx_exchange_rows(void* stream, void* comm, int dtype, int64_t n,
   return ::ofx::guarded(__func__, [&]() -> int {
     ncclDataType_t t;
     OFX_REQUIRE(nccl_dtype(dtype, &t), OFX_EUNSUPPORTED, "exchange_rows: unsupported dtype %d", dtype);
-    OFX_REQUIRE(comm && send_counts && send_offsets && recv_counts && recv_offsets && n >= 0,
+    OFX_REQUIRE(send_counts && send_offsets && recv_counts && recv_offsets && n >= 0,
                 OFX_EINVAL, "exchange_rows: NULL argument");
-    ncclComm_t c = static_cast<ncclComm_t>(comm);
+    OFX_LIVE_COMM(comm, "exchange_rows");
     int nranks = 0, rank = 0;
     OFX_NCCL_CHECK(ncclCommCount(c, &nranks));
     OFX_NCCL_CHECK(ncclCommUserRank(c, &rank));
@@ -267,8 +382,8 @@ extern "C" int ofx_exchange_rows(void* stream, void* comm, int dtype, int64_t n,
         OFX_NCCL_GROUPED(ncclRecv(rb + (size_t)recv_offsets[from] * row_bytes,
                                   (size_t)(recv_counts[from] * n), t, from, c, s));
     }
-    OFX_NCCL_CALL(c, ncclGroupEnd());
-    return OFX_OK;
+    OFX_NCCL_CALL(ofx_cm_, ncclGroupEnd());
+    return device_deadline(ofx_cm_, s, "exchange_rows");
   });
 }
 
@@ -283,11 +398,10 @@ extern "C" int ofx_spmm_rowsplit(void* stream, void* comm, int idx_dtype, int va
                                  void* b_gathered, void* c, int64_t ldc, void* workspace,
                                  size_t workspace_bytes, const ofx_spmm_options* opts) {
   return ::ofx::guarded(__func__, [&]() -> int {
-    OFX_REQUIRE(comm && k_padded >= 0 && n >= 0, OFX_EINVAL, "spmm_rowsplit: bad arguments");
+    OFX_REQUIRE(k_padded >= 0 && n >= 0, OFX_EINVAL, "spmm_rowsplit: bad arguments");
     int nranks = 0, rank = 0;
-    ncclComm_t cm = static_cast<ncclComm_t>(comm);
-    OFX_NCCL_CHECK(ncclCommCount(cm, &nranks));
-    OFX_NCCL_CHECK(ncclCommUserRank(cm, &rank));
+    const int rc0 = ofx_comm_count(comm, &nranks, &rank);  // a live communicator, or its error
+    if (rc0 != OFX_OK) return rc0;
     OFX_REQUIRE(k_padded % nranks == 0, OFX_EINVAL,
                 "spmm_rowsplit: k_padded=%lld is not a multiple of %d ranks", (long long)k_padded,
                 nranks);

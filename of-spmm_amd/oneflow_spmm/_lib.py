@@ -18,7 +18,7 @@ DT_FLOAT, DT_DOUBLE, DT_INT32, DT_INT64, DT_FLOAT16, DT_BFLOAT16 = 2, 3, 5, 6, 9
 (OFX_OK, OFX_EINVAL, OFX_EDEVICE, OFX_ENOMEM, OFX_EUNSUPPORTED, OFX_ECOMM, OFX_EWORKSPACE, OFX_EPLAN,
  OFX_EINTERNAL) = range(9)
 # test knobs of ofx_debug_set (include/ofx_spmm.h)
-DEBUG_PLAN_SPIN_LIMIT, DEBUG_THROW_IN_COMPUTE = 1, 2
+DEBUG_PLAN_SPIN_LIMIT, DEBUG_THROW_IN_COMPUTE, DEBUG_EXCHANGE_STALL = 1, 2, 3
 MEMCPY_H2D, MEMCPY_D2H, MEMCPY_D2D, MEMCPY_DEFAULT = 1, 2, 3, 4
 UNIQUE_ID_BYTES = 128
 
@@ -157,6 +157,7 @@ def _load():
         "ofx_comm_get_unique_id": ([p], i32),
         "ofx_comm_init_rank": ([ctypes.POINTER(p), i32, p, i32], i32),
         "ofx_comm_init_rank_deadline": ([ctypes.POINTER(p), i32, p, i32, ctypes.c_double], i32),
+        "ofx_comm_set_timeouts": ([p, ctypes.c_double, ctypes.c_double], i32),
         "ofx_comm_abort": ([p], i32),
         "ofx_comm_destroy": ([p], i32),
         "ofx_comm_count": ([p, ctypes.POINTER(i32), ctypes.POINTER(i32)], i32),

@@ -141,13 +141,38 @@ def _host_staged(group, *tensors) -> bool:
     return dist.get_backend(group) != "nccl" and any(t.is_cuda for t in tensors)
 
 
-def _torch_exchange(send, send_counts, send_offsets, recv, recv_counts, recv_offsets, group):
+class ExchangeTimeout(RuntimeError):
+    """An exchange of B that did not complete within its deadline: a peer that
+    never joined.  On the RCCL path the native communicator was aborted first (its queued
+    kernels dropped, the peers' calls fail); the message names the exchange."""
+
+
+def _await(works, deadline_s: float, what: str):
+    """Waits for torch.distributed work handles; with deadline_s > 0 a stalled one raises
+    ExchangeTimeout instead of blocking forever (the torch/gloo form of ofx_comm_set_timeouts'
+    device deadline)."""
+    if deadline_s <= 0:
+        for w in works:
+            w.wait()
+        return
+    t0 = time.monotonic()
+    for w in works:
+        while not w.is_completed():
+            if time.monotonic() - t0 > deadline_s:
+                raise ExchangeTimeout(f"{what}: not complete after {deadline_s:.1f} s "
+                                      f"(a peer did not join the exchange)")
+            time.sleep(1e-3)
+        w.wait()
+
+
+def _torch_exchange(send, send_counts, send_offsets, recv, recv_counts, recv_offsets, group,
+                    deadline_s: float = 0.0):
     """Grouped point-to-point rows exchange through torch.distributed (the CPU/gloo path of
     ofx_exchange_rows; same counts/offsets convention, rows of the buffers' width)."""
     if _host_staged(group, send, recv):
         host = recv.cpu()
         _torch_exchange(send.cpu(), send_counts, send_offsets, host, recv_counts, recv_offsets,
-                        group)
+                        group, deadline_s)
         recv.copy_(host)
         return
     world, rank = dist.get_world_size(group), dist.get_rank(group)
@@ -163,8 +188,7 @@ def _torch_exchange(send, send_counts, send_offsets, recv, recv_counts, recv_off
             o = recv_offsets[p]
             reqs.append(dist.P2POp(dist.irecv, recv[o:o + recv_counts[p]], gp, group))
     if reqs:
-        for r in dist.batch_isend_irecv(reqs):
-            r.wait()
+        _await(dist.batch_isend_irecv(reqs), deadline_s, "rows exchange")
 
 
 class GridPlan:
@@ -269,7 +293,7 @@ class GridPlan:
     def _exchange(self, owner, send, counts, c_counts, recv, stream=None):
         if owner.comm_kind == "torch":
             _torch_exchange(send.view(-1, self.w), counts[0], counts[1], recv.view(-1, self.w),
-                            counts[2], counts[3], owner.group)
+                            counts[2], counts[3], owner.group, owner.exchange_deadline_s)
             return
         sc, so, rc, ro = c_counts
         s = stream if stream is not None else current_stream_handle(recv)
@@ -540,15 +564,30 @@ class RowSplitSpmm:
         check(LIB.ofx_comm_init_rank_deadline(ctypes.byref(comm), self.world, uid, self.rank,
                                               self.comm_timeout_s), "comm_init_rank_deadline")
         self._comm = comm
+        if self.exchange_deadline_s > 0:
+            check(LIB.ofx_comm_set_timeouts(comm, 0.0, self.exchange_deadline_s),
+                  "comm_set_timeouts")
 
     comm_timeout_s = float(os.environ.get("OFX_COMM_TIMEOUT", "300"))
+    # seconds an exchange may take to complete, awaited after each one (0 = asynchronous, as in a
+    # timed step); OFX_EXCHANGE_DEADLINE sets the default
+    exchange_deadline_s = float(os.environ.get("OFX_EXCHANGE_DEADLINE", "0"))
+
+    def set_exchange_deadline(self, seconds: float):
+        """Every exchange of this operator (all-gathers, halo and grid send/recv groups) waits for
+        its completion for at most `seconds`, then raises ExchangeTimeout naming it -- on RCCL
+        after aborting this operator's communicator (ofx_comm_set_timeouts' device deadline, the
+        communicator's own).  0 turns the wait off (exchanges stay asynchronous)."""
+        self.exchange_deadline_s = float(seconds)
+        if self._comm is not None:
+            check(LIB.ofx_comm_set_timeouts(self._comm, 0.0, self.exchange_deadline_s),
+                  "comm_set_timeouts")
 
     def abort(self):
         """ncclCommAbort of the native communicator (a stalled rank's watchdog, before it exits):
         peers blocked on this rank then fail instead of waiting forever."""
         if self._comm is not None:
-            LIB.ofx_comm_abort(self._comm)
-            self._comm = None
+            LIB.ofx_comm_abort(self._comm)  # the handle stays valid: close() frees it
 
     def comm_size(self):
         """(ranks, this rank) of the native RCCL communicator, None without one."""
@@ -578,7 +617,9 @@ class RowSplitSpmm:
         if self.comm_kind == "torch":
             host = blk.cpu() if _host_staged(self.group, blk) else blk
             parts = list(host.view(self.world, self.pad, self.nc).unbind(0))
-            dist.all_gather(parts, parts[self.rank].clone(), group=self.group)  # views: in place
+            work = dist.all_gather(parts, parts[self.rank].clone(), group=self.group,
+                                   async_op=True)  # views: in place
+            _await([work], self.exchange_deadline_s, f"all-gather of B, column block {c}")
             if host is not blk:
                 blk.copy_(host)
             return
@@ -753,7 +794,8 @@ class RowSplitSpmm:
             if h.send_rows:
                 torch.index_select(comp, 0, h.send_idx, out=send)
             _torch_exchange(send, h.send_counts, h.send_offsets, comp,
-                            h.recv_counts, [h.k_own + o for o in h.recv_offsets], self.group)
+                            h.recv_counts, [h.k_own + o for o in h.recv_offsets], self.group,
+                            self.exchange_deadline_s)
             return
         s = stream if stream is not None else current_stream_handle(comp)
         esz, nc = comp.element_size(), self.halo_nc
@@ -957,6 +999,8 @@ class RowSplitSpmm:
                     for _ in range(reps):
                         self.step(out)
                     ms = (time.perf_counter() - t0) * 1e3 / reps
+            except ExchangeTimeout:
+                raise  # a peer that never joined: no candidate can be timed, the rank ends
             except Exception as e:  # noqa: BLE001 -- reported, candidate dropped
                 self.tune_errors[f"{self.exchange}/{self.comm_kind}/p{self.chunks}"] = repr(e)
             return max_over_ranks(ms)

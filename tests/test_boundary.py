@@ -138,3 +138,10 @@ def test_workspace_query_bounds_every_row_range(m):
             continue
         d = ops.describe(m, k, n, nnz, torch.float32, row_begin=lo, row_end=hi)
         assert d["ws"] <= whole, (m, lo, hi, d["ws"], whole)
+
+
+def test_comm_calls_on_a_null_handle_are_refused():
+    assert LIB.ofx_comm_set_timeouts(None, 1.0, 1.0) == _lib.OFX_EINVAL
+    nr, rk = ctypes.c_int(), ctypes.c_int()
+    assert LIB.ofx_comm_count(None, ctypes.byref(nr), ctypes.byref(rk)) == _lib.OFX_EINVAL
+    assert LIB.ofx_comm_abort(None) == _lib.OFX_OK and LIB.ofx_comm_destroy(None) == _lib.OFX_OK

@@ -211,3 +211,44 @@ def test_row_range_within_the_matrix_workspace(device):
     kern(*d, out, row_begin=1, row_end=m)
     torch.cuda.synchronize()
     assert_bitwise(out, oracle_spmm(rp, ci, v, b)[1:], "rows [1, m)")
+
+
+def test_comm_device_deadline_aborts_once_and_the_handle_stays_safe(device):
+    """VERDICT r4 item 6 + ADVICE r4: a communicator's own device deadline (ofx_comm_set_timeouts)
+    bounds an exchange whose completion never comes (test knob OFX_DEBUG_EXCHANGE_STALL): the call
+    aborts the communicator and names the exchange; the handle stays valid (every later call
+    returns OFX_ECOMM, a second abort is a no-op) and ofx_comm_destroy only frees it -- nothing
+    touches the freed NCCL object.  RCCL at one rank (the box has one GPU)."""
+    uid = ctypes.create_string_buffer(_lib.UNIQUE_ID_BYTES)
+    _lib.check(LIB.ofx_set_device(device.index or 0))
+    _lib.check(LIB.ofx_comm_get_unique_id(uid))
+    comm = ctypes.c_void_p()
+    _lib.check(LIB.ofx_comm_init_rank_deadline(ctypes.byref(comm), 1, uid, 0, 60.0))
+    x = torch.arange(1000, dtype=torch.float32, device=device)
+    y = torch.empty_like(x)
+    s = fs._C.current_stream_handle(x)
+    _lib.check(LIB.ofx_comm_set_timeouts(comm, 0.0, 0.5))
+    _lib.check(LIB.ofx_allgather(s, x.data_ptr(), y.data_ptr(), 1000, _lib.DT_FLOAT, comm))
+    assert torch.equal(x, y)  # awaited already: the device deadline waits for completion
+    try:
+        LIB.ofx_debug_set(_lib.DEBUG_EXCHANGE_STALL, 1)
+        rc = LIB.ofx_allgather(s, x.data_ptr(), y.data_ptr(), 1000, _lib.DT_FLOAT, comm)
+        assert rc == _lib.OFX_ECOMM and "did not complete on the device within 0.5 s" in _lib.last_error()
+    finally:
+        LIB.ofx_debug_set(_lib.DEBUG_EXCHANGE_STALL, -1)
+    rc = LIB.ofx_allgather(s, x.data_ptr(), y.data_ptr(), 1000, _lib.DT_FLOAT, comm)
+    assert rc == _lib.OFX_ECOMM and "was aborted" in _lib.last_error()
+    nr, rk = ctypes.c_int(), ctypes.c_int()
+    assert LIB.ofx_comm_count(comm, ctypes.byref(nr), ctypes.byref(rk)) == _lib.OFX_ECOMM
+    assert LIB.ofx_comm_abort(comm) == _lib.OFX_OK  # idempotent
+    assert LIB.ofx_comm_destroy(comm) == _lib.OFX_OK
+    torch.cuda.synchronize()
+    # a live communicator with the deadline off: asynchronous exchange, finalize + destroy
+    comm2 = ctypes.c_void_p()
+    _lib.check(LIB.ofx_comm_get_unique_id(uid))
+    _lib.check(LIB.ofx_comm_init_rank_deadline(ctypes.byref(comm2), 1, uid, 0, 60.0))
+    _lib.check(LIB.ofx_comm_set_timeouts(comm2, 30.0, 0.0))
+    _lib.check(LIB.ofx_allgather(s, x.data_ptr(), y.data_ptr(), 1000, _lib.DT_FLOAT, comm2))
+    torch.cuda.synchronize()
+    assert torch.equal(x, y)
+    _lib.check(LIB.ofx_comm_destroy(comm2))

@@ -187,3 +187,20 @@ def test_bench_eight_ranks_refuses_a_short_launch():
     p = _bench(["--gpus", "8", "--device", "cpu", "--backend", "gloo"],
                {"WORLD_SIZE": "4", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode == 2 and "WORLD_SIZE=4" in p.stderr and p.stdout == ""
+
+
+def test_bench_exchange_that_never_completes_is_named_and_fails():
+    """a rank whose exchange of B was issued but never completes (injected:
+    rank 1 never joins its first all-gather, so rank 0's is stuck after its enqueue) does not hang
+    until a phase limit: its exchange deadline fires, the communicator is aborted, the rank names
+    the phase and the exchange and exits 76; the launcher ends the run with that status."""
+    import time
+    t0 = time.monotonic()
+    p = _bench(["--gpus", "2", "--backend", "gloo", "--device", "cpu", "--config", "tiny",
+                "--steps", "1", "--warmup", "0", "--exchange-deadline", "3"],
+               {"OMP_NUM_THREADS": "1", "OFX_BENCH_STALL": "1:exchange"}, drop=_SPAWN_ENV_DROP)
+    assert p.returncode == 76, p.stderr[-3000:]
+    assert "[rank 0/2] EXCHANGE STALLED in phase 'tune: torch/p1'" in p.stderr, p.stderr[-3000:]
+    assert "all-gather of B" in p.stderr and "not complete after 3.0 s" in p.stderr
+    assert p.stdout == ""
+    assert time.monotonic() - t0 < 90
