@@ -13,7 +13,7 @@ mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
 run() {  # name, rocprofv3 options...
   local name=$1; shift
-  timeout -k 10 300 rocprofv3 "$@" --output-format csv -d $OUT/$name -o run -- python3 $PROG $ARGS \
+  timeout -k 10 200 rocprofv3 "$@" --output-format csv -d $OUT/$name -o run -- python3 $PROG $ARGS \
     > $OUT/${name}_bench.json 2> $OUT/${name}.err
 }
 run trace --kernel-trace --stats || exit $?
@@ -22,4 +22,7 @@ run write --pmc WRITE_SIZE || exit $?
 run rdreq --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_BUBBLE_sum || exit $?
 run rd128 --pmc TCC_EA0_RDREQ_128B TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum || exit $?
 run hit --pmc TCC_HIT_sum TCC_MISS_sum || exit $?
+if [ -n "${SQ_PASS:-}" ]; then  # where the waves' time goes (parked on s_waitcnt / issue / active)
+  run sq --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE || exit $?
+fi
 echo done
