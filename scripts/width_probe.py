@@ -84,9 +84,10 @@ def main():
     for _ in range(args.rounds):
         for c in cases:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(s)
-            c["graph"].replay()
-            e1.record(s)
+            with torch.cuda.stream(s):  # replay() launches on the current stream
+                e0.record(s)
+                c["graph"].replay()
+                e1.record(s)
             torch.cuda.synchronize()
             c["us"].append(e0.elapsed_time(e1) * 1e3 / args.reps)
     for c in cases:
