@@ -243,8 +243,15 @@ struct BRows {
         return __builtin_bit_cast(P, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, 0, aux));
       } else if constexpr (sizeof(P) == 4) {
         return __builtin_bit_cast(P, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, aux));
+      } else if constexpr (sizeof(P) == 32) {
+        // two 16-B halves (8-element fp32 lanes); row k (past the range) reads zeros for both
+        typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+        const auto lo = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, aux);
+        const auto hi = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16u, 0, aux);
+        const u32x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(P, v);
       } else {
-        static_assert(sizeof(P) == 2, "B-row slice of 2, 4, 8 or 16 bytes");
+        static_assert(sizeof(P) == 2, "B-row slice of 2, 4, 8, 16 or 32 bytes");
         return __builtin_bit_cast(P, __builtin_amdgcn_raw_buffer_load_b16(rsrc, off, 0, aux));
       }
     } else {

@@ -80,6 +80,26 @@ int launch_tuned(const Launch& L, int id) {
       case 82: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L); break;
       case 83: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, P, false, W, false, true, 16, 8, false, kLR>>(L); break;
       case 84: if (rows_of(4)) return launch_cfg<T, I, Cfg<4, 4, 4, 4, false, P, false, W, false, true, 16, 32, false, kLR>>(L); break;
+      // round 5: 8-element (32-B) lanes with the shifted window, so that rows of 17-32 columns
+      // take 4 lanes (16 rows per wave, the N = 16 narrow form's packing) and rows of 33-64 take 8
+      case 90: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 4, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
+      case 91: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 4, 4, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
+      case 92: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
+      case 93: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 4, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
+      case 94: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 4, 8, 4, false, P, false, W, false, true, 16, 8, true, kLR>>(L); break;
+      default: break;
+    }
+  }
+  // round 5: 16-bit rows of odd widths with the shifted window (windows at 2-B alignment:
+  // scripts/unaligned_probe.hip) -- 4- and 8-element lanes over 4-16 lanes
+  if constexpr (sizeof(T) == 2 && std::is_same<I, int32_t>::value) {
+    constexpr bool P = true, W = true;
+    switch (id) {
+      case 95: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
+      case 96: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
+      case 97: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 4, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
+      case 98: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
+      case 99: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 16, 16, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
       default: break;
     }
   }
