@@ -172,7 +172,7 @@ def main():
                     help="threads of the cpu_baseline (default: the cores this process may use, "
                          "min(nproc, affinity, cgroup quota); never more)")
     ap.add_argument("--variant", type=int, default=0, help="force a kernel variant (VEC*100+LPR)")
-    ap.add_argument("--comm", choices=["rccl", "rccl-p2p"], default=None,
+    ap.add_argument("--comm", choices=["rccl", "rccl-p2p", "rccl-pull"], default=None,
                     help="all-gather schedule for N>1 (default: measured at setup, faster kept)")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="column blocks for gather/SpMM overlap at N>1 (default: measured)")

@@ -377,6 +377,35 @@ int ofx_allgather(void* stream, const void* in, void* out, size_t count, int dty
 /* The same all-gather as grouped point-to-point send/recv with every peer (in place: this
  * rank's slot of `buf` is the send buffer).  Same result bytes as ofx_allgather.           */
 int ofx_allgather_p2p(void* stream, void* buf, size_t count, int dtype, void* comm);
+/* ---- the pull form of the same all-gather (peer reads over xGMI) ------------
+ * Every rank's gathered buffer has one layout, so a rank can read each peer's slot straight out
+ * of the peer's buffer (IPC-mapped) into its own.  Replaces ncclAllGather's ring
+ * (cuda_all_gather.cpp:25-47) as a tune() candidate; same result bytes.
+ * ofx_peer_export: IPC handle (OFX_PEER_HANDLE_BYTES) of the allocation holding `ptr`, with the
+ *   offset of ptr in it.  ofx_peer_open maps a peer's handle (a handle opened twice maps once,
+ *   reference-counted); ofx_peer_close unmaps a pointer ofx_peer_open returned.
+ * ofx_peer_publish: system-scope release on every XCD, stream-ordered: this rank's earlier
+ *   stores reach HBM, where peers' reads find them.
+ * ofx_peer_pull: for every peer p != rank, bytes [p*slot_bytes, (p+1)*slot_bytes) of
+ *   peer_bufs[p] (peer p's buffer, mapped) into the same bytes of buf; peer_bufs[rank] unused.
+ *   The caller orders it: every peer's slot written and published before (a barrier), no peer
+ *   rewrites its slot until every rank's pull is done (a second barrier).
+ * ofx_peer_pull_host: the same tile plan over host memory (tests).
+ * ofx_allgather_pull: the composed exchange on a communicator: publish, a stream-ordered RCCL
+ *   barrier (1-element all-reduce), pull, barrier; count elements per slot as ofx_allgather_p2p
+ *   (in place: this rank's slot of buf is already written).                                   */
+#define OFX_PEER_HANDLE_BYTES 96
+#define OFX_PEER_MAX_RANKS 16
+int ofx_peer_export(const void* ptr, void* handle_out);
+int ofx_peer_open(const void* handle, void** ptr_out);
+int ofx_peer_close(void* ptr);
+int ofx_peer_publish(void* stream);
+int ofx_peer_pull(void* stream, int nranks, int rank, const void* const* peer_bufs, void* buf,
+                  uint64_t slot_bytes);
+int ofx_peer_pull_host(int nranks, int rank, const void* const* peer_bufs, void* buf,
+                       uint64_t slot_bytes);
+int ofx_allgather_pull(void* stream, void* comm, const void* const* peer_bufs, void* buf,
+                       size_t count, int dtype);
 /* One row-split step on this rank: in-place all-gather of the padded B shards
  * in b_gathered [k_padded, n] (k_padded = ranks * P; this rank's rows already at
  * [rank * P, rank * P + K_r)), then the local SpMM of this rank's m_local rows (row_ptr rebased

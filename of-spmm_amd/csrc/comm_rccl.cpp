@@ -85,6 +85,11 @@ struct OfxComm {
   std::mutex mu;
   std::atomic<bool> aborted{false};
   std::string why;
+  int* barrier_word = nullptr;  // device int of the stream-ordered barrier (ofx_allgather_pull)
+
+  ~OfxComm() {
+    if (barrier_word != nullptr) (void)hipFree(barrier_word);
+  }
 
   // ncclCommAbort once; the caller holds no lock
   void abort(const std::string& reason) {
@@ -347,6 +352,48 @@ extern "C" int ofx_allgather_p2p(void* stream, void* buf, size_t count, int dtyp
     }
     OFX_NCCL_CALL(ofx_cm_, ncclGroupEnd());
     return device_deadline(ofx_cm_, s, "allgather_p2p");
+  });
+}
+
+// A stream-ordered barrier: a 1-element max all-reduce.  When it completes on this rank's stream,
+// every rank's stream has reached it, i.e. finished everything enqueued before it.
+static int stream_barrier(OfxComm* cm, hipStream_t s, const char* what) {
+  if (cm->barrier_word == nullptr) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    OFX_HIP_CHECK(hipStreamIsCapturing(s, &cap));
+    OFX_REQUIRE(cap == hipStreamCaptureStatusNone, OFX_EINVAL,
+                "%s: run the exchange once before capturing it (its barrier word is allocated on "
+                "first use)", what);
+    OFX_HIP_CHECK(hipMalloc(&cm->barrier_word, 256));
+    OFX_HIP_CHECK(hipMemsetAsync(cm->barrier_word, 0, 256, s));
+  }
+  OFX_NCCL_CALL(cm, ncclAllReduce(cm->barrier_word, cm->barrier_word, 1, ncclInt32, ncclMax,
+                                  cm->nccl, s));
+  return OFX_OK;
+}
+
+// The pull all-gather (include/ofx_spmm.h): publish this rank's slot, barrier (every slot ready),
+// read every peer's slot out of its buffer, barrier (no rank rewrites its slot -- the next step's
+// shard -- while a peer still reads it).  Same bytes as ofx_allgather.
+extern "C" int ofx_allgather_pull(void* stream, void* comm, const void* const* peer_bufs, void* buf,
+                                  size_t count, int dtype) {
+  return ::ofx::guarded(__func__, [&]() -> int {
+    ncclDataType_t t;
+    OFX_REQUIRE(nccl_dtype(dtype, &t), OFX_EUNSUPPORTED, "allgather_pull: unsupported dtype %d", dtype);
+    OFX_LIVE_COMM(comm, "allgather_pull");
+    int nranks = 0, rank = 0;
+    OFX_NCCL_CHECK(ncclCommCount(c, &nranks));
+    OFX_NCCL_CHECK(ncclCommUserRank(c, &rank));
+    if (nranks == 1 || count == 0) return OFX_OK;
+    OFX_REQUIRE(peer_bufs && buf, OFX_EINVAL, "allgather_pull: NULL argument");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint64_t slot = (uint64_t)count * (uint64_t)ofx::dtype_size(dtype);
+    int rc = ofx_peer_publish(s);
+    if (rc == OFX_OK) rc = stream_barrier(ofx_cm_, s, "allgather_pull (slots ready)");
+    if (rc == OFX_OK) rc = ofx_peer_pull(s, nranks, rank, peer_bufs, buf, slot);
+    if (rc == OFX_OK) rc = stream_barrier(ofx_cm_, s, "allgather_pull (pulls done)");
+    if (rc != OFX_OK) return rc;
+    return device_deadline(ofx_cm_, s, "allgather_pull");
   });
 }
 

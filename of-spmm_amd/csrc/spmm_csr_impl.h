@@ -83,6 +83,9 @@ struct alignas(sizeof(T) * VEC) Pack {
 // last columns takes the VEC-wide window ending at column n - 1 (16-B accesses at 4-B alignment).
 // LR: the hubs' chunk partials are added by the last chunk to finish, inside spmm_main (hub_tail),
 // instead of by the spmm_reduce launch (the mid-size forms, where a launch is a tenth of the call).
+// HV (with HL): elements per lane of the wave items' HL-lane groups (1: one element per lane), so
+// that 16-bit rows of 33-64 columns take one pass of 32 lanes; with SH the last window is shifted
+// there as in the light rows.
 #ifndef OFX_AB_NO_LR
 constexpr bool kLR = true;  // the mid-size forms (prefetching, mid, narrow <= kPrefetchNnz): LR
 #else
@@ -90,12 +93,12 @@ constexpr bool kLR = false;  // A/B builds only (scripts/ab_build.sh): the spmm_
 #endif
 template <int VEC_, int LPR_, int U_ = 8, int WPB_ = 4, bool NT_ = false, bool PF_ = false,
           bool BNT_ = false, bool WH_ = false, bool BI_ = false, bool BUF_ = true, int HL_ = 0,
-          int HU_ = 16, bool SH_ = false, bool LR_ = false>
+          int HU_ = 16, bool SH_ = false, bool LR_ = false, int HV_ = 1>
 struct Cfg {
   static constexpr int VEC = VEC_, LPR = LPR_, U = U_, WPB = WPB_;
   static constexpr bool NT = NT_, PF = PF_, BNT = BNT_, WH = WH_, BI = BI_, BUF = BUF_, SH = SH_;
   static constexpr bool LR = LR_;
-  static constexpr int HL = HL_, HU = HU_;
+  static constexpr int HL = HL_, HU = HU_, HV = HV_;
   // loads in flight per lane of the wave-item form: G * UW * VEC cross-lane moves per batch are
   // unrolled, so UW keeps that at <= 256 (4..32)
   static constexpr int G = LPR < 64 ? 64 / LPR : 1;
@@ -103,11 +106,11 @@ struct Cfg {
   static constexpr int UW = UW_RAW > 32 ? 32 : (UW_RAW < 4 ? 4 : UW_RAW);
 };
 
-// The lane mapping of the wave items (accumulate_wave): the light rows' one, or HL lanes of one
-// element each (HL > 0).
+// The lane mapping of the wave items (accumulate_wave): the light rows' one, or HL lanes of HV
+// elements each (HL > 0).
 template <typename K>
 struct WaveMap {
-  static constexpr int VEC = K::HL > 0 ? 1 : K::VEC;
+  static constexpr int VEC = K::HL > 0 ? K::HV : K::VEC;
   static constexpr int LPR = K::HL > 0 ? K::HL : K::LPR;
   static constexpr int UW = K::HL > 0 ? K::HU : K::UW;
   static constexpr bool BNT = K::BNT, BUF = K::BUF;
@@ -1048,8 +1051,11 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
           j1 = (re - j0 - chunk < chunk) ? re : j0 + chunk;
         }
         for (int64_t c0 = 0; c0 < n; c0 += (int64_t)WL * WV) {
-          const int64_t cc = c0 + (int64_t)wgl * WV;
+          int64_t cc = c0 + (int64_t)wgl * WV;
           const bool active = cc < n;
+          if constexpr (K::SH && WV > 1) {
+            if (active && cc + WV > n) cc = n - WV;  // the window ending at column n - 1
+          }
           A acc[WV];
 #pragma unroll
           for (int e = 0; e < WV; ++e) acc[e] = A(0);
@@ -1064,7 +1070,7 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
         }
         if constexpr (K::LR) {
           if (wc >= 0)
-            hub_tail<T, WV, WL, false>(arrive, w - wc, num_chunks(re - rs, chunk), part, C, ldc,
+            hub_tail<T, WV, WL, K::SH && (WV > 1)>(arrive, w - wc, num_chunks(re - rs, chunk), part, C, ldc,
                                        wr, n, wgl, lane < WL, 0, bias, act);
         }
       }
@@ -1345,9 +1351,9 @@ int describe_cfg(const Launch& L, const char* kind) {
                         : ws_layout(L.nrows, L.nnz, L.n, sizeof(typename Num<T>::acc), L.sched).total;
   std::snprintf(L.describe, L.describe_bytes,
                 "form=%s kernel=%s VEC=%d LPR=%d U=%d WPB=%d NT=%d PF=%d WH=%d BI=%d BUF=%d SH=%d "
-                "HL=%d HU=%d LR=%d elem=%d idx=%d ws=%zu",
+                "HL=%d HU=%d HV=%d LR=%d elem=%d idx=%d ws=%zu",
                 form, kind, K::VEC, K::LPR, K::U, K::WPB, (int)K::NT, (int)K::PF, (int)K::WH,
-                (int)K::BI, (int)K::BUF, (int)K::SH, K::HL, K::HU, (int)K::LR, (int)sizeof(T),
+                (int)K::BI, (int)K::BUF, (int)K::SH, K::HL, K::HU, K::HV, (int)K::LR, (int)sizeof(T),
                 (int)sizeof(I), ws);
   return OFX_OK;
 }

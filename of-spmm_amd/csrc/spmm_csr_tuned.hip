@@ -87,6 +87,16 @@ int launch_tuned(const Launch& L, int id) {
       case 92: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
       case 93: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 4, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
       case 94: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 4, 8, 4, false, P, false, W, false, true, 16, 8, true, kLR>>(L); break;
+      // the wave items (hub chunks, heavy rows) in 32-lane groups: one column pass at N <= 32
+      case 100: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR>>(L); break;
+      case 101: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 4, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR>>(L); break;
+      case 102: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 32, 8, true, kLR>>(L); break;
+      case 103: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 32, 32, true, kLR>>(L); break;
+      case 104: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 4, 4, false, P, false, W, false, true, 32, 16, true, kLR>>(L); break;
+      // rows of 33-64 columns: 32-lane wave items of 2-element (8-B) lanes, one pass
+      case 117: if (L.n >= 8) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR, 2>>(L); break;
+      case 118: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR, 2>>(L); break;
+      case 119: if (L.n >= 8) return launch_cfg<T, I, Cfg<4, 16, 4, 4, false, P, false, W, false, true, 32, 16, true, kLR, 2>>(L); break;
       default: break;
     }
   }
@@ -100,6 +110,21 @@ int launch_tuned(const Launch& L, int id) {
       case 97: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 4, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
       case 98: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
       case 99: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 16, 16, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
+      // the prefetching form's layout without wave items (the N = 64 automatic one), shifted
+      case 105: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 16, 16, 4, false, P, false, false, false, true, 0, 16, true, kLR>>(L); break;
+      case 106: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 16, 4, false, P, false, false, false, true, 0, 16, true, kLR>>(L); break;
+      case 107: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 16, 4, false, P, false, false, false, true, 0, 16, true, kLR>>(L); break;
+      // 32-lane wave items
+      case 108: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR>>(L); break;
+      case 109: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR>>(L); break;
+      case 110: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR>>(L); break;
+      case 111: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 4, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR>>(L); break;
+      // 32-lane wave items of 2-element (4-B) lanes: one pass up to 64 columns
+      case 112: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR, 2>>(L); break;
+      case 113: if (L.n >= 8) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR, 2>>(L); break;
+      case 114: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 32, 8, true, kLR, 2>>(L); break;
+      case 115: if (L.n >= 8) return launch_cfg<T, I, Cfg<4, 16, 16, 4, false, P, false, W, false, true, 32, 16, true, kLR, 2>>(L); break;
+      case 116: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 4, 4, false, P, false, W, false, true, 32, 16, true, kLR, 2>>(L); break;
       default: break;
     }
   }

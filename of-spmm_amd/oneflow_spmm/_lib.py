@@ -21,6 +21,8 @@ DT_FLOAT, DT_DOUBLE, DT_INT32, DT_INT64, DT_FLOAT16, DT_BFLOAT16 = 2, 3, 5, 6, 9
 DEBUG_PLAN_SPIN_LIMIT, DEBUG_THROW_IN_COMPUTE, DEBUG_EXCHANGE_STALL = 1, 2, 3
 MEMCPY_H2D, MEMCPY_D2H, MEMCPY_D2D, MEMCPY_DEFAULT = 1, 2, 3, 4
 UNIQUE_ID_BYTES = 128
+PEER_HANDLE_BYTES = 96   # OFX_PEER_HANDLE_BYTES
+PEER_MAX_RANKS = 16      # OFX_PEER_MAX_RANKS
 
 
 class OfxError(RuntimeError):
@@ -163,6 +165,13 @@ def _load():
         "ofx_comm_count": ([p, ctypes.POINTER(i32), ctypes.POINTER(i32)], i32),
         "ofx_allgather": ([p, p, p, sz, i32, p], i32),
         "ofx_allgather_p2p": ([p, p, sz, i32, p], i32),
+        "ofx_peer_export": ([p, p], i32),
+        "ofx_peer_open": ([p, ctypes.POINTER(p)], i32),
+        "ofx_peer_close": ([p], i32),
+        "ofx_peer_publish": ([p], i32),
+        "ofx_peer_pull": ([p, i32, i32, p, p, u64], i32),
+        "ofx_peer_pull_host": ([i32, i32, p, p, u64], i32),
+        "ofx_allgather_pull": ([p, p, p, p, sz, i32], i32),
         "ofx_exchange_rows": ([p, p, i32, i64, p, p, p, p, p, p], i32),
         "ofx_spmm_rowsplit": ([p, p, i32, i32, i64, i64, i64, i64, p, p, p, p, p, i64, p, sz, popt], i32),
         "ofx_padded_owner_remap": ([p, i32, i64, i64, i64, p, p], i32),

@@ -28,7 +28,7 @@ import torch.distributed as dist
 
 from . import ops
 from ._C import balanced_range, current_stream_handle, dtype_code
-from ._lib import LIB, UNIQUE_ID_BYTES, check
+from ._lib import LIB, PEER_HANDLE_BYTES, PEER_MAX_RANKS, UNIQUE_ID_BYTES, check
 
 
 def padded_owner_remap(col_idx: torch.Tensor, k: int, world: int) -> torch.Tensor:
@@ -443,10 +443,11 @@ class RowSplitSpmm:
         self.options = ops.make_options(split=ops.default_split(n))
         if comm == "auto":
             comm = "rccl" if self.device.type == "cuda" else "torch"
-        if comm not in ("rccl", "rccl-p2p", "torch"):
+        if comm not in ("rccl", "rccl-p2p", "rccl-pull", "torch"):
             raise ValueError(f"RowSplitSpmm: unknown comm {comm!r}")
         self.comm_kind = comm
         self._comm = None
+        self._peers = None  # (gathered tensor, [peer p's gathered buffer, mapped]) of rccl-pull
         self.comm_stream = None
         if self.device.type == "cuda":
             # high priority: the exchange kernels of a pipelined step get CUs as soon as SpMM
@@ -597,7 +598,57 @@ class RowSplitSpmm:
         check(LIB.ofx_comm_count(self._comm, ctypes.byref(nr), ctypes.byref(rk)), "comm_count")
         return nr.value, rk.value
 
+    def _close_peers(self):
+        if self._peers is not None:
+            _, ptrs = self._peers
+            self._peers = None
+            for r, p in enumerate(ptrs):
+                if r != self.rank:
+                    check(LIB.ofx_peer_close(ctypes.c_void_p(p)), "peer_close")
+
+    def _peer_map(self) -> list:
+        """rccl-pull: every rank's gathered buffer, mapped into this process (IPC handles swapped
+        over the group once per buffer: after set_pipeline re-lays it out, at the next exchange).
+        Collective: every rank reaches it in the same exchange."""
+        if self._peers is not None and self._peers[0] is self.gathered:
+            return self._peers[1]
+        self._close_peers()
+        if self.world > PEER_MAX_RANKS:
+            raise ValueError(f"rccl-pull: at most {PEER_MAX_RANKS} ranks, not {self.world}")
+        h = ctypes.create_string_buffer(PEER_HANDLE_BYTES)
+        rc = LIB.ofx_peer_export(ctypes.c_void_p(self.gathered.data_ptr()), h)
+        handles = [None] * self.world
+        dist.all_gather_object(handles, bytes(h.raw) if rc == 0 else None, group=self.group)
+        if any(x is None for x in handles):  # every rank raises, none waits in a barrier
+            raise RuntimeError(f"rccl-pull: ranks {[r for r, x in enumerate(handles) if x is None]} "
+                               f"could not export their buffers (rank {self.rank}: rc {rc})")
+        ptrs, err = [], None
+        try:
+            for r, hb in enumerate(handles):
+                if r == self.rank:
+                    ptrs.append(self.gathered.data_ptr())
+                    continue
+                ptr = ctypes.c_void_p()
+                check(LIB.ofx_peer_open(ctypes.create_string_buffer(hb, PEER_HANDLE_BYTES),
+                                        ctypes.byref(ptr)), "peer_open")
+                ptrs.append(ptr.value)
+        except Exception as e:  # noqa: BLE001 -- agreed on below
+            err = f"rank {self.rank}: {e}"
+        # every rank learns whether every rank mapped its peers: a rank that raised alone would
+        # leave the others blocked in the pull's barriers
+        status = [None] * self.world
+        dist.all_gather_object(status, err, group=self.group)
+        failed = [s for s in status if s is not None]
+        if failed:
+            for r, p in enumerate(ptrs):
+                if r != self.rank:
+                    LIB.ofx_peer_close(ctypes.c_void_p(p))
+            raise RuntimeError(f"rccl-pull: peer buffers not mapped: {failed[0]}")
+        self._peers = (self.gathered, ptrs)
+        return ptrs
+
     def close(self):
+        self._close_peers()
         if self._comm is not None:
             check(LIB.ofx_comm_destroy(self._comm), "comm_destroy")
             self._comm = None
@@ -627,6 +678,12 @@ class RowSplitSpmm:
         if self.comm_kind == "rccl":
             check(LIB.ofx_allgather(s, slot.data_ptr(), blk.data_ptr(), count,
                                     dtype_code(self.dtype), self._comm), "allgather")
+        elif self.comm_kind == "rccl-pull":
+            # every peer's block c at the same offset of its buffer as ours
+            off = blk.data_ptr() - self.gathered.data_ptr()
+            bufs = (ctypes.c_void_p * self.world)(*[p + off for p in self._peer_map()])
+            check(LIB.ofx_allgather_pull(s, self._comm, bufs, blk.data_ptr(), count,
+                                         dtype_code(self.dtype)), "allgather_pull")
         else:
             check(LIB.ofx_allgather_p2p(s, blk.data_ptr(), count, dtype_code(self.dtype),
                                         self._comm), "allgather_p2p")
@@ -943,8 +1000,8 @@ class RowSplitSpmm:
              budget_s: float | None = None, prune: float = 3.0,
              first: tuple | None = None, log=None, on_candidate=None) -> dict:
         """Times every exchange on this node with the real step over the bound CSR: all-gather
-        (ring / point-to-point) x pipeline depth, the halo exchange and the grid plans if built.
-        Keeps the fastest.  Timings are max-reduced over ranks, so all ranks choose the same; every
+        (ring / point-to-point / peer pull) x pipeline depth, the halo exchange and the grid plans
+        if built.  Keeps the fastest.  Timings are max-reduced over ranks, so all ranks choose the same; every
         candidate produces the same bytes.  Returns {"<comm>/p<C>" | "halo[/p<C>]" | "nsplit[/s<S>]"
         | "grid<R>x<C>[/s<S>]": ms} of the candidates measured.
 
@@ -968,7 +1025,8 @@ class RowSplitSpmm:
         if self.world == 1 and not force:
             return {}
         native = self.comm_kind.startswith("rccl")
-        kinds = ("rccl", "rccl-p2p") if native else ("torch",)
+        kinds = (("rccl", "rccl-p2p") + (("rccl-pull",) if self.world <= PEER_MAX_RANKS else ())
+                 if native else ("torch",))
         base = "rccl" if native else "torch"
         on_gpu = self.device.type == "cuda"
         red_dev = self.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")

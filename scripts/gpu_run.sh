@@ -23,7 +23,7 @@ export AMD_LOG_LEVEL=${AMD_LOG_LEVEL:-1}
 export OFX_FAULTHANDLER_FILE=$GRAFT_REPO_ROOT/gpurun_out/${TAG}_faulthandler.txt
 mkdir -p gpurun_out
 L=$GRAFT_REPO_ROOT/of-spmm_amd/oneflow_spmm
-PT="python -u -m pytest tests -m gpu -q --capture=tee-sys --timeout 300 --timeout-method thread -p no:cacheprovider -p no:faulthandler"
+PT="python -u -m pytest tests -m gpu -q -rs --capture=tee-sys --timeout 300 --timeout-method thread -p no:cacheprovider -p no:faulthandler"
 n=0
 for step in "$@"; do
   n=$((n + 1))

@@ -73,7 +73,7 @@ def _worker(rank, world, port, kind, rp, ci, v, b, q):
         q.put((rank, "err", traceback.format_exc()))
 
 
-@pytest.mark.parametrize("kind", ["rccl", "rccl-p2p", "halo", "halo/p2", "nsplit", "nsplit/s2",
+@pytest.mark.parametrize("kind", ["rccl", "rccl-p2p", "rccl-pull", "halo", "halo/p2", "nsplit", "nsplit/s2",
                                   "tune"])
 def test_row_split_two_ranks(kind):
     if not torch.cuda.is_available():
@@ -108,5 +108,5 @@ def test_row_split_two_ranks(kind):
         assert_bitwise(out, ref[lo:hi], f"{kind} rows [{lo},{hi})")
         kinds.add(ck)
         if kind == "tune":
-            assert {t.split("/")[0] for t in times} == {"rccl", "rccl-p2p", "halo", "nsplit"}
+            assert {t.split("/")[0] for t in times} == {"rccl", "rccl-p2p", "rccl-pull", "halo", "nsplit"}
     assert len(kinds) == 1  # every rank made the same choice

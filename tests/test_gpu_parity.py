@@ -313,8 +313,20 @@ def test_products_scale_sampled_rows(device):
     heavy = np.argsort(deg)[-20:]
     rows = np.unique(np.concatenate([hubs[:200], heavy, hubs[-1:]]))
     check_sampled_rows(rp_n, ci_n, v, b, out, rows, 1e-5, "products hubs")
-    # a checksum of checksums over all rows (size-independent): row sums vs oracle's
+    # every row, through linearity (size-independent): the row checksums C.1 against A.(B.1) taken
+    # in float64 on the host (scipy), each within 1e-5 of its row's |A|.(|B|.1); then the checksum
+    # of those checksums, 1'.C.1 against 1'.A.(B.1), within 1e-5 of 1'.|A|.(|B|.1)
+    import scipy.sparse as sp
     assert torch.isfinite(out_h).all()
+    a64 = sp.csr_matrix((v_n.astype(np.float64), ci_n, rp_n), shape=(m, k))
+    b64 = b_n.astype(np.float64)
+    want = a64 @ b64.sum(axis=1)
+    scale = abs(a64) @ np.abs(b64).sum(axis=1)
+    got = out.double().sum(dim=1).cpu().numpy()
+    err = np.abs(got - want)
+    bad = np.nonzero(err > 1e-5 * np.maximum(scale, 1e-30))[0]
+    assert len(bad) == 0, f"{len(bad)} rows off, first {bad[:5]}, worst {float(np.max(err / np.maximum(scale, 1e-30)))}"
+    assert abs(got.sum() - want.sum()) <= 1e-5 * scale.sum()
 
 
 def test_row_split_rccl_single_rank(device):
@@ -341,8 +353,9 @@ def test_row_split_rccl_single_rank(device):
         out = rs(rp.to(device), rs.remap_columns(ci.to(device)), v.to(device))
         torch.cuda.synchronize()
         assert_bitwise(out, oracle_spmm(rp, ci, v, b), "rccl row split")
-        # column-block pipeline on the side stream (ring and point-to-point schedules)
-        for kind, chunks in (("rccl", 4), ("rccl-p2p", 2)):
+        # column-block pipeline on the side stream (ring, point-to-point and pull schedules; one
+        # rank's pull has no peer to read, its barriers and buffer mapping still run)
+        for kind, chunks in (("rccl", 4), ("rccl-p2p", 2), ("rccl-pull", 2)):
             rs.comm_kind = kind
             rs.set_pipeline(chunks)
             out2 = torch.full_like(out, float("nan"))
@@ -362,7 +375,7 @@ def test_row_split_rccl_single_rank(device):
         rs.bind(*d, halo=True, full_csr=d, grid_subs=(1, 4))
         assert rs.halo.halo_rows == 0 and rs.halo.k_compact == k  # one rank owns every row
         times = rs.tune(out2, reps=1, force=True)
-        assert len(times) == 11 and "halo" in times and "nsplit" in times and "nsplit/s4" in times
+        assert len(times) == 14 and "rccl-pull/p4" in times and "halo" in times and "nsplit" in times and "nsplit/s4" in times
         assert "halo/p2" in times and "halo/p4" in times
         for exchange in ("allgather", "halo", "halo/p4", "nsplit", "nsplit/s4"):
             rs.exchange = exchange.split("/p")[0]
