@@ -1656,22 +1656,6 @@ int launch_shift_pf(const Launch& L) {
   }
 }
 
-// fp32 rows of 17-32 columns in the prefetching form: the shifted 16-B window (any N, 4-B
-// alignment) over 8 lanes with U = 8 and the hub chunks / heavy rows as 16-lane one-element wave
-// items (tuning entry 10071; profiles/r04s_f32mid.jsonl): arxiv-shaped N = 17 / 24 / 25 / 32
-// 112 / 88 / 120 / 89 -> 76 / 76 / 77 / 75 us, 60k x 1.5M 106 / 82 / 110 / 82 -> 71 / 72 / 73 /
-// 71 us.  From 33 columns the automatic layouts stay (as fast or faster there).
-template <typename T, typename I>
-int launch_shift_wh_pf(const Launch& L) {
-  return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, true, false, true, false, true, 16, 16, true, kLR>>(L);
-}
-
-bool use_shift_wh_pf_form(const Launch& L, int elem_bytes) {
-  return L.sched.variant == 0 && elem_bytes == 4 && L.n > 16 && L.n <= 32 &&
-         use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched) && ((uintptr_t)L.b % 4) == 0 &&
-         ((uintptr_t)L.c % 4) == 0;
-}
-
 bool use_shift_pf_form(const Launch& L, int elem_bytes) {
   return L.sched.variant == 0 && elem_bytes == 4 && L.n > 16 && L.n % 4 != 0 &&
          use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched) &&
@@ -1715,47 +1699,49 @@ bool use_narrow_form(const Launch& L, int elem_bytes) {
 // (profiles/r04k_variants.jsonl; arxiv-shaped / 60k x 1.5M / 169k x 2M): bf16 N = 16 86 / 77 / 94
 // -> 50 / 45 / 58 us and N = 8 99 / 82 / 105 -> 50 / 45 / 55 (U = 8, entry 51), fp32 N = 8 74 /
 // 66 / 74 -> 46 / 43 / 53 (U = 4, entry 63).  Same bits: only who adds changes.
-// 16-bit rows of 17-32 columns (even widths) the same way: 8-B lanes over 8 lanes (4-B over 16 for
-// views only 4-B aligned), U = 8, 16-lane wave items; their automatic layouts (2-element lanes)
-// unrolled the wave items to 259 VGPRs.  Entries 10073 / 10077 (profiles/r04u_16bit_mid.jsonl):
-// arxiv-shaped bf16 N = 20 / 24 / 28 / 32 148 / 148 / 148 / 221 -> 83 / 82 / 83 / 83 us, 60k x
-// 1.5M 87 / 87 / 88 / 159 -> 76 / 77 / 78 / 78 us, f16 N = 32 218 -> 82 us.
+// (Round 4's 16-bit rows of 17-32 columns and odd 16-bit widths took this shape too, with
+// 16-lane wave items; round 5's launch_mid_width_pf below replaced them.)
 template <typename T, typename I>
 int launch_narrow_pf(const Launch& L) {
   if constexpr (sizeof(T) == 2) {
-    if (L.n <= 16)
-      return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
-    if (pick_vec(2, L, 0, 4) == 4)
-      return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
-    return launch_cfg<T, I, Cfg<2, 16, 8, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
+    return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
   } else {
     return launch_cfg<T, I, Cfg<2, 4, 4, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
   }
 }
 
-// Odd 16-bit widths of mid-size launches (round 4): no vector layout applies (an element is 2 B,
-// a window would be unaligned), so lanes hold one element each; the automatic layout gave a row
-// 64 lanes (one row per wave).  16-lane groups with ceil(N / 16) column passes and 16-lane wave
-// items (U = 16) up to N = 48, 32-lane groups with two passes above: tuning entries 10064-10068
-// (profiles/r04j_odd16.jsonl), arxiv-shaped bf16 N = 17 / 41 / 47 / 63 152 / 264 / 261 / 264 ->
-// 91 / 127 / 128 / 155 us, 60k x 1.5M 88 / 136 / 135 / 136 -> 78 / 116 / 117 / 117.
+// Rows of 17-64 columns of mid-size launches (round 5): the narrow form's
+// shape for every width -- shifted windows (Cfg::SH, any N; 2-B-aligned 8 / 16-B accesses are
+// exact and as fast on gfx950, scripts/unaligned_probe.hip) over 8 lanes, hubs added in the
+// kernel -- with the wave items (hub chunks, heavy rows) in 32-lane groups, one column pass
+// (the reference gather's word choice, gather_kernel_util.cu:69-104, falls to 2-B words at odd
+// 16-bit widths; the shifted window keeps 8 / 16-B words at any width):
+// 1-element lanes up to 32 columns, 2-element lanes up to 64 (Cfg::HV).  The wave items' column
+// passes were what held these widths: the round-4 layouts ran 16-lane one-element wave items, two
+// to four passes per chunk.  Tuning entries 10100 / 10110 / 10117 / 10112 (profiles/
+// r05_width_sweep_midsize.jsonl), arxiv-shaped 169k x 1.17M: fp32 N = 17-32 77 -> 58 us, fp32
+// 33-64 97-103 -> 79-82, bf16 17 / 24 94 / 84 -> 68 / 66, bf16 33-63 125-160 -> 81-82 and N = 64
+// 94 -> 79; 60k x 1.5M fp32 N = 17 72 -> 55, bf16 N = 47 / 63 118 / -> 79.  Same bits: only who
+// adds changes.
 template <typename T, typename I>
-int launch_odd16_pf(const Launch& L) {
-  if (L.n <= 48)
-    return launch_cfg<T, I, Cfg<1, 16, 16, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
-  return launch_cfg<T, I, Cfg<1, 32, 16, 4, false, true, false, true, false, true, 32, 16, false, kLR>>(L);
+int launch_mid_width_pf(const Launch& L) {
+  if (L.n <= 32)
+    return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, true, false, true, false, true, 32, 16, true, kLR>>(L);
+  if constexpr (sizeof(T) == 2)
+    return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, true, false, true, false, true, 32, 16, true, kLR, 2>>(L);
+  else
+    return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, true, false, true, false, true, 32, 16, true, kLR, 2>>(L);
 }
 
-bool use_odd16_pf_form(const Launch& L, int elem_bytes) {
-  return L.sched.variant == 0 && elem_bytes == 2 && L.n > 16 && L.n <= 64 &&
-         pick_vec(2, L, 0) == 1 && use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched);
+bool use_mid_width_pf_form(const Launch& L, int elem_bytes) {
+  return L.sched.variant == 0 && (elem_bytes == 2 || elem_bytes == 4) && L.n > 16 && L.n <= 64 &&
+         use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched) &&
+         ((uintptr_t)L.b % elem_bytes) == 0 && ((uintptr_t)L.c % elem_bytes) == 0;
 }
 
 bool use_narrow_pf_form(const Launch& L, int elem_bytes) {
   if (L.sched.variant != 0 || !use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched)) return false;
-  if (elem_bytes == 2)
-    return ((L.n == 8 || L.n == 16) && pick_vec(2, L, 0, 4) == 4) ||
-           (L.n > 16 && L.n <= 32 && pick_vec(2, L, 0, 4) >= 2);
+  if (elem_bytes == 2) return (L.n == 8 || L.n == 16) && pick_vec(2, L, 0, 4) == 4;
   if (elem_bytes == 4) return L.n == 8 && pick_vec(4, L, 0, 2) == 2;
   return false;
 }
@@ -1770,18 +1756,16 @@ int launch_typed(const Launch& L) {
                 "spmm_csr: tuning variant %d needs B under 4 GiB", L.sched.variant);
     return launch_tuned<T, I>(L, L.sched.variant - 10000);
   }
+  if constexpr (sizeof(T) == 2 || sizeof(T) == 4) {
+    if (use_mid_width_pf_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
+      return launch_mid_width_pf<T, I>(L);
+  }
   if constexpr (sizeof(T) <= 4) {
     if (use_narrow_pf_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
       return launch_narrow_pf<T, I>(L);
   }
-  if constexpr (sizeof(T) == 2) {
-    if (use_odd16_pf_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
-      return launch_odd16_pf<T, I>(L);
-  }
   if constexpr (sizeof(T) == 4) {
     if (use_narrow_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L)) return launch_narrow<T, I>(L);
-    if (use_shift_wh_pf_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
-      return launch_shift_wh_pf<T, I>(L);
     if (use_shift_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
       return launch_shift<T, I>(L, (L.b_rows * L.ldb * (int64_t)sizeof(T)) > kNtBytes);
 #ifndef OFX_AB_NO_SHIFT_PF  // A/B builds only (scripts/ab_build.sh)

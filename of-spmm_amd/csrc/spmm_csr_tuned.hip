@@ -125,6 +125,14 @@ int launch_tuned(const Launch& L, int id) {
       case 114: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 32, 8, true, kLR, 2>>(L); break;
       case 115: if (L.n >= 8) return launch_cfg<T, I, Cfg<4, 16, 16, 4, false, P, false, W, false, true, 32, 16, true, kLR, 2>>(L); break;
       case 116: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 4, 4, false, P, false, W, false, true, 32, 16, true, kLR, 2>>(L); break;
+      // 16-bit rows of more than 64 columns, any width: shifted 16-B windows (the fp32 shifted
+      // configurations' shape), prefetching (120, 121, 125) and bandwidth (122-124) forms
+      case 120: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 16, 4, false, P, false, false, false, true, 0, 16, true, kLR>>(L); break;
+      case 121: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 32, 16, 4, false, P, false, false, false, true, 0, 16, true, kLR>>(L); break;
+      case 122: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L); break;
+      case 123: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 32, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L); break;
+      case 124: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 64, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L); break;
+      case 125: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR, 4>>(L); break;
       default: break;
     }
   }

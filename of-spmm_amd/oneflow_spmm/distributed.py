@@ -19,6 +19,7 @@ Layout choices (MI355X-first):
 from __future__ import annotations
 
 import ctypes
+import datetime
 import math
 import os
 import time
@@ -155,14 +156,19 @@ def _await(works, deadline_s: float, what: str):
         for w in works:
             w.wait()
         return
+    # Work.wait(timeout), not a poll of is_completed(): gloo's point-to-point works only record
+    # their completion inside wait(), so a poll never sees them finish
     t0 = time.monotonic()
     for w in works:
-        while not w.is_completed():
-            if time.monotonic() - t0 > deadline_s:
-                raise ExchangeTimeout(f"{what}: not complete after {deadline_s:.1f} s "
-                                      f"(a peer did not join the exchange)")
-            time.sleep(1e-3)
-        w.wait()
+        left = max(deadline_s - (time.monotonic() - t0), 1e-3)
+        try:
+            done = w.wait(timeout=datetime.timedelta(seconds=left))
+        except RuntimeError as e:
+            raise ExchangeTimeout(f"{what}: not complete after {deadline_s:.1f} s (a peer did not "
+                                  f"join the exchange): {e}") from e
+        if done is False:
+            raise ExchangeTimeout(f"{what}: not complete after {deadline_s:.1f} s "
+                                  f"(a peer did not join the exchange)")
 
 
 def _torch_exchange(send, send_counts, send_offsets, recv, recv_counts, recv_offsets, group,

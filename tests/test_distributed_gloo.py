@@ -238,6 +238,9 @@ def _tune_worker(rank, world, port, q, device="cpu"):
         rs.bind(lrp.to(dev), ci[n0:n1].to(dev), v[n0:n1].to(dev), halo=True,
                 full_csr=(rp.to(dev), ci.to(dev), v.to(dev)), grid_subs=(1, 2))
         out = torch.empty((hi - lo, n), device=dev)
+        # every exchange awaited under a deadline, as the bench's set-up runs them (round 5: gloo's
+        # point-to-point works report completion only from wait(), which a poll never saw)
+        rs.set_exchange_deadline(60.0)
         times = rs.tune(out, reps=1, prune=float("inf"))  # every candidate runs
         want = {"torch/p1", "torch/p2", "torch/p4", "halo", "halo/p2", "halo/p4", "grid2x2",
                 "grid2x2/s2", "nsplit", "nsplit/s2"}

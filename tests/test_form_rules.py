@@ -39,15 +39,16 @@ def test_mid_form_bounds():
     assert form(K_SMALL_ROWS, K_MID_ELEMS // 128, 128)["form"] == "mid"
     above = form(K_SMALL_ROWS, K_MID_ELEMS // 128 + 1, 128)
     assert above["form"] == "prefetch" and above["BI"] == 0
-    assert form(K_SMALL_ROWS + 1, 400_000, 64)["form"] == "prefetch"  # rows bound it too
+    assert form(K_SMALL_ROWS + 1, 400_000, 64)["form"] == "narrow"  # rows bound it too (the
+    assert form(K_SMALL_ROWS + 1, 400_000, 128)["form"] == "prefetch"  # prefetching range)
 
 
 @pytest.mark.parametrize("n", [32, 64, 128])
 def test_prefetch_form_bound(n):
     m = 120_000
     below, above = form(m, K_PREFETCH_NNZ, n), form(m, K_PREFETCH_NNZ + 1, n)
-    # 17-32 fp32 columns: the shifted window with 16-lane wave items ("narrow", round 4)
-    assert below["form"] == ("narrow" if n <= 32 else "prefetch") and below["PF"] == 1
+    # 17-64 columns: the shifted window with 32-lane wave items ("narrow", round 5)
+    assert below["form"] == ("narrow" if n <= 64 else "prefetch") and below["PF"] == 1
     assert above["form"] == "bandwidth" and above["PF"] == 0 and above["U"] == 8
     # wave items only at 16 < N <= 64
     assert below["WH"] == (1 if n <= 64 else 0)
@@ -62,7 +63,7 @@ def test_narrow_form_n16_fp32():
     # above kPrefetchNnz fp32 only (16-bit N = 16 below it: test_narrow_rows_of_mid_size_launches),
     # N = 16 only, 16-B aligned only
     assert form(m, K_PREFETCH_NNZ + 1, 16, BF16)["form"] != "narrow"
-    assert form(m, K_PREFETCH_NNZ, 33)["form"] == "prefetch"
+    assert form(m, K_PREFETCH_NNZ, 65)["form"] == "prefetch"
     assert form(m, K_PREFETCH_NNZ + 1, 32)["form"] == "bandwidth"
     assert form(m, K_PREFETCH_NNZ, 16, b_addr=260)["form"] != "narrow"
 
@@ -108,7 +109,7 @@ def test_row_range_uses_its_share_of_nonzeros():
     d = form(m, nnz, 128, row_begin=0, row_end=m // 8)
     assert d["form"] == "bandwidth"
     # a small slice of a mid-size graph drops to the prefetching or mid form
-    d = form(169_343, 1_166_243, 64, row_begin=0, row_end=40_000)
+    d = form(169_343, 1_166_243, 128, row_begin=0, row_end=40_000)
     assert d["form"] == "prefetch"
 
 
@@ -148,21 +149,16 @@ def test_prefetch_form_layouts():
     """The prefetching form's lane layouts (round 4): odd fp32 widths above 16 take 16-B lanes
     with the shifted last window; 16-bit rows of <= 128 B take N / 16 elements per lane."""
     m, nnz = 169_343, 1_166_243
-    for n, lpr in ((41, 16), (47, 16), (99, 32)):
+    # above 64 columns: the shifted 16-B window of the prefetching form
+    for n, lpr in ((99, 32), (127, 32), (255, 64)):
         d = form(m, nnz, n)
-        assert d["form"] == "prefetch" and d["SH"] == 1 and d["VEC"] == 4 and d["LPR"] == lpr, d
-    # 17-32 columns: the shifted window with 16-lane wave items (round 4)
-    for n in (17, 24, 25, 32):
-        d = form(m, nnz, n)
-        assert (d["form"], d["SH"], d["VEC"], d["LPR"], d["U"], d["HL"], d["LR"]) == \
-            ("narrow", 1, 4, 8, 8, 16, 1), (n, d)
-    assert form(m, nnz, 33)["HL"] == 0
+        assert d["SH"] == 1 and d["VEC"] == 4 and d["LPR"] == lpr and d["HL"] == 0, d
+        assert d["form"] == ("prefetch" if lpr < 64 else "bandwidth"), d  # 64 lanes: one row a wave
     assert form(m, nnz, 15)["SH"] == 0  # 16 columns or fewer: one element per lane
     assert form(m, nnz, 17, b_addr=258 + 2)["SH"] == 1
     for dt in (BF16, F16):
-        for n, vec in ((48, 2), (64, 4), (128, 8)):  # 32: the narrow shape (below)
-            d = form(m, nnz, n, dt)
-            assert d["form"] == "prefetch" and d["VEC"] == vec, (dt, n, d)
+        d = form(m, nnz, 128, dt)
+        assert d["form"] == "prefetch" and d["VEC"] == 8, (dt, d)
 
 
 def test_narrow_rows_of_mid_size_launches():
@@ -176,15 +172,7 @@ def test_narrow_rows_of_mid_size_launches():
             assert (d["form"], d["VEC"], d["LPR"], d["U"], d["HL"], d["LR"]) == \
                 ("narrow", 4, 4, 8, 16, 1), (dt, n, d)
         assert form(m, nnz, 16, dt, b_addr=258)["form"] == "prefetch"  # 2-B aligned B
-        # 17-32 even columns: 8-B lanes over 8 lanes, or 4-B lanes over 16 for a 4-B aligned view
-        for n in (20, 24, 32):
-            d = form(m, nnz, n, dt)
-            assert (d["form"], d["VEC"], d["LPR"], d["U"], d["HL"]) == ("narrow", 4, 8, 8, 16), (n, d)
-        d = form(m, nnz, 32, dt, b_addr=260)
-        assert (d["form"], d["VEC"], d["LPR"], d["U"], d["HL"]) == ("narrow", 2, 16, 8, 16), d
-        d = form(m, nnz, 18, dt)
-        assert (d["form"], d["VEC"], d["LPR"]) == ("narrow", 2, 16), d
-        assert form(m, nnz, 34, dt)["HL"] == 0                           # past 32: unchanged
+        # 17-64 columns: launch_mid_width_pf (test_mid_width_rule)
         assert form(m, K_PREFETCH_NNZ + 1, 16, dt)["form"] == "bandwidth"
         assert form(20_000, 400_000, 16, dt)["form"] == "mid"
     d = form(m, nnz, 8)
@@ -204,23 +192,34 @@ def test_in_kernel_hub_reduce_only_in_mid_size_forms():
     assert form(2708, 10556, 16)["LR"] == 0                     # small form: no plan
 
 
-def test_odd_16bit_widths_of_mid_size_launches():
-    """Round 4: odd 16-bit widths 17-64 in the prefetching form's size range take one-element lanes
-    in 16-lane groups (several column passes) up to N = 48 and 32-lane groups above, with wave
-    items of the same width, instead of one 64-lane row per wave; past kPrefetchNnz and for even
-    (vector) widths the layouts are unchanged."""
+def test_mid_width_rule():
+    """Round 5 (launch_mid_width_pf): rows of 17-64 columns of mid-size launches, fp32 and 16-bit,
+    any width and any element-aligned view, take shifted windows over 8 lanes (VEC 4 up to 32
+    columns; above, VEC 8 for 16-bit and VEC 4 over 16 lanes for fp32) with 32-lane wave items of
+    HV elements (one column pass), hubs added in the kernel.  Both sides of every bound: 16 and 65
+    columns, kPrefetchNnz, the mid / small forms below, f64."""
     m, nnz = 169_343, 1_166_243
-    for dt in (BF16, F16):
-        for n, lpr in ((17, 16), (41, 16), (47, 16), (48, 16), (49, 32), (63, 32)):
-            if n % 2 == 0:
-                continue
+    for dt in (F32, BF16, F16):
+        for n in (17, 18, 24, 25, 31, 32, 33, 40, 41, 47, 48, 57, 63, 64):
             d = form(m, nnz, n, dt)
-            assert (d["form"], d["VEC"], d["LPR"], d["U"], d["HL"], d["LR"]) == \
-                ("narrow", 1, lpr, 16, lpr, 1), (dt, n, d)
-        assert form(m, nnz, 48, dt)["VEC"] == 2                 # even: a vector layout
-        assert form(m, nnz, 48, dt, b_addr=258)["LPR"] == 16    # an unaligned view: one-element lanes
-        assert form(m, nnz, 65, dt)["LPR"] == 64                # past 64 columns: unchanged
+            if n <= 32:
+                want = ("narrow", 1, 4, 8, 8, 32, 1, 1)
+            elif dt == F32:
+                want = ("narrow", 1, 4, 16, 8, 32, 2, 1)
+            else:
+                want = ("narrow", 1, 8, 8, 8, 32, 2, 1)
+            got = (d["form"], d["SH"], d["VEC"], d["LPR"], d["U"], d["HL"], d["HV"], d["LR"])
+            assert got == want, (dt, n, d)
+            # element-aligned views with odd offsets and strides take the same configuration
+            e = 2 if dt != F32 else 4
+            v = form(m, nnz, n, dt, b_addr=256 + e, c_addr=256 + 3 * e, ldb=n + 3, ldc=n + 1)
+            assert (v["form"], v["VEC"], v["LPR"], v["HL"], v["HV"]) == got[:1] + got[2:4] + got[5:7], v
+        assert form(m, nnz, 16, dt)["HL"] == 16                  # 16 columns: the narrow form's own
+        assert form(m, nnz, 65, dt)["HL"] == 0                   # past 64 columns
         assert form(m, K_PREFETCH_NNZ + 1, 41, dt)["form"] == "bandwidth"
+        assert form(20_000, 400_000, 41, dt)["form"] == "mid"
+        assert form(19_717, 88_648, 41, dt)["form"] == "small"
+    assert form(m, nnz, 41, F64)["HV"] == 1 and form(m, nnz, 41, F64)["form"] != "narrow"
 
 
 

@@ -822,3 +822,46 @@ def test_prefetch_form_lane_layouts(device, dtype, n):
     torch.cuda.synchronize()
     assert_bitwise(sub, ref[5_000:35_000], "row range")
     assert torch.equal(o1.view(torch.uint8), out.view(torch.uint8))
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("n", [16, 17, 24, 31, 32, 33, 41, 47, 48, 63, 64, 65])
+def test_mid_width_rule_bitexact(device, dtype, n):
+    """Round 5's rows of 17-64 columns of mid-size launches (launch_mid_width_pf: shifted windows,
+    32-lane wave items of HV elements, hubs added in the kernel) and the widths either side (16:
+    the narrow form, 65: the prefetching form).  Bit-exact against the oracle for the automatic
+    launch (hub rows and heavy rows included), element-offset strided views, a row range and the
+    fused epilogue (the hub tail writes it)."""
+    rng = np.random.default_rng(7300 + n)
+    m, k = 60_000, 60_000
+    deg = rng.integers(0, 30, size=m)
+    deg[11], deg[777], deg[5] = 4000, 600, 1500
+    dt = DTYPES[dtype]
+    rp, ci, v = random_csr(m, k, deg, rng, torch.int32, dt)
+    b = random_dense(k, n, rng, dt)
+    d = (rp.to(device), ci.to(device), v.to(device), b.to(device))
+    desc = ops.describe(m, k, n, ci.numel(), dt, b_addr=d[3].data_ptr(), c_addr=256)
+    assert (desc["form"] == "narrow") == (16 <= n <= 64), desc
+    assert desc["HL"] == (32 if 16 < n <= 64 else (16 if n == 16 else 0)), desc
+    ref = oracle_spmm(rp, ci, v, b)
+    out = fs.spmm(d[0], d[1], d[2], m, k, d[3])
+    torch.cuda.synchronize()
+    assert_bitwise(out, ref, f"{dtype} n={n} auto")
+    # views one element off their allocation, ldb = n + 3, ldc = n + 2
+    bbig = torch.zeros((k, n + 3), dtype=dt, device=device)
+    bbig[:, 1:n + 1] = d[3]
+    cbig = torch.full((m, n + 2), float("nan"), dtype=dt, device=device)
+    ops.spmm_csr_device(d[0], d[1], d[2], bbig[:, 1:n + 1], m, k, out=cbig[:, 1:n + 1])
+    torch.cuda.synchronize()
+    assert_bitwise(cbig[:, 1:n + 1], ref, f"{dtype} n={n} offset views")
+    assert torch.isnan(cbig[:, 0]).all() and torch.isnan(cbig[:, n + 1]).all()
+    kern = ops.SpmmCsrKernel(m, k, n, ci.numel(), torch.int32, dt, device)
+    sub = torch.full((30_000, n), float("nan"), dtype=dt, device=device)
+    kern(*d, sub, row_begin=5_000, row_end=35_000)
+    torch.cuda.synchronize()
+    assert_bitwise(sub, ref[5_000:35_000], f"{dtype} n={n} row range")
+    bias = random_dense(1, n, rng, dt)[0]
+    o3 = torch.full((m, n), float("nan"), dtype=dt, device=device)
+    kern(*d, o3, bias=bias.to(device), relu=True)
+    torch.cuda.synchronize()
+    assert_bitwise(o3, oracle.bias_act(ref, to_oracle(bias), "relu", dtype=dtype), f"{dtype} n={n} epilogue")
