@@ -1627,18 +1627,24 @@ int launch_vec(const Launch& L, int lpr, bool nt) {
 // several 64-lane passes there: products N = 99 / 301 10.6 / 31.2 -> 8.5 / 25.2 ms.  At 17-63
 // columns one pass of single elements is as fast or faster (N = 41 / 47 / 63: 4.6 / 5.0 / 6.1 ms
 // against 4.8 / 5.2 / 6.2; such rows cost whole 128-B lines either way); profiles/r03ad_sweep.jsonl.
+// Round 5: 16-bit rows whose width is not a multiple of 8 above N = 64 the same way (8-element
+// windows at 2-B alignment, scripts/unaligned_probe.hip) instead of one element per lane over 64
+// lanes: 1M power-law bf16 N = 99 / 127 / 255 1,490 / 1,556 / 3,031 -> 917 / 1,040 / 1,799 us
+// (tuning entries 10122 / 10123, gpurun_out/r05h_2_py.txt; N = 128 / 256: 853 / 1,489).
 template <typename T, typename I>
 int launch_shift(const Launch& L, bool nt) {
-  const int lpr = pick_lpr(L.n, 4);
+  constexpr int V = 16 / (int)sizeof(T);
+  const int lpr = pick_lpr(L.n, V);
   switch (lpr) {
-    case 8: return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L);
-    case 16: return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L);
+    case 4: return launch_cfg<T, I, Cfg<V, 4, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L);
+    case 8: return launch_cfg<T, I, Cfg<V, 8, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L);
+    case 16: return launch_cfg<T, I, Cfg<V, 16, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L);
     case 32:
-      return nt ? launch_cfg<T, I, Cfg<4, 32, 8, 4, true, false, false, false, false, true, 0, 16, true>>(L)
-                : launch_cfg<T, I, Cfg<4, 32, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L);
+      return nt ? launch_cfg<T, I, Cfg<V, 32, 8, 4, true, false, false, false, false, true, 0, 16, true>>(L)
+                : launch_cfg<T, I, Cfg<V, 32, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L);
     default:
-      return nt ? launch_cfg<T, I, Cfg<4, 64, 8, 4, true, false, false, false, false, true, 0, 16, true>>(L)
-                : launch_cfg<T, I, Cfg<4, 64, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L);
+      return nt ? launch_cfg<T, I, Cfg<V, 64, 8, 4, true, false, false, false, false, true, 0, 16, true>>(L)
+                : launch_cfg<T, I, Cfg<V, 64, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L);
   }
 }
 
@@ -1663,11 +1669,12 @@ bool use_shift_pf_form(const Launch& L, int elem_bytes) {
 }
 
 bool use_shift_form(const Launch& L, int elem_bytes) {
-  return L.sched.variant == 0 && elem_bytes == 4 && L.n > 64 && L.n % 4 != 0 &&
+  const bool odd = (elem_bytes == 4 && L.n % 4 != 0) || (elem_bytes == 2 && L.n % 8 != 0);
+  return L.sched.variant == 0 && (elem_bytes == 4 || elem_bytes == 2) && L.n > 64 && odd &&
          !use_small_form(L.nrows, L.nnz_est, L.n, L.sched) &&
          !use_mid_form(L.nrows, L.nnz_est, L.n, L.sched) &&
          !use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched) &&
-         ((uintptr_t)L.b % 4) == 0 && ((uintptr_t)L.c % 4) == 0;
+         ((uintptr_t)L.b % elem_bytes) == 0 && ((uintptr_t)L.c % elem_bytes) == 0;
 }
 
 // Rows of 64 B in fp32 (N = 16) above the mid form: four lanes of float4 per light row (16 rows
@@ -1764,10 +1771,12 @@ int launch_typed(const Launch& L) {
     if (use_narrow_pf_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
       return launch_narrow_pf<T, I>(L);
   }
-  if constexpr (sizeof(T) == 4) {
-    if (use_narrow_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L)) return launch_narrow<T, I>(L);
+  if constexpr (sizeof(T) == 2 || sizeof(T) == 4) {
     if (use_shift_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
       return launch_shift<T, I>(L, (L.b_rows * L.ldb * (int64_t)sizeof(T)) > kNtBytes);
+  }
+  if constexpr (sizeof(T) == 4) {
+    if (use_narrow_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L)) return launch_narrow<T, I>(L);
 #ifndef OFX_AB_NO_SHIFT_PF  // A/B builds only (scripts/ab_build.sh)
     if (use_shift_pf_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L)) return launch_shift_pf<T, I>(L);
 #endif

@@ -97,6 +97,17 @@ int launch_tuned(const Launch& L, int id) {
       case 117: if (L.n >= 8) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR, 2>>(L); break;
       case 118: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR, 2>>(L); break;
       case 119: if (L.n >= 8) return launch_cfg<T, I, Cfg<4, 16, 4, 4, false, P, false, W, false, true, 32, 16, true, kLR, 2>>(L); break;
+      // the same shape either side of 17-64 columns: 65-128 (4-element wave lanes), 129-256
+      // (8-element, 32-B wave lanes), and 1-15 columns (16-lane one-element wave items)
+      case 126: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 32, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR, 4>>(L); break;
+      case 127: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 32, 4, 4, false, P, false, W, false, true, 32, 16, true, kLR, 4>>(L); break;
+      case 128: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR, 4>>(L); break;
+      case 129: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 32, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR, 8>>(L); break;
+      case 130: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
+      case 131: return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L);
+      case 132: if (L.n >= 2) return launch_cfg<T, I, Cfg<2, 4, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
+      case 139: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 32, 8, 4, false, P, false, W, false, true, 32, 8, true, kLR, 8>>(L); break;
+      case 141: return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, P, false, W, false, true, 4, 16, false, kLR>>(L);
       default: break;
     }
   }
@@ -133,6 +144,13 @@ int launch_tuned(const Launch& L, int id) {
       case 123: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 32, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L); break;
       case 124: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 64, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L); break;
       case 125: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR, 4>>(L); break;
+      case 134: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 32, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR, 8>>(L); break;
+      case 135: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
+      case 136: return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, P, false, W, false, true, 16, 16, false, kLR>>(L);
+      case 137: if (L.n >= 2) return launch_cfg<T, I, Cfg<2, 4, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
+      case 138: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 4, 4, false, P, false, W, false, true, 32, 16, true, kLR, 4>>(L); break;
+      case 140: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 32, 8, 4, false, P, false, W, false, true, 32, 8, true, kLR, 8>>(L); break;
+      case 142: return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, P, false, W, false, true, 4, 16, false, kLR>>(L);
       default: break;
     }
   }

@@ -77,6 +77,14 @@ def test_shifted_window_bandwidth_only():
     assert form(m, big, 99, b_addr=260)["SH"] == 1  # 16-B accesses at 4-B alignment
     with pytest.raises(ops._lib.OfxError):  # an fp32 view off 4-B alignment has no lane layout
         form(m, big, 99, b_addr=258)
+    # round 5: 16-bit widths above 64 that are not a multiple of 8 (8-element windows, 2-B aligned)
+    for dt in (BF16, F16):
+        for n, lpr in ((65, 16), (98, 16), (99, 16), (127, 16), (255, 32), (301, 64)):
+            d = form(m, big, n, dt)
+            assert (d["form"], d["SH"], d["VEC"], d["LPR"]) == ("bandwidth", 1, 8, lpr), (dt, n, d)
+            assert form(m, big, n, dt, b_addr=258, c_addr=262)["SH"] == 1
+        assert form(m, big, 104, dt)["SH"] == 0 and form(m, big, 104, dt)["VEC"] == 8
+        assert form(m, big, 63, dt)["SH"] == 0  # 64 columns or fewer: N / 16 elements per lane
 
 
 def test_narrow16_lanes():

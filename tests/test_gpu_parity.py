@@ -865,3 +865,38 @@ def test_mid_width_rule_bitexact(device, dtype, n):
     kern(*d, o3, bias=bias.to(device), relu=True)
     torch.cuda.synchronize()
     assert_bitwise(o3, oracle.bias_act(ref, to_oracle(bias), "relu", dtype=dtype), f"{dtype} n={n} epilogue")
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+@pytest.mark.parametrize("n", [64, 65, 66, 99, 104, 127, 255])
+def test_shifted_window_16bit_wide_rows(device, dtype, n):
+    """Round 5: 16-bit widths above 64 that are not a multiple of 8 in the bandwidth
+    configuration (above kPrefetchNnz) run 8-element windows at 2-B alignment, the last one
+    shifted to end at column n - 1 (launch_shift).  Bit-exact against the oracle for contiguous
+    operands, element-offset strided views and hub rows, and equal to the one-element-per-lane
+    configuration forced; 64 and 104 columns (the widths either side) keep their layouts."""
+    rng = np.random.default_rng(8100 + n)
+    m, k = 120_000, 90_000
+    deg = rng.integers(0, 60, size=m)
+    deg[17], deg[9_999] = 3000, 700
+    dt = DTYPES[dtype]
+    rp, ci, v = random_csr(m, k, deg, rng, torch.int32, dt)
+    assert ci.numel() > (3 << 20)
+    b = random_dense(k, n, rng, dt)
+    d = (rp.to(device), ci.to(device), v.to(device), b.to(device))
+    desc = ops.describe(m, k, n, ci.numel(), dt, b_addr=d[3].data_ptr(), c_addr=256)
+    assert desc["form"] == "bandwidth" and desc["SH"] == (1 if n > 64 and n % 8 else 0), desc
+    ref = oracle_spmm(rp, ci, v, b)
+    out = fs.spmm(d[0], d[1], d[2], m, k, d[3])
+    torch.cuda.synchronize()
+    assert_bitwise(out, ref, f"{dtype} n={n} auto")
+    o1 = ops.spmm_csr_device(*d, m, k, options=ops.make_options(variant=164))
+    torch.cuda.synchronize()
+    assert torch.equal(o1.view(torch.int16), out.view(torch.int16))
+    bbig = torch.zeros((k, n + 3), dtype=dt, device=device)
+    bbig[:, 1:n + 1] = d[3]
+    cbig = torch.full((m, n + 2), float("nan"), dtype=dt, device=device)
+    ops.spmm_csr_device(d[0], d[1], d[2], bbig[:, 1:n + 1], m, k, out=cbig[:, 1:n + 1])
+    torch.cuda.synchronize()
+    assert_bitwise(cbig[:, 1:n + 1], ref, f"{dtype} n={n} offset views")
+    assert torch.isnan(cbig[:, 0]).all() and torch.isnan(cbig[:, n + 1]).all()
