@@ -1652,20 +1652,25 @@ int launch_shift(const Launch& L, bool nt) {
 // last window, U = 16 loads in flight and the next (col, val) batch prefetched, instead of one
 // element per lane (N <= 64: up to 64 lanes, one row per wave).  Hubs added in the kernel (LR), as
 // in the rest of the prefetching form.
+// (Round 5: rows up to 128 / 256 columns take launch_mid_width_pf; this serves the wider ones,
+// and 16-bit rows in 8-element windows the same way.)
 template <typename T, typename I>
 int launch_shift_pf(const Launch& L) {
-  switch (pick_lpr(L.n, 4)) {
-    case 8: return launch_cfg<T, I, Cfg<4, 8, 16, 4, false, true, false, false, false, true, 0, 16, true, kLR>>(L);
-    case 16: return launch_cfg<T, I, Cfg<4, 16, 16, 4, false, true, false, false, false, true, 0, 16, true, kLR>>(L);
-    case 32: return launch_cfg<T, I, Cfg<4, 32, 16, 4, false, true, false, false, false, true, 0, 16, true, kLR>>(L);
-    default: return launch_cfg<T, I, Cfg<4, 64, 16, 4, false, false, false, false, false, true, 0, 16, true, kLR>>(L);
+  constexpr int V = 16 / (int)sizeof(T);
+  switch (pick_lpr(L.n, V)) {
+    case 4: return launch_cfg<T, I, Cfg<V, 4, 16, 4, false, true, false, false, false, true, 0, 16, true, kLR>>(L);
+    case 8: return launch_cfg<T, I, Cfg<V, 8, 16, 4, false, true, false, false, false, true, 0, 16, true, kLR>>(L);
+    case 16: return launch_cfg<T, I, Cfg<V, 16, 16, 4, false, true, false, false, false, true, 0, 16, true, kLR>>(L);
+    case 32: return launch_cfg<T, I, Cfg<V, 32, 16, 4, false, true, false, false, false, true, 0, 16, true, kLR>>(L);
+    default: return launch_cfg<T, I, Cfg<V, 64, 16, 4, false, false, false, false, false, true, 0, 16, true, kLR>>(L);
   }
 }
 
 bool use_shift_pf_form(const Launch& L, int elem_bytes) {
-  return L.sched.variant == 0 && elem_bytes == 4 && L.n > 16 && L.n % 4 != 0 &&
+  const bool odd = (elem_bytes == 4 && L.n % 4 != 0) || (elem_bytes == 2 && L.n % 8 != 0);
+  return L.sched.variant == 0 && (elem_bytes == 4 || elem_bytes == 2) && L.n > 16 && odd &&
          use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched) &&
-         ((uintptr_t)L.b % 4) == 0 && ((uintptr_t)L.c % 4) == 0;
+         ((uintptr_t)L.b % elem_bytes) == 0 && ((uintptr_t)L.c % elem_bytes) == 0;
 }
 
 bool use_shift_form(const Launch& L, int elem_bytes) {
@@ -1730,18 +1735,39 @@ int launch_narrow_pf(const Launch& L) {
 // 33-64 97-103 -> 79-82, bf16 17 / 24 94 / 84 -> 68 / 66, bf16 33-63 125-160 -> 81-82 and N = 64
 // 94 -> 79; 60k x 1.5M fp32 N = 17 72 -> 55, bf16 N = 47 / 63 118 / -> 79.  Same bits: only who
 // adds changes.
+// The same shape either side (entries 10130-10142, gpurun_out/r05i_1_py.txt, arxiv-shaped):
+// rows of 1-15 columns (8 and 16 keep the narrow forms when aligned) in 4-lane groups, one
+// element per lane below 4 columns and shifted 4-element windows above, with 16-lane wave items
+// -- fp32 N = 1 / 4 / 12 / 15 75 / 86 / 73 / 83 -> 45 / 46 / 47 / 49 us, bf16 100 / 105 / 83 / 92
+// -> 47 / 48 / 50 / 50; rows of 65-128 columns in 8-element windows over 16 lanes with 4-element
+// wave lanes -- fp32 N = 65 / 99 / 128 143 / 148 / 147 -> 110 / 113 / 114, bf16 N = 65 / 99 / 128
+// 463 / 467 / 151 -> 111 / 112 / 109; and 16-bit rows of 129-256 columns, 8-element wave lanes
+// with 8 in flight -- bf16 N = 129 / 200 / 255 / 256 656 / 166 / 857 / 164 -> 155 / 150 / 158 /
+// 150.  fp32 rows above 128 columns keep their layouts (as fast: 173-210 us either way).
 template <typename T, typename I>
 int launch_mid_width_pf(const Launch& L) {
+  if (L.n < 4)
+    return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
+  if (L.n <= 16)
+    return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 16, 16, true, kLR>>(L);
   if (L.n <= 32)
     return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, true, false, true, false, true, 32, 16, true, kLR>>(L);
-  if constexpr (sizeof(T) == 2)
-    return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, true, false, true, false, true, 32, 16, true, kLR, 2>>(L);
-  else
-    return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, true, false, true, false, true, 32, 16, true, kLR, 2>>(L);
+  if (L.n <= 64) {
+    if constexpr (sizeof(T) == 2)
+      return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, true, false, true, false, true, 32, 16, true, kLR, 2>>(L);
+    else
+      return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, true, false, true, false, true, 32, 16, true, kLR, 2>>(L);
+  }
+  if constexpr (sizeof(T) == 2) {
+    if (L.n > 128)
+      return launch_cfg<T, I, Cfg<8, 32, 8, 4, false, true, false, true, false, true, 32, 8, true, kLR, 8>>(L);
+  }
+  return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, true, false, true, false, true, 32, 16, true, kLR, 4>>(L);
 }
 
 bool use_mid_width_pf_form(const Launch& L, int elem_bytes) {
-  return L.sched.variant == 0 && (elem_bytes == 2 || elem_bytes == 4) && L.n > 16 && L.n <= 64 &&
+  const int64_t top = elem_bytes == 2 ? 256 : 128;
+  return L.sched.variant == 0 && (elem_bytes == 2 || elem_bytes == 4) && L.n >= 1 && L.n <= top &&
          use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched) &&
          ((uintptr_t)L.b % elem_bytes) == 0 && ((uintptr_t)L.c % elem_bytes) == 0;
 }
@@ -1763,20 +1789,22 @@ int launch_typed(const Launch& L) {
                 "spmm_csr: tuning variant %d needs B under 4 GiB", L.sched.variant);
     return launch_tuned<T, I>(L, L.sched.variant - 10000);
   }
-  if constexpr (sizeof(T) == 2 || sizeof(T) == 4) {
-    if (use_mid_width_pf_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
-      return launch_mid_width_pf<T, I>(L);
-  }
+  // the narrow forms first (8 / 16 columns with aligned rows), then every other width of a
+  // mid-size launch up to 128 (fp32) / 256 (16-bit) columns
   if constexpr (sizeof(T) <= 4) {
     if (use_narrow_pf_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
       return launch_narrow_pf<T, I>(L);
   }
+  if constexpr (sizeof(T) == 4) {
+    if (use_narrow_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L)) return launch_narrow<T, I>(L);
+  }
   if constexpr (sizeof(T) == 2 || sizeof(T) == 4) {
+    if (use_mid_width_pf_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
+      return launch_mid_width_pf<T, I>(L);
     if (use_shift_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
       return launch_shift<T, I>(L, (L.b_rows * L.ldb * (int64_t)sizeof(T)) > kNtBytes);
   }
-  if constexpr (sizeof(T) == 4) {
-    if (use_narrow_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L)) return launch_narrow<T, I>(L);
+  if constexpr (sizeof(T) == 2 || sizeof(T) == 4) {
 #ifndef OFX_AB_NO_SHIFT_PF  // A/B builds only (scripts/ab_build.sh)
     if (use_shift_pf_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L)) return launch_shift_pf<T, I>(L);
 #endif

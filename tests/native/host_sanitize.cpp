@@ -418,10 +418,10 @@ void check_describe() {
     EXPECT(form(OFX_DT_FLOAT, n).find("VEC=4 LPR=16") != std::string::npos &&
                form(OFX_DT_FLOAT, n).find("SH=1") != std::string::npos,
            "shifted window LPR 16, fp32 N=%lld: %s", (long long)n, form(OFX_DT_FLOAT, n).c_str());
-  for (int64_t n : {65, 99, 127})
-    EXPECT(form(OFX_DT_FLOAT, n).find("LPR=32") != std::string::npos &&
-               form(OFX_DT_FLOAT, n).find("SH=1") != std::string::npos,
-           "shifted window LPR 32, fp32 N=%lld: %s", (long long)n, form(OFX_DT_FLOAT, n).c_str());
+  for (int64_t n : {65, 99, 127})  // round 5: launch_mid_width_pf up to 128 columns
+    EXPECT(form(OFX_DT_FLOAT, n).find("VEC=8 LPR=16") != std::string::npos &&
+               form(OFX_DT_FLOAT, n).find("HV=4") != std::string::npos,
+           "mid-width 8-element windows, fp32 N=%lld: %s", (long long)n, form(OFX_DT_FLOAT, n).c_str());
   for (int64_t n : {131, 301})
     EXPECT(form(OFX_DT_FLOAT, n).find("LPR=64") != std::string::npos &&
                form(OFX_DT_FLOAT, n).find("SH=1") != std::string::npos,

@@ -38,20 +38,18 @@ def test_small_form_bounds():
 def test_mid_form_bounds():
     assert form(K_SMALL_ROWS, K_MID_ELEMS // 128, 128)["form"] == "mid"
     above = form(K_SMALL_ROWS, K_MID_ELEMS // 128 + 1, 128)
-    assert above["form"] == "prefetch" and above["BI"] == 0
+    assert above["form"] == "narrow" and above["BI"] == 0 and above["PF"] == 1
     assert form(K_SMALL_ROWS + 1, 400_000, 64)["form"] == "narrow"  # rows bound it too (the
-    assert form(K_SMALL_ROWS + 1, 400_000, 128)["form"] == "prefetch"  # prefetching range)
+    assert form(K_SMALL_ROWS + 1, 400_000, 256)["form"] != "mid"     # prefetching range)
 
 
 @pytest.mark.parametrize("n", [32, 64, 128])
 def test_prefetch_form_bound(n):
     m = 120_000
     below, above = form(m, K_PREFETCH_NNZ, n), form(m, K_PREFETCH_NNZ + 1, n)
-    # 17-64 columns: the shifted window with 32-lane wave items ("narrow", round 5)
-    assert below["form"] == ("narrow" if n <= 64 else "prefetch") and below["PF"] == 1
+    # up to 128 columns: the shifted window with 32-lane wave items ("narrow", round 5)
+    assert below["form"] == "narrow" and below["PF"] == 1 and below["WH"] == 1
     assert above["form"] == "bandwidth" and above["PF"] == 0 and above["U"] == 8
-    # wave items only at 16 < N <= 64
-    assert below["WH"] == (1 if n <= 64 else 0)
 
 
 def test_narrow_form_n16_fp32():
@@ -63,9 +61,10 @@ def test_narrow_form_n16_fp32():
     # above kPrefetchNnz fp32 only (16-bit N = 16 below it: test_narrow_rows_of_mid_size_launches),
     # N = 16 only, 16-B aligned only
     assert form(m, K_PREFETCH_NNZ + 1, 16, BF16)["form"] != "narrow"
-    assert form(m, K_PREFETCH_NNZ, 65)["form"] == "prefetch"
+    assert form(m, K_PREFETCH_NNZ, 129)["HL"] == 0
     assert form(m, K_PREFETCH_NNZ + 1, 32)["form"] == "bandwidth"
-    assert form(m, K_PREFETCH_NNZ, 16, b_addr=260)["form"] != "narrow"
+    unaligned = form(m, K_PREFETCH_NNZ, 16, b_addr=260)  # the mid-width shape, shifted windows
+    assert (unaligned["VEC"], unaligned["LPR"], unaligned["SH"]) == (4, 4, 1), unaligned
 
 
 def test_shifted_window_bandwidth_only():
@@ -118,7 +117,7 @@ def test_row_range_uses_its_share_of_nonzeros():
     assert d["form"] == "bandwidth"
     # a small slice of a mid-size graph drops to the prefetching or mid form
     d = form(169_343, 1_166_243, 128, row_begin=0, row_end=40_000)
-    assert d["form"] == "prefetch"
+    assert d["PF"] == 1 and d["form"] == "narrow"  # the prefetching range's mid-width shape
 
 
 def test_row_range_with_its_known_nonzeros():
@@ -130,7 +129,7 @@ def test_row_range_with_its_known_nonzeros():
     rng = dict(row_begin=0, row_end=m // 8)
     est = form(m, nnz, 128, **rng)
     assert form(m, nnz, 128, options=ops.make_options(range_nnz=0), **rng) == est
-    assert form(m, nnz, 128, options=ops.make_options(range_nnz=2_000_000), **rng)["form"] == "prefetch"
+    assert form(m, nnz, 128, options=ops.make_options(range_nnz=2_000_000), **rng)["PF"] == 1
     arxiv = dict(row_begin=0, row_end=30_000)  # estimated 206k nonzeros: the mid form
     assert form(169_343, 1_166_243, 64, **arxiv)["form"] == "mid"
     assert form(169_343, 1_166_243, 64, options=ops.make_options(range_nnz=100_000),
@@ -157,16 +156,16 @@ def test_prefetch_form_layouts():
     """The prefetching form's lane layouts (round 4): odd fp32 widths above 16 take 16-B lanes
     with the shifted last window; 16-bit rows of <= 128 B take N / 16 elements per lane."""
     m, nnz = 169_343, 1_166_243
-    # above 64 columns: the shifted 16-B window of the prefetching form
-    for n, lpr in ((99, 32), (127, 32), (255, 64)):
+    # above 128 columns: the shifted 16-B window of the prefetching form
+    for n, lpr in ((129, 64), (255, 64)):
         d = form(m, nnz, n)
         assert d["SH"] == 1 and d["VEC"] == 4 and d["LPR"] == lpr and d["HL"] == 0, d
         assert d["form"] == ("prefetch" if lpr < 64 else "bandwidth"), d  # 64 lanes: one row a wave
-    assert form(m, nnz, 15)["SH"] == 0  # 16 columns or fewer: one element per lane
     assert form(m, nnz, 17, b_addr=258 + 2)["SH"] == 1
     for dt in (BF16, F16):
-        d = form(m, nnz, 128, dt)
-        assert d["form"] == "prefetch" and d["VEC"] == 8, (dt, d)
+        d = form(m, nnz, 257, dt)  # above 256 columns: 8-element shifted windows
+        assert d["SH"] == 1 and d["VEC"] == 8 and d["HL"] == 0, (dt, d)
+        assert form(m, nnz, 512, dt)["VEC"] == 8
 
 
 def test_narrow_rows_of_mid_size_launches():
@@ -179,14 +178,16 @@ def test_narrow_rows_of_mid_size_launches():
             d = form(m, nnz, n, dt)
             assert (d["form"], d["VEC"], d["LPR"], d["U"], d["HL"], d["LR"]) == \
                 ("narrow", 4, 4, 8, 16, 1), (dt, n, d)
-        assert form(m, nnz, 16, dt, b_addr=258)["form"] == "prefetch"  # 2-B aligned B
+        d = form(m, nnz, 16, dt, b_addr=258)  # 2-B aligned B: the mid-width shape
+        assert (d["form"], d["VEC"], d["LPR"], d["SH"]) == ("narrow", 4, 4, 1), d
         # 17-64 columns: launch_mid_width_pf (test_mid_width_rule)
         assert form(m, K_PREFETCH_NNZ + 1, 16, dt)["form"] == "bandwidth"
         assert form(20_000, 400_000, 16, dt)["form"] == "mid"
     d = form(m, nnz, 8)
     assert (d["form"], d["VEC"], d["LPR"], d["U"], d["HL"]) == ("narrow", 2, 4, 4, 16), d
-    assert form(m, nnz, 8, b_addr=260)["form"] == "prefetch"  # 4-B aligned B: one element per lane
-    assert form(m, nnz, 4)["form"] == "prefetch"
+    d = form(m, nnz, 8, b_addr=260)  # 4-B aligned B: the mid-width shape
+    assert (d["form"], d["VEC"], d["LPR"], d["SH"]) == ("narrow", 4, 4, 1), d
+    assert form(m, nnz, 4)["form"] == "narrow"
 
 
 def test_in_kernel_hub_reduce_only_in_mid_size_forms():
@@ -201,29 +202,41 @@ def test_in_kernel_hub_reduce_only_in_mid_size_forms():
 
 
 def test_mid_width_rule():
-    """Round 5 (launch_mid_width_pf): rows of 17-64 columns of mid-size launches, fp32 and 16-bit,
-    any width and any element-aligned view, take shifted windows over 8 lanes (VEC 4 up to 32
-    columns; above, VEC 8 for 16-bit and VEC 4 over 16 lanes for fp32) with 32-lane wave items of
-    HV elements (one column pass), hubs added in the kernel.  Both sides of every bound: 16 and 65
-    columns, kPrefetchNnz, the mid / small forms below, f64."""
+    """Round 5 (launch_mid_width_pf): rows of 1-128 columns (fp32) / 1-256 (16-bit) of mid-size
+    launches, any width and any element-aligned view, except 8 / 16 columns with aligned rows (the
+    narrow forms): shifted windows (one element per lane below 4 columns) with wave items of HL
+    lanes x HV elements, one column pass, hubs added in the kernel.  Both sides of every bound:
+    3 / 4, 16 / 17, 32 / 33, 64 / 65, 128 / 129, 256 / 257 columns, kPrefetchNnz, the mid / small
+    forms below, f64."""
     m, nnz = 169_343, 1_166_243
     for dt in (F32, BF16, F16):
-        for n in (17, 18, 24, 25, 31, 32, 33, 40, 41, 47, 48, 57, 63, 64):
+        top = 128 if dt == F32 else 256
+        for n in (1, 2, 3, 4, 5, 7, 9, 12, 15, 17, 18, 24, 25, 31, 32, 33, 40, 41, 47, 48, 57, 63,
+                  64, 65, 99, 127, 128, 129, 200, 255, 256):
+            if n > top:
+                continue
             d = form(m, nnz, n, dt)
-            if n <= 32:
+            if n < 4:
+                want = ("narrow", 0, 1, 4, 8, 16, 1, 1)
+            elif n <= 16:
+                want = ("narrow", 1, 4, 4, 8, 16, 1, 1)
+            elif n <= 32:
                 want = ("narrow", 1, 4, 8, 8, 32, 1, 1)
-            elif dt == F32:
-                want = ("narrow", 1, 4, 16, 8, 32, 2, 1)
+            elif n <= 64:
+                want = ("narrow", 1, 4, 16, 8, 32, 2, 1) if dt == F32 else ("narrow", 1, 8, 8, 8, 32, 2, 1)
+            elif n <= 128:
+                want = ("narrow", 1, 8, 16, 8, 32, 4, 1)
             else:
-                want = ("narrow", 1, 8, 8, 8, 32, 2, 1)
+                want = ("narrow", 1, 8, 32, 8, 32, 8, 1)
             got = (d["form"], d["SH"], d["VEC"], d["LPR"], d["U"], d["HL"], d["HV"], d["LR"])
             assert got == want, (dt, n, d)
             # element-aligned views with odd offsets and strides take the same configuration
             e = 2 if dt != F32 else 4
             v = form(m, nnz, n, dt, b_addr=256 + e, c_addr=256 + 3 * e, ldb=n + 3, ldc=n + 1)
             assert (v["form"], v["VEC"], v["LPR"], v["HL"], v["HV"]) == got[:1] + got[2:4] + got[5:7], v
-        assert form(m, nnz, 16, dt)["HL"] == 16                  # 16 columns: the narrow form's own
-        assert form(m, nnz, 65, dt)["HL"] == 0                   # past 64 columns
+        for n in (8, 16):  # aligned 8 / 16 columns: the narrow forms' own shapes
+            assert form(m, nnz, n, dt)["SH"] == 0 and form(m, nnz, n, dt)["HL"] == 16
+        assert form(m, nnz, top + 1, dt)["HL"] == 0              # past the rule's widths
         assert form(m, K_PREFETCH_NNZ + 1, 41, dt)["form"] == "bandwidth"
         assert form(20_000, 400_000, 41, dt)["form"] == "mid"
         assert form(19_717, 88_648, 41, dt)["form"] == "small"

@@ -44,10 +44,9 @@ def test_prefetch_form_threshold(device, side, dtype, n, idx):
     v = v32.to(dt)
     nnz = ci.numel()
     d_form = ops.describe(M, M, n, nnz, dt, idx)
-    # below kPrefetchNnz: the narrow shape for 8 / 16 columns (16-bit; fp32 8) and, round 5, for
-    # every width of 17-64 columns (launch_mid_width_pf)
-    narrow_below = ((dtype, n) in (("f32", 8), ("bf16", 8), ("bf16", 16), ("f16", 8), ("f16", 16))
-                    or 16 < n <= 64)
+    # below kPrefetchNnz: the narrow shapes for 8 / 16 columns and, round 5, launch_mid_width_pf
+    # for every other width up to 128 (fp32) / 256 (16-bit) columns
+    narrow_below = n <= (128 if dtype == "f32" else 256)
     assert d_form["form"] == (("narrow" if narrow_below else "prefetch") if side == "below" else
                               ("narrow" if (dtype, n) == ("f32", 16) else "bandwidth")), d_form
     rng = np.random.default_rng(7000 + n)

@@ -825,11 +825,11 @@ def test_prefetch_form_lane_layouts(device, dtype, n):
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
-@pytest.mark.parametrize("n", [16, 17, 24, 31, 32, 33, 41, 47, 48, 63, 64, 65])
+@pytest.mark.parametrize("n", [1, 3, 4, 7, 12, 15, 16, 17, 24, 31, 32, 33, 41, 47, 48, 63, 64, 65,
+                               99, 128, 129, 255])
 def test_mid_width_rule_bitexact(device, dtype, n):
-    """Round 5's rows of 17-64 columns of mid-size launches (launch_mid_width_pf: shifted windows,
-    32-lane wave items of HV elements, hubs added in the kernel) and the widths either side (16:
-    the narrow form, 65: the prefetching form).  Bit-exact against the oracle for the automatic
+    """Round 5's rows of 17-128 columns of mid-size launches (launch_mid_width_pf: shifted windows,
+    32-lane wave items of HV elements, hubs added in the kernel) and 16 columns (the narrow forms).  Bit-exact against the oracle for the automatic
     launch (hub rows and heavy rows included), element-offset strided views, a row range and the
     fused epilogue (the hub tail writes it)."""
     rng = np.random.default_rng(7300 + n)
@@ -841,8 +841,9 @@ def test_mid_width_rule_bitexact(device, dtype, n):
     b = random_dense(k, n, rng, dt)
     d = (rp.to(device), ci.to(device), v.to(device), b.to(device))
     desc = ops.describe(m, k, n, ci.numel(), dt, b_addr=d[3].data_ptr(), c_addr=256)
-    assert (desc["form"] == "narrow") == (16 <= n <= 64), desc
-    assert desc["HL"] == (32 if 16 < n <= 64 else (16 if n == 16 else 0)), desc
+    top = 128 if dtype == "f32" else 256  # the rule's widths (fp32 above 128: the prefetch form)
+    assert (desc["form"] == "narrow") == (n <= top), desc
+    assert desc["HL"] == (16 if n <= 16 else 32 if n <= top else 0), desc
     ref = oracle_spmm(rp, ci, v, b)
     out = fs.spmm(d[0], d[1], d[2], m, k, d[3])
     torch.cuda.synchronize()
