@@ -103,6 +103,7 @@ constexpr int kBins = 2;
 constexpr int kPlanVals = 2 + kBins;  // hubs, chunks, bins...
 constexpr int64_t kOwnItems = 8;      // hubs with more chunks get their items written wave-wide
 constexpr int kLookWords = 16;        // per plan block: status, totals[4], inclusive prefix[4]
+constexpr int kLookWin = 4;           // windows of 64 predecessors polled per look-back step
 constexpr unsigned long long kAgg = 1, kInc = 2;  // status = tag << 2 | state
 // counters[]: the list's sizes, then the validity words (above)
 constexpr int kEpoch = 4, kHostTag = 5, kOk = 6, kFail = 7, kPoison = 8, kCounterWords = 9;
@@ -306,18 +307,24 @@ __global__ void __launch_bounds__(kBlock)
   int64_t nc[RPT], v[kPlanVals], tot[kPlanVals];
   const int64_t b = blockIdx.x;
   const int64_t base = (b * kBlock + (int64_t)threadIdx.x) * RPT;
+  // this launch's tag (see the top of the file): wave 0 reads the epoch word before it publishes
+  // anything (here, in flight with the row loads below), and the last block advances it only
+  // after every block has published
+  const unsigned long long dev_epoch = threadIdx.x < 64 ? coh_load(counters + kEpoch) : 0ull;
   plan_thread<RPT>(rp, row_begin, nrows, base, split, chunk, heavy, cls, nc, v);
   block_scan_vals(v, tot);
   if (threadIdx.x < 64) {
-    // this launch's tag (see the top of the file): wave 0 reads the epoch word before it
-    // publishes anything, and the last block advances it only after every block has published
-    const unsigned long long dev_epoch = coh_load(counters + kEpoch);
     const unsigned long long epoch = plan_tag(dev_epoch, host_tag);
     // Wave 0 publishes this block's totals (block 0: its inclusive prefix at once), then looks
-    // back over 64 predecessors per step, one per lane: the nearest one holding its inclusive
-    // prefix ends the walk, the aggregates of those after it are added.  One lane per step (the
-    // round-4 first cut) made the chain ~nblocks / 2 memory round trips long: products' 2,392
-    // plan blocks took ~0.7 ms (profiles/r04e_ab.jsonl); 64 lanes cut it 64-fold.
+    // back over up to kLookWin windows of 64 predecessors per step, one predecessor per lane and
+    // window, every window's status polled in the same round trip: the nearest predecessor
+    // holding its inclusive prefix ends the walk, the aggregates of those after it are added.
+    // One lane per step (the round-4 first cut) made the chain ~nblocks / 2 memory round trips
+    // long: products' 2,392 plan blocks took ~0.7 ms (profiles/r04e_ab.jsonl); 64 lanes cut it
+    // 64-fold.  Round 5: one window per step still cost a block b >= 64 two round trips per window
+    // (the poll, then the payload) while the inclusive prefixes of its nearest window were not
+    // yet out; kLookWin windows at once make that one poll and one payload round trip for every
+    // block of a launch of <= 256 plan blocks (every mid-size launch).
     const int lane = threadIdx.x;
     unsigned long long* my = look + b * kLookWords;
     if (lane == 0) {
@@ -330,34 +337,62 @@ __global__ void __launch_bounds__(kBlock)
     }
     int64_t pre[kPlanVals] = {};
     bool failed = spin_limit == 0 && b > 0;  // test knob: give up without polling
-    for (int64_t end = failed ? 0 : b; end > 0; end -= 64) {
-      const int64_t p = end - 1 - lane;  // lane 0: the nearest predecessor
-      unsigned long long st = epoch << 2 | kAgg;
-      if (p >= 0) {
-        int spins = 0;  // bounded: a predecessor that never publishes cannot hang the launch
-        while (((st = look_status(look, p)) >> 2) != epoch && ++spins < spin_limit)
-          __builtin_amdgcn_s_sleep(1);
+    for (int64_t end = failed ? 0 : b; end > 0; end -= 64 * kLookWin) {
+      // window w, lane l: predecessor end - 1 - 64 w - l (window 0, lane 0: the nearest)
+      int64_t p[kLookWin];
+      unsigned long long st[kLookWin];
+#pragma unroll
+      for (int w = 0; w < kLookWin; ++w) {
+        p[w] = end - 1 - 64 * w - lane;
+        st[w] = 0;  // no tag: polled below (lanes past block 0 are never read)
       }
-      asm volatile("" ::: "memory");  // the payload loads below issue after the status returned
-      if (__ballot(p >= 0 && (st >> 2) != epoch)) {
+      // every window's status in one round trip; bounded: a predecessor that never publishes
+      // cannot hang the launch
+      for (int spins = 0;;) {
+        bool waiting = false;
+#pragma unroll
+        for (int w = 0; w < kLookWin; ++w)
+          if (p[w] >= 0 && (st[w] >> 2) != epoch) st[w] = look_status(look, p[w]);
+#pragma unroll
+        for (int w = 0; w < kLookWin; ++w) waiting |= p[w] >= 0 && (st[w] >> 2) != epoch;
+        if (!waiting || ++spins >= spin_limit) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      asm volatile("" ::: "memory");  // the payload loads below issue after the statuses returned
+      bool missing = false;
+#pragma unroll
+      for (int w = 0; w < kLookWin; ++w) missing |= p[w] >= 0 && (st[w] >> 2) != epoch;
+      if (__ballot(missing)) {
         failed = true;  // no prefix: this block writes nothing and publishes no prefix
         break;
       }
-      const unsigned long long incs = __ballot(p >= 0 && (st & 3) == kInc);
-      const int stop = incs ? __ffsll((long long)incs) - 1 : 64;  // nearest inclusive lane
-      int64_t x[kPlanVals];
-      const unsigned long long* pw = look + (p >= 0 ? p : 0) * kLookWords;
+      // the nearest inclusive predecessor: the first window holding one, its lowest lane
+      int stop_w = kLookWin, stop = 64;
 #pragma unroll
-      for (int i = 0; i < kPlanVals; ++i)
-        x[i] = (p < 0 || lane > stop) ? 0
-               : (int64_t)coh_load(pw + (lane == stop ? 1 + kPlanVals + i : 1 + i));
+      for (int w = kLookWin - 1; w >= 0; --w) {
+        const unsigned long long incs = __ballot(p[w] >= 0 && (st[w] & 3) == kInc);
+        if (incs) {
+          stop_w = w;
+          stop = __ffsll((long long)incs) - 1;
+        }
+      }
+      int64_t x[kPlanVals] = {};
+#pragma unroll
+      for (int w = 0; w < kLookWin; ++w) {
+        const bool take = p[w] >= 0 && (w < stop_w || (w == stop_w && lane <= stop));
+        const unsigned long long* pw = look + (p[w] >= 0 ? p[w] : 0) * kLookWords;
+        const bool inc = w == stop_w && lane == stop;
+#pragma unroll
+        for (int i = 0; i < kPlanVals; ++i)
+          x[i] += take ? (int64_t)coh_load(pw + (inc ? 1 + kPlanVals + i : 1 + i)) : 0;
+      }
 #pragma unroll
       for (int w = 1; w < 64; w <<= 1)
 #pragma unroll
         for (int i = 0; i < kPlanVals; ++i) x[i] += (int64_t)__shfl_xor((long long)x[i], w, 64);
 #pragma unroll
       for (int i = 0; i < kPlanVals; ++i) pre[i] += x[i];
-      if (incs) break;
+      if (stop_w < kLookWin) break;
     }
     if (lane == 0) {
       s_fail = failed ? 1 : 0;

@@ -95,13 +95,15 @@ def check_planner(ins):
         errs.append(f"{publishes} status publishes behind an inline store wait (expected the totals "
                     f"and the inclusive prefix)")
     # polls: sc1 loads followed by a vmcnt(0) wait within a few instructions, inside a sleep loop
+    # (round 5: the statuses of up to four windows are polled together, each load behind its own
+    # exec mask, the wait after the last, the sleep after the checks)
     loads = [(i, x) for i, x in enumerate(ins) if VMEM_LOAD.match(x)]
     sc1_loads = [(i, x) for i, x in loads if has_sc1(x)]
     if not sc1_loads:
         return errs + ["no sc1 load in the look-back"]
     sleep = [i for i, x in enumerate(ins) if x.startswith("s_sleep")]
-    polls = [i for i, x in sc1_loads if any(WAIT_VM0.match(y) for y in ins[i + 1:i + 5])
-             and any(abs(i - s) < 12 for s in sleep)]
+    polls = [i for i, x in sc1_loads if any(WAIT_VM0.match(y) for y in ins[i + 1:i + 8])
+             and any(0 < s - i < 48 for s in sleep)]
     if not polls:
         return errs + ["no status poll (sc1 load + vmcnt(0) inside the sleep loop)"]
     first, last_poll = min(polls), max(polls)
