@@ -139,14 +139,20 @@ struct PeerHandle {
 };
 static_assert(sizeof(PeerHandle) <= OFX_PEER_HANDLE_BYTES, "peer handle does not fit");
 
-// Opened allocations, by handle bytes (a handle opened twice in one process maps once).
+// Opened allocations, by handle bytes (a handle opened twice in one process maps once), and the
+// pointers handed out, each with its own count (a pointer closed more often than opened is refused
+// rather than taken off another pointer's count).
 struct Opened {
   void* base;
   int refs;
 };
+struct Handed {
+  std::string key;
+  int refs = 0;
+};
 std::mutex g_open_mu;
 std::map<std::string, Opened> g_opened;
-std::map<void*, std::string> g_opened_by_ptr;
+std::map<void*, Handed> g_opened_by_ptr;
 
 int choose_unit(const void* const* bufs, int nranks, const void* dst, uint64_t slot_bytes) {
   auto ok = [&](uint64_t a) {
@@ -195,7 +201,9 @@ extern "C" int ofx_peer_open(const void* handle, void** ptr_out) {
     it->second.refs += 1;
     void* p = static_cast<char*>(it->second.base) + h.offset;
     *ptr_out = p;
-    g_opened_by_ptr[p] = key;
+    Handed& hd = g_opened_by_ptr[p];
+    hd.key = key;
+    hd.refs += 1;
     return OFX_OK;
   });
 }
@@ -206,11 +214,10 @@ extern "C" int ofx_peer_close(void* ptr) {
     std::lock_guard<std::mutex> lock(g_open_mu);
     auto pk = g_opened_by_ptr.find(ptr);
     OFX_REQUIRE(pk != g_opened_by_ptr.end(), OFX_EINVAL, "peer_close: %p was not opened here", ptr);
-    auto it = g_opened.find(pk->second);
+    const std::string key = pk->second.key;
+    if (--pk->second.refs == 0) g_opened_by_ptr.erase(pk);
+    auto it = g_opened.find(key);
     if (--it->second.refs == 0) {
-      // erase the pointer entries of this allocation (every offset opened from it)
-      for (auto q = g_opened_by_ptr.begin(); q != g_opened_by_ptr.end();)
-        q = q->second == pk->second ? g_opened_by_ptr.erase(q) : std::next(q);
       void* base = it->second.base;
       g_opened.erase(it);
       OFX_HIP_CHECK(hipIpcCloseMemHandle(base));
