@@ -108,6 +108,17 @@ int launch_tuned(const Launch& L, int id) {
       case 132: if (L.n >= 2) return launch_cfg<T, I, Cfg<2, 4, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR>>(L); break;
       case 139: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 32, 8, 4, false, P, false, W, false, true, 32, 8, true, kLR, 8>>(L); break;
       case 141: return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, P, false, W, false, true, 4, 16, false, kLR>>(L);
+      // wave items in more, narrower groups (more nonzeros per batch: fewer dependent B-load
+      // rounds per 512-nonzero hub chunk): light rows of the round-5 rule, wave HL x HV, HU
+      case 143: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR, 2>>(L); break;
+      case 144: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 8, 16, true, kLR, 4>>(L); break;
+      case 145: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 8, 8, true, kLR, 4>>(L); break;
+      case 146: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 16, 32, true, kLR, 2>>(L); break;
+      case 147: if (L.n >= 8) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR, 4>>(L); break;
+      case 148: if (L.n >= 8) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 8, 8, true, kLR, 8>>(L); break;
+      case 149: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR, 8>>(L); break;
+      case 150: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 4, 16, true, kLR, 4>>(L); break;
+      case 151: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 8, 16, true, kLR, 2>>(L); break;
       default: break;
     }
   }
@@ -151,6 +162,12 @@ int launch_tuned(const Launch& L, int id) {
       case 138: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 4, 4, false, P, false, W, false, true, 32, 16, true, kLR, 4>>(L); break;
       case 140: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 32, 8, 4, false, P, false, W, false, true, 32, 8, true, kLR, 8>>(L); break;
       case 142: return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, P, false, W, false, true, 4, 16, false, kLR>>(L);
+      case 152: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR, 4>>(L); break;
+      case 153: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 8, 16, true, kLR, 8>>(L); break;
+      case 154: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 8, 8, true, kLR, 8>>(L); break;
+      case 155: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 8, 16, true, kLR, 4>>(L); break;
+      case 156: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR, 2>>(L); break;
+      case 157: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR, 8>>(L); break;
       default: break;
     }
   }

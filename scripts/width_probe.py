@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Mid-size widths, one configuration per spec <graph>:<dtype>:<N>[:<variant>] (graphs of
-scripts/probe_split.py, synthetic power-law, generated once per graph):
+scripts/probe_split.py, synthetic power-law, generated once per graph; <graph>@g<gamma> sets the
+degree exponent, e.g. arxiv@g50 for nearly even degrees, 2.5 by default):
 
   --mode time   (default) per spec: the form the launch takes (ofx_spmm_csr_describe), the median
                 device time of one call over a replayed hipGraph of REPS calls (no host launch
@@ -46,9 +47,10 @@ def main():
         parts = spec.split(":")
         g, dname, n = parts[0], parts[1], int(parts[2])
         variant = int(parts[3]) if len(parts) > 3 else 0
-        if g not in graphs:
-            m, nnz = GRAPHS[g]
-            rp, ci, v = synth.csr(m, m, nnz)
+        if g not in graphs:  # <graph>[@g<gamma>]: the degree exponent (2.5 default; large = even)
+            name, _, gam = g.partition("@g")
+            m, nnz = GRAPHS[name]
+            rp, ci, v = synth.csr(m, m, nnz, gamma=float(gam) if gam else 2.5)
             graphs[g] = (m, nnz, rp, ci, v)
         m, nnz, rp, ci, v = graphs[g]
         dt = DT[dname]
