@@ -1750,8 +1750,15 @@ int launch_mid_width_pf(const Launch& L) {
     return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
   if (L.n <= 16)
     return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 16, 16, true, kLR>>(L);
-  if (L.n <= 32)
-    return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, true, false, true, false, true, 32, 16, true, kLR>>(L);
+  if (L.n <= 32) {
+    // 16-bit: 16-lane wave items of 2-element lanes (entry 10156: bf16 N = 32 64.6 -> 57.3 us
+    // arxiv-shaped, 63.8 -> 57.4 on 60k x 1.5M; fp32 lost with the same shape, 55.4 -> 59.0,
+    // and every narrower wave group lost for both, gpurun_out/r05o_1_py.txt)
+    if constexpr (sizeof(T) == 2)
+      return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, true, false, true, false, true, 16, 16, true, kLR, 2>>(L);
+    else
+      return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, true, false, true, false, true, 32, 16, true, kLR>>(L);
+  }
   if (L.n <= 64) {
     if constexpr (sizeof(T) == 2)
       return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, true, false, true, false, true, 32, 16, true, kLR, 2>>(L);

@@ -221,7 +221,7 @@ def test_mid_width_rule():
             elif n <= 16:
                 want = ("narrow", 1, 4, 4, 8, 16, 1, 1)
             elif n <= 32:
-                want = ("narrow", 1, 4, 8, 8, 32, 1, 1)
+                want = ("narrow", 1, 4, 8, 8, 32, 1, 1) if dt == F32 else ("narrow", 1, 4, 8, 8, 16, 2, 1)
             elif n <= 64:
                 want = ("narrow", 1, 4, 16, 8, 32, 2, 1) if dt == F32 else ("narrow", 1, 8, 8, 8, 32, 2, 1)
             elif n <= 128:

@@ -843,7 +843,8 @@ def test_mid_width_rule_bitexact(device, dtype, n):
     desc = ops.describe(m, k, n, ci.numel(), dt, b_addr=d[3].data_ptr(), c_addr=256)
     top = 128 if dtype == "f32" else 256  # the rule's widths (fp32 above 128: the prefetch form)
     assert (desc["form"] == "narrow") == (n <= top), desc
-    assert desc["HL"] == (16 if n <= 16 else 32 if n <= top else 0), desc
+    hl = 16 if n <= 16 or (n <= 32 and dtype != "f32") else 32 if n <= top else 0
+    assert desc["HL"] == hl, desc
     ref = oracle_spmm(rp, ci, v, b)
     out = fs.spmm(d[0], d[1], d[2], m, k, d[3])
     torch.cuda.synchronize()
