@@ -1631,9 +1631,19 @@ int launch_vec(const Launch& L, int lpr, bool nt) {
 // windows at 2-B alignment, scripts/unaligned_probe.hip) instead of one element per lane over 64
 // lanes: 1M power-law bf16 N = 99 / 127 / 255 1,490 / 1,556 / 3,031 -> 917 / 1,040 / 1,799 us
 // (tuning entries 10122 / 10123, gpurun_out/r05h_2_py.txt; N = 128 / 256: 853 / 1,489).
+// And 16-bit rows of 17-63 columns (but 32) in the bandwidth form, where the N / 16-element
+// lanes left them one element per lane over 32-64 lanes: 4-element windows over 8 lanes up to 31
+// columns, 8-element windows over 8 lanes above (entries 10175 / 10177, gpurun_out/r05t_1_py.txt,
+// 1M power-law bf16 N = 17 / 31 / 33 / 47 / 63: 521 / 551 / 823 / 841 / 862 -> 403 / 487 / 555 /
+// 609 / 674 us; N = 32 / 64 369 / 465 keep their layouts).  fp32 there stays one element per
+// lane: shifted windows moved it by -6..+3% on that graph and +4% on products (round 3).
 template <typename T, typename I>
 int launch_shift(const Launch& L, bool nt) {
   constexpr int V = 16 / (int)sizeof(T);
+  if constexpr (sizeof(T) == 2) {
+    if (L.n < 32)
+      return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L);
+  }
   const int lpr = pick_lpr(L.n, V);
   switch (lpr) {
     case 4: return launch_cfg<T, I, Cfg<V, 4, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L);
@@ -1674,8 +1684,10 @@ bool use_shift_pf_form(const Launch& L, int elem_bytes) {
 }
 
 bool use_shift_form(const Launch& L, int elem_bytes) {
-  const bool odd = (elem_bytes == 4 && L.n % 4 != 0) || (elem_bytes == 2 && L.n % 8 != 0);
-  return L.sched.variant == 0 && (elem_bytes == 4 || elem_bytes == 2) && L.n > 64 && odd &&
+  const bool odd = (elem_bytes == 4 && L.n > 64 && L.n % 4 != 0) ||
+                   (elem_bytes == 2 && L.n > 64 && L.n % 8 != 0) ||
+                   (elem_bytes == 2 && L.n > 16 && L.n < 64 && L.n != 32);
+  return L.sched.variant == 0 && (elem_bytes == 4 || elem_bytes == 2) && odd &&
          !use_small_form(L.nrows, L.nnz_est, L.n, L.sched) &&
          !use_mid_form(L.nrows, L.nnz_est, L.n, L.sched) &&
          !use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched) &&

@@ -119,6 +119,14 @@ int launch_tuned(const Launch& L, int id) {
       case 149: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR, 8>>(L); break;
       case 150: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 4, 16, true, kLR, 4>>(L); break;
       case 151: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 8, 16, true, kLR, 2>>(L); break;
+      // the bandwidth form (above kPrefetchNnz) at widths between the multiples of 16: shifted
+      // windows (170-172), and the wave-item shape without the in-kernel reduce (173, 174)
+      case 170: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L); break;
+      case 171: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L); break;
+      case 172: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L); break;
+      case 173: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 32, 8, true>>(L); break;
+      case 174: if (L.n >= 8) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 32, 8, true, false, 2>>(L); break;
+      case 180: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 16, 8, true>>(L); break;
       default: break;
     }
   }
@@ -168,6 +176,13 @@ int launch_tuned(const Launch& L, int id) {
       case 155: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 8, 16, true, kLR, 4>>(L); break;
       case 156: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR, 2>>(L); break;
       case 157: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR, 8>>(L); break;
+      case 175: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L); break;
+      case 176: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 4, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L); break;
+      case 177: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L); break;
+      case 178: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 32, 8, true, false, 2>>(L); break;
+      case 179: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L); break;
+      case 181: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 16, 8, true, false, 2>>(L); break;
+      case 182: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 16, 8, true>>(L); break;
       default: break;
     }
   }

@@ -83,14 +83,18 @@ def test_shifted_window_bandwidth_only():
             assert (d["form"], d["SH"], d["VEC"], d["LPR"]) == ("bandwidth", 1, 8, lpr), (dt, n, d)
             assert form(m, big, n, dt, b_addr=258, c_addr=262)["SH"] == 1
         assert form(m, big, 104, dt)["SH"] == 0 and form(m, big, 104, dt)["VEC"] == 8
-        assert form(m, big, 63, dt)["SH"] == 0  # 64 columns or fewer: N / 16 elements per lane
+        assert form(m, big, 64, dt)["SH"] == 0 and form(m, big, 32, dt)["SH"] == 0
 
 
 def test_narrow16_lanes():
     m, big = 120_000, K_PREFETCH_NNZ + 1
-    for n, vec in ((8, 1), (16, 1), (32, 2), (48, 2), (64, 4), (128, 8)):
+    for n, vec in ((8, 1), (16, 1), (32, 2), (64, 4), (128, 8)):
         d = form(m, big, n, BF16)
-        assert d["form"] == "bandwidth" and d["VEC"] == vec, (n, d)
+        assert d["form"] == "bandwidth" and d["VEC"] == vec and d["SH"] == 0, (n, d)
+    # round 5: the other widths of 17-63 columns in shifted windows (4 elements to 31, 8 above)
+    for n, vec, lpr in ((17, 4, 8), (24, 4, 8), (31, 4, 8), (33, 8, 8), (48, 8, 8), (63, 8, 8)):
+        d = form(m, big, n, BF16)
+        assert (d["form"], d["VEC"], d["LPR"], d["SH"]) == ("bandwidth", vec, lpr, 1), (n, d)
 
 
 def test_bandwidth_narrow_rows_take_eight_lanes():

@@ -730,9 +730,10 @@ def test_mid_form_block_items(device, dtype, idx, n):
 @pytest.mark.parametrize("n", [8, 16, 24, 48, 64])
 def test_narrow_16bit_bandwidth_layout(device, dtype, idx, n):
     """16-bit rows of <= 128 B in the bandwidth configuration (above kPrefetchNnz nonzeros) take
-    N / 16 elements per lane over >= 16 lanes (launch_typed, narrow16; rounded down to a power of
-    two: N = 24 / 48 -> 1 / 2) instead of the widest vector.  Lane layout only: the same bits as
-    the oracle and as the widest-vector configuration forced."""
+    N / 16 elements per lane over >= 16 lanes (launch_typed, narrow16) at 8 / 16 / 32 / 64
+    columns, and (round 5) shifted 4 / 8-element windows at the other widths (24, 48) instead of
+    the widest vector.  Lane layout only: the same bits as the oracle and as the widest-vector
+    configuration forced."""
     rng = np.random.default_rng(4100 + n)
     m, k = 120_000, 90_000
     deg = rng.integers(0, 60, size=m)
@@ -870,11 +871,11 @@ def test_mid_width_rule_bitexact(device, dtype, n):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
-@pytest.mark.parametrize("n", [64, 65, 66, 99, 104, 127, 255])
+@pytest.mark.parametrize("n", [16, 17, 24, 31, 32, 33, 47, 48, 63, 64, 65, 66, 99, 104, 127, 255])
 def test_shifted_window_16bit_wide_rows(device, dtype, n):
-    """Round 5: 16-bit widths above 64 that are not a multiple of 8 in the bandwidth
-    configuration (above kPrefetchNnz) run 8-element windows at 2-B alignment, the last one
-    shifted to end at column n - 1 (launch_shift).  Bit-exact against the oracle for contiguous
+    """Round 5: 16-bit widths above 64 that are not a multiple of 8, and 17-63 but 32, in the
+    bandwidth configuration (above kPrefetchNnz) run 4 / 8-element windows at 2-B alignment, the
+    last one shifted to end at column n - 1 (launch_shift).  Bit-exact against the oracle for contiguous
     operands, element-offset strided views and hub rows, and equal to the one-element-per-lane
     configuration forced; 64 and 104 columns (the widths either side) keep their layouts."""
     rng = np.random.default_rng(8100 + n)
@@ -887,7 +888,8 @@ def test_shifted_window_16bit_wide_rows(device, dtype, n):
     b = random_dense(k, n, rng, dt)
     d = (rp.to(device), ci.to(device), v.to(device), b.to(device))
     desc = ops.describe(m, k, n, ci.numel(), dt, b_addr=d[3].data_ptr(), c_addr=256)
-    assert desc["form"] == "bandwidth" and desc["SH"] == (1 if n > 64 and n % 8 else 0), desc
+    shifted = (n > 64 and n % 8 != 0) or (16 < n < 64 and n != 32)
+    assert desc["form"] == "bandwidth" and desc["SH"] == (1 if shifted else 0), desc
     ref = oracle_spmm(rp, ci, v, b)
     out = fs.spmm(d[0], d[1], d[2], m, k, d[3])
     torch.cuda.synchronize()
