@@ -1042,9 +1042,21 @@ class RowSplitSpmm:
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
             return float(t.item())
 
+        ref_digest = []
+
+        def digest():
+            # every candidate writes the same bytes: a weighted sum of a strided
+            # sample of this rank's output bits (<= 4M elements), compared with the first one's
+            bits = out.reshape(-1).view({2: torch.int16, 4: torch.int32, 8: torch.int64}[out.element_size()])
+            step = max(1, bits.numel() // 4_000_000)
+            x = bits[::step].to(torch.int64)
+            w = torch.arange(x.numel(), dtype=torch.int64, device=x.device) % 1_000_003 + 1
+            return int((x * w).sum().item()), int(x.numel())
+
         def measure():
             # A candidate that raises on any rank (a host-side error, deterministic across ranks)
-            # is timed as +inf everywhere by the max-reduce, so no rank keeps it.
+            # is timed as +inf everywhere by the max-reduce, so no rank keeps it; so is one whose
+            # output differs from the first candidate's on any rank (a wrong exchange).
             ms = float("inf")
             try:
                 self.step(out)
@@ -1067,7 +1079,18 @@ class RowSplitSpmm:
                 raise  # a peer that never joined: no candidate can be timed, the rank ends
             except Exception as e:  # noqa: BLE001 -- reported, candidate dropped
                 self.tune_errors[f"{self.exchange}/{self.comm_kind}/p{self.chunks}"] = repr(e)
-            return max_over_ranks(ms)
+            ms = max_over_ranks(ms)
+            if not math.isfinite(ms):
+                return ms
+            d = digest()
+            if not ref_digest:  # the first candidate every rank ran: the reference bytes
+                ref_digest.append(d)
+                return ms
+            if max_over_ranks(1.0 if d != ref_digest[0] else 0.0) > 0:
+                self.tune_errors[f"{self.exchange}/{self.comm_kind}/p{self.chunks}"] = \
+                    "output differs from the first candidate's"
+                return float("inf")
+            return ms
 
         # the candidates: (name, setter)
         cands = []

@@ -274,6 +274,65 @@ def test_tune_over_gloo_keeps_one_choice_everywhere():
     _tune_run("cpu")
 
 
+def _tune_corrupt_worker(rank, world, port, q):
+    """tune() compares every candidate's output bits with the first candidate's (a sampled
+    digest, max-reduced over ranks): a candidate made to write other bytes on ONE rank (the
+    pipelined halo exchange, +1 on rank 1's first output row) is dropped on every rank."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    import sys
+    for p in (root, os.path.join(root, "of-spmm_amd")):
+        sys.path.insert(0, p)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oneflow_spmm import ops
+        from oneflow_spmm.distributed import RowSplitSpmm
+        from tests.helpers import power_law_degrees, random_csr, random_dense
+
+        rng = np.random.default_rng(56)
+        m, k, n = 600, 500, 8
+        rp, ci, v = random_csr(m, k, power_law_degrees(m, 9000, k, rng), rng)
+        b = random_dense(k, n, rng)
+        from oracle import oracle
+        lo, hi = oracle.balanced_range(m, world, rank)
+        lrp, n0, n1 = ops.csr_row_slice(rp, lo, hi)
+        rs = RowSplitSpmm(m, k, n, n1 - n0, torch.float32, torch.int32, torch.device("cpu"),
+                          comm="torch")
+        klo, khi = rs.k_range
+        rs.load_shard(b[klo:khi])
+        rs.bind(lrp, ci[n0:n1], v[n0:n1], halo=True)
+        step = rs.step
+
+        def corrupt_step(out, *a, **kw):
+            r = step(out, *a, **kw)
+            if rs.exchange == "halo" and rs.halo_chunks == 2 and rank == 1:
+                out[0] += 1.0
+            return r
+        rs.step = corrupt_step
+        out = torch.empty((hi - lo, n))
+        times = rs.tune(out, reps=1, prune=float("inf"))
+        q.put((rank, sorted(times), " ".join(rs.tune_errors.values())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tune_drops_a_candidate_whose_output_differs():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tune_corrupt_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=5) for _ in range(world)))
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    for rank, (names, err) in res.items():
+        assert "halo/p2" not in names and "halo" in names and "torch/p1" in names, (rank, names)
+        assert "differs" in err, (rank, err)
+
+
 # ---- the same ranks on the GPU --------------------------------------------------------------
 # RCCL refuses two ranks on one GPU, so on a one-GPU box these tests put every rank on cuda:0 and
 # let gloo carry the exchanged bytes (host-staged).  Everything else is the device path the
