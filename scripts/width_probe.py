@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Mid-size widths, one configuration per spec <graph>:<dtype>:<N>[:<variant>] (graphs of
+"""Mid-size widths, one configuration per spec <graph>:<dtype>:<N>[:<variant>[:<heavy>]] (graphs of
 scripts/probe_split.py, synthetic power-law, generated once per graph; <graph>@g<gamma> sets the
 degree exponent, e.g. arxiv@g50 for nearly even degrees, 2.5 by default):
 
@@ -47,6 +47,7 @@ def main():
         parts = spec.split(":")
         g, dname, n = parts[0], parts[1], int(parts[2])
         variant = int(parts[3]) if len(parts) > 3 else 0
+        heavy = int(parts[4]) if len(parts) > 4 else 0  # options.heavy (0: automatic)
         if g not in graphs:  # <graph>[@g<gamma>]: the degree exponent (2.5 default; large = even)
             name, _, gam = g.partition("@g")
             m, nnz = GRAPHS[name]
@@ -56,7 +57,7 @@ def main():
         dt = DT[dname]
         b = synth.dense(0, m, n, dt, device=dev)
         d = (rp.to(dev), ci.to(dev), v.to(dt).to(dev), b)
-        opts = ops.make_options(variant=variant) if variant else None
+        opts = ops.make_options(variant=variant, heavy=heavy) if (variant or heavy) else None
         kern = ops.SpmmCsrKernel(m, m, n, nnz, torch.int32, dt, dev, opts)
         out = torch.empty((m, n), dtype=dt, device=dev)
         desc = ops.describe(m, m, n, nnz, dt, b_addr=b.data_ptr(), c_addr=out.data_ptr(),
