@@ -93,12 +93,16 @@ constexpr bool kLR = false;  // A/B builds only (scripts/ab_build.sh): the spmm_
 #endif
 template <int VEC_, int LPR_, int U_ = 8, int WPB_ = 4, bool NT_ = false, bool PF_ = false,
           bool BNT_ = false, bool WH_ = false, bool BI_ = false, bool BUF_ = true, int HL_ = 0,
-          int HU_ = 16, bool SH_ = false, bool LR_ = false, int HV_ = 1>
+          int HU_ = 16, bool SH_ = false, bool LR_ = false, int HV_ = 1, bool XL_ = false>
 struct Cfg {
   static constexpr int VEC = VEC_, LPR = LPR_, U = U_, WPB = WPB_;
   static constexpr bool NT = NT_, PF = PF_, BNT = BNT_, WH = WH_, BI = BI_, BUF = BUF_, SH = SH_;
   static constexpr bool LR = LR_;
   static constexpr int HL = HL_, HU = HU_, HV = HV_;
+  // XL (with WH and HL): the wave items' products go through LDS instead of cross-lane moves
+  // (accumulate_wave_xl): one group adds them all in nonzero order, so a wave can hold many
+  // narrow groups -- many nonzeros per round of B-row loads -- without G x the moves
+  static constexpr bool XL = XL_;
   // loads in flight per lane of the wave-item form: G * UW * VEC cross-lane moves per batch are
   // unrolled, so UW keeps that at <= 256 (4..32)
   static constexpr int G = LPR < 64 ? 64 / LPR : 1;
@@ -114,6 +118,8 @@ struct WaveMap {
   static constexpr int LPR = K::HL > 0 ? K::HL : K::LPR;
   static constexpr int UW = K::HL > 0 ? K::HU : K::UW;
   static constexpr bool BNT = K::BNT, BUF = K::BUF;
+  // XL: LDS floats per wave for one batch of products (G * UW nonzeros x LPR * VEC columns)
+  static constexpr int XL_FLOATS = (64 / LPR) * UW * LPR * VEC;
 };
 
 template <typename X>
@@ -546,6 +552,89 @@ __device__ __forceinline__ void accumulate_wave(const I* __restrict__ col, const
 #pragma unroll
           for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + x[g2][e];
     }
+  }
+}
+
+// The wave items with the products exchanged through LDS (Cfg::XL): the same batches as
+// accumulate_wave (group q of G loads the B rows of nonzeros G*u + q, u < U), but each lane writes
+// its products to the wave's LDS region, nonzero-major, and group 0 alone adds the batch's
+// products in nonzero order: the contract's order and roundings, without the G x VEC cross-lane
+// moves per nonzero that make narrow groups expensive in accumulate_wave.  Only group 0's
+// accumulators hold the sum (the callers store and reduce from lanes < LPR).  The LDS region is
+// reused batch to batch: a wave's LDS operations complete in order, so the next batch's writes
+// cannot overtake this batch's reads.
+template <typename T, typename I, typename K>
+__device__ __forceinline__ void accumulate_wave_xl(const I* __restrict__ col, const T* __restrict__ val,
+                                                   const I* __restrict__ vperm,
+                                                   const BRows<T, K::BUF>& br, int64_t j0, int64_t j1,
+                                                   int lane, int gl, typename Num<T>::acc* lds,
+                                                   typename Num<T>::acc (&acc)[K::VEC]) {
+#pragma clang fp contract(off)
+  constexpr int VEC = K::VEC, LPR = K::LPR, U = K::UW, G = 64 / LPR;
+  constexpr int BATCH = G * U;
+  constexpr int R = (BATCH + 63) / 64;
+  constexpr int W = LPR * VEC;  // floats per nonzero in LDS
+  static_assert(LPR < 64, "accumulate_wave_xl needs several groups per wave");
+  using A = typename Num<T>::acc;
+  using P = Pack<T, VEC>;
+  const int q = lane / LPR;
+  auto load_batch = [&](int64_t jb, I (&c)[R], A (&v)[R]) {
+    const int n_ = (int)((j1 - jb) < BATCH ? (j1 - jb) : BATCH);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      c[r] = 0;
+      v[r] = 0;
+      const int idx = r * 64 + lane;
+      if (idx < n_) {
+        c[r] = OFX_LD(col + (jb + idx));
+        const int64_t jv = vperm ? (int64_t)OFX_LD(vperm + (jb + idx)) : jb + idx;
+        v[r] = Num<T>::load(OFX_LD(val + jv));
+      }
+    }
+  };
+  I nxc[R];
+  A nxv[R];
+  if (j0 < j1) load_batch(j0, nxc, nxv);
+  for (int64_t jb = j0; jb < j1; jb += BATCH) {
+    const int cnt = (int)((j1 - jb) < BATCH ? (j1 - jb) : BATCH);
+    I myc[R];
+    A myv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      myc[r] = nxc[r];
+      myv[r] = nxv[r];
+    }
+    if (jb + BATCH < j1) load_batch(jb + BATCH, nxc, nxv);  // in flight during this batch
+    I cuv[U];
+    A vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = G * u + q;
+      cuv[u] = shfl(myc[(G * u) >> 6], i & 63);
+      vv[u] = shfl(myv[(G * u) >> 6], i & 63);
+    }
+    P bv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      bv[u] = br.template load<K::BNT, P>(G * u + q < cnt ? cuv[u] : I(0));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = G * u + q;
+      if (i < cnt) {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) lds[i * W + gl * VEC + e] = Num<T>::mul(vv[u], Num<T>::load(bv[u].v[e]));
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (q == 0) {
+#pragma unroll 8
+      for (int i = 0; i < cnt; ++i)
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[e] = acc[e] + lds[i * W + gl * VEC + e];
+    }
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -1059,8 +1148,14 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
           A acc[WV];
 #pragma unroll
           for (int e = 0; e < WV; ++e) acc[e] = A(0);
-          accumulate_wave<T, I, KW>(col, val, vperm, brows<T, K::BUF>(B, c0, cc, active, ldb, kb),
-                                    j0, j1, lane, wgl, acc);
+          if constexpr (K::XL) {
+            __shared__ A xl_lds[K::WPB][KW::XL_FLOATS];
+            accumulate_wave_xl<T, I, KW>(col, val, vperm, brows<T, K::BUF>(B, c0, cc, active, ldb, kb),
+                                         j0, j1, lane, wgl, xl_lds[wave], acc);
+          } else {
+            accumulate_wave<T, I, KW>(col, val, vperm, brows<T, K::BUF>(B, c0, cc, active, ldb, kb),
+                                      j0, j1, lane, wgl, acc);
+          }
           if (active && lane < WL) {
             if (wc >= 0)
               store_partial<A, WV, K::LR>(part + w * n + cc, acc);

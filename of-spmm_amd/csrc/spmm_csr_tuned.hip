@@ -127,6 +127,14 @@ int launch_tuned(const Launch& L, int id) {
       case 173: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 32, 8, true>>(L); break;
       case 174: if (L.n >= 8) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 32, 8, true, false, 2>>(L); break;
       case 180: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 16, 8, true>>(L); break;
+      // wave items with the products exchanged through LDS (Cfg::XL): narrow groups, many
+      // nonzeros per round of B-row loads
+      case 183: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 8, 8, true, kLR, 4, true>>(L); break;
+      case 184: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 8, 16, true, kLR, 4, true>>(L); break;
+      case 185: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 4, 16, true, kLR, 4, true>>(L); break;
+      case 186: if (L.n >= 8) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 8, 8, true, kLR, 8, true>>(L); break;
+      case 187: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR, 4, true>>(L); break;
+      case 191: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR, 2, true>>(L); break;
       default: break;
     }
   }
@@ -183,6 +191,9 @@ int launch_tuned(const Launch& L, int id) {
       case 179: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, false, false, false, false, true, 0, 16, true>>(L); break;
       case 181: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 16, 8, true, false, 2>>(L); break;
       case 182: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 16, 8, true>>(L); break;
+      case 188: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 8, 8, true, kLR, 4, true>>(L); break;
+      case 189: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 8, 8, true, kLR, 8, true>>(L); break;
+      case 190: if (L.n >= 4) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR, 4, true>>(L); break;
       default: break;
     }
   }

@@ -904,3 +904,40 @@ def test_shifted_window_16bit_wide_rows(device, dtype, n):
     torch.cuda.synchronize()
     assert_bitwise(cbig[:, 1:n + 1], ref, f"{dtype} n={n} offset views")
     assert torch.isnan(cbig[:, 0]).all() and torch.isnan(cbig[:, n + 1]).all()
+
+
+ROUND5_ENTRIES = (list(range(90, 105)) + list(range(105, 158)) + list(range(170, 183)))
+
+
+@pytest.fixture(scope="module")
+def round5_graph():
+    rng = np.random.default_rng(9100)
+    m, k = 60_000, 60_000
+    deg = rng.integers(0, 30, size=m)
+    deg[11], deg[777], deg[5] = 4000, 600, 1500
+    return m, k, deg, rng
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("n", [13, 47])
+def test_tuning_table_round5_bitexact(device, round5_graph, dtype, n):
+    """Every round-5 tuning entry (variant 10000 + id: the mid-size shapes, wave-item group
+    shapes, LDS-exchanged wave items, the bandwidth form's in-between widths) that exists for the
+    dtype computes the oracle's bits on a mid-size graph with hub rows, every row compared."""
+    m, k, deg, rng = round5_graph
+    dt = DTYPES[dtype]
+    rp, ci, v = random_csr(m, k, deg, np.random.default_rng(9200 + n), torch.int32, dt)
+    b = random_dense(k, n, np.random.default_rng(9300 + n), dt)
+    d = (rp.to(device), ci.to(device), v.to(device), b.to(device))
+    ref = oracle_spmm(rp, ci, v, b)
+    ran = 0
+    for tid in ROUND5_ENTRIES:
+        try:
+            out = ops.spmm_csr_device(*d, m, k, options=ops.make_options(variant=10000 + tid))
+        except ops._lib.OfxError as e:  # not an entry of this dtype / width
+            assert "tuning variant" in str(e) or "not applicable" in str(e), (tid, str(e))
+            continue
+        torch.cuda.synchronize()
+        assert_bitwise(out, ref, f"{dtype} n={n} tuning entry {10000 + tid}")
+        ran += 1
+    assert ran >= 15, ran
