@@ -1446,9 +1446,10 @@ int describe_cfg(const Launch& L, const char* kind) {
                         : ws_layout(L.nrows, L.nnz, L.n, sizeof(typename Num<T>::acc), L.sched).total;
   std::snprintf(L.describe, L.describe_bytes,
                 "form=%s kernel=%s VEC=%d LPR=%d U=%d WPB=%d NT=%d PF=%d WH=%d BI=%d BUF=%d SH=%d "
-                "HL=%d HU=%d HV=%d LR=%d elem=%d idx=%d ws=%zu",
+                "HL=%d HU=%d HV=%d XL=%d LR=%d elem=%d idx=%d ws=%zu",
                 form, kind, K::VEC, K::LPR, K::U, K::WPB, (int)K::NT, (int)K::PF, (int)K::WH,
-                (int)K::BI, (int)K::BUF, (int)K::SH, K::HL, K::HU, K::HV, (int)K::LR, (int)sizeof(T),
+                (int)K::BI, (int)K::BUF, (int)K::SH, K::HL, K::HU, K::HV, (int)K::XL, (int)K::LR,
+                (int)sizeof(T),
                 (int)sizeof(I), ws);
   return OFX_OK;
 }
@@ -1806,9 +1807,11 @@ int launch_narrow(const Launch& L) {
 }
 
 bool use_narrow_form(const Launch& L, int elem_bytes) {
+  // up to kPrefetchNnz the mid-width shape (its LDS-exchanged wave items) is faster since round 5
   return L.sched.variant == 0 && elem_bytes == 4 && L.n == 16 && pick_vec(4, L, 0) == 4 &&
          !use_small_form(L.nrows, L.nnz_est, L.n, L.sched) &&
-         !use_mid_form(L.nrows, L.nnz_est, L.n, L.sched);
+         !use_mid_form(L.nrows, L.nnz_est, L.n, L.sched) &&
+         !use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched);
 }
 
 // Narrow rows of mid-size launches (round 4): 16-bit rows of 8 or 16 columns and fp32 rows of 8
@@ -1851,26 +1854,29 @@ int launch_narrow_pf(const Launch& L) {
 // 463 / 467 / 151 -> 111 / 112 / 109; and 16-bit rows of 129-256 columns, 8-element wave lanes
 // with 8 in flight -- bf16 N = 129 / 200 / 255 / 256 656 / 166 / 857 / 164 -> 155 / 150 / 158 /
 // 150.  fp32 rows above 128 columns keep their layouts (as fast: 173-210 us either way).
+// Up to 64 columns the wave items exchange their products through LDS (Cfg::XL,
+// accumulate_wave_xl): 8- / 16-lane groups of 2-4 elements, 32-64 nonzeros per round of B-row
+// loads without the cross-lane moves that made narrow groups lose (entries 10183-10198,
+// gpurun_out/r05aa_2_py.txt / r05z_2_py.txt, arxiv-shaped / 60k x 1.5M): fp32 N = 8 / 12 / 16
+// 43 / 44 / 44 -> 38 / 39 / 39 us, fp32 17-32 56 -> 48, fp32 47 / 64 78 -> 73 / 72 (76 -> 70),
+// bf16 17 / 24 57 -> 54 / 53, bf16 47 / 64 80 / 78 -> 71 / 65 (80 / 79 -> 77 / 74).
 template <typename T, typename I>
 int launch_mid_width_pf(const Launch& L) {
   if (L.n < 4)
     return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
-  if (L.n <= 16)
-    return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 16, 16, true, kLR>>(L);
-  if (L.n <= 32) {
-    // 16-bit: 16-lane wave items of 2-element lanes (entry 10156: bf16 N = 32 64.6 -> 57.3 us
-    // arxiv-shaped, 63.8 -> 57.4 on 60k x 1.5M; fp32 lost with the same shape, 55.4 -> 59.0,
-    // and every narrower wave group lost for both, gpurun_out/r05o_1_py.txt)
-    if constexpr (sizeof(T) == 2)
-      return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, true, false, true, false, true, 16, 16, true, kLR, 2>>(L);
+  if (L.n <= 16) {
+    if constexpr (sizeof(T) == 4)
+      return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 8, 8, true, kLR, 2, true>>(L);
     else
-      return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, true, false, true, false, true, 32, 16, true, kLR>>(L);
+      return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 16, 16, true, kLR>>(L);
   }
+  if (L.n <= 32)
+    return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, true, false, true, false, true, 8, 8, true, kLR, 4, true>>(L);
   if (L.n <= 64) {
     if constexpr (sizeof(T) == 2)
-      return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, true, false, true, false, true, 32, 16, true, kLR, 2>>(L);
+      return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, true, false, true, false, true, 16, 8, true, kLR, 4, true>>(L);
     else
-      return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, true, false, true, false, true, 32, 16, true, kLR, 2>>(L);
+      return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, true, false, true, false, true, 16, 8, true, kLR, 4, true>>(L);
   }
   if constexpr (sizeof(T) == 2) {
     if (L.n > 128)
@@ -1889,8 +1895,7 @@ bool use_mid_width_pf_form(const Launch& L, int elem_bytes) {
 bool use_narrow_pf_form(const Launch& L, int elem_bytes) {
   if (L.sched.variant != 0 || !use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched)) return false;
   if (elem_bytes == 2) return (L.n == 8 || L.n == 16) && pick_vec(2, L, 0, 4) == 4;
-  if (elem_bytes == 4) return L.n == 8 && pick_vec(4, L, 0, 2) == 2;
-  return false;
+  return false;  // fp32 N = 8 (round 4's 2-element narrow shape): launch_mid_width_pf since round 5
 }
 
 }  // namespace

@@ -135,6 +135,10 @@ int launch_tuned(const Launch& L, int id) {
       case 186: if (L.n >= 8) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 8, 8, true, kLR, 8, true>>(L); break;
       case 187: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR, 4, true>>(L); break;
       case 191: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR, 2, true>>(L); break;
+      case 192: if (L.n >= 8) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 8, 4, true, kLR, 8, true>>(L); break;
+      case 193: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 16, 8, true, kLR, 4, true>>(L); break;
+      case 196: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 8, 4, true, kLR, 4, true>>(L); break;
+      case 197: if (L.n >= 2) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 8, 8, true, kLR, 2, true>>(L); break;
       default: break;
     }
   }
@@ -194,6 +198,9 @@ int launch_tuned(const Launch& L, int id) {
       case 188: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 8, 8, true, kLR, 4, true>>(L); break;
       case 189: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 8, 8, true, kLR, 8, true>>(L); break;
       case 190: if (L.n >= 4) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR, 4, true>>(L); break;
+      case 194: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 8, 4, true, kLR, 8, true>>(L); break;
+      case 195: if (L.n >= 4) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 16, 8, true, kLR, 4, true>>(L); break;
+      case 198: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 8, 4, true, kLR, 4, true>>(L); break;
       default: break;
     }
   }

@@ -430,7 +430,7 @@ void check_describe() {
          form(OFX_DT_BFLOAT16, 16).c_str());
   // round 5: rows of 17-64 columns take launch_mid_width_pf (2-element lanes in the wave items)
   EXPECT(form(OFX_DT_BFLOAT16, 48).find("form=narrow") != std::string::npos &&
-             form(OFX_DT_BFLOAT16, 48).find("HV=2") != std::string::npos,
+             form(OFX_DT_BFLOAT16, 48).find("HV=4 XL=1") != std::string::npos,
          "bf16 N=48: %s", form(OFX_DT_BFLOAT16, 48).c_str());
   EXPECT(form(OFX_DT_FLOAT16, 8).find("form=narrow") != std::string::npos, "f16 N=8: %s",
          form(OFX_DT_FLOAT16, 8).c_str());

@@ -56,7 +56,9 @@ def test_narrow_form_n16_fp32():
     m = 169_343
     below, above = form(m, K_PREFETCH_NNZ, 16), form(m, K_PREFETCH_NNZ + 1, 16)
     assert below["form"] == above["form"] == "narrow"
-    assert (below["VEC"], below["LPR"], below["U"], below["HL"], below["HU"]) == (4, 4, 8, 16, 16)
+    # below kPrefetchNnz: the mid-width shape with LDS-exchanged wave items (round 5)
+    assert (below["VEC"], below["LPR"], below["U"], below["HL"], below["HU"], below["XL"]) == \
+        (4, 4, 8, 8, 8, 1)
     assert (above["VEC"], above["LPR"], above["U"], above["HL"], above["HU"]) == (2, 8, 8, 16, 8)
     # above kPrefetchNnz fp32 only (16-bit N = 16 below it: test_narrow_rows_of_mid_size_launches),
     # N = 16 only, 16-B aligned only
@@ -187,8 +189,8 @@ def test_narrow_rows_of_mid_size_launches():
         # 17-64 columns: launch_mid_width_pf (test_mid_width_rule)
         assert form(m, K_PREFETCH_NNZ + 1, 16, dt)["form"] == "bandwidth"
         assert form(20_000, 400_000, 16, dt)["form"] == "mid"
-    d = form(m, nnz, 8)
-    assert (d["form"], d["VEC"], d["LPR"], d["U"], d["HL"]) == ("narrow", 2, 4, 4, 16), d
+    d = form(m, nnz, 8)  # round 5: the mid-width shape (LDS-exchanged wave items)
+    assert (d["form"], d["VEC"], d["LPR"], d["U"], d["HL"], d["XL"]) == ("narrow", 4, 4, 8, 8, 1), d
     d = form(m, nnz, 8, b_addr=260)  # 4-B aligned B: the mid-width shape
     assert (d["form"], d["VEC"], d["LPR"], d["SH"]) == ("narrow", 4, 4, 1), d
     assert form(m, nnz, 4)["form"] == "narrow"
@@ -223,11 +225,11 @@ def test_mid_width_rule():
             if n < 4:
                 want = ("narrow", 0, 1, 4, 8, 16, 1, 1)
             elif n <= 16:
-                want = ("narrow", 1, 4, 4, 8, 16, 1, 1)
+                want = ("narrow", 1, 4, 4, 8, 8, 2, 1) if dt == F32 else ("narrow", 1, 4, 4, 8, 16, 1, 1)
             elif n <= 32:
-                want = ("narrow", 1, 4, 8, 8, 32, 1, 1) if dt == F32 else ("narrow", 1, 4, 8, 8, 16, 2, 1)
+                want = ("narrow", 1, 4, 8, 8, 8, 4, 1)
             elif n <= 64:
-                want = ("narrow", 1, 4, 16, 8, 32, 2, 1) if dt == F32 else ("narrow", 1, 8, 8, 8, 32, 2, 1)
+                want = ("narrow", 1, 4, 16, 8, 16, 4, 1) if dt == F32 else ("narrow", 1, 8, 8, 8, 16, 4, 1)
             elif n <= 128:
                 want = ("narrow", 1, 8, 16, 8, 32, 4, 1)
             else:
@@ -238,8 +240,9 @@ def test_mid_width_rule():
             e = 2 if dt != F32 else 4
             v = form(m, nnz, n, dt, b_addr=256 + e, c_addr=256 + 3 * e, ldb=n + 3, ldc=n + 1)
             assert (v["form"], v["VEC"], v["LPR"], v["HL"], v["HV"]) == got[:1] + got[2:4] + got[5:7], v
-        for n in (8, 16):  # aligned 8 / 16 columns: the narrow forms' own shapes
-            assert form(m, nnz, n, dt)["SH"] == 0 and form(m, nnz, n, dt)["HL"] == 16
+        if dt != F32:
+            for n in (8, 16):  # aligned 8 / 16 columns (16-bit): the narrow forms' own shapes
+                assert form(m, nnz, n, dt)["SH"] == 0 and form(m, nnz, n, dt)["HL"] == 16
         assert form(m, nnz, top + 1, dt)["HL"] == 0              # past the rule's widths
         assert form(m, K_PREFETCH_NNZ + 1, 41, dt)["form"] == "bandwidth"
         assert form(20_000, 400_000, 41, dt)["form"] == "mid"
