@@ -201,6 +201,11 @@ int launch_tuned(const Launch& L, int id) {
       case 194: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 8, 4, true, kLR, 8, true>>(L); break;
       case 195: if (L.n >= 4) return launch_cfg<T, I, Cfg<8, 8, 8, 4, false, P, false, W, false, true, 16, 8, true, kLR, 4, true>>(L); break;
       case 198: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 8, 4, true, kLR, 4, true>>(L); break;
+      // 16-bit, 16 columns and fewer: narrow LDS-exchanged wave items (199-202)
+      case 199: if (L.n >= 2) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 8, 8, true, kLR, 2, true>>(L); break;
+      case 200: if (L.n >= 2) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR, 2, true>>(L); break;
+      case 201: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 4, 16, true, kLR, 4, true>>(L); break;
+      case 202: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 8, 8, true, kLR, 4, true>>(L); break;
       default: break;
     }
   }

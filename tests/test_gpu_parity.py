@@ -911,7 +911,7 @@ def test_shifted_window_16bit_wide_rows(device, dtype, n):
     assert torch.isnan(cbig[:, 0]).all() and torch.isnan(cbig[:, n + 1]).all()
 
 
-ROUND5_ENTRIES = (list(range(90, 105)) + list(range(105, 158)) + list(range(170, 199)))
+ROUND5_ENTRIES = (list(range(90, 105)) + list(range(105, 158)) + list(range(170, 203)))
 
 
 @pytest.fixture(scope="module")
