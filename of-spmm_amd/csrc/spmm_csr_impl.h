@@ -1799,10 +1799,8 @@ bool use_shift_form(const Launch& L, int elem_bytes) {
 // 396 -> 402 us).  profiles/r03n_graph.jsonl.  Same bits: only who adds changes.
 template <typename T, typename I>
 int launch_narrow(const Launch& L) {
-  // round 4: U = 8 with the in-kernel reduce (entry 10082, profiles/r04ac_n16_u.jsonl: 60k x
-  // 1.5M 42.8 -> 41.3 us, 2M nonzeros 50.9 -> 45.7, arxiv-shaped 45.4 -> 45.1)
-  if (L.nnz_est <= kPrefetchNnz)
-    return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
+  // past kPrefetchNnz only (round 4's U = 8 in-kernel-reduce shape below it, entry 10082, gave
+  // way to launch_mid_width_pf's LDS-exchanged wave items in round 5)
   return launch_cfg<T, I, Cfg<2, 8, 8, 4, false, true, false, true, false, true, 16, 8>>(L);
 }
 
@@ -1814,23 +1812,10 @@ bool use_narrow_form(const Launch& L, int elem_bytes) {
          !use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched);
 }
 
-// Narrow rows of mid-size launches (round 4): 16-bit rows of 8 or 16 columns and fp32 rows of 8
-// in the prefetching form take the narrow form's shape -- four lanes per light row (8 B per lane),
-// hub chunks and heavy rows as 16-lane one-element wave items, hubs added in the kernel -- instead
-// of one element per lane over 8-16 lanes.  Tuning entries 10050-10063 on three mid-size graphs
-// (profiles/r04k_variants.jsonl; arxiv-shaped / 60k x 1.5M / 169k x 2M): bf16 N = 16 86 / 77 / 94
-// -> 50 / 45 / 58 us and N = 8 99 / 82 / 105 -> 50 / 45 / 55 (U = 8, entry 51), fp32 N = 8 74 /
-// 66 / 74 -> 46 / 43 / 53 (U = 4, entry 63).  Same bits: only who adds changes.
-// (Round 4's 16-bit rows of 17-32 columns and odd 16-bit widths took this shape too, with
-// 16-lane wave items; round 5's launch_mid_width_pf below replaced them.)
-template <typename T, typename I>
-int launch_narrow_pf(const Launch& L) {
-  if constexpr (sizeof(T) == 2) {
-    return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
-  } else {
-    return launch_cfg<T, I, Cfg<2, 4, 4, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
-  }
-}
+// Narrow rows of mid-size launches (round 4, launch_narrow_pf, removed in round 5): 16-bit rows
+// of 8 or 16 columns and fp32 rows of 8 took four lanes per light row (8 B per lane) with 16-lane
+// one-element wave items (entries 10050-10063, profiles/r04k_variants.jsonl); the LDS-exchanged
+// wave items of launch_mid_width_pf below replaced it at every such width.
 
 // Rows of 17-64 columns of mid-size launches (round 5): the narrow form's
 // shape for every width -- shifted windows (Cfg::SH, any N; 2-B-aligned 8 / 16-B accesses are
@@ -1859,17 +1844,16 @@ int launch_narrow_pf(const Launch& L) {
 // loads without the cross-lane moves that made narrow groups lose (entries 10183-10198,
 // gpurun_out/r05aa_2_py.txt / r05z_2_py.txt, arxiv-shaped / 60k x 1.5M): fp32 N = 8 / 12 / 16
 // 43 / 44 / 44 -> 38 / 39 / 39 us, fp32 17-32 56 -> 48, fp32 47 / 64 78 -> 73 / 72 (76 -> 70),
-// bf16 17 / 24 57 -> 54 / 53, bf16 47 / 64 80 / 78 -> 71 / 65 (80 / 79 -> 77 / 74).
+// bf16 17 / 24 57 -> 54 / 53, bf16 47 / 64 80 / 78 -> 71 / 65 (80 / 79 -> 77 / 74); and 16-bit
+// rows of 4-16 columns, aligned 8 / 16 included (round 4's narrow shape, launch_narrow_pf, is
+// gone; entries 10199-10202, gpurun_out/r05ae_1_py.txt): bf16 N = 4 / 8 / 12 / 16 44 / 46 / 47 /
+// 47 -> 37 / 40 / 42 / 42 us (60k x 1.5M 45 -> 43).
 template <typename T, typename I>
 int launch_mid_width_pf(const Launch& L) {
   if (L.n < 4)
     return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
-  if (L.n <= 16) {
-    if constexpr (sizeof(T) == 4)
-      return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 8, 8, true, kLR, 2, true>>(L);
-    else
-      return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 16, 16, true, kLR>>(L);
-  }
+  if (L.n <= 16)
+    return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 8, 8, true, kLR, 2, true>>(L);
   if (L.n <= 32)
     return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, true, false, true, false, true, 8, 8, true, kLR, 4, true>>(L);
   if (L.n <= 64) {
@@ -1892,11 +1876,6 @@ bool use_mid_width_pf_form(const Launch& L, int elem_bytes) {
          ((uintptr_t)L.b % elem_bytes) == 0 && ((uintptr_t)L.c % elem_bytes) == 0;
 }
 
-bool use_narrow_pf_form(const Launch& L, int elem_bytes) {
-  if (L.sched.variant != 0 || !use_prefetch_form(L.nrows, L.nnz_est, L.n, L.sched)) return false;
-  if (elem_bytes == 2) return (L.n == 8 || L.n == 16) && pick_vec(2, L, 0, 4) == 4;
-  return false;  // fp32 N = 8 (round 4's 2-element narrow shape): launch_mid_width_pf since round 5
-}
 
 }  // namespace
 
@@ -1908,12 +1887,8 @@ int launch_typed(const Launch& L) {
                 "spmm_csr: tuning variant %d needs B under 4 GiB", L.sched.variant);
     return launch_tuned<T, I>(L, L.sched.variant - 10000);
   }
-  // the narrow forms first (8 / 16 columns with aligned rows), then every other width of a
-  // mid-size launch up to 128 (fp32) / 256 (16-bit) columns
-  if constexpr (sizeof(T) <= 4) {
-    if (use_narrow_pf_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L))
-      return launch_narrow_pf<T, I>(L);
-  }
+  // the narrow form (fp32 N = 16 past kPrefetchNnz), then every width of a mid-size launch up
+  // to 128 (fp32) / 256 (16-bit) columns
   if constexpr (sizeof(T) == 4) {
     if (use_narrow_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L)) return launch_narrow<T, I>(L);
   }

@@ -175,15 +175,16 @@ def test_prefetch_form_layouts():
 
 
 def test_narrow_rows_of_mid_size_launches():
-    """Round 4: 16-bit N = 8 / 16 and fp32 N = 8 in the prefetching form's size range take the
-    narrow shape (4 lanes per light row, 8 B per lane; 16-lane wave items; hubs added in the
-    kernel); unaligned views and the sizes either side keep their forms."""
+    """16-bit N = 8 / 16 and fp32 N = 8 in the prefetching form's size range: round 4's narrow
+    shape (4 lanes per light row, 16-lane wave items) gave way in round 5 to the mid-width shape
+    with LDS-exchanged 8-lane wave items of 2 elements, aligned or not; the sizes either side
+    keep their forms."""
     m, nnz = 169_343, 1_166_243
     for dt in (BF16, F16):
         for n in (8, 16):
             d = form(m, nnz, n, dt)
-            assert (d["form"], d["VEC"], d["LPR"], d["U"], d["HL"], d["LR"]) == \
-                ("narrow", 4, 4, 8, 16, 1), (dt, n, d)
+            assert (d["form"], d["VEC"], d["LPR"], d["U"], d["HL"], d["HV"], d["XL"], d["LR"]) == \
+                ("narrow", 4, 4, 8, 8, 2, 1, 1), (dt, n, d)
         d = form(m, nnz, 16, dt, b_addr=258)  # 2-B aligned B: the mid-width shape
         assert (d["form"], d["VEC"], d["LPR"], d["SH"]) == ("narrow", 4, 4, 1), d
         # 17-64 columns: launch_mid_width_pf (test_mid_width_rule)
@@ -209,15 +210,15 @@ def test_in_kernel_hub_reduce_only_in_mid_size_forms():
 
 def test_mid_width_rule():
     """Round 5 (launch_mid_width_pf): rows of 1-128 columns (fp32) / 1-256 (16-bit) of mid-size
-    launches, any width and any element-aligned view, except 8 / 16 columns with aligned rows (the
-    narrow forms): shifted windows (one element per lane below 4 columns) with wave items of HL
+    launches, any width and any element-aligned view (8 / 16 aligned columns too since the
+    LDS-exchanged wave items, Cfg::XL, up to 64 columns): shifted windows (one element per lane below 4 columns) with wave items of HL
     lanes x HV elements, one column pass, hubs added in the kernel.  Both sides of every bound:
     3 / 4, 16 / 17, 32 / 33, 64 / 65, 128 / 129, 256 / 257 columns, kPrefetchNnz, the mid / small
     forms below, f64."""
     m, nnz = 169_343, 1_166_243
     for dt in (F32, BF16, F16):
         top = 128 if dt == F32 else 256
-        for n in (1, 2, 3, 4, 5, 7, 9, 12, 15, 17, 18, 24, 25, 31, 32, 33, 40, 41, 47, 48, 57, 63,
+        for n in (1, 2, 3, 4, 5, 7, 8, 9, 12, 15, 16, 17, 18, 24, 25, 31, 32, 33, 40, 41, 47, 48, 57, 63,
                   64, 65, 99, 127, 128, 129, 200, 255, 256):
             if n > top:
                 continue
@@ -225,7 +226,7 @@ def test_mid_width_rule():
             if n < 4:
                 want = ("narrow", 0, 1, 4, 8, 16, 1, 1)
             elif n <= 16:
-                want = ("narrow", 1, 4, 4, 8, 8, 2, 1) if dt == F32 else ("narrow", 1, 4, 4, 8, 16, 1, 1)
+                want = ("narrow", 1, 4, 4, 8, 8, 2, 1)
             elif n <= 32:
                 want = ("narrow", 1, 4, 8, 8, 8, 4, 1)
             elif n <= 64:
@@ -236,13 +237,11 @@ def test_mid_width_rule():
                 want = ("narrow", 1, 8, 32, 8, 32, 8, 1)
             got = (d["form"], d["SH"], d["VEC"], d["LPR"], d["U"], d["HL"], d["HV"], d["LR"])
             assert got == want, (dt, n, d)
+            assert d["XL"] == (1 if 4 <= n <= 64 else 0), (dt, n, d)
             # element-aligned views with odd offsets and strides take the same configuration
             e = 2 if dt != F32 else 4
             v = form(m, nnz, n, dt, b_addr=256 + e, c_addr=256 + 3 * e, ldb=n + 3, ldc=n + 1)
             assert (v["form"], v["VEC"], v["LPR"], v["HL"], v["HV"]) == got[:1] + got[2:4] + got[5:7], v
-        if dt != F32:
-            for n in (8, 16):  # aligned 8 / 16 columns (16-bit): the narrow forms' own shapes
-                assert form(m, nnz, n, dt)["SH"] == 0 and form(m, nnz, n, dt)["HL"] == 16
         assert form(m, nnz, top + 1, dt)["HL"] == 0              # past the rule's widths
         assert form(m, K_PREFETCH_NNZ + 1, 41, dt)["form"] == "bandwidth"
         assert form(20_000, 400_000, 41, dt)["form"] == "mid"

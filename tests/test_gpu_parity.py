@@ -844,13 +844,8 @@ def test_mid_width_rule_bitexact(device, dtype, n):
     desc = ops.describe(m, k, n, ci.numel(), dt, b_addr=d[3].data_ptr(), c_addr=256)
     top = 128 if dtype == "f32" else 256  # the rule's widths (fp32 above 128: the prefetch form)
     assert (desc["form"] == "narrow") == (n <= top), desc
-    if n > top:
-        hl = 0
-    elif dtype == "f32":
-        hl = 16 if n < 4 else 8 if n <= 32 else 16 if n <= 64 else 32
-    else:
-        hl = 16 if n <= 16 else 8 if n <= 32 else 16 if n <= 64 else 32
-    assert desc["HL"] == hl and desc["XL"] == (1 if (4 <= n <= 64 and (dtype == "f32" or n > 16)) else 0), desc
+    hl = 0 if n > top else 16 if n < 4 else 8 if n <= 32 else 16 if n <= 64 else 32
+    assert desc["HL"] == hl and desc["XL"] == (1 if 4 <= n <= 64 else 0), desc
     ref = oracle_spmm(rp, ci, v, b)
     out = fs.spmm(d[0], d[1], d[2], m, k, d[3])
     torch.cuda.synchronize()
