@@ -1847,7 +1847,10 @@ bool use_narrow_form(const Launch& L, int elem_bytes) {
 // bf16 17 / 24 57 -> 54 / 53, bf16 47 / 64 80 / 78 -> 71 / 65 (80 / 79 -> 77 / 74); and 16-bit
 // rows of 4-16 columns, aligned 8 / 16 included (round 4's narrow shape, launch_narrow_pf, is
 // gone; entries 10199-10202, gpurun_out/r05ae_1_py.txt): bf16 N = 4 / 8 / 12 / 16 44 / 46 / 47 /
-// 47 -> 37 / 40 / 42 / 42 us (60k x 1.5M 45 -> 43).
+// 47 -> 37 / 40 / 42 / 42 us (60k x 1.5M 45 -> 43); fp32 rows of 65-128 columns too, two
+// 32-lane groups of 8 nonzeros (entry 10204, gpurun_out/r05ag_2_py.txt): N = 65 / 99 / 128 107 /
+// 111 / 112 -> 101 / 106 / 107 us (60k x 1.5M 101 / 106 / 107 -> 97 / 103 / 105); 16-bit rows
+// there gained nothing from it (-1..+3%) and keep the cross-lane groups.
 template <typename T, typename I>
 int launch_mid_width_pf(const Launch& L) {
   if (L.n < 4)
@@ -1865,8 +1868,10 @@ int launch_mid_width_pf(const Launch& L) {
   if constexpr (sizeof(T) == 2) {
     if (L.n > 128)
       return launch_cfg<T, I, Cfg<8, 32, 8, 4, false, true, false, true, false, true, 32, 8, true, kLR, 8>>(L);
+    return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, true, false, true, false, true, 32, 16, true, kLR, 4>>(L);
+  } else {
+    return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, true, false, true, false, true, 32, 8, true, kLR, 4, true>>(L);
   }
-  return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, true, false, true, false, true, 32, 16, true, kLR, 4>>(L);
 }
 
 bool use_mid_width_pf_form(const Launch& L, int elem_bytes) {

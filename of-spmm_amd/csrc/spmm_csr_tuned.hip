@@ -139,6 +139,10 @@ int launch_tuned(const Launch& L, int id) {
       case 193: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 16, 8, 4, false, P, false, W, false, true, 16, 8, true, kLR, 4, true>>(L); break;
       case 196: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 8, 4, true, kLR, 4, true>>(L); break;
       case 197: if (L.n >= 2) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 8, 8, true, kLR, 2, true>>(L); break;
+      // 65-128 columns: LDS-exchanged wave items (203-205)
+      case 203: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 16, 8, true, kLR, 8, true>>(L); break;
+      case 204: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 32, 8, true, kLR, 4, true>>(L); break;
+      case 205: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR, 4, true>>(L); break;
       default: break;
     }
   }
@@ -206,6 +210,10 @@ int launch_tuned(const Launch& L, int id) {
       case 200: if (L.n >= 2) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 16, 16, true, kLR, 2, true>>(L); break;
       case 201: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 4, 16, true, kLR, 4, true>>(L); break;
       case 202: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 8, 8, true, kLR, 4, true>>(L); break;
+      // 65-128 columns: LDS-exchanged wave items (203-205)
+      case 203: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 16, 8, true, kLR, 8, true>>(L); break;
+      case 204: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 32, 8, true, kLR, 4, true>>(L); break;
+      case 205: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR, 4, true>>(L); break;
       default: break;
     }
   }
