@@ -1850,11 +1850,13 @@ bool use_narrow_form(const Launch& L, int elem_bytes) {
 // 47 -> 37 / 40 / 42 / 42 us (60k x 1.5M 45 -> 43); fp32 rows of 65-128 columns too, two
 // 32-lane groups of 8 nonzeros (entry 10204, gpurun_out/r05ag_2_py.txt): N = 65 / 99 / 128 107 /
 // 111 / 112 -> 101 / 106 / 107 us (60k x 1.5M 101 / 106 / 107 -> 97 / 103 / 105); 16-bit rows
-// there gained nothing from it (-1..+3%) and keep the cross-lane groups.
+// there gained nothing from it (-1..+3%) and keep the cross-lane groups.  Rows of 1-3 columns:
+// 16 four-lane groups of 8 nonzeros, 128 nonzeros per round of B-row loads (entry 10207,
+// gpurun_out/r05aj_2_py.txt): fp32 / bf16 N = 1-3 42-45 -> 29-31 us on both mid-size graphs.
 template <typename T, typename I>
 int launch_mid_width_pf(const Launch& L) {
   if (L.n < 4)
-    return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, true, false, true, false, true, 16, 16, false, kLR>>(L);
+    return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, true, false, true, false, true, 4, 8, false, kLR, 1, true>>(L);
   if (L.n <= 16)
     return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, true, false, true, false, true, 8, 8, true, kLR, 2, true>>(L);
   if (L.n <= 32)

@@ -143,6 +143,9 @@ int launch_tuned(const Launch& L, int id) {
       case 203: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 16, 8, true, kLR, 8, true>>(L); break;
       case 204: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 32, 8, true, kLR, 4, true>>(L); break;
       case 205: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR, 4, true>>(L); break;
+      // 1-3 columns: LDS-exchanged one-element wave items (206-207)
+      case 206: if (L.n >= 1) return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, P, false, W, false, true, 8, 8, false, kLR, 1, true>>(L); break;
+      case 207: if (L.n >= 1) return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, P, false, W, false, true, 4, 8, false, kLR, 1, true>>(L); break;
       default: break;
     }
   }
@@ -214,6 +217,9 @@ int launch_tuned(const Launch& L, int id) {
       case 203: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 16, 8, true, kLR, 8, true>>(L); break;
       case 204: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 32, 8, true, kLR, 4, true>>(L); break;
       case 205: if (L.n >= 8) return launch_cfg<T, I, Cfg<8, 16, 8, 4, false, P, false, W, false, true, 32, 16, true, kLR, 4, true>>(L); break;
+      // 1-3 columns: LDS-exchanged one-element wave items (206-207)
+      case 206: if (L.n >= 1) return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, P, false, W, false, true, 8, 8, false, kLR, 1, true>>(L); break;
+      case 207: if (L.n >= 1) return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, P, false, W, false, true, 4, 8, false, kLR, 1, true>>(L); break;
       default: break;
     }
   }

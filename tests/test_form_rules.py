@@ -224,7 +224,7 @@ def test_mid_width_rule():
                 continue
             d = form(m, nnz, n, dt)
             if n < 4:
-                want = ("narrow", 0, 1, 4, 8, 16, 1, 1)
+                want = ("narrow", 0, 1, 4, 8, 4, 1, 1)
             elif n <= 16:
                 want = ("narrow", 1, 4, 4, 8, 8, 2, 1)
             elif n <= 32:
@@ -237,7 +237,7 @@ def test_mid_width_rule():
                 want = ("narrow", 1, 8, 32, 8, 32, 8, 1)
             got = (d["form"], d["SH"], d["VEC"], d["LPR"], d["U"], d["HL"], d["HV"], d["LR"])
             assert got == want, (dt, n, d)
-            assert d["XL"] == (1 if 4 <= n <= 64 or (dt == F32 and n > 64) else 0), (dt, n, d)
+            assert d["XL"] == (1 if n <= 64 or dt == F32 else 0), (dt, n, d)
             # element-aligned views with odd offsets and strides take the same configuration
             e = 2 if dt != F32 else 4
             v = form(m, nnz, n, dt, b_addr=256 + e, c_addr=256 + 3 * e, ldb=n + 3, ldc=n + 1)

@@ -844,8 +844,8 @@ def test_mid_width_rule_bitexact(device, dtype, n):
     desc = ops.describe(m, k, n, ci.numel(), dt, b_addr=d[3].data_ptr(), c_addr=256)
     top = 128 if dtype == "f32" else 256  # the rule's widths (fp32 above 128: the prefetch form)
     assert (desc["form"] == "narrow") == (n <= top), desc
-    hl = 0 if n > top else 16 if n < 4 else 8 if n <= 32 else 16 if n <= 64 else 32
-    xl = 1 if 4 <= n <= 64 or (dtype == "f32" and 64 < n <= top) else 0
+    hl = 0 if n > top else 4 if n < 4 else 8 if n <= 32 else 16 if n <= 64 else 32
+    xl = 1 if n <= 64 or (dtype == "f32" and n <= top) else 0
     assert desc["HL"] == hl and desc["XL"] == xl, desc
     ref = oracle_spmm(rp, ci, v, b)
     out = fs.spmm(d[0], d[1], d[2], m, k, d[3])
@@ -907,7 +907,7 @@ def test_shifted_window_16bit_wide_rows(device, dtype, n):
     assert torch.isnan(cbig[:, 0]).all() and torch.isnan(cbig[:, n + 1]).all()
 
 
-ROUND5_ENTRIES = (list(range(90, 105)) + list(range(105, 158)) + list(range(170, 206)))
+ROUND5_ENTRIES = (list(range(90, 105)) + list(range(105, 158)) + list(range(170, 208)))
 
 
 @pytest.fixture(scope="module")
