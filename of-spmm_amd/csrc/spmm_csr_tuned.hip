@@ -146,6 +146,9 @@ int launch_tuned(const Launch& L, int id) {
       // 1-3 columns: LDS-exchanged one-element wave items (206-207)
       case 206: if (L.n >= 1) return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, P, false, W, false, true, 8, 8, false, kLR, 1, true>>(L); break;
       case 207: if (L.n >= 1) return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, P, false, W, false, true, 4, 8, false, kLR, 1, true>>(L); break;
+      // 4-32 columns: 16 four-lane LDS-exchanged groups (208-209)
+      case 208: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 4, 8, true, kLR, 2, true>>(L); break;
+      case 209: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 4, 8, true, kLR, 4, true>>(L); break;
       default: break;
     }
   }
@@ -220,6 +223,9 @@ int launch_tuned(const Launch& L, int id) {
       // 1-3 columns: LDS-exchanged one-element wave items (206-207)
       case 206: if (L.n >= 1) return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, P, false, W, false, true, 8, 8, false, kLR, 1, true>>(L); break;
       case 207: if (L.n >= 1) return launch_cfg<T, I, Cfg<1, 4, 8, 4, false, P, false, W, false, true, 4, 8, false, kLR, 1, true>>(L); break;
+      // 4-32 columns: 16 four-lane LDS-exchanged groups (208-209)
+      case 208: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 4, 8, 4, false, P, false, W, false, true, 4, 8, true, kLR, 2, true>>(L); break;
+      case 209: if (L.n >= 4) return launch_cfg<T, I, Cfg<4, 8, 8, 4, false, P, false, W, false, true, 4, 8, true, kLR, 4, true>>(L); break;
       default: break;
     }
   }

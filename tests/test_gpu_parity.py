@@ -907,7 +907,7 @@ def test_shifted_window_16bit_wide_rows(device, dtype, n):
     assert torch.isnan(cbig[:, 0]).all() and torch.isnan(cbig[:, n + 1]).all()
 
 
-ROUND5_ENTRIES = (list(range(90, 105)) + list(range(105, 158)) + list(range(170, 208)))
+ROUND5_ENTRIES = (list(range(90, 105)) + list(range(105, 158)) + list(range(170, 210)))
 
 
 @pytest.fixture(scope="module")
