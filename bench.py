@@ -5,8 +5,10 @@ Workload (config.workload): ogbn-products-shaped synthetic power-law CSR (2,449,
 123,718,280 nnz) x dense N=128 fp32 — the config BASELINE.json's north-star target is quoted on
 (configs[2]); it fits one GPU.  A "step" is one SpMM over that matrix with inputs resident in HBM:
   N=1   oneflow_spmm.spmm(...) (op layer -> C-ABI -> plan/main/reduce HIP kernels)
-  N>1   row split over N ranks: RCCL all-gather of the Split(0) dense shards + local SpMM
-        (strong scaling: the same matrix is divided across ranks).
+  N>1   1-D row split over N ranks (BalancedSplitter rows): exchange of the Split(0) dense
+        shards (RCCL all-gather, or the halo rows only; the fastest kept at setup) + local SpMM
+        (strong scaling: the same matrix is divided across ranks).  config.parallelism names the
+        exchange that ran; 2-D grids are measured but only reported (extra.grid_best).
 value = 2*nnz*N FLOPs per step (whole job) / max-over-ranks step time, in GFLOP/s.
 
 Extra objects: `roofline` (dominant kernel spmm_main, HIP events on its stream, algorithmic
@@ -177,8 +179,11 @@ def main():
     ap.add_argument("--pipeline", type=int, default=0,
                     help="column blocks for gather/SpMM overlap at N>1 (default: measured)")
     ap.add_argument("--exchange", default="auto",
-                    help="B exchange for N>1: auto | allgather | halo | nsplit | grid<R>x<C> "
-                         "(default: measured at setup)")
+                    help="B exchange for N>1: auto | any | allgather | halo | nsplit | grid<R>x<C>"
+                         "[/s<S>].  auto (default): the fastest 1-D row-split exchange measured at "
+                         "setup (all-gather or halo, the north star's partition); the 2-D grids "
+                         "are measured too but only reported (extra.grid_best).  any: the fastest "
+                         "of all, grids included")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend at N>1; gloo is a rehearsal of the multi-rank code "
                          "path on fewer GPUs (ranks share devices, bytes are host-staged: not a "
@@ -317,19 +322,20 @@ def main():
         rs.load_shard(synth.dense(klo, khi, n, dt, device=device))
         full = None
         pinned_sub = int(args.exchange.split("/s")[1]) if "/s" in args.exchange else 1
-        if args.exchange == "auto" or args.exchange.startswith(("nsplit", "grid")):
+        auto = args.exchange in ("auto", "any")
+        if auto or args.exchange.startswith(("nsplit", "grid")):
             # the grid / column-split candidates need the whole CSR on every rank
             f_ci = torch.from_numpy(synth.columns(m, k, rp_full, threads=threads)).to(device)
             full = (torch.from_numpy(rp_full.astype(np.int32)).to(device), f_ci,
                     synth.values(0, nnz, dt).to(device))
-        rs.bind(d_rp, d_ci, d_v, halo=args.exchange in ("auto", "halo"), full_csr=full,
+        rs.bind(d_rp, d_ci, d_v, halo=auto or args.exchange == "halo", full_csr=full,
                 grid_subs=tuple(sorted({1, 2, pinned_sub})))
         # exchange: all-gather (ring / point-to-point) x pipeline depth (column blocks gathered
         # while the previous block computes), or halo-only rows; measured here, untimed, the
-        # fastest kept (every candidate gives the same bytes)
+        # fastest 1-D row-split candidate kept (every candidate gives the same bytes)
         comm_times, tune_s = {}, None
-        if args.comm or args.pipeline or args.exchange != "auto":
-            rs.exchange = args.exchange if args.exchange != "auto" else "allgather"
+        if args.comm or args.pipeline or not auto:
+            rs.exchange = args.exchange if not auto else "allgather"
             if rs.exchange not in ("allgather", "halo") and rs.exchange not in rs.grids:
                 raise SystemExit(f"--exchange {rs.exchange}: not available (grids: {list(rs.grids)})")
             rs.comm_kind = args.comm or rs.comm_kind
@@ -340,7 +346,8 @@ def main():
         else:
             t_tune = time.time()
             comm_times = rs.tune(out, force=args.force_rowsplit, budget_s=args.tune_budget, log=log,
-                                 on_candidate=lambda nm: enter_phase(f"tune: {nm}", 180))
+                                 on_candidate=lambda nm: enter_phase(f"tune: {nm}", 180),
+                                 rowsplit_only=args.exchange == "auto")
             tune_s = time.time() - t_tune
             log("[bench] exchange candidates (ms, max over ranks; model-predicted): " +
                 ", ".join(f"{kk} {vv:.3f} ({rs.tune_report[kk]['predicted_ms']:.3f})"
@@ -466,10 +473,11 @@ def main():
         "data": "synthetic (deterministic Chung-Lu power-law CSR, gamma 2.5; dataset-shaped)",
         "config": {"workload": f"{args.config}: CSR {m}x{k}, {nnz} nnz x dense N={n}",
                    "m": m, "k": k, "nnz": nnz, "n": n, "index": "int32",
+                   # built from the exchange tune() kept (or the one pinned), never a constant
                    "parallelism": "single GPU" if not rowsplit else
-                   (f"REHEARSAL: row-split x{world} with gloo on {torch.cuda.device_count()} GPU(s), "
-                    "host-staged bytes; not a performance number") if rehearsal else
-                   f"row-split x{world} + RCCL all-gather of B (padded shards)"},
+                   (f"REHEARSAL with gloo on {torch.cuda.device_count() if on_gpu else 0} GPU(s), "
+                    f"host-staged bytes, not a performance number: {rs.describe()}")
+                   if rehearsal else rs.describe()},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_unit": "bytes per launch (beyond L2: Infinity Cache + HBM)",
@@ -491,9 +499,18 @@ def main():
             dist.all_reduce(nz[:1], op=dist.ReduceOp.MAX)
             dist.all_reduce(nz[1:], op=dist.ReduceOp.SUM)
         comm_size = rs.comm_size()
+        g2d = getattr(rs, "tune_best_2d", None)
         result["extra"].update({
             "ranks_seen": dist.get_world_size(),
             "rccl_comm_ranks": comm_size[0] if comm_size else None,
+            # ranks of the communicator the kept exchange ran on (RCCL's, or the torch group's)
+            "exchange_comm_ranks": comm_size[0] if comm_size and rs.comm_kind != "torch"
+            else dist.get_world_size(rs.group),
+            "exchange_is_rowsplit": rs.is_rowsplit_exchange(rs.exchange),
+            # the fastest 2-D partition measured by tune(): reported, never the value (a grid needs
+            # the whole CSR on every rank and is not the north star's 1-D row split)
+            "grid_best": ({"exchange": g2d[0], "ms": round(g2d[1], 4),
+                           "gflops": round(flops / (g2d[1] * 1e-3) / 1e9, 2)} if g2d else None),
             "allgather_ms_rank0": round(gather_mean, 4),
             "spmm_ms_rank0": round(kern_ms, 4),
             "allgather_ms_max": round(phase["gather_ms_max"], 4),

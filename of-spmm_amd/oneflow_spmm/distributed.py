@@ -1002,24 +1002,76 @@ class RowSplitSpmm:
         x, t = recv / r_x * 1e3, spmm / r_h * 1e3
         return x + t if depth <= 1 else max(x, t) + min(x, t) / depth
 
+    # exchange candidates that keep the north star's 1-D row split: every rank
+    # owns its BalancedSplitter rows at full width; grids / the column split are 2-D partitions
+    @staticmethod
+    def is_rowsplit_exchange(name: str) -> bool:
+        return not name.startswith(("grid", "nsplit"))
+
+    @classmethod
+    def pick_best(cls, times: dict, rowsplit_only: bool):
+        """The fastest finite candidate of `times` ({name: ms}); with `rowsplit_only` the fastest
+        1-D row-split one (None if none completed).  Ties go to the name first in sort order."""
+        pool = {nm: ms for nm, ms in times.items() if math.isfinite(ms)
+                and (not rowsplit_only or cls.is_rowsplit_exchange(nm))}
+        return min(sorted(pool), key=pool.get) if pool else None
+
+    def describe(self) -> str:
+        """The partition and exchange this operator runs, as the bench's config.parallelism
+        names it (built from the kept exchange, never a constant)."""
+        w = self.world
+        if self.exchange in self.grids:
+            gp = self.grids[self.exchange]
+            return (f"2-D grid {gp.rg}x{gp.cn} over {w} ranks ({self.exchange}): row groups x "
+                    f"column blocks, B exchanged by {self.comm_kind} send/recv, C returned in the "
+                    f"row group; sub-blocks {gp.sub}")
+        via = {"rccl": "RCCL ring all-gather (ncclAllGather)",
+               "rccl-p2p": "RCCL grouped send/recv all-gather",
+               "rccl-pull": "IPC peer-pull all-gather (RCCL barriers)",
+               "torch": "torch.distributed all-gather"}[self.comm_kind]
+        if self.exchange == "halo":
+            via = {"torch": "torch.distributed"}.get(self.comm_kind, "RCCL") + \
+                " grouped send/recv of the halo rows only"
+            depth = self.halo_chunks
+        else:
+            via += " of the padded Split(0) shards of B"
+            depth = self.chunks
+        pipe = f", {depth} column blocks pipelined" if depth > 1 else ""
+        return f"1-D row split x{w} (BalancedSplitter rows) + {via}{pipe}"
+
+    # tests only: "name-prefix:factor[,...]" multiplies the measured time of matching candidates
+    # (a grid made to look fastest, to check the 1-D choice); never set in a measured run
+    _TEST_SCALE_ENV = "OFX_TUNE_TEST_SCALE"
+
     def tune(self, out, pipelines=(1, 2, 4), reps: int = 3, force: bool = False,
              budget_s: float | None = None, prune: float = 3.0,
-             first: tuple | None = None, log=None, on_candidate=None) -> dict:
+             first: tuple | None = None, log=None, on_candidate=None,
+             rowsplit_only: bool = False, kinds: tuple | None = None) -> dict:
         """Times every exchange on this node with the real step over the bound CSR: all-gather
-        (ring / point-to-point / peer pull) x pipeline depth, the halo exchange and the grid plans
-        if built.  Keeps the fastest.  Timings are max-reduced over ranks, so all ranks choose the same; every
-        candidate produces the same bytes.  Returns {"<comm>/p<C>" | "halo[/p<C>]" | "nsplit[/s<S>]"
-        | "grid<R>x<C>[/s<S>]": ms} of the candidates measured.
+        (ring / point-to-point) x pipeline depth, the halo exchange and the grid plans if built.
+        Keeps the fastest -- with `rowsplit_only`, the fastest 1-D row-split candidate (all-gather
+        or halo: the north star's partition); grids are then still measured, after every 1-D
+        candidate, and reported in `self.tune_best_2d` but never kept.  Timings are max-reduced
+        over ranks, so all ranks choose the same; every candidate produces the same bytes.
+        Returns {"<comm>/p<C>" | "halo[/p<C>]" | "nsplit[/s<S>]" | "grid<R>x<C>[/s<S>]": ms} of
+        the candidates measured.
+
+        The all-gather kinds are `kinds`, default ring + grouped point-to-point.  The IPC peer
+        pull ("rccl-pull") is opt-in (kinds=(..., "rccl-pull") or RowSplitSpmm(comm="rccl-pull")
+        pinned by the caller): its cross-GPU visibility has not run on two devices yet.
 
         Order and bounds (so the first 8-GPU run ends in bounded time): the candidates named in
-        `first` (default: the plain row split + all-gather of the north star, "<comm>/p1", then the
-        2x4 grid with sub-block overlap, DESIGN.md §4's expected best at 8 GPUs), then the rest in
-        ascending model time (_model_ms).  After the first measurement R_X is refitted to it; a
-        candidate whose refitted model time exceeds `prune` x the best measured time is skipped,
-        and once `budget_s` seconds have passed (max over ranks) the rest are skipped.  The plain
-        all-gather is never skipped (the north star's number is always
-        measured, whichever candidate wins).  `on_candidate(name)` is called before each
-        measurement (the bench's per-rank phase log and watchdog).
+        `first` (default: the plain row split + all-gather of the north star, "<comm>/p1"; without
+        `rowsplit_only` also the 2x4 grid with sub-block overlap), then the rest in ascending
+        model time (_model_ms), 1-D candidates before grids under `rowsplit_only`.  After the
+        first measurement R_X is refitted to it; a candidate whose refitted model time exceeds
+        `prune` x the best measured time is skipped, and once `budget_s` seconds have passed (max
+        over ranks) the rest are skipped.  The plain all-gather is never skipped (VERDICT r3 item
+        4: the north star's number is always measured, whichever candidate wins).
+        `on_candidate(name)` is called before each measurement (the bench's per-rank phase log
+        and watchdog).  Each candidate's first (untimed) step runs under the exchange deadline
+        (a peer that never joins is named); its timed reps run with the deadline off, as the
+        timed steps do, so a pipelined exchange overlaps its SpMM there too.
         Every decision uses max-reduced values, so all ranks take the same path.  The record is in
         `self.tune_report`: per candidate the model time, the measured time and the status.
         One rank has nothing to exchange, so it keeps its setting unless `force` (tests).  With
@@ -1028,11 +1080,24 @@ class RowSplitSpmm:
         if self._bound is None:
             raise RuntimeError("tune: bind() the CSR first")
         self.tune_report = {}
+        self.tune_best_2d = None
         if self.world == 1 and not force:
             return {}
         native = self.comm_kind.startswith("rccl")
-        kinds = (("rccl", "rccl-p2p") + (("rccl-pull",) if self.world <= PEER_MAX_RANKS else ())
-                 if native else ("torch",))
+        if kinds is None:
+            kinds = ("rccl", "rccl-p2p") if native else ("torch",)
+        if native:
+            bad = [kd for kd in kinds if kd not in ("rccl", "rccl-p2p", "rccl-pull")]
+            if "rccl-pull" in kinds and self.world > PEER_MAX_RANKS:
+                bad.append("rccl-pull")
+        else:
+            bad = [kd for kd in kinds if kd != "torch"]
+        if bad:
+            raise ValueError(f"tune: all-gather kinds {bad} not available on this communicator")
+        test_scale = []
+        for item in filter(None, os.environ.get(self._TEST_SCALE_ENV, "").split(",")):
+            pre, _, f = item.partition(":")
+            test_scale.append((pre, float(f)))
         base = "rccl" if native else "torch"
         on_gpu = self.device.type == "cuda"
         red_dev = self.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
@@ -1058,10 +1123,14 @@ class RowSplitSpmm:
             # is timed as +inf everywhere by the max-reduce, so no rank keeps it; so is one whose
             # output differs from the first candidate's on any rank (a wrong exchange).
             ms = float("inf")
+            deadline = self.exchange_deadline_s
             try:
-                self.step(out)
+                self.step(out)  # untimed, under the deadline: every exchange awaited
                 if on_gpu:
                     torch.cuda.synchronize(self.device)
+                if deadline > 0:  # the timed reps run as the timed steps do: asynchronous
+                    self.set_exchange_deadline(0)
+                if on_gpu:
                     e0 = torch.cuda.Event(enable_timing=True)
                     e1 = torch.cuda.Event(enable_timing=True)
                     e0.record()
@@ -1079,6 +1148,12 @@ class RowSplitSpmm:
                 raise  # a peer that never joined: no candidate can be timed, the rank ends
             except Exception as e:  # noqa: BLE001 -- reported, candidate dropped
                 self.tune_errors[f"{self.exchange}/{self.comm_kind}/p{self.chunks}"] = repr(e)
+            finally:
+                if deadline > 0 and self.exchange_deadline_s != deadline:
+                    self.set_exchange_deadline(deadline)
+            for pre, f in test_scale:
+                if cur_name[0].startswith(pre):
+                    ms *= f
             ms = max_over_ranks(ms)
             if not math.isfinite(ms):
                 return ms
@@ -1126,15 +1201,19 @@ class RowSplitSpmm:
         prior = {nm: self._model_ms(*model[nm], self.R_X, self.R_HBM) for nm in model}
         always = {f"{base}/p1"}
         if first is None:
-            first = (f"{base}/p1", "grid2x4/s2")
+            first = (f"{base}/p1",) if rowsplit_only else (f"{base}/p1", "grid2x4/s2")
+        oned = self.is_rowsplit_exchange
         cands.sort(key=lambda c: (c[0] not in first,
-                                  first.index(c[0]) if c[0] in first else 0, prior[c[0]], c[0]))
+                                  first.index(c[0]) if c[0] in first else 0,
+                                  rowsplit_only and not oned(c[0]), prior[c[0]], c[0]))
 
         times = {}
         self.tune_errors = {}
         r_x = self.R_X
         t_start = time.perf_counter()
+        cur_name = [None]
         for name, setter, _, _ in cands:
+            cur_name[0] = name
             rec = {"predicted_ms": round(prior[name], 4), "recv_mb": round(model[name][0] / 1e6, 2),
                    "spmm_mb": round(model[name][1] / 1e6, 2)}
             self.tune_report[name] = rec
@@ -1174,7 +1253,14 @@ class RowSplitSpmm:
         self.tune_rate_fit = r_x
         if not times:
             raise RuntimeError(f"RowSplitSpmm.tune: every exchange failed: {self.tune_errors}")
-        best = min(times, key=times.get)
+        best = self.pick_best(times, rowsplit_only)
+        two_d = {nm: ms for nm, ms in times.items() if not oned(nm)}
+        if two_d:
+            g = min(two_d, key=two_d.get)
+            self.tune_best_2d = (g, two_d[g])
+        if best is None:
+            raise RuntimeError(f"RowSplitSpmm.tune: no 1-D row-split exchange completed: "
+                               f"{self.tune_errors}")
         if self.halo is not None:
             self.set_halo_pipeline(int(best.split("/p")[1]) if best.startswith("halo/p") else 1)
         if best.startswith("halo"):

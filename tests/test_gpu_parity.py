@@ -374,7 +374,10 @@ def test_row_split_rccl_single_rank(device):
         d = (rp.to(device), ci.to(device), v.to(device))
         rs.bind(*d, halo=True, full_csr=d, grid_subs=(1, 4))
         assert rs.halo.halo_rows == 0 and rs.halo.k_compact == k  # one rank owns every row
+        # the IPC pull is opt-in: absent from the default kinds, measured when named
         times = rs.tune(out2, reps=1, force=True)
+        assert len(times) == 11 and not any(t.startswith("rccl-pull") for t in times)
+        times = rs.tune(out2, reps=1, force=True, kinds=("rccl", "rccl-p2p", "rccl-pull"))
         assert len(times) == 14 and "rccl-pull/p4" in times and "halo" in times and "nsplit" in times and "nsplit/s4" in times
         assert "halo/p2" in times and "halo/p4" in times
         for exchange in ("allgather", "halo", "halo/p4", "nsplit", "nsplit/s4"):

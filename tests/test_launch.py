@@ -141,7 +141,10 @@ def test_bench_eight_rank_tune_is_ordered_and_bounded():
     cands = line["extra"]["tune_candidates"]
     assert len(cands) >= 12  # 3 all-gather depths (gloo: one kind), 3 halo, 6 grids
     assert all("predicted_ms" in c for c in cands.values())
-    assert list(cands)[:2] == ["torch/p1", "grid2x4/s2"]  # the measurement order
+    order = list(cands)  # the measurement order: the north star first, every 1-D before grids
+    assert order[0] == "torch/p1"
+    is_2d = [k.startswith(("grid", "nsplit")) for k in order]
+    assert is_2d == sorted(is_2d) and any(is_2d)
     measured = [k for k, c in cands.items() if c["status"] == "measured"]
     assert measured == ["torch/p1"]
     assert all(c["status"] == "skipped: budget" for k, c in cands.items() if k != "torch/p1")
@@ -152,6 +155,46 @@ def test_bench_eight_rank_tune_is_ordered_and_bounded():
     for r in range(8):
         assert f"[rank {r}/8]" in p.stderr and "phase: tune: torch/p1" in p.stderr
 
+
+def test_bench_eight_rank_value_is_the_rowsplit_even_when_a_grid_is_faster():
+    """at 8 ranks the line's value and label come from the 1-D row split the
+    north star names (all-gather or halo), even when a 2-D grid measured faster (injected: the
+    tests-only OFX_TUNE_TEST_SCALE divides every grid's measured time by 10^4).  The label is
+    built from the kept exchange, the grid is reported under extra.grid_best, and every rank
+    joined the exchange's communicator."""
+    p = _bench(["--gpus", "8", "--backend", "gloo", "--device", "cpu", "--config", "tiny",
+                "--steps", "2", "--warmup", "1", "--tune-budget", "600"],
+               {"OMP_NUM_THREADS": "1", "OFX_TUNE_TEST_SCALE": "grid:1e-4,nsplit:1e-4"},
+               drop=_SPAWN_ENV_DROP)
+    line = _bench_line(p)
+    ex = line["extra"]
+    cands = ex["tune_candidates"]
+    kept = ex["exchange"]
+    assert kept in ("allgather", "halo") and ex["exchange_is_rowsplit"]
+    # the grid measured fastest, and was not kept
+    g = ex["grid_best"]
+    assert g is not None and g["exchange"].startswith(("grid", "nsplit"))
+    tune = {k: v for k, v in ex["allgather_tune_ms"].items() if v is not None}
+    assert min(tune, key=tune.get) == g["exchange"]
+    kept_name = min((k for k in tune if not k.startswith(("grid", "nsplit"))), key=tune.get)
+    assert cands[kept_name]["status"] == "measured"
+    # the label names what ran
+    par = line["config"]["parallelism"]
+    assert par.startswith("REHEARSAL") and "1-D row split x8" in par
+    if kept == "halo":
+        assert "halo rows only" in par and kept_name.startswith("halo")
+    else:
+        assert "all-gather" in par and kept_name.startswith("torch/p")
+        depth = int(kept_name.split("/p")[1])
+        assert ex["pipeline_blocks"] == depth
+        assert (f"{depth} column blocks pipelined" in par) == (depth > 1)
+    assert "grid" not in par
+    # value = the whole job's FLOPs over the timed steps of that exchange
+    c = line["config"]
+    assert abs(line["value"] - 2 * c["nnz"] * c["n"] / (line["ms_per_step"] * 1e-3) / 1e9) \
+        <= 1e-3 * line["value"] + 0.02
+    assert ex["ranks_seen"] == ex["exchange_comm_ranks"] == line["n_gpus"] == 8
+    assert ex["rccl_comm_ranks"] is None  # gloo rehearsal: no RCCL communicator
 
 def test_bench_stalled_rank_names_its_phase_and_fails():
     """A rank stalled in a phase past its limit (injected: rank 1 sleeps in its first tune
