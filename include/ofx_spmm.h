@@ -106,13 +106,20 @@ int ofx_debug_set(int knob, int64_t value);
  * in chunk order into acc = 0.  split_threshold <= 0 selects the default
  * ofx_spmm_default_split(n); split_threshold == INT64_MAX (or `ordered` != 0) never splits,
  * which is exactly the reference composition's order.                                      */
+/* Versioned structs (ofx_spmm_options, ofx_tensor_desc, ofx_placement) open with two tagged
+ * words: struct_size = sizeof the struct as the CALLER was compiled, then magic =
+ * OFX_STRUCT_MAGIC ("OFX1").  The library checks the tag FIRST and refuses (OFX_EINVAL) a struct
+ * without it, before it trusts struct_size: an unversioned caller's first 8 bytes are data (the
+ * round-4 options began with int64 split_threshold, whose low half would otherwise read as a
+ * size), and no such layout holds the tag.  With the tag present, only the fields inside
+ * struct_size are read and the rest take their defaults (a caller built against an older
+ * versioned header keeps working); a size below the first tagged layout is refused.  Always
+ * initialise with the OFX_*_INIT macros.                                                      */
+#define OFX_STRUCT_MAGIC 0x4F465831u /* "OFX1" */
+
 typedef struct ofx_spmm_options {
-  uint32_t struct_size;    /* sizeof(ofx_spmm_options) as the CALLER was compiled: the library *
-                            * reads only the fields inside it and takes the defaults for the   *
-                            * rest (a caller built against an older header keeps working); a   *
-                            * size below OFX_SPMM_OPTIONS_MIN_SIZE (e.g. 0: not set) is refused *
-                            * with OFX_EINVAL.  Initialise with OFX_SPMM_OPTIONS_INIT.          */
-  int32_t reserved0;       /* 0                                                              */
+  uint32_t struct_size;    /* sizeof(ofx_spmm_options) as the CALLER was compiled (above)    */
+  uint32_t magic;          /* OFX_STRUCT_MAGIC                                               */
   int64_t split_threshold; /* 0 = default                                                    */
   int64_t chunk;           /* 0 = same as split_threshold                                    */
   int32_t ordered;         /* != 0: never split (reference order, slower on hub rows)       */
@@ -132,9 +139,10 @@ typedef struct ofx_spmm_options {
                             * nnz * rows / m.  Picks the kernel form only (launches of a few *
                             * rows of a degree-sorted graph); no numeric effect.             */
 } ofx_spmm_options;
-/* The first versioned layout ended at `reserved` (48 bytes); range_nnz came after it.         */
+/* The first tagged layout ended at `reserved` (48 bytes); range_nnz came after it.            */
 #define OFX_SPMM_OPTIONS_MIN_SIZE 48u
-#define OFX_SPMM_OPTIONS_INIT {(uint32_t)sizeof(ofx_spmm_options), 0, 0, 0, 0, 0, 0, 0, 0, 0}
+#define OFX_SPMM_OPTIONS_INIT \
+  {(uint32_t)sizeof(ofx_spmm_options), OFX_STRUCT_MAGIC, 0, 0, 0, 0, 0, 0, 0, 0}
 
 /* The default split threshold for dense width n (a fixed function of n; part of the numeric
  * contract).  Written out in DESIGN.md §3 and restated by oracle/oracle.py.                */
@@ -466,15 +474,18 @@ int ofx_synth_dense_host(int val_dtype, int64_t r_begin, int64_t r_end, int64_t 
 typedef struct ofx_tensor_desc {
   uint32_t struct_size; /* sizeof(ofx_tensor_desc) as the caller was compiled (checked, as in   *
                          * ofx_spmm_options; OFX_TENSOR_DESC_INIT)                              */
+  uint32_t magic;       /* OFX_STRUCT_MAGIC                                                     */
   int32_t dtype;
   int32_t device;
   int32_t ndim;
+  int32_t reserved;     /* 0                                                                    */
   int64_t shape[2];
   int64_t stride[2];
   void* data;
 } ofx_tensor_desc;
-#define OFX_TENSOR_DESC_MIN_SIZE 56u
-#define OFX_TENSOR_DESC_INIT {(uint32_t)sizeof(ofx_tensor_desc), 0, 0, 0, {0, 0}, {0, 0}, 0}
+#define OFX_TENSOR_DESC_MIN_SIZE 64u
+#define OFX_TENSOR_DESC_INIT \
+  {(uint32_t)sizeof(ofx_tensor_desc), OFX_STRUCT_MAGIC, 0, 0, 0, 0, {0, 0}, {0, 0}, 0}
 /* Shape/dtype inference of op "spmm_csr" (oneflow/user/ops/spmm_op.cpp mirror). Fills
  * out->dtype/ndim/shape; returns OFX_EINVAL with the op's error message on mismatch.      */
 int ofx_functional_spmm_csr_infer(const ofx_tensor_desc* row_ptr, const ofx_tensor_desc* col_idx,
@@ -575,14 +586,16 @@ int ofx_process_ctx_init(int64_t rank, int64_t world, ofx_kv_push_fn push, ofx_k
 typedef struct ofx_placement {
   uint32_t struct_size; /* sizeof(ofx_placement) as the caller was compiled (checked, as in     *
                          * ofx_spmm_options; OFX_PLACEMENT_INIT)                                */
+  uint32_t magic;       /* OFX_STRUCT_MAGIC                                                     */
   int32_t device_type;
+  int32_t reserved;     /* 0                                                                    */
   int64_t parallel_num;
   int64_t parallel_id;
   const int64_t* machine_ids;
   const int64_t* device_ids;
 } ofx_placement;
-#define OFX_PLACEMENT_MIN_SIZE 40u
-#define OFX_PLACEMENT_INIT {(uint32_t)sizeof(ofx_placement), 0, 0, 0, 0, 0}
+#define OFX_PLACEMENT_MIN_SIZE 48u
+#define OFX_PLACEMENT_INIT {(uint32_t)sizeof(ofx_placement), OFX_STRUCT_MAGIC, 0, 0, 0, 0, 0, 0}
 /* Whether ccl::AllGather and a ccl::CommunicationContext are registered for a device type
  * (REGISTER_COLLECTIVE_COMMUNICATION, collective_communication/include/all_gather.h:24-38). */
 int ofx_ccl_registered(int device_type, int* all_gather, int* communication_context);

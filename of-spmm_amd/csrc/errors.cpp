@@ -41,18 +41,32 @@ int guard_exception(const char* fn) {
   }
 }
 
+const char* versioned_struct_problem(const void* p, uint32_t min_size) {
+  if (p == nullptr) return nullptr;
+  uint32_t head[2];  // struct_size, magic: as bytes (the caller's struct may be a shorter layout)
+  std::memcpy(head, p, sizeof(head));
+  if (head[1] != OFX_STRUCT_MAGIC)
+    return "has no OFX_STRUCT_MAGIC tag: an unversioned caller, or a struct not initialised with "
+           "its OFX_*_INIT macro";
+  if (head[0] < min_size) return "has a struct_size below the first tagged layout";
+  return nullptr;
+}
+
 int read_options(const ofx_spmm_options* in, ofx_spmm_options* out, const char* fn) {
   std::memset(out, 0, sizeof(*out));
   out->struct_size = sizeof(*out);
+  out->magic = OFX_STRUCT_MAGIC;
   if (in == nullptr) return OFX_OK;  // every field at its default
-  // the caller's object may be shorter than this header's struct: its first 4 bytes only, as bytes
+  if (const char* why = versioned_struct_problem(in, OFX_SPMM_OPTIONS_MIN_SIZE)) {
+    uint32_t head[2];
+    std::memcpy(head, in, sizeof(head));
+    return fail(OFX_EINVAL,
+                "%s: ofx_spmm_options %s (struct_size %u, tag 0x%08x; the first tagged layout is "
+                "%u bytes): initialise the struct with OFX_SPMM_OPTIONS_INIT",
+                fn, why, head[0], head[1], OFX_SPMM_OPTIONS_MIN_SIZE);
+  }
   uint32_t size = 0;
   std::memcpy(&size, in, sizeof(size));
-  if (size < OFX_SPMM_OPTIONS_MIN_SIZE)
-    return fail(OFX_EINVAL,
-                "%s: ofx_spmm_options.struct_size = %u is below the first versioned layout (%u "
-                "bytes): initialise the struct with OFX_SPMM_OPTIONS_INIT",
-                fn, size, OFX_SPMM_OPTIONS_MIN_SIZE);
   std::memcpy(out, in, size < sizeof(*out) ? size : sizeof(*out));
   out->struct_size = sizeof(*out);
   return OFX_OK;

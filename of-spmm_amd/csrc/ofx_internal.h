@@ -38,10 +38,16 @@ int take_device_error(const char* where);
 // Test knobs (ofx_debug_set): the value of `knob`, or `dflt` when unset.
 int64_t debug_knob(int knob, int64_t dflt);
 
-// Versioned C-ABI structs (include/ofx_spmm.h): a caller's options are read up to its struct_size
-// (the fields it was compiled with), the rest are defaults; a size below the first versioned
-// layout is refused (OFX_EINVAL), which also catches an unversioned (round-3) caller.  Tensor
-// descriptors and placements are checked where they are read (functional/*.cpp).
+// Versioned C-ABI structs (include/ofx_spmm.h).  The tag word (offset 4) is checked before
+// struct_size is trusted: every struct of every layout is at least 8 bytes, and no unversioned
+// layout holds OFX_STRUCT_MAGIC there (the round-4 options had the high half of an int64
+// split_threshold; the round-5 descriptors dtype / device_type), so an unversioned caller is
+// refused for certain, never misread.  Returns NULL when the struct is usable, else why not.
+const char* versioned_struct_problem(const void* p, uint32_t min_size);
+// A caller's options are read up to its struct_size (the fields it was compiled with), the rest
+// are defaults; an untagged struct or a size below the first tagged layout is refused
+// (OFX_EINVAL).  Tensor descriptors and placements are checked where they are read
+// (functional/*.cpp) with versioned_struct_problem.
 int read_options(const ofx_spmm_options* in, ofx_spmm_options* out, const char* fn);
 }  // namespace ofx
 

@@ -46,9 +46,9 @@ DeviceType DeviceOf(int32_t code) {
 
 Maybe<void> MakeParallelDesc(const ofx_placement* pl, ParallelDesc* pd) {
   CHECK_OR_RETURN(pl != nullptr) << Error::RuntimeError() << "NULL placement";
-  CHECK_OR_RETURN(pl->struct_size >= OFX_PLACEMENT_MIN_SIZE)
-      << Error::RuntimeError() << "ofx_placement.struct_size = " << pl->struct_size
-      << " is below the first versioned layout (" << OFX_PLACEMENT_MIN_SIZE
+  const char* why = ofx::versioned_struct_problem(pl, OFX_PLACEMENT_MIN_SIZE);
+  CHECK_OR_RETURN(why == nullptr)
+      << Error::RuntimeError() << "ofx_placement " << why << " (" << OFX_PLACEMENT_MIN_SIZE
       << " bytes): initialise it with OFX_PLACEMENT_INIT";
   CHECK_OR_RETURN(pl->parallel_num >= 1 && pl->parallel_id >= 0 &&
                   pl->parallel_id < pl->parallel_num)
@@ -72,10 +72,10 @@ Shape ShapeOf(const ofx_tensor_desc* d) {
 
 Maybe<void> CheckContiguous(const ofx_tensor_desc* t, const char* name) {
   CHECK_OR_RETURN(t != nullptr) << Error::RuntimeError() << "NULL " << name;
-  CHECK_OR_RETURN(t->struct_size >= OFX_TENSOR_DESC_MIN_SIZE)
-      << Error::RuntimeError() << name << ": ofx_tensor_desc.struct_size = " << t->struct_size
-      << " is below the first versioned layout (" << OFX_TENSOR_DESC_MIN_SIZE
-      << " bytes): initialise it with OFX_TENSOR_DESC_INIT";
+  const char* why = ofx::versioned_struct_problem(t, OFX_TENSOR_DESC_MIN_SIZE);
+  CHECK_OR_RETURN(why == nullptr)
+      << Error::RuntimeError() << name << ": ofx_tensor_desc " << why << " ("
+      << OFX_TENSOR_DESC_MIN_SIZE << " bytes): initialise it with OFX_TENSOR_DESC_INIT";
   CHECK_OR_RETURN(t->ndim >= 1 && t->ndim <= 2) << Error::RuntimeError() << name << " must be 1-D or 2-D";
   if (t->ndim == 2 && t->shape[0] > 1)
     CHECK_OR_RETURN(t->stride[0] == t->shape[1] && (t->shape[1] <= 1 || t->stride[1] == 1))
@@ -315,8 +315,7 @@ class SpmmJob {
              ofx_tensor_desc* d_rp, ofx_tensor_desc* d_ci, ofx_tensor_desc* d_v,
              ofx_tensor_desc* d_b, ofx_tensor_desc* d_o) const {
     auto vec = [&](ofx_tensor_desc* d, int dt, int64_t len, const void* p) {
-      std::memset(d, 0, sizeof(*d));
-      d->struct_size = sizeof(*d);
+      *d = ofx_tensor_desc OFX_TENSOR_DESC_INIT;
       d->dtype = dt;
       d->device = device_;
       d->ndim = 1;
@@ -325,8 +324,7 @@ class SpmmJob {
       d->data = const_cast<void*>(p);
     };
     auto mat = [&](ofx_tensor_desc* d, int64_t r, const void* p) {
-      std::memset(d, 0, sizeof(*d));
-      d->struct_size = sizeof(*d);
+      *d = ofx_tensor_desc OFX_TENSOR_DESC_INIT;
       d->dtype = val_dtype_;
       d->device = device_;
       d->ndim = 2;

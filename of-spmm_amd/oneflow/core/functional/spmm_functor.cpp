@@ -34,11 +34,12 @@ int ToStatus(const Maybe<void>& m) {
   return ofx::fail(OFX_EINVAL, "%s: %s", m.kind().c_str(), m.message().c_str());
 }
 
-// A versioned descriptor (include/ofx_spmm.h): struct_size at least the first layout's.
+// A versioned descriptor (include/ofx_spmm.h): the tag, then struct_size at least the first
+// tagged layout's.
 Maybe<void> CheckDesc(const ofx_tensor_desc* d, const char* name) {
-  CHECK_OR_RETURN(d == nullptr || d->struct_size >= OFX_TENSOR_DESC_MIN_SIZE)
-      << Error::RuntimeError() << name << ": ofx_tensor_desc.struct_size = "
-      << (d ? d->struct_size : 0) << " is below the first versioned layout ("
+  const char* why = ofx::versioned_struct_problem(d, OFX_TENSOR_DESC_MIN_SIZE);
+  CHECK_OR_RETURN(why == nullptr)
+      << Error::RuntimeError() << name << ": ofx_tensor_desc " << why << " ("
       << OFX_TENSOR_DESC_MIN_SIZE << " bytes): initialise it with OFX_TENSOR_DESC_INIT";
   return Maybe<void>::Ok();
 }

@@ -33,27 +33,29 @@ class OfxError(RuntimeError):
         self.code = code
 
 
+STRUCT_MAGIC = 0x4F465831  # OFX_STRUCT_MAGIC, "OFX1"
+
+
 class _Versioned(ctypes.Structure):
-    """A versioned C-ABI struct: struct_size (its first field) is set to this layout's size, as
-    the OFX_*_INIT initialisers of include/ofx_spmm.h do."""
+    """A versioned C-ABI struct: struct_size and magic (its first two fields) are set to this
+    layout's size and OFX_STRUCT_MAGIC, as the OFX_*_INIT initialisers of include/ofx_spmm.h do;
+    positional fields start after them."""
 
     def __init__(self, *args, **kw):
-        super().__init__(ctypes.sizeof(type(self)), *args, **kw)
+        super().__init__(ctypes.sizeof(type(self)), STRUCT_MAGIC, *args, **kw)
 
 
 class Options(_Versioned):
-    _fields_ = [("struct_size", ctypes.c_uint32), ("reserved0", ctypes.c_int32),
+    _fields_ = [("struct_size", ctypes.c_uint32), ("magic", ctypes.c_uint32),
                 ("split_threshold", ctypes.c_int64), ("chunk", ctypes.c_int64),
                 ("ordered", ctypes.c_int32), ("variant", ctypes.c_int32),
                 ("heavy_threshold", ctypes.c_int64), ("planned", ctypes.c_int32),
                 ("reserved", ctypes.c_int32), ("range_nnz", ctypes.c_int64)]
 
-    def __init__(self, *args, **kw):  # positional fields start after struct_size / reserved0
-        super().__init__(0, *args, **kw)
-
 
 class Placement(_Versioned):
-    _fields_ = [("struct_size", ctypes.c_uint32), ("device_type", ctypes.c_int32),
+    _fields_ = [("struct_size", ctypes.c_uint32), ("magic", ctypes.c_uint32),
+                ("device_type", ctypes.c_int32), ("reserved", ctypes.c_int32),
                 ("parallel_num", ctypes.c_int64), ("parallel_id", ctypes.c_int64),
                 ("machine_ids", ctypes.POINTER(ctypes.c_int64)),
                 ("device_ids", ctypes.POINTER(ctypes.c_int64))]
@@ -70,8 +72,9 @@ DEV_CPU, DEV_HIP = 1, 4
 
 
 class TensorDesc(_Versioned):
-    _fields_ = [("struct_size", ctypes.c_uint32), ("dtype", ctypes.c_int32),
-                ("device", ctypes.c_int32), ("ndim", ctypes.c_int32),
+    _fields_ = [("struct_size", ctypes.c_uint32), ("magic", ctypes.c_uint32),
+                ("dtype", ctypes.c_int32), ("device", ctypes.c_int32), ("ndim", ctypes.c_int32),
+                ("reserved", ctypes.c_int32),
                 ("shape", ctypes.c_int64 * 2), ("stride", ctypes.c_int64 * 2),
                 ("data", ctypes.c_void_p)]
 

@@ -59,13 +59,13 @@ int main(void) {
                           NULL) == OFX_EINVAL); /* ldb < n */
   EXPECT(ofx_spmm_default_split(128) == 512);
 
-  /* versioned options (include/ofx_spmm.h): a caller compiled against the first versioned layout
-   * (48 bytes, before range_nnz) is read with range_nnz at its default; the round-3 layout, which
-   * had no struct_size field (its first 4 bytes are the low half of split_threshold), is refused
-   * instead of misread */
+  /* versioned options (include/ofx_spmm.h): a caller compiled against the first tagged layout
+   * (48 bytes, before range_nnz) is read with range_nnz at its default; the unversioned (round-3
+   * and round-4) layout, which had no struct_size and no tag (its first 4 bytes are the low half
+   * of split_threshold), is refused instead of misread, whatever split_threshold holds */
   struct options_v1 {
     uint32_t struct_size;
-    int32_t reserved0;
+    uint32_t magic;
     int64_t split_threshold, chunk;
     int32_t ordered, variant;
     int64_t heavy_threshold;
@@ -80,6 +80,7 @@ int main(void) {
   EXPECT(sizeof(v1) == OFX_SPMM_OPTIONS_MIN_SIZE && sizeof(ofx_spmm_options) > sizeof(v1));
   memset(&v1, 0, sizeof(v1));
   v1.struct_size = sizeof(v1);
+  v1.magic = OFX_STRUCT_MAGIC;
   v1.split_threshold = 1; /* every row of 2 nonzeros splits: same bits (exact inputs) */
   memset(c, 0xff, sizeof(c));
   EXPECT(ofx_spmm_csr_cpu(1, OFX_DT_INT32, OFX_DT_FLOAT, 2, 3, 2, 3, rp, col, val, b, 2, c, 2, 0, 2,
@@ -92,9 +93,18 @@ int main(void) {
   EXPECT(ofx_spmm_csr_cpu(1, OFX_DT_INT32, OFX_DT_FLOAT, 2, 3, 2, 3, rp, col, val, b, 2, c, 2, 0, 2,
                           (const ofx_spmm_options*)&r3) == OFX_EINVAL);
   EXPECT(strstr(ofx_last_error(), "OFX_SPMM_OPTIONS_INIT") != NULL);
+  /* split_threshold = 128 reads as struct_size 128 (>= the minimum) without the tag */
+  r3.split_threshold = 128;
+  EXPECT(ofx_spmm_csr_cpu(1, OFX_DT_INT32, OFX_DT_FLOAT, 2, 3, 2, 3, rp, col, val, b, 2, c, 2, 0, 2,
+                          (const ofx_spmm_options*)&r3) == OFX_EINVAL);
+  EXPECT(strstr(ofx_last_error(), "OFX_STRUCT_MAGIC") != NULL);
+  /* a tagged first layout whose tag was overwritten is refused too */
+  v1.magic = 0;
+  EXPECT(ofx_spmm_csr_cpu(1, OFX_DT_INT32, OFX_DT_FLOAT, 2, 3, 2, 3, rp, col, val, b, 2, c, 2, 0, 2,
+                          (const ofx_spmm_options*)&v1) == OFX_EINVAL);
   {
     ofx_spmm_options cur = OFX_SPMM_OPTIONS_INIT;
-    EXPECT(cur.struct_size == sizeof(ofx_spmm_options));
+    EXPECT(cur.struct_size == sizeof(ofx_spmm_options) && cur.magic == OFX_STRUCT_MAGIC);
     EXPECT(ofx_spmm_csr_cpu(1, OFX_DT_INT32, OFX_DT_FLOAT, 2, 3, 2, 3, rp, col, val, b, 2, c, 2, 0,
                             2, &cur) == OFX_OK);
   }

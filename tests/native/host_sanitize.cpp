@@ -327,6 +327,31 @@ void check_error_paths() {
   EXPECT(ofx_boxing_check_ccl_s2b(&pl, 2, shape, "S(0)", "B") == OFX_OK, "placement");
   pl.struct_size = 4;
   EXPECT(ofx_boxing_check_ccl_s2b(&pl, 2, shape, "S(0)", "B") == OFX_EINVAL, "placement size");
+  pl.struct_size = sizeof(pl);
+  pl.magic = 0;  // a size that looks right is not trusted without the tag
+  EXPECT(ofx_boxing_check_ccl_s2b(&pl, 2, shape, "S(0)", "B") == OFX_EINVAL, "placement tag");
+  ofx_tensor_desc untagged = ci;
+  untagged.magic = 0;
+  EXPECT(ofx_functional_spmm_csr(nullptr, &rp, &untagged, &v, m, k, &bd, &od, nullptr, 0) ==
+             OFX_EINVAL,
+         "descriptor tag");
+  // the unversioned options layout (no struct_size, no tag) in a heap block of exactly its size,
+  // with split_threshold = 128: its low half would read as a plausible struct_size; ASan checks
+  // that nothing past the 40 bytes is read and the call is refused
+  struct options_unversioned {
+    int64_t split_threshold, chunk;
+    int32_t ordered, variant;
+    int64_t heavy_threshold;
+    int32_t planned, reserved;
+  };
+  auto* r4 = static_cast<options_unversioned*>(std::malloc(sizeof(options_unversioned)));
+  std::memset(r4, 0, sizeof(*r4));
+  r4->split_threshold = 128;
+  EXPECT(ofx_spmm_csr_cpu(1, OFX_DT_INT32, OFX_DT_FLOAT, m, k, n, nnz, a.rp.data(), a.ci.data(),
+                          a.val.data(), b.data(), n, c.data(), n, 0, m,
+                          reinterpret_cast<const ofx_spmm_options*>(r4)) == OFX_EINVAL,
+         "unversioned options, split_threshold 128");
+  std::free(r4);
   EXPECT(ofx_debug_set(99, 0) == OFX_EINVAL, "unknown knob");
 }
 

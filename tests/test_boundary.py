@@ -76,6 +76,32 @@ def test_options_struct_size_is_checked():
     o.struct_size = 47
     with pytest.raises(_lib.OfxError):
         ops.spmm_csr_cpu(rp, ci, v, b, m, k, options=o)
+    # the tag is checked before struct_size is trusted
+    o = ops.make_options()
+    assert o.magic == _lib.STRUCT_MAGIC == 0x4F465831
+    o.magic = 0
+    with pytest.raises(_lib.OfxError) as ei:
+        ops.spmm_csr_cpu(rp, ci, v, b, m, k, options=o)
+    assert ei.value.code == _lib.OFX_EINVAL and "OFX_STRUCT_MAGIC" in str(ei.value)
+
+
+def test_unversioned_options_are_refused_whatever_split_threshold_holds():
+    """The unversioned (round-3/4) layout began with int64 split_threshold: with 128 there its
+    low half reads as a plausible struct_size.  The missing tag refuses it before any field is
+    read (the 40-byte object sits at the end of a buffer whose tail is poisoned)."""
+    rp, ci, v, b, m, k = small_problem(3)
+
+    class Unversioned(ctypes.Structure):
+        _fields_ = [("split_threshold", ctypes.c_int64), ("chunk", ctypes.c_int64),
+                    ("ordered", ctypes.c_int32), ("variant", ctypes.c_int32),
+                    ("heavy_threshold", ctypes.c_int64), ("planned", ctypes.c_int32),
+                    ("reserved", ctypes.c_int32)]
+    for split in (128, 48, 56, 1 << 40):
+        u = Unversioned(split_threshold=split)
+        with pytest.raises(_lib.OfxError) as ei:
+            ops.spmm_csr_cpu(rp, ci, v, b, m, k,
+                             options=ctypes.cast(ctypes.pointer(u), ctypes.POINTER(_lib.Options)).contents)
+        assert ei.value.code == _lib.OFX_EINVAL and "OFX_STRUCT_MAGIC" in str(ei.value)
 
 
 def test_options_older_layout_takes_defaults_for_newer_fields():
@@ -115,6 +141,10 @@ def test_tensor_desc_and_placement_struct_size_are_checked():
     rc = LIB.ofx_functional_spmm_csr_infer(ctypes.byref(d[0]), ctypes.byref(d[1]), ctypes.byref(d[2]),
                                            m, k, ctypes.byref(d[3]), ctypes.byref(out))
     assert rc == _lib.OFX_EINVAL and "OFX_TENSOR_DESC_INIT" in _lib.last_error()
+    d[1].struct_size, d[1].magic = ctypes.sizeof(_lib.TensorDesc), 0  # a round-5 (untagged) caller
+    rc = LIB.ofx_functional_spmm_csr_infer(ctypes.byref(d[0]), ctypes.byref(d[1]), ctypes.byref(d[2]),
+                                           m, k, ctypes.byref(d[3]), ctypes.byref(out))
+    assert rc == _lib.OFX_EINVAL and "OFX_STRUCT_MAGIC" in _lib.last_error()
     pl = _lib.Placement()
     pl.device_type, pl.parallel_num, pl.parallel_id = _lib.DEV_CPU, 2, 0
     shape = (ctypes.c_int64 * 2)(10, 4)
@@ -122,6 +152,9 @@ def test_tensor_desc_and_placement_struct_size_are_checked():
     pl.struct_size = 8
     assert LIB.ofx_boxing_check_ccl_s2b(ctypes.byref(pl), 2, shape, b"S(0)", b"B") == _lib.OFX_EINVAL
     assert "OFX_PLACEMENT_INIT" in _lib.last_error()
+    pl.struct_size, pl.magic = ctypes.sizeof(_lib.Placement), 0
+    assert LIB.ofx_boxing_check_ccl_s2b(ctypes.byref(pl), 2, shape, b"S(0)", b"B") == _lib.OFX_EINVAL
+    assert "OFX_STRUCT_MAGIC" in _lib.last_error()
 
 
 # ---- workspace bound over row ranges --------------------------------------------
