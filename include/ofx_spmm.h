@@ -58,8 +58,9 @@ extern "C" {
 #define OFX_EUNSUPPORTED 4 /* dtype / layout combination not registered (OpKernelNotFound)     */
 #define OFX_ECOMM 5        /* RCCL error                                                       */
 #define OFX_EWORKSPACE 6   /* workspace smaller than ofx_spmm_csr_workspace_size()             */
-#define OFX_EPLAN 7        /* an EARLIER asynchronous launch wrote nothing: its device-side     *
-                            * work-list plan gave up, or it found no valid plan in its workspace *
+#define OFX_EPLAN 7        /* an EARLIER asynchronous launch failed and poisoned its output     *
+                            * (NaN): its device-side work-list plan gave up, or it found no     *
+                            * valid plan in its workspace                                        *
                             * (reported once, at the next launching call or sync; see            *
                             * ofx_device_error_check)                                            */
 #define OFX_EINTERNAL 8    /* an unexpected C++ exception inside the library, caught at the     *
@@ -78,11 +79,17 @@ const char* ofx_last_error(void);
 /* Library version string, e.g. "ofx-spmm 0.2.0 gfx950". */
 const char* ofx_version(void);
 
-/* Device-side loud failures.  A kernel that cannot produce its output writes none of it and raises
- * a device-error word (host-mapped memory); the library reports it as OFX_EPLAN, once, at the
- * next launching entry (ofx_spmm_csr*, ofx_sddmm_csr), at ofx_stream_sync / ofx_event_sync /
- * ofx_device_synchronize / ofx_graph_launch, or here (after the caller's own synchronisation,
- * e.g. torch.cuda.synchronize()).  Mirrors the reference's fatal kernel CHECKs
+/* Device-side loud failures.  A kernel that cannot produce its output (its work-list plan failed
+ * or is not valid) fills the whole output with one canonical quiet NaN (f32 0x7fc00000, f64
+ * 0x7ff8000000000000, bf16 0x7fc0, f16 0x7e00; the nonzeros of its rows for SDDMM), so no stale
+ * or uninitialised value can be read as a result, and raises a device-error word (host-mapped
+ * memory).  The library reports it as OFX_EPLAN, once, at the next launching entry
+ * (ofx_spmm_csr*, ofx_sddmm_csr, ofx_functional_spmm_csr*), at ofx_stream_sync /
+ * ofx_event_sync / ofx_device_synchronize / ofx_graph_launch, or here.  A foreign
+ * synchronisation (hipStreamSynchronize, torch.cuda.synchronize()) does not look at the word:
+ * call this after it, or read the NaN.  The words are process-wide, not per stream or device:
+ * with several threads or streams the report reaches whichever entry comes next, which may not
+ * be the caller of the failed launch.  Mirrors the reference's fatal kernel CHECKs
  * (oneflow/user/kernels/matrix_vector_product_kernel.cpp:98-105) as a status code.            */
 int ofx_device_error_check(void);
 
@@ -520,6 +527,40 @@ int ofx_functional_spmm_csr_global(void* stream, const ofx_tensor_desc* row_ptr,
                                    size_t tmp_bytes, int hierarchy_ndim, const int64_t* hierarchy,
                                    const int32_t* out_split_axes, int64_t parallel_id,
                                    int num_threads, size_t* tmp_size_out);
+/* Op attributes of "spmm_csr" beyond a_num_rows / a_num_cols (a tagged, versioned struct as
+ * ofx_spmm_options; OFX_SPMM_ATTRS_INIT).
+ *   static_csr: attr `static_csr` (SI64, default 0).  Non-zero promises that the CSR at these
+ *     addresses (row_ptr above all) is not rewritten while the op instance lives; the value is
+ *     part of the plan's key, so a caller that frees a static CSR and builds another one at the
+ *     same addresses gives it a new value.  The HIP kernel's OpKernelState
+ *     (OpKernel::CreateOpKernelState, oneflow/core/framework/op_kernel.h:292) then keeps the
+ *     work-list plan in a device workspace of its own, keyed on (static_csr, row_ptr's address,
+ *     m, k, n, nnz, row range, dtypes, schedule, stream), and later calls launch with
+ *     options.planned = 1: the planner kernel runs once per static CSR instead of once per call.
+ *     The first call of a key allocates and plans (not while the stream is capturing a graph:
+ *     such a call takes the ordinary path through the tmp buffer); at most 8 plans per state,
+ *     least recently used evicted.  No numeric effect; the kCPU kernel has no plan and ignores
+ *     it.  The eager entries below hold one state per (kernel registration, device), as
+ *     OneFlow's functor keeps one StatefulOpKernel per op expression and device.            */
+typedef struct ofx_spmm_attrs {
+  uint32_t struct_size; /* sizeof(ofx_spmm_attrs) as the caller was compiled                     */
+  uint32_t magic;       /* OFX_STRUCT_MAGIC                                                      */
+  int64_t static_csr;   /* 0 = plan every call (default)                                         */
+} ofx_spmm_attrs;
+#define OFX_SPMM_ATTRS_MIN_SIZE 16u
+#define OFX_SPMM_ATTRS_INIT {(uint32_t)sizeof(ofx_spmm_attrs), OFX_STRUCT_MAGIC, 0}
+/* ofx_functional_spmm_csr_global with the op's attributes (attrs == NULL: every default).  */
+int ofx_functional_spmm_csr_global_attrs(
+    void* stream, const ofx_tensor_desc* row_ptr, const ofx_tensor_desc* col_idx,
+    const ofx_tensor_desc* values, int64_t a_num_rows, int64_t a_num_cols,
+    const ofx_tensor_desc* b, int64_t b_logical_cols, ofx_tensor_desc* out, void* tmp,
+    size_t tmp_bytes, int hierarchy_ndim, const int64_t* hierarchy, const int32_t* out_split_axes,
+    int64_t parallel_id, int num_threads, size_t* tmp_size_out, const ofx_spmm_attrs* attrs);
+/* The static-CSR plans the eager op states hold, summed over devices: live entries, plans built
+ * (planner launches) and calls that reused a plan.  release != 0 first frees every entry's
+ * workspace (after a device synchronisation) so the next static call plans again.            */
+int ofx_spmm_static_plans(int64_t* entries, int64_t* plans, int64_t* hits, int release);
+
 /* 1-D shorthand of ofx_functional_spmm_csr_global: hierarchy {parallel_num}, out split on
  * out_split_axis (0 or -1; a column split needs the logical width, so it takes the _global form).
  * 2-D tensors must have unit column stride (refused with OFX_EINVAL otherwise).            */
@@ -641,6 +682,12 @@ int ofx_spmm_job_destroy(void* job);
  * ignore graph mode.  Stats: captures, launches of a captured graph without re-capture, and
  * captures that updated the executable in place.                                            */
 int ofx_spmm_job_set_graph(void* job, int enable);
+/* The compiled job's spmm_csr with attr static_csr (see ofx_spmm_attrs): the job's own kernel
+ * state (as a lazy UserKernel owns its OpKernelState) keeps the plan of its row_ptr, so eager
+ * runs and graph replays after the first launch no planner kernel.  0 turns it off (the
+ * default).  Stats: plans built and runs that reused one.                                   */
+int ofx_spmm_job_set_static(void* job, int64_t static_csr);
+int ofx_spmm_job_static_stats(void* job, int64_t* plans, int64_t* hits);
 int ofx_spmm_job_graph_stats(void* job, int64_t* captures, int64_t* replays, int64_t* updates);
 
 #ifdef __cplusplus

@@ -38,9 +38,13 @@
     if (ofx_rc_ != OFX_OK) return ofx_rc_;                                                     \
   } while (0)
 // The communicator behind a handle, or OFX_ECOMM if it was aborted (its NCCL object is gone).
+// The entry holds an EnqueueGuard for its whole body: an abort from another thread
+// (a watchdog) meanwhile only marks the communicator, and ncclCommAbort runs when the last entry
+// using it returns, so no enqueue ever reaches a freed communicator.
 #define OFX_LIVE_COMM(h, fn)                                                                   \
   OfxComm* ofx_cm_ = static_cast<OfxComm*>(h);                                                 \
   OFX_REQUIRE(ofx_cm_ != nullptr, OFX_EINVAL, "%s: NULL communicator", fn);                     \
+  EnqueueGuard ofx_eg_(ofx_cm_);                                                               \
   OFX_REQUIRE(!ofx_cm_->aborted.load(), OFX_ECOMM, "%s: the communicator was aborted (%s)", fn, \
               ofx_cm_->why.c_str());                                                           \
   ncclComm_t c = ofx_cm_->nccl
@@ -77,7 +81,10 @@ double seconds_since(std::chrono::steady_clock::time_point t0) {
 // aborted flag.  An abort (a deadline expiring, or ofx_comm_abort from a watchdog) frees the NCCL
 // object at once and leaves the handle alive: every later call returns OFX_ECOMM naming why, and
 // ofx_comm_destroy only frees the handle, so nothing touches the freed communicator.  `mu`
-// serialises an abort against a poll of the same communicator from another thread.
+// serialises an abort against a poll of the same communicator from another thread; `entries`
+// counts the C-ABI calls using the NCCL object (EnqueueGuard), and an abort while any is inside
+// only sets `aborted` (those calls see it and return OFX_ECOMM): ncclCommAbort then runs when the
+// last of them leaves.
 struct OfxComm {
   ncclComm_t nccl = nullptr;
   double call_timeout_s = 300.0;  // a call left ncclInProgress (non-blocking communicators)
@@ -85,21 +92,48 @@ struct OfxComm {
   std::mutex mu;
   std::atomic<bool> aborted{false};
   std::string why;
+  int entries = 0;             // calls inside (under mu)
+  bool abort_pending = false;  // aborted while entries > 0: ncclCommAbort at the last exit
   int* barrier_word = nullptr;  // device int of the stream-ordered barrier (ofx_allgather_pull)
 
   ~OfxComm() {
     if (barrier_word != nullptr) (void)hipFree(barrier_word);
   }
 
-  // ncclCommAbort once; the caller holds no lock
+  // ncclCommAbort once (deferred while a call is inside); the caller holds no lock
   void abort(const std::string& reason) {
     std::lock_guard<std::mutex> lock(mu);
     if (aborted.load()) return;
     why = reason;
     aborted.store(true);
+    if (entries > 0) {
+      abort_pending = true;
+      return;
+    }
     (void)ncclCommAbort(nccl);
     nccl = nullptr;
   }
+  void enter() {
+    std::lock_guard<std::mutex> lock(mu);
+    ++entries;
+  }
+  void leave() {
+    std::lock_guard<std::mutex> lock(mu);
+    if (--entries == 0 && abort_pending) {
+      abort_pending = false;
+      (void)ncclCommAbort(nccl);
+      nccl = nullptr;
+    }
+  }
+};
+
+// A C-ABI call using a communicator's NCCL object (OFX_LIVE_COMM).
+struct EnqueueGuard {
+  OfxComm* cm;
+  explicit EnqueueGuard(OfxComm* c) : cm(c) { cm->enter(); }
+  ~EnqueueGuard() { cm->leave(); }
+  EnqueueGuard(const EnqueueGuard&) = delete;
+  EnqueueGuard& operator=(const EnqueueGuard&) = delete;
 };
 
 // Completes a call that returned ncclInProgress (non-blocking communicator): polls the

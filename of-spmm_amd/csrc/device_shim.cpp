@@ -66,8 +66,8 @@ int take_device_error(const char* where) {
   vw[0] = 0;
   vw[1] = 0;
   return fail(OFX_EPLAN,
-              "%s: an earlier launch wrote nothing: %s (reported at the next call; its output "
-              "buffer holds whatever it held before)",
+              "%s: an earlier launch failed: %s (reported at the next call, process-wide; its "
+              "output was filled with quiet NaN)",
               where,
               failed ? "its device-side work-list plan gave up waiting for a predecessor block "
                        "(look-back spin limit)"

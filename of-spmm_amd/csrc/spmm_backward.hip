@@ -220,13 +220,22 @@ __device__ __forceinline__ bool sddmm_item(const I* __restrict__ rp, int64_t g, 
   return j0 < j1;
 }
 
-// A work list from a failed, superseded or never-built plan: the launch writes nothing and reports
-// it (spmm_plan.h plan_valid; the host's next entry returns OFX_EPLAN).
+// A work list from a failed, superseded or never-built plan: the launch fills its output (the
+// nonzeros of its rows, out[rp[row_begin] .. rp[row_begin + nrows])) with the canonical quiet NaN
+// and reports it (spmm_plan.h plan_valid; the host's next entry returns OFX_EPLAN).  Every launch
+// of a cut grid poisons the whole range (idempotent).
+template <typename T, typename I>
 __device__ __forceinline__ bool sddmm_plan_invalid(const unsigned long long* __restrict__ counters,
-                                                   int64_t block_base, unsigned* err) {
+                                                   int64_t block_base, unsigned* err,
+                                                   const I* __restrict__ rp, int64_t row_begin,
+                                                   int64_t nrows, T* __restrict__ out) {
   if (counters == nullptr || plan::plan_valid(counters)) return false;
   if (block_base + blockIdx.x == 0 && threadIdx.x == 0)
     plan::raise_device_error(err, plan::kErrPlanInvalid);
+  const int64_t j0 = (int64_t)rp[row_begin], j1 = (int64_t)rp[row_begin + nrows];
+  const T p = poison_value<T>();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j = j0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < j1; j += stride) out[j] = p;
   return true;
 }
 
@@ -243,7 +252,7 @@ __global__ void __launch_bounds__(kBlock)
 #pragma clang fp contract(off)
   using A = typename Num<T>::acc;
   constexpr int GPW = 64 / LG;
-  if (sddmm_plan_invalid(counters, block_base, err)) return;
+  if (sddmm_plan_invalid(counters, block_base, err, rp, row_begin, nrows, out)) return;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int gl = lane & (LG - 1);
@@ -323,7 +332,7 @@ __global__ void __launch_bounds__(kBlock)
 #pragma clang fp contract(off)
   using A = typename Num<T>::acc;
   constexpr int L = kWideLeaves / 64, U = 2;
-  if (sddmm_plan_invalid(counters, block_base, err)) return;
+  if (sddmm_plan_invalid(counters, block_base, err, rp, row_begin, nrows, out)) return;
   const int lane = threadIdx.x & 63;
   const int64_t g = (block_base + (int64_t)blockIdx.x) * (kBlock / 64) +
                     __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

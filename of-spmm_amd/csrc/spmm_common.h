@@ -121,6 +121,14 @@ OFX_HD T epilogue(typename Num<T>::acc acc, const T* bias, int64_t c, int act) {
   return y;
 }
 
+// The poison a launch with no valid work plan writes over its whole output:
+// one canonical quiet NaN of T (f32 0x7fc00000, f64 0x7ff8000000000000, bf16 0x7fc0,
+// f16 0x7e00), so no stale or uninitialised value can be read as a result.
+template <typename T>
+OFX_HD T poison_value() {
+  return Num<T>::store(typename Num<T>::acc(__builtin_nan("")));
+}
+
 OFX_HD int dtype_size(int dt) {
   switch (dt) {
     case OFX_DT_FLOAT: return 4;

@@ -1086,6 +1086,18 @@ __global__ void __launch_bounds__(64 * K::WPB)
 #else
 #define OFX_MAIN_WPE
 #endif
+// C[0, nrows) x [0, n) (row stride ldc) = the canonical quiet NaN, grid-stride over this launch.
+// The first consumer of an invalid plan runs it instead of its rows (spmm_plan.h plan_valid).
+template <typename T>
+__device__ __attribute__((noinline)) void poison_output(T* __restrict__ C, int64_t ldc,
+                                                        int64_t nrows, int64_t n) {
+  const T p = poison_value<T>();
+  const int64_t total = nrows * n;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride)
+    C[(e / n) * ldc + e % n] = p;
+}
+
 template <typename T, typename I, typename K>
 __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
     spmm_main_kernel(const I* __restrict__ rp, const I* __restrict__ col,
@@ -1101,9 +1113,11 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
   using A = typename Num<T>::acc;
   constexpr int VEC = K::VEC, LPR = K::LPR, kWaves = K::WPB;
   const int64_t bid = block_base + (int64_t)blockIdx.x;  // launches of > 2^31 threads are cut
-  // a plan that failed, was superseded or never built: write nothing, loudly (spmm_plan.h)
+  // a plan that failed, was superseded or never built: poison the output, loudly (spmm_plan.h);
+  // every launch of a cut grid poisons all of C (idempotent) and spmm_reduce then writes nothing
   if (counters != nullptr && !plan::plan_valid(counters)) {
     if (bid == 0 && threadIdx.x == 0) plan::raise_device_error(err, plan::kErrPlanInvalid);
+    poison_output<T>(C, ldc, nrows, n);
     return;
   }
   constexpr int GPW = 64 / LPR;
@@ -1336,7 +1350,7 @@ __global__ void __launch_bounds__(kBlock)
   using A = typename Num<T>::acc;
   using P = Pack<A, VEC>;
   constexpr int kPre = 16;  // partial rows in flight per lane (the adds stay in chunk order)
-  if (!plan::plan_valid(counters)) return;  // spmm_main reported it and wrote nothing either
+  if (!plan::plan_valid(counters)) return;  // spmm_main reported it and poisoned C
   const int64_t nhubs = (int64_t)OFX_LD(counters + 1);
   const int gl = threadIdx.x % L;
   const int64_t groups = (int64_t)gridDim.x * (kBlock / L);

@@ -83,9 +83,11 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // a block whose look-back gives up records the tag as failed (counters[kFail]), refuses the tag a
 // replay of the same capture would take next (counters[kPoison]: a block of this launch that had
 // not started yet may publish under it), and sets the library's device-error word.  Every
-// consumer of the work list (spmm_main, spmm_reduce, SDDMM) checks plan_valid() at entry and
-// writes nothing for a failed, stale or never-built plan; the host reports the error word at its
-// next entry (ofx_device_error_check).
+// consumer of the work list (spmm_main, spmm_reduce, SDDMM) checks plan_valid() at entry; for a
+// failed, stale or never-built plan the first consumer (spmm_main, SDDMM) fills its whole output
+// with one canonical quiet NaN (poison_value, VERDICT r5 item 3: no stale or uninitialised value
+// reads as a result) and the rest write nothing; the host reports the error word at its next
+// entry (ofx_device_error_check).
 //
 // Because heavy rows fill the order array from its end and light rows from its start, no block
 // needs a grand total.  A block
@@ -406,7 +408,7 @@ __global__ void __launch_bounds__(kBlock)
       for (int i = 0; i < kPlanVals; ++i) s_off[i] = pre[i];
     }
     if (lane == 0 && failed) {
-      // Loud failure: the consumers see counters[kFail] == the tag and write nothing, and the
+      // Loud failure: the consumers see counters[kFail] == the tag and poison their output, and the
       // host reports the error word at its next entry.  A predecessor that had not published may
       // not even have started; it can read the advanced epoch word and publish under the NEXT
       // launch's tag (a replay of the same capture), so that tag is refused too (kPoison).

@@ -13,6 +13,7 @@ REGISTER_USER_OP("spmm_csr")
     .Output("out")
     .Attr<int64_t>("a_num_rows", 0)
     .Attr<int64_t>("a_num_cols", 0)
+    .Attr<int64_t>("static_csr", 0)
     .SetLogicalTensorDescInferFn(SpmmCsrOp::InferLogicalTensorDesc)
     .SetPhysicalTensorDescInferFn(SpmmCsrOp::InferPhysicalTensorDesc)
     .SetGetSbpFn(SpmmCsrOp::GetSbp)

@@ -20,6 +20,7 @@
 #include "oneflow/core/boxing/ccl_boxing_function.h"
 #include "oneflow/core/control/ctrl_client.h"
 #include "oneflow/core/framework/framework.h"
+#include "oneflow/core/functional/spmm_functor.h"
 #include "oneflow/core/job/eager_rccl_comm_manager.h"
 #include "oneflow/core/job_rewriter/insert_nccl_logical_op_pass.h"
 #include "oneflow/user/kernels/collective_communication/include/all_gather.h"
@@ -189,6 +190,16 @@ class SpmmJob {
     if (!graph_enabled_) graph_.reset();
     return OFX_OK;
   }
+  // attr static_csr of the job's spmm_csr (include/ofx_spmm.h ofx_spmm_attrs): the job's own
+  // kernel state keeps the plan of the row_ptr it runs on, so the eager first run plans and
+  // every later run (or graph replay) launches planned.
+  void set_static(int64_t static_csr) { static_csr_ = static_csr; }
+  void static_stats(int64_t* plans, int64_t* hits) const {
+    int64_t e = 0, p = 0, h = 0;
+    if (spmm_state_) SpmmCsrPlanStateStats(spmm_state_.get(), &e, &p, &h, false);
+    if (plans) *plans = p;
+    if (hits) *hits = h;
+  }
   void graph_stats(int64_t* captures, int64_t* replays, int64_t* updates) const {
     if (captures) *captures = captures_;
     if (replays) *replays = replays_;
@@ -278,8 +289,9 @@ class SpmmJob {
     const int64_t h = pd_.parallel_num();
     const int32_t ax = 0;
     char* spmm_tmp = spmm_tmp_bytes_ ? static_cast<char*>(tmp) + gathered_bytes_ : nullptr;
-    return ofx_functional_spmm_csr_global(stream, &rp, &ci, &v, m_, k_, &b, -1, &o, spmm_tmp,
-                                          spmm_tmp_bytes_, 1, &h, &ax, pc_.parallel_id(), 0, nullptr);
+    return SpmmCsrGlobalWithState(stream, &rp, &ci, &v, m_, k_, &b, -1, &o, spmm_tmp,
+                                  spmm_tmp_bytes_, 1, &h, &ax, pc_.parallel_id(), static_csr_,
+                                  &spmm_state_);
   }
 
   Maybe<void> CompileGather(const Shape& b_logical, const std::string& stream_name) {
@@ -350,6 +362,8 @@ class SpmmJob {
   Shape b_shard_, b_full_;
   std::unique_ptr<user_op::OpKernel> gather_kernel_;
   std::shared_ptr<user_op::OpKernelState> gather_state_;
+  std::shared_ptr<user_op::OpKernelState> spmm_state_;  // spmm_csr's state (static_csr plans)
+  int64_t static_csr_ = 0;
   bool graph_enabled_ = false, ready_ = false;
   void* capture_stream_ = nullptr;
   std::unique_ptr<ep::HipGraphExecutable> graph_;
@@ -547,6 +561,22 @@ extern "C" int ofx_spmm_job_set_graph(void* job, int enable) {
   return ::ofx::guarded(__func__, [&]() -> int {
     OFX_REQUIRE(job, OFX_EINVAL, "spmm_job_set_graph: NULL job");
     return static_cast<SpmmJob*>(job)->set_graph(enable != 0);
+  });
+}
+
+extern "C" int ofx_spmm_job_set_static(void* job, int64_t static_csr) {
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(job, OFX_EINVAL, "spmm_job_set_static: NULL job");
+    static_cast<SpmmJob*>(job)->set_static(static_csr);
+    return OFX_OK;
+  });
+}
+
+extern "C" int ofx_spmm_job_static_stats(void* job, int64_t* plans, int64_t* hits) {
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_REQUIRE(job, OFX_EINVAL, "spmm_job_static_stats: NULL job");
+    static_cast<const SpmmJob*>(job)->static_stats(plans, hits);
+    return OFX_OK;
   });
 }
 

@@ -15,6 +15,7 @@
 #include <mutex>
 
 #include "oneflow/core/framework/framework.h"
+#include "oneflow/core/functional/spmm_functor.h"
 #include "ofx_internal.h"
 #include "ofx_spmm.h"
 
@@ -166,12 +167,37 @@ Maybe<void> Choose(const ofx_tensor_desc* row_ptr, const ofx_tensor_desc* b, int
   return user_op::UserOpRegistryMgr::Get().GetOpKernelRegistryResult("spmm_csr", rc, reg);
 }
 
+// The eager op's kernel states: one per (kernel registration, device), as OneFlow's functor
+// holds one op expression whose StatefulOpKernel keeps a state per device
+// (stateful_opkernel.cpp:887-908).  Created on first use through CreateOpKernelState.
+// Never destroyed: a state frees device memory, which must not happen from a static destructor
+// after the HIP runtime has gone at process exit.
+std::mutex g_eager_states_mu;
+auto& g_eager_states =
+    *new std::map<std::pair<const void*, int>, std::shared_ptr<user_op::OpKernelState>>();
+
+user_op::OpKernelState* EagerKernelState(const user_op::OpKernelRegistryResult* reg,
+                                         const user_op::OpKernel* kernel, int device,
+                                         DeviceType dev) {
+  std::lock_guard<std::mutex> lock(g_eager_states_mu);
+  auto key = std::make_pair(static_cast<const void*>(reg), device);
+  auto it = g_eager_states.find(key);
+  if (it != g_eager_states.end()) return it->second.get();
+  user_op::KernelInitContext ictx(ParallelContext(0, 1), ParallelDesc(Shape({1})), dev);
+  auto st = kernel->CreateOpKernelState(&ictx);
+  user_op::OpKernelState* raw = st.get();
+  g_eager_states[key] = std::move(st);
+  return raw;
+}
+
 // functional::SpmmCsr on a local or global tensor set: inference, kernel choice, then either the
-// tmp size (tmp_size_out != NULL) or the kernel's cache init + Compute on the stream.
+// tmp size (tmp_size_out != NULL) or the kernel's cache init + Compute on the stream.  `state`:
+// the compiled job's own kernel state (NULL: the eager op's, per registration and device).
 int RunSpmmCsr(void* stream, const ofx_tensor_desc* row_ptr, const ofx_tensor_desc* col_idx,
                const ofx_tensor_desc* values, int64_t m, int64_t k, const ofx_tensor_desc* b,
                int64_t b_logical_cols, ofx_tensor_desc* out, void* tmp, size_t tmp_bytes,
-               const Placement& pl, int num_threads, size_t* tmp_size_out) {
+               const Placement& pl, int num_threads, size_t* tmp_size_out, int64_t static_csr = 0,
+               std::shared_ptr<user_op::OpKernelState>* state = nullptr) {
   user_op::TensorDesc logical_od, od;
   int rc = ToStatus(Infer(row_ptr, col_idx, values, m, k, b, b_logical_cols, pl, &logical_od, &od));
   if (rc) return rc;
@@ -189,6 +215,9 @@ int RunSpmmCsr(void* stream, const ofx_tensor_desc* row_ptr, const ofx_tensor_de
     return OFX_OK;
   }
   OFX_REQUIRE(out, OFX_EINVAL, "spmm_csr: out is NULL");
+  // an earlier launch's loud failure comes back here as OFX_EPLAN, before this call launches
+  // (the functional call is a library entry like ofx_spmm_csr)
+  OFX_TAKE_DEVICE_ERROR("spmm_csr");
   rc = ToStatus(CheckDesc(out, "out"));
   if (rc) return rc;
   const int64_t phys_rows = od.shape().At(0);
@@ -216,7 +245,26 @@ int RunSpmmCsr(void* stream, const ofx_tensor_desc* row_ptr, const ofx_tensor_de
   ep::HipStream hip_stream(stream, b->device);
   ep::Stream* s = dev == DeviceType::kCPU ? static_cast<ep::Stream*>(&cpu_stream)
                                           : static_cast<ep::Stream*>(&hip_stream);
-  const user_op::AttrMap attrs = {{"a_num_rows", m}, {"a_num_cols", k}};
+  // the op's attributes: the registered defaults, then this call's values
+  user_op::AttrMap attrs;
+  if (const user_op::OpRegistryResult* op =
+          user_op::UserOpRegistryMgr::Get().GetOpRegistryResult("spmm_csr"))
+    for (const auto& a : op->attrs) attrs[a.first] = a.second;
+  attrs["a_num_rows"] = m;
+  attrs["a_num_cols"] = k;
+  attrs["static_csr"] = static_csr;
+  user_op::OpKernelState* kstate = nullptr;
+  if (state != nullptr) {
+    if (!*state) {
+      // a compiled op's launches are ordered on its one (named) stream
+      user_op::KernelInitContext ictx(ParallelContext(pl.parallel_id, pl.parallel_num()),
+                                      ParallelDesc(pl.hierarchy), dev, "compiled_job");
+      *state = kernel->CreateOpKernelState(&ictx);
+    }
+    kstate = state->get();
+  } else if (static_csr != 0) {
+    kstate = EagerKernelState(reg, kernel, b->device, dev);
+  }
   user_op::KernelCacheContext cache_ctx(ParallelContext(pl.parallel_id, pl.parallel_num()),
                                         ParallelDesc(pl.hierarchy),
                                         {{"out", pl.out_sbp}, {"b", pl.b_sbp}},
@@ -227,7 +275,7 @@ int RunSpmmCsr(void* stream, const ofx_tensor_desc* row_ptr, const ofx_tensor_de
     if (phys_rows == 0 || od.shape().At(1) == 0) {
       if (!kernel->AlwaysComputeWhenAllOutputsEmpty()) return OFX_OK;
     }
-    kernel->Compute(&ctx, nullptr, cache.get());
+    kernel->Compute(&ctx, kstate, cache.get());
   } catch (const KernelCheckError& e) {
     return ofx::fail(OFX_EINVAL, "%s", e.msg.c_str());
   }
@@ -235,6 +283,21 @@ int RunSpmmCsr(void* stream, const ofx_tensor_desc* row_ptr, const ofx_tensor_de
 }
 
 }  // namespace
+
+int SpmmCsrGlobalWithState(void* stream, const ofx_tensor_desc* row_ptr,
+                           const ofx_tensor_desc* col_idx, const ofx_tensor_desc* values,
+                           int64_t m, int64_t k, const ofx_tensor_desc* b, int64_t b_logical_cols,
+                           ofx_tensor_desc* out, void* tmp, size_t tmp_bytes, int hierarchy_ndim,
+                           const int64_t* hierarchy, const int32_t* out_split_axes,
+                           int64_t parallel_id, int64_t static_csr,
+                           std::shared_ptr<user_op::OpKernelState>* state) {
+  Placement pl;
+  int rc = ToStatus(MakePlacement(hierarchy_ndim, hierarchy, out_split_axes, parallel_id, &pl));
+  if (rc) return rc;
+  return RunSpmmCsr(stream, row_ptr, col_idx, values, m, k, b, b_logical_cols, out, tmp,
+                    tmp_bytes, pl, 0, nullptr, static_csr, state);
+}
+
 }  // namespace oneflow
 
 using namespace oneflow;
@@ -285,6 +348,43 @@ extern "C" int ofx_functional_spmm_csr_global(
     if (rc) return rc;
     return RunSpmmCsr(stream, row_ptr, col_idx, values, a_num_rows, a_num_cols, b, b_logical_cols,
                       out, tmp, tmp_bytes, pl, num_threads, tmp_size_out);
+  });
+}
+
+extern "C" int ofx_functional_spmm_csr_global_attrs(
+    void* stream, const ofx_tensor_desc* row_ptr, const ofx_tensor_desc* col_idx,
+    const ofx_tensor_desc* values, int64_t a_num_rows, int64_t a_num_cols,
+    const ofx_tensor_desc* b, int64_t b_logical_cols, ofx_tensor_desc* out, void* tmp,
+    size_t tmp_bytes, int hierarchy_ndim, const int64_t* hierarchy, const int32_t* out_split_axes,
+    int64_t parallel_id, int num_threads, size_t* tmp_size_out, const ofx_spmm_attrs* attrs) {
+  return ::ofx::guarded(__func__, [&]() -> int {
+    int64_t static_csr = 0;
+    if (attrs != nullptr) {
+      const char* why = ofx::versioned_struct_problem(attrs, OFX_SPMM_ATTRS_MIN_SIZE);
+      OFX_REQUIRE(why == nullptr, OFX_EINVAL,
+                  "spmm_csr: ofx_spmm_attrs %s (%u bytes): initialise it with OFX_SPMM_ATTRS_INIT",
+                  why ? why : "", OFX_SPMM_ATTRS_MIN_SIZE);
+      static_csr = attrs->static_csr;
+    }
+    Placement pl;
+    int rc = ToStatus(MakePlacement(hierarchy_ndim, hierarchy, out_split_axes, parallel_id, &pl));
+    if (rc) return rc;
+    return RunSpmmCsr(stream, row_ptr, col_idx, values, a_num_rows, a_num_cols, b, b_logical_cols,
+                      out, tmp, tmp_bytes, pl, num_threads, tmp_size_out, static_csr);
+  });
+}
+
+extern "C" int ofx_spmm_static_plans(int64_t* entries, int64_t* plans, int64_t* hits,
+                                     int release) {
+  return ::ofx::guarded(__func__, [&]() -> int {
+    int64_t e = 0, p = 0, h = 0;
+    std::lock_guard<std::mutex> lock(g_eager_states_mu);
+    for (auto& kv : g_eager_states)
+      if (kv.second) SpmmCsrPlanStateStats(kv.second.get(), &e, &p, &h, release != 0);
+    if (entries) *entries = e;
+    if (plans) *plans = p;
+    if (hits) *hits = h;
+    return OFX_OK;
   });
 }
 

@@ -9,10 +9,150 @@
  * ofx_spmm_csr_cpu (host).  Kernel errors are fatal CHECKs as in
  * oneflow/user/kernels/matrix_vector_product_kernel.cpp:98-109.
  */
+#include <list>
+#include <mutex>
+
 #include "oneflow/core/framework/framework.h"
+#include "oneflow/core/functional/spmm_functor.h"
 #include "ofx_spmm.h"
 
 namespace oneflow {
+
+// ---- static CSR: the work-list plan kept across calls (attr static_csr) -----
+// The kernel state of OpKernel::CreateOpKernelState (oneflow/core/framework/op_kernel.h:292),
+// which OneFlow keeps per StatefulOpKernel (eager: per op expression and device) or per
+// UserKernel (lazy).  For a caller that promises an unchanged CSR (static_csr != 0) it holds the
+// planner's work list in a device workspace of its own, so the launch skips the planner kernel
+// (options.planned = 1, ofx_spmm_csr_plan).  A plan is a pure function of row_ptr, the row range,
+// the shapes and the schedule; the key holds those plus the static_csr value (the caller's name
+// for this CSR: a new CSR at reused addresses gets a new one) and the stream (the in-kernel hub
+// reduce's arrival counters live in the workspace, so two streams never share one).
+class SpmmCsrPlanState final : public user_op::OpKernelState {
+ public:
+  struct Key {
+    int64_t static_csr;
+    const void* row_ptr;
+    const void* stream;
+    int device, idx_dt, val_dt;
+    int64_t m, k, n, nnz, row_begin, row_end, split, chunk, heavy, range_nnz;
+    bool operator==(const Key& o) const {
+      return static_csr == o.static_csr && row_ptr == o.row_ptr && stream == o.stream &&
+             device == o.device && idx_dt == o.idx_dt && val_dt == o.val_dt && m == o.m &&
+             k == o.k && n == o.n && nnz == o.nnz && row_begin == o.row_begin &&
+             row_end == o.row_end && split == o.split && chunk == o.chunk && heavy == o.heavy &&
+             range_nnz == o.range_nnz;
+    }
+  };
+  static constexpr size_t kMaxPlans = 8;
+
+  // key_on_stream: an eager op's state may see calls on any stream, so the stream is part of the
+  // key; a lazy op's (a compiled job's) launches are ordered on its one named stream, and its
+  // graph is captured on another stream than it replays on, so the key leaves the stream out.
+  explicit SpmmCsrPlanState(bool key_on_stream) : key_on_stream_(key_on_stream) {}
+  ~SpmmCsrPlanState() override { Release(); }
+  bool key_on_stream() const { return key_on_stream_; }
+
+  // The workspace for `key`: *planned = true when it already holds key's plan (a hit).  On a miss
+  // a workspace of `bytes` is allocated on the key's device (the least recently used entry is
+  // evicted past kMaxPlans) and the caller plans into it; a miss while the stream is capturing a
+  // graph takes no workspace (*ws = NULL: the ordinary path), as allocation and eviction are not
+  // capturable.
+  int Acquire(const Key& key, size_t bytes, bool capturing, void** ws, bool* planned) {
+    std::lock_guard<std::mutex> lock(mu_);
+    *ws = nullptr;
+    *planned = false;
+    for (auto it = entries_.begin(); it != entries_.end(); ++it) {
+      if (it->key == key && it->bytes >= bytes) {
+        entries_.splice(entries_.begin(), entries_, it);  // most recently used first
+        *ws = it->ws;
+        *planned = true;
+        ++hits_;
+        return OFX_OK;
+      }
+    }
+    if (capturing) return OFX_OK;
+    int rc = OFX_OK;
+    if (entries_.size() >= kMaxPlans) {
+      // an in-flight launch may still read the evicted plan: the device drains first
+      rc = WithDevice(entries_.back().key.device, [&]() {
+        const int r = ofx_device_synchronize();
+        return r != OFX_OK ? r : ofx_free(entries_.back().ws);
+      });
+      entries_.pop_back();
+      if (rc != OFX_OK) return rc;
+    }
+    void* p = nullptr;
+    rc = WithDevice(key.device, [&]() { return ofx_malloc(&p, bytes); });
+    if (rc != OFX_OK) return rc;
+    entries_.push_front(Entry{key, p, bytes});
+    *ws = p;
+    ++plans_;
+    return OFX_OK;
+  }
+
+  // Forget key's plan (its launch failed): the next call plans again.
+  void Drop(const Key& key) {
+    std::lock_guard<std::mutex> lock(mu_);
+    for (auto it = entries_.begin(); it != entries_.end(); ++it) {
+      if (it->key == key) {
+        WithDevice(it->key.device, [&]() {
+          ofx_device_synchronize();
+          return ofx_free(it->ws);
+        });
+        entries_.erase(it);
+        return;
+      }
+    }
+  }
+
+  void Stats(int64_t* entries, int64_t* plans, int64_t* hits) {
+    std::lock_guard<std::mutex> lock(mu_);
+    *entries += (int64_t)entries_.size();
+    *plans += plans_;
+    *hits += hits_;
+  }
+
+  void Release() {
+    std::lock_guard<std::mutex> lock(mu_);
+    for (Entry& e : entries_) {
+      WithDevice(e.key.device, [&]() {
+        ofx_device_synchronize();
+        return ofx_free(e.ws);
+      });
+    }
+    entries_.clear();
+  }
+
+ private:
+  struct Entry {
+    Key key;
+    void* ws;
+    size_t bytes;
+  };
+  template <typename F>
+  static int WithDevice(int device, F&& f) {
+    int prev = -1;
+    if (ofx_get_device(&prev) != OFX_OK) prev = -1;
+    if (prev != device && ofx_set_device(device) != OFX_OK) return OFX_EDEVICE;
+    const int rc = f();
+    if (prev >= 0 && prev != device) ofx_set_device(prev);
+    return rc;
+  }
+
+  const bool key_on_stream_;
+  std::mutex mu_;
+  std::list<Entry> entries_;
+  int64_t plans_ = 0, hits_ = 0;
+};
+
+bool SpmmCsrPlanStateStats(user_op::OpKernelState* state, int64_t* entries, int64_t* plans,
+                           int64_t* hits, bool release) {
+  auto* s = dynamic_cast<SpmmCsrPlanState*>(state);
+  if (s == nullptr) return false;
+  if (release) s->Release();
+  s->Stats(entries, plans, hits);
+  return true;
+}
 
 namespace {
 
@@ -65,7 +205,8 @@ int DtCode(DataType dt) { return static_cast<int>(dt); }
 // epilogue; the plain op passes none (ofx_spmm_csr_fused with NULL/none == ofx_spmm_csr).
 template <DeviceType device_type>
 void ComputeSpmmCsr(user_op::KernelComputeContext* ctx, const user_op::OpKernelCache* cache,
-                    const user_op::Tensor* bias, bool relu, const char* op_name) {
+                    const user_op::Tensor* bias, bool relu, const char* op_name,
+                    SpmmCsrPlanState* plans = nullptr, int64_t static_csr = 0) {
   TestHookCompute(op_name);
   const user_op::Tensor* row_ptr = ctx->Tensor4ArgNameAndIndex("a_csr_row_ptr", 0);
   const user_op::Tensor* col_idx = ctx->Tensor4ArgNameAndIndex("a_csr_col_idx", 0);
@@ -87,7 +228,7 @@ void ComputeSpmmCsr(user_op::KernelComputeContext* ctx, const user_op::OpKernelC
     row_begin = range->lower();
     row_end = range->upper();
   }
-  const ofx_spmm_options opts = OptionsOf(range);
+  ofx_spmm_options opts = OptionsOf(range);
   OFX_KERNEL_CHECK(out->shape_view().At(0) == row_end - row_begin,
                    "out rows " << out->shape_view().At(0) << " != row range "
                                << row_end - row_begin);
@@ -102,12 +243,47 @@ void ComputeSpmmCsr(user_op::KernelComputeContext* ctx, const user_op::OpKernelC
   if (device_type == DeviceType::kHIP) {
     user_op::Tensor* tmp = ctx->Tensor4ArgNameAndIndex("tmp_buffer", 0);
     void* ws = tmp ? tmp->mut_dptr() : nullptr;
-    const size_t ws_bytes = tmp ? (size_t)tmp->shape_view().elem_cnt() : 0;
-    void* stream = ctx->stream()->As<ep::HipStream>()->hip_stream();
+    size_t ws_bytes = tmp ? (size_t)tmp->shape_view().elem_cnt() : 0;
+    ep::HipStream* hs = ctx->stream()->As<ep::HipStream>();
+    void* stream = hs->hip_stream();
+    SpmmCsrPlanState::Key key{};
+    bool keyed = false;
+    if (plans != nullptr && static_csr != 0 && row_end > row_begin && n > 0) {
+      size_t need = 0;
+      rc = ofx_spmm_csr_workspace_size(idx_dt, val_dt, m, k, n, nnz, &opts, &need);
+      OFX_KERNEL_CHECK(rc == OFX_OK, op_name << " workspace query failed: " << ofx_last_error());
+      if (need > 0) {  // a launch that plans at all (the small form needs no work list)
+        key = SpmmCsrPlanState::Key{static_csr, row_ptr->dptr(),
+                                    plans->key_on_stream() ? stream : nullptr, hs->device_index(),
+                                    idx_dt, val_dt, m, k, n, nnz, row_begin, row_end,
+                                    opts.split_threshold, opts.chunk, opts.heavy_threshold,
+                                    opts.range_nnz};
+        void* sws = nullptr;
+        bool planned = false;
+        rc = plans->Acquire(key, need, hs->IsGraphCapturing(), &sws, &planned);
+        OFX_KERNEL_CHECK(rc == OFX_OK,
+                         op_name << " static_csr plan workspace: " << ofx_last_error());
+        if (sws != nullptr) {
+          keyed = true;
+          if (!planned) {
+            rc = ofx_spmm_csr_plan(stream, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
+                                   row_begin, row_end, sws, need, &opts);
+            if (rc != OFX_OK) plans->Drop(key);
+            OFX_KERNEL_CHECK(rc == OFX_OK, op_name << " kernel failed (" << rc
+                                                   << "): " << ofx_last_error());
+          }
+          opts.planned = 1;
+          ws = sws;
+          ws_bytes = need;
+        }
+      }
+    }
     rc = ofx_spmm_csr_fused(stream, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
                             col_idx->dptr(), values->dptr(), b->dptr(), b->row_stride(),
                             out->mut_dptr(), out->row_stride(), row_begin, row_end, bias_ptr, act,
                             ws, ws_bytes, &opts);
+    // an earlier launch's loud failure (OFX_EPLAN) may have been this key's plan: plan again
+    if (rc != OFX_OK && keyed) plans->Drop(key);
   } else {
     const int threads = ctx->stream()->As<ep::CpuStream>()->num_threads();
     rc = ofx_spmm_csr_fused_cpu(threads, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
@@ -129,13 +305,22 @@ class SpmmCsrKernel final : public user_op::OpKernel, public user_op::CudaGraphS
     return CreateSpmmCsrOpKernelCache(ctx);
   }
 
+  // The plans of static CSRs (HIP only: the kCPU kernel has no work list).
+  std::shared_ptr<user_op::OpKernelState> CreateOpKernelState(
+      user_op::KernelInitContext* ctx) const override {
+    if (device_type != DeviceType::kHIP) return nullptr;
+    return std::make_shared<SpmmCsrPlanState>(!ctx->has_stream_name_hint());
+  }
+
   bool AlwaysComputeWhenAllOutputsEmpty() const override { return false; }
 
  private:
   using user_op::OpKernel::Compute;
-  void Compute(user_op::KernelComputeContext* ctx, user_op::OpKernelState*,
+  void Compute(user_op::KernelComputeContext* ctx, user_op::OpKernelState* state,
                const user_op::OpKernelCache* cache) const override {
-    ComputeSpmmCsr<device_type>(ctx, cache, nullptr, false, "spmm_csr");
+    const int64_t static_csr = ctx->Attr<int64_t>("static_csr");
+    ComputeSpmmCsr<device_type>(ctx, cache, nullptr, false, "spmm_csr",
+                                dynamic_cast<SpmmCsrPlanState*>(state), static_csr);
   }
 };
 

@@ -90,8 +90,14 @@ def _placement(_parallel, _placement_nd):
 def spmm_csr(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor,
              a_csr_values: torch.Tensor, a_num_rows: int, a_num_cols: int, b: torch.Tensor, *,
              out: torch.Tensor | None = None, _parallel=None, _placement_nd=None,
-             num_threads: int = 0) -> torch.Tensor:
+             num_threads: int = 0, static_csr: int = 0) -> torch.Tensor:
     """out[M, N] = CSR(a_csr_row_ptr, a_csr_col_idx, a_csr_values; M x K) @ b[K, N].
+
+    static_csr (op attr, include/ofx_spmm.h ofx_spmm_attrs): non-zero (True = 1) promises that
+    the CSR at these addresses is not rewritten while the process calls the op with this value;
+    the HIP kernel's state then plans its work list once and every later call launches planned
+    (no planner kernel).  A caller that frees a static CSR and builds another one gives the new
+    one another value.  No numeric effect.
 
     Global form (one rank of a placement; `b` and `out` are this rank's physical tensors):
       `_parallel=(parallel_id, parallel_num, out_split_axis[, logical_n])` for a 1-D placement
@@ -148,15 +154,33 @@ def spmm_csr(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor,
     tmp = None
     if tmp_bytes.value:
         tmp = torch.empty(tmp_bytes.value, dtype=torch.uint8, device=bb.device)
-    check(LIB.ofx_functional_spmm_csr_global(current_stream_handle(bb), *common, ctypes.byref(d_o),
-                                             tmp.data_ptr() if tmp is not None else None,
-                                             tmp_bytes.value, *tail, None), "spmm_csr")
+    if static_csr:
+        attrs = _lib.SpmmAttrs()
+        attrs.static_csr = int(static_csr)
+        check(LIB.ofx_functional_spmm_csr_global_attrs(
+            current_stream_handle(bb), *common, ctypes.byref(d_o),
+            tmp.data_ptr() if tmp is not None else None, tmp_bytes.value, *tail, None,
+            ctypes.byref(attrs)), "spmm_csr")
+    else:
+        check(LIB.ofx_functional_spmm_csr_global(current_stream_handle(bb), *common,
+                                                 ctypes.byref(d_o),
+                                                 tmp.data_ptr() if tmp is not None else None,
+                                                 tmp_bytes.value, *tail, None), "spmm_csr")
     if memo is None and len(_SIG_MEMO) < 4096:
         _SIG_MEMO[key] = (tuple(out.shape), out.dtype, tmp_bytes.value)
     return out
 
 
 _SIG_MEMO: dict = {}
+
+
+def static_plans(release: bool = False) -> dict:
+    """The static-CSR plans the eager op states hold (ofx_spmm_static_plans): live entries,
+    planner launches and calls that reused a plan; release=True frees them first."""
+    e, p, h = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    check(LIB.ofx_spmm_static_plans(ctypes.byref(e), ctypes.byref(p), ctypes.byref(h),
+                                    1 if release else 0), "spmm_static_plans")
+    return {"entries": e.value, "plans": p.value, "hits": h.value}
 
 
 def fused_spmm_csr(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor,

@@ -53,6 +53,12 @@ class Options(_Versioned):
                 ("reserved", ctypes.c_int32), ("range_nnz", ctypes.c_int64)]
 
 
+class SpmmAttrs(_Versioned):
+    """ofx_spmm_attrs: op "spmm_csr"'s attributes beyond a_num_rows / a_num_cols."""
+    _fields_ = [("struct_size", ctypes.c_uint32), ("magic", ctypes.c_uint32),
+                ("static_csr", ctypes.c_int64)]
+
+
 class Placement(_Versioned):
     _fields_ = [("struct_size", ctypes.c_uint32), ("magic", ctypes.c_uint32),
                 ("device_type", ctypes.c_int32), ("reserved", ctypes.c_int32),
@@ -90,6 +96,7 @@ def _load():
     popt = ctypes.POINTER(Options)
     pdesc = ctypes.POINTER(TensorDesc)
     ppl = ctypes.POINTER(Placement)
+    pattrs = ctypes.POINTER(SpmmAttrs)
     sigs = {
         "ofx_last_error": ([], ctypes.c_char_p),
         "ofx_device_error_check": ([], i32),
@@ -193,6 +200,12 @@ def _load():
         "ofx_functional_spmm_csr_global": ([p, pdesc, pdesc, pdesc, i64, i64, pdesc, i64, pdesc, p,
                                             sz, i32, ctypes.POINTER(i64), ctypes.POINTER(i32), i64,
                                             i32, ctypes.POINTER(sz)], i32),
+        "ofx_functional_spmm_csr_global_attrs": ([p, pdesc, pdesc, pdesc, i64, i64, pdesc, i64, pdesc,
+                                                  p, sz, i32, ctypes.POINTER(i64),
+                                                  ctypes.POINTER(i32), i64, i32, ctypes.POINTER(sz),
+                                                  pattrs], i32),
+        "ofx_spmm_static_plans": ([ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i64),
+                                   i32], i32),
         "ofx_functional_sddmm_csr": ([p, pdesc, pdesc, pdesc, pdesc, i64, i64, pdesc, p, sz,
                                       ctypes.POINTER(sz)], i32),
         "ofx_functional_spmm_csr_gathered": ([p, pdesc, pdesc, pdesc, pdesc, pdesc, i64, i64, pdesc,
@@ -215,6 +228,8 @@ def _load():
         "ofx_spmm_job_run": ([p, p, p, p, p, p, p, p, sz], i32),
         "ofx_spmm_job_destroy": ([p], i32),
         "ofx_spmm_job_set_graph": ([p, i32], i32),
+        "ofx_spmm_job_set_static": ([p, i64], i32),
+        "ofx_spmm_job_static_stats": ([p, ctypes.POINTER(i64), ctypes.POINTER(i64)], i32),
         "ofx_spmm_job_graph_stats": ([p, ctypes.POINTER(i64), ctypes.POINTER(i64),
                                       ctypes.POINTER(i64)], i32),
         "ofx_op_sbp_signatures": ([ctypes.c_char_p, ctypes.c_char_p, p, sz], i32),

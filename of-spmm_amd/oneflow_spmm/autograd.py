@@ -52,6 +52,8 @@ def sddmm(row_ptr: torch.Tensor, col_idx: torch.Tensor, a: torch.Tensor, b: torc
 class _TransposeCache:
     def __init__(self, capacity: int = 4):
         self.capacity = capacity
+        self.static_ids: dict = {}  # id(row_ptr_T) -> its static_csr value (while cached)
+        self._next_id = 1 << 40  # clear of the small values callers pass
         self.entries: OrderedDict = OrderedDict()
         self.value_entries: OrderedDict = OrderedDict()
         self.seen: OrderedDict = OrderedDict()  # value keys met once (not yet worth a copy)
@@ -64,11 +66,20 @@ class _TransposeCache:
             self.entries.move_to_end(key)
             return hit[2]
         t = csr_transpose(row_ptr, col_idx, k)
-        # keep the source tensors alive so their storage (and so the key) cannot be reused
+        # keep the source tensors alive so their storage (and so the key) cannot be reused; the
+        # entry's A^T is static while it lives, so its SpMMs run with static_csr = a value no
+        # other entry ever had (a later transpose at recycled addresses gets a new one)
+        self._next_id += 1
+        self.static_ids[id(t[0])] = self._next_id
         self.entries[key] = (row_ptr, col_idx, t)
         while len(self.entries) > self.capacity:
-            self.entries.popitem(last=False)
+            _, (_, _, old) = self.entries.popitem(last=False)
+            self.static_ids.pop(id(old[0]), None)
         return t
+
+    def static_id(self, rp_t) -> int:
+        """The static_csr value of a cached A^T (0 if it is not cached any more)."""
+        return self.static_ids.get(id(rp_t), 0)
 
 
     def values_t(self, row_ptr, col_idx, values, k):
@@ -104,7 +115,8 @@ class _TransposeCache:
                 self.seen.popitem(last=False)
             return _C.spmm_csr_gathered(rp_t, ci_t, values, perm, k, m, d_out)
         _, _, vals_t = self.values_t(row_ptr, col_idx, values, k)
-        return spmm_csr(rp_t, ci_t, vals_t, k, m, d_out)
+        # the cached A^T: its plan is kept across steps (static_csr, a value unique to the entry)
+        return spmm_csr(rp_t, ci_t, vals_t, k, m, d_out, static_csr=self.static_id(rp_t))
 
 
 TRANSPOSE_CACHE = _TransposeCache()
@@ -112,8 +124,8 @@ TRANSPOSE_CACHE = _TransposeCache()
 
 class SpmmCsrFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, row_ptr, col_idx, values, m, k, b):
-        out = spmm_csr(row_ptr, col_idx, values, m, k, b)
+    def forward(ctx, row_ptr, col_idx, values, m, k, b, static_csr=0):
+        out = spmm_csr(row_ptr, col_idx, values, m, k, b, static_csr=static_csr)
         ctx.save_for_backward(row_ptr, col_idx, values, b)
         ctx.m, ctx.k = m, k
         return out
@@ -127,18 +139,22 @@ class SpmmCsrFunction(torch.autograd.Function):
             d_values = sddmm(row_ptr, col_idx, d_out, b)
         if ctx.needs_input_grad[5]:
             d_b = TRANSPOSE_CACHE.grad_b(row_ptr, col_idx, values.detach(), ctx.m, ctx.k, d_out)
-        return None, None, d_values, None, None, d_b
+        return None, None, d_values, None, None, d_b, None
 
 
-def spmm(a_csr_row_ptr, a_csr_col_idx, a_csr_values, a_num_rows, a_num_cols, b, *, out=None):
+def spmm(a_csr_row_ptr, a_csr_col_idx, a_csr_values, a_num_rows, a_num_cols, b, *, out=None,
+         static_csr=0):
     """`oneflow.spmm` with autograd: differentiable in `a_csr_values` and `b`.
-    `out=` (a preallocated result) is only accepted when no gradient is being recorded."""
+    `out=` (a preallocated result) is only accepted when no gradient is being recorded.
+    `static_csr` (op attr; True = 1): the CSR is not rewritten while calls carry this value, so
+    the forward plans its work list once (_C.spmm_csr)."""
     if torch.is_grad_enabled() and (a_csr_values.requires_grad or b.requires_grad):
         if out is not None:
             raise RuntimeError("spmm: out= is not supported when gradients are required")
         return SpmmCsrFunction.apply(a_csr_row_ptr, a_csr_col_idx, a_csr_values, int(a_num_rows),
-                                     int(a_num_cols), b)
-    return spmm_csr(a_csr_row_ptr, a_csr_col_idx, a_csr_values, a_num_rows, a_num_cols, b, out=out)
+                                     int(a_num_cols), b, int(static_csr))
+    return spmm_csr(a_csr_row_ptr, a_csr_col_idx, a_csr_values, a_num_rows, a_num_cols, b, out=out,
+                    static_csr=int(static_csr))
 
 
 class FusedSpmmCsrFunction(torch.autograd.Function):

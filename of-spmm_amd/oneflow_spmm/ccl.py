@@ -183,7 +183,7 @@ class SpmmJob:
 
     def __init__(self, placement: PlacementSpec, m: int, k: int, n: int, nnz: int,
                  idx_dtype: torch.dtype, dtype: torch.dtype, device, stream_name: str = "",
-                 graph: bool = False):
+                 graph: bool = False, static_csr: int = 0):
         self.placement, self.m, self.k, self.n, self.nnz = placement, m, k, n, nnz
         self.dtype, self.idx_dtype, self.device = dtype, idx_dtype, torch.device(device)
         self._job = ctypes.c_void_p()
@@ -199,6 +199,22 @@ class SpmmJob:
         self.row_range = (lo, hi)
         if graph:
             self.set_graph(True)
+        if static_csr:
+            self.set_static(static_csr)
+
+    def set_static(self, static_csr: int = 1):
+        """Attr static_csr of the job's spmm_csr (include/ofx_spmm.h ofx_spmm_attrs): the caller
+        promises the CSR it runs on is not rewritten; the job's kernel state keeps its work-list
+        plan, so only the first run launches the planner (0 turns it off)."""
+        check(LIB.ofx_spmm_job_set_static(self._job, int(static_csr)), "spmm_job_set_static")
+
+    @property
+    def static_stats(self):
+        """{"plans", "hits"}: planner launches of the static CSR and runs that reused a plan."""
+        p, h = ctypes.c_int64(), ctypes.c_int64()
+        check(LIB.ofx_spmm_job_static_stats(self._job, ctypes.byref(p), ctypes.byref(h)),
+              "spmm_job_static_stats")
+        return {"plans": p.value, "hits": h.value}
 
     def set_graph(self, enable: bool = True):
         """Graph mode (user_kernel.cpp:676-707): after one eager run, a run is captured into a

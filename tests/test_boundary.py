@@ -9,6 +9,7 @@
 - the workspace query over the matrix's m bounds the workspace of every row range of it.
 """
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -178,3 +179,50 @@ def test_comm_calls_on_a_null_handle_are_refused():
     nr, rk = ctypes.c_int(), ctypes.c_int()
     assert LIB.ofx_comm_count(None, ctypes.byref(nr), ctypes.byref(rk)) == _lib.OFX_EINVAL
     assert LIB.ofx_comm_abort(None) == _lib.OFX_OK and LIB.ofx_comm_destroy(None) == _lib.OFX_OK
+
+
+# ---- attr static_csr: the host side ------------------------------------
+def test_static_csr_attr_on_the_cpu_kernel_is_the_same_op():
+    """kCPU has no work-list plan: static_csr changes nothing there (same bits, no plan state),
+    and the attrs struct is checked like every tagged struct."""
+    rp, ci, v, b, m, k = small_problem(4)
+    ref = fs.spmm_csr(rp, ci, v, m, k, b)
+    before = fs._C.static_plans()
+    for val in (1, True, 12345):
+        out = fs.spmm_csr(rp, ci, v, m, k, b, static_csr=val)
+        assert torch.equal(out.view(torch.uint8), ref.view(torch.uint8))
+    out = fs.spmm(rp, ci, v, m, k, b, static_csr=True)
+    assert torch.equal(out.view(torch.uint8), ref.view(torch.uint8))
+    assert fs._C.static_plans() == before  # no state for the CPU kernel
+    # the attrs struct: tagged, versioned
+    a = _lib.SpmmAttrs()
+    assert a.struct_size == ctypes.sizeof(_lib.SpmmAttrs) == 16 and a.magic == _lib.STRUCT_MAGIC
+    d = [fs._C.desc(t) for t in (rp, ci, v, b)]
+    od = fs._C.desc(out)
+    hier, axes = (ctypes.c_int64 * 1)(1), (ctypes.c_int32 * 1)(-1)
+    a.magic = 0
+    rc = LIB.ofx_functional_spmm_csr_global_attrs(None, *[ctypes.byref(x) for x in d[:3]], m, k,
+                                                  ctypes.byref(d[3]), -1, ctypes.byref(od), None,
+                                                  0, 1, hier, axes, 0, 1, None, ctypes.byref(a))
+    assert rc == _lib.OFX_EINVAL and "OFX_SPMM_ATTRS_INIT" in _lib.last_error()
+    a.magic = _lib.STRUCT_MAGIC
+    a.static_csr = 3
+    rc = LIB.ofx_functional_spmm_csr_global_attrs(None, *[ctypes.byref(x) for x in d[:3]], m, k,
+                                                  ctypes.byref(d[3]), -1, ctypes.byref(od), None,
+                                                  0, 1, hier, axes, 0, 1, None, ctypes.byref(a))
+    assert rc == _lib.OFX_OK
+    assert torch.equal(out.view(torch.uint8), ref.view(torch.uint8))
+
+
+def test_static_csr_is_a_registered_attr_with_default_zero():
+    """The op schema carries the attribute (ODS / op_generated.cpp) and the functional YAML the
+    argument, so `oneflow._C.spmm_csr(..., static_csr=...)` binds."""
+    import re
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "of-spmm_amd")
+    gen = open(os.path.join(root, "oneflow/core/framework/op_generated.cpp")).read()
+    spmm_block = gen.split('REGISTER_USER_OP("spmm_csr")')[1].split("REGISTER_USER_OP")[0]
+    assert '.Attr<int64_t>("static_csr", 0)' in spmm_block
+    td = open(os.path.join(root, "oneflow/ir/spmm_csr.td")).read()
+    assert re.search(r'DefaultValuedAttr<SI64Attr, "0">:\$static_csr', td)
+    yaml = open(os.path.join(root, "oneflow/core/functional/spmm_functional_api.yaml")).read()
+    assert "Int64 static_csr=0) => SpmmCsr" in yaml

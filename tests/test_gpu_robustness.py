@@ -2,9 +2,11 @@
 ADVICE r4 high + mediums).
 
 - A look-back that gives up (test knob OFX_DEBUG_PLAN_SPIN_LIMIT: 0 = every block but the first
-  gives up at once, 1 = one poll) makes every consumer of the work list write nothing, and the
-  host reports OFX_EPLAN at the next entry / ofx_device_error_check.  The output buffer keeps its
-  sentinel bits: no result from a partial or earlier plan ever appears.
+  gives up at once, 1 = one poll) makes the first consumer of the work list fill its whole output
+  with the canonical quiet NaN (the poison replaces "write nothing", so neither
+  an uninitialised buffer nor an earlier step's result can be read as this one's), and the host
+  reports OFX_EPLAN at the next entry / ofx_device_error_check.  torch.cuda.synchronize() alone
+  does not report it; the next fs.spmm call does.
 - options.planned over a workspace that holds no valid plan is refused the same way.
 - A launch captured in a hipGraph re-plans on every replay under a fresh tag (the device epoch
   word): rewriting row_ptr / col_idx in place between replays gives the new graph's bits.
@@ -25,6 +27,8 @@ from tests.helpers import assert_bitwise, oracle_spmm, power_law_degrees, random
 pytestmark = pytest.mark.gpu
 
 SENTINEL = 0x7FC0DEAD  # a NaN payload no kernel writes
+POISON = {torch.float32: (torch.int32, 0x7FC00000), torch.float64: (torch.int64, 0x7FF8000000000000),
+          torch.bfloat16: (torch.int16, 0x7FC0), torch.float16: (torch.int16, 0x7E00)}
 
 
 @pytest.fixture(autouse=True)
@@ -44,6 +48,12 @@ def untouched(out):
     return bool((out.view(torch.int32) == SENTINEL).all().item())
 
 
+def poisoned(out):
+    """Every element is the canonical quiet NaN of its dtype (spmm_common.h poison_value)."""
+    it, bits = POISON[out.dtype]
+    return bool((out.contiguous().view(it) == bits).all().item())
+
+
 def hub_graph(m, k, rng, hubs=((11, 4000), (777, 600))):
     deg = rng.integers(0, 30, size=m)
     for r, d in hubs:
@@ -52,10 +62,10 @@ def hub_graph(m, k, rng, hubs=((11, 4000), (777, 600))):
 
 
 @pytest.mark.parametrize("variant", [0, 30001, 30003, 30004])
-def test_forced_look_back_failure_writes_nothing_and_is_reported(device, variant):
+def test_forced_look_back_failure_poisons_the_output_and_is_reported(device, variant):
     """Knob 0: the plan of a 60k-row launch (59 planner blocks) fails in every block but the
     first; whichever form consumes it (prefetching / mid / bandwidth + reduce / wave items)
-    writes nothing and the error surfaces once."""
+    fills the output with the canonical quiet NaN and the error surfaces once."""
     rng = np.random.default_rng(500 + variant)
     m, k, n = 60_000, 60_000, 64
     rp, ci, v = random_csr(m, k, hub_graph(m, k, rng), rng)
@@ -67,7 +77,7 @@ def test_forced_look_back_failure_writes_nothing_and_is_reported(device, variant
     assert LIB.ofx_debug_set(_lib.DEBUG_PLAN_SPIN_LIMIT, 0) == _lib.OFX_OK
     kern(*d, out)  # asynchronous: accepted
     torch.cuda.synchronize()
-    assert untouched(out), "a failed plan's launch wrote output"
+    assert poisoned(out), "a failed plan's launch left output that is not the poison"
     assert LIB.ofx_device_error_check() == _lib.OFX_EPLAN
     assert "gave up" in _lib.last_error()
     assert LIB.ofx_device_error_check() == _lib.OFX_OK  # reported once
@@ -75,11 +85,12 @@ def test_forced_look_back_failure_writes_nothing_and_is_reported(device, variant
     kern(*d, out)
     torch.cuda.synchronize()
     LIB.ofx_debug_set(_lib.DEBUG_PLAN_SPIN_LIMIT, -1)
+    out.view(torch.int32).fill_(SENTINEL)
     with pytest.raises(_lib.OfxError) as ei:
         kern(*d, out)
     assert ei.value.code == _lib.OFX_EPLAN
     torch.cuda.synchronize()
-    assert untouched(out)
+    assert untouched(out)  # the refused call launched nothing
     kern(*d, out)  # the default limit: an ordinary launch
     torch.cuda.synchronize()
     assert LIB.ofx_device_error_check() == _lib.OFX_OK
@@ -104,13 +115,13 @@ def test_failed_plan_never_returns_a_stale_plan(device):
     LIB.ofx_debug_set(_lib.DEBUG_PLAN_SPIN_LIMIT, 0)
     kern(rp_b.to(device), ci_b.to(device), v_b.to(device), b, out_b)
     torch.cuda.synchronize()
-    assert untouched(out_b), "graph B's launch ran on a stale plan"
+    assert poisoned(out_b), "graph B's launch ran on a stale plan"
     assert LIB.ofx_device_error_check() == _lib.OFX_EPLAN
 
 
 def test_one_poll_look_back_is_exact_or_loud(device):
     """Knob 1 (a single poll per predecessor) on a 250k-row launch (245 planner blocks): each run
-    either completes bit-exact or writes nothing and reports; never a partial list."""
+    either completes bit-exact or poisons its output and reports; never a partial list."""
     rng = np.random.default_rng(520)
     m, k, n = 250_000, 250_000, 16
     rp, ci, v = random_csr(m, k, power_law_degrees(m, 2_500_000, k, rng), rng)
@@ -126,7 +137,7 @@ def test_one_poll_look_back_is_exact_or_loud(device):
         torch.cuda.synchronize()
         rc = LIB.ofx_device_error_check()
         if rc == _lib.OFX_EPLAN:
-            assert untouched(out)
+            assert poisoned(out)
             outcomes.append("loud")
         else:
             assert rc == _lib.OFX_OK
@@ -151,7 +162,7 @@ def test_planned_launch_over_an_unplanned_workspace_is_refused(device):
                                     d[2].data_ptr(), d[3].data_ptr(), n, out.data_ptr(), n, 0, m,
                                     kern.workspace.data_ptr(), kern.ws_bytes, ctypes.byref(o)))
         torch.cuda.synchronize()
-        assert untouched(out), f"planned launch over a workspace filled with {fill:#x} wrote output"
+        assert poisoned(out), f"planned launch over a workspace filled with {fill:#x}: not poisoned"
         assert LIB.ofx_device_error_check() == _lib.OFX_EPLAN
         assert "no valid work-list plan" in _lib.last_error()
     # plan() then the planned launch: accepted and exact
@@ -252,3 +263,62 @@ def test_comm_device_deadline_aborts_once_and_the_handle_stays_safe(device):
     torch.cuda.synchronize()
     assert torch.equal(x, y)
     _lib.check(LIB.ofx_comm_destroy(comm2))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
+def test_failed_plan_poisons_only_the_view_it_was_given(device, dtype):
+    """A column-block view of a wider output (ldc > n, the pipelined row split's layout): the
+    poison covers exactly rows x [0, n) of the view, in every value dtype; the columns around it
+    keep their bits."""
+    rng = np.random.default_rng(560)
+    m, k, n, wide = 60_000, 60_000, 32, 80
+    rp, ci, v = random_csr(m, k, hub_graph(m, k, rng), rng)
+    d = [t.to(device) for t in (rp, ci)] + [v.to(device, dtype), random_dense(k, n, rng).to(device, dtype)]
+    kern = ops.SpmmCsrKernel(m, k, n, ci.numel(), torch.int32, dtype, device)
+    full = torch.full((m, wide), 3.0, dtype=dtype, device=device)
+    view = full[:, 16:16 + n]
+    LIB.ofx_debug_set(_lib.DEBUG_PLAN_SPIN_LIMIT, 0)
+    kern(*d, view)
+    torch.cuda.synchronize()
+    assert LIB.ofx_device_error_check() == _lib.OFX_EPLAN
+    assert poisoned(view)
+    assert bool((full[:, :16] == 3).all()) and bool((full[:, 16 + n:] == 3).all())
+
+
+def test_failed_plan_surfaces_at_the_next_fs_spmm_call_not_at_synchronize(device):
+    """The documented contract (README / INTEGRATION.md): torch.cuda.synchronize() does not look
+    at the library's error words, so a caller that synchronises and reads the output sees the
+    poison (NaN), never a plausible value; the next fs.spmm call (or ofx_device_error_check)
+    raises OFX_EPLAN, once."""
+    rng = np.random.default_rng(570)
+    m, k, n = 60_000, 60_000, 64
+    rp, ci, v = random_csr(m, k, hub_graph(m, k, rng), rng)
+    b = random_dense(k, n, rng)
+    d = [t.to(device) for t in (rp, ci, v)]
+    db = b.to(device)
+    LIB.ofx_debug_set(_lib.DEBUG_PLAN_SPIN_LIMIT, 0)
+    out = fs.spmm(*d, m, k, db)
+    torch.cuda.synchronize()  # no error here
+    assert torch.isnan(out).all()
+    LIB.ofx_debug_set(_lib.DEBUG_PLAN_SPIN_LIMIT, -1)
+    with pytest.raises(_lib.OfxError) as ei:
+        fs.spmm(*d, m, k, db)
+    assert ei.value.code == _lib.OFX_EPLAN
+    out = fs.spmm(*d, m, k, db)  # reported once; the next call is ordinary
+    torch.cuda.synchronize()
+    assert_bitwise(out, oracle_spmm(rp, ci, v, b), "after the reported failure")
+
+
+def test_failed_sddmm_plan_poisons_its_nonzeros(device):
+    """SDDMM (the d(values) gradient) consumes the same work-list plan: a failed plan fills the
+    nonzeros of its rows with the poison and reports OFX_EPLAN."""
+    rng = np.random.default_rng(580)
+    m, k, n = 60_000, 60_000, 64
+    rp, ci, v = random_csr(m, k, hub_graph(m, k, rng), rng)
+    dc = random_dense(m, n, rng).to(device)
+    b = random_dense(k, n, rng).to(device)
+    LIB.ofx_debug_set(_lib.DEBUG_PLAN_SPIN_LIMIT, 0)
+    out = fs._C.sddmm_csr(rp.to(device), ci.to(device), dc, b, m, k)
+    torch.cuda.synchronize()
+    assert LIB.ofx_device_error_check() == _lib.OFX_EPLAN
+    assert poisoned(out)
