@@ -79,7 +79,11 @@ int64_t debug_knob(int knob, int64_t dflt) {
 }  // namespace ofx
 
 extern "C" const char* ofx_last_error(void) { return g_last_error; }
-extern "C" const char* ofx_version(void) { return "ofx-spmm 0.2.0 gfx950"; }
+#ifdef OFX_TUNING_TABLE
+extern "C" const char* ofx_version(void) { return "ofx-spmm 0.3.0 gfx950+tuning"; }
+#else
+extern "C" const char* ofx_version(void) { return "ofx-spmm 0.3.0 gfx950"; }
+#endif
 
 extern "C" int ofx_debug_set(int knob, int64_t value) {
   return ::ofx::guarded(__func__, [&]() -> int {

@@ -1,11 +1,26 @@
 // spmm_csr_tuned.hip — the tuning table of the SpMM forward (variant = 10000 + id): forced
 // configurations for A/B runs (scripts/ab.py) and the tuning-table parity tests.
+//
+// No automatic rule launches through this table (the rules in spmm_csr_impl.h call launch_cfg
+// directly), so the release library is built without it: only
+// `make -C of-spmm_amd tuning` compiles it (-DOFX_TUNING_TABLE, oneflow_spmm/libofx_spmm_tuning.so,
+// selected with OFX_SPMM_LIB), and ofx_version() then ends in "+tuning".  The tuning-table
+// tests skip on a library without it.
 #pragma clang fp contract(off)
 
 #include "spmm_csr_impl.h"
 
 namespace ofx {
 
+#ifndef OFX_TUNING_TABLE
+template <typename T, typename I>
+int launch_tuned(const Launch& L, int) {
+  return fail(OFX_EUNSUPPORTED,
+              "spmm_csr: tuning variant %d: this library was built without the tuning table "
+              "(make -C of-spmm_amd tuning; OFX_SPMM_LIB=.../libofx_spmm_tuning.so)",
+              L.sched.variant);
+}
+#else
 // Tuning table (variant = 10000 + id), float values / int32 indices only; every entry computes the
 // same bits (the accumulation order does not depend on the launch shape).
 template <typename T, typename I>
@@ -291,6 +306,7 @@ int launch_tuned(const Launch& L, int id) {
   }
   return fail(OFX_EINVAL, "spmm_csr: unknown tuning variant %d for this dtype", L.sched.variant);
 }
+#endif  // OFX_TUNING_TABLE
 
 #define OFX_TUNED(T, I) template int launch_tuned<T, I>(const Launch& L, int id);
 OFX_TUNED(float, int32_t)

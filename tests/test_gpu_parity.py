@@ -52,6 +52,13 @@ def test_forced_variants_bitexact(device, variant):
     assert_bitwise(out, oracle_spmm(rp, ci, v, b), f"variant {variant}")
 
 
+# The tuning table is an A/B build's (make -C of-spmm_amd tuning): its tests
+# run when OFX_SPMM_LIB selects that library and skip on the release one.
+needs_tuning_table = pytest.mark.skipif(not fs.__version__.endswith("+tuning"),
+                                        reason="release library: no tuning table (make tuning)")
+
+
+@needs_tuning_table
 @pytest.mark.parametrize("n", [16, 128])
 @pytest.mark.parametrize("tuned", list(range(1, 18)) + list(range(21, 45)))
 def test_tuning_table_bitexact(device, tuned, n):
@@ -248,13 +255,13 @@ def test_baseline_configs_bitexact(device, name):
     assert ok, worst
 
 
-@pytest.mark.parametrize("n,alt_variant", [(16, 10021), (32, 408)])
+@pytest.mark.parametrize("n,alt_variant", [(16, 116), (32, 408)])
 def test_plaw1m_narrow_widths_bitexact(device, n, alt_variant):
     """1M power-law (20M nonzeros) at N=16 / 32, the whole output bit for bit against the oracle
     and against a second configuration of the same width.  The automatic picks: at N=16 the narrow
     form past kPrefetchNnz (2-lane float2 light rows, 16-lane wave items for the hub chunks and
-    heavy rows), against tuning variant 10021 (one element per lane over 16 lanes, 16 loads in
-    flight); at N=32 the bandwidth configuration, against VEC 4 / LPR 8 forced (variant 408)."""
+    heavy rows), against VEC 1 / LPR 16 forced (variant 116: one element per lane over 16
+    lanes); at N=32 the bandwidth configuration, against VEC 4 / LPR 8 forced (variant 408)."""
     cfg = fs.synth.CONFIGS["plaw1m"]
     m, k, nnz = cfg["m"], cfg["k"], cfg["nnz"]
     rp, ci, v = fs.synth.csr(m, k, nnz)
@@ -270,15 +277,15 @@ def test_plaw1m_narrow_widths_bitexact(device, n, alt_variant):
 def test_mid_size_n16_narrow_form_bitexact(device):
     """A 15M-nonzero power-law graph (750k rows) at N=16: the narrow form past kPrefetchNnz
     (2-lane float2 light rows, hub chunks and heavy rows as 16-lane wave items); the output bit for
-    bit against the oracle, the one-element bandwidth configuration (tuning variant 10021) and the
-    mid form forced (variant 30002, block items)."""
+    bit against the oracle, the one-element bandwidth configuration (VEC 1 / LPR 16 forced,
+    variant 116) and the mid form forced (variant 30002, block items)."""
     m = k = 750_000
     nnz, n = 15_000_000, 16
     rp, ci, v = fs.synth.csr(m, k, nnz)
     b = fs.synth.dense(0, k, n)
     d = (rp.to(device), ci.to(device), v.to(device), b.to(device))
     out = fs.spmm(*d[:3], m, k, d[3])
-    for variant in (10021, 30002):
+    for variant in (116, 30002):
         alt = ops.spmm_csr_device(*d, m, k, options=ops.make_options(variant=variant))
         torch.cuda.synchronize()
         assert torch.equal(out.view(torch.int32), alt.view(torch.int32)), variant
@@ -922,6 +929,7 @@ def round5_graph():
     return m, k, deg, rng
 
 
+@needs_tuning_table
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("n", [13, 47])
 def test_tuning_table_round5_bitexact(device, round5_graph, dtype, n):
