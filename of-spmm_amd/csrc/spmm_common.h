@@ -39,7 +39,7 @@ OFX_HD float bf16_to_f32(uint16_t h) { return bits_to_f32(uint32_t(h) << 16); }
 // Round-to-nearest-even; NaN stays NaN (quiet bit forced).
 // On the device this is gfx950's v_cvt_pk_bf16_f32 (emitted for the conversion to __bf16), which
 // gives the same bits as the software rounding for all 2^32 f32 inputs, NaNs included
-// (scripts/bf16_cvt_probe.hip, profiles/r02_bf16_cvt_probe.json); the host (CPU kernel) keeps
+// (probes/bf16_cvt_probe.hip, profiles/r02_bf16_cvt_probe.json); the host (CPU kernel) keeps
 // the software form.
 OFX_HD uint16_t f32_to_bf16(float f) {
 #if defined(__HIP_DEVICE_COMPILE__)

@@ -89,7 +89,7 @@ struct alignas(sizeof(T) * VEC) Pack {
 #ifndef OFX_AB_NO_LR
 constexpr bool kLR = true;  // the mid-size forms (prefetching, mid, narrow <= kPrefetchNnz): LR
 #else
-constexpr bool kLR = false;  // A/B builds only (scripts/ab_build.sh): the spmm_reduce launch
+constexpr bool kLR = false;  // A/B builds only (probes/ab_build.sh): the spmm_reduce launch
 #endif
 template <int VEC_, int LPR_, int U_ = 8, int WPB_ = 4, bool NT_ = false, bool PF_ = false,
           bool BNT_ = false, bool WH_ = false, bool BI_ = false, bool BUF_ = true, int HL_ = 0,
@@ -231,7 +231,7 @@ struct BRows {
   uint32_t ldb_bytes, cc_bytes, k32;
   template <typename I>
   __device__ __forceinline__ uint32_t clamp_row(I c) const {
-#ifdef OFX_AB_NO_ZERO_FILL  // A/B builds only (scripts/ab_build.sh): no bound
+#ifdef OFX_AB_NO_ZERO_FILL  // A/B builds only (probes/ab_build.sh): no bound
     return (uint32_t)c;
 #else
     if constexpr (sizeof(I) == 4) return __builtin_elementwise_min((uint32_t)c, k32);
@@ -726,7 +726,7 @@ __device__ __forceinline__ void hub_tail(unsigned* __restrict__ arrive, int64_t 
   if (gl == 0) coh_store(arrive + slot0, 0u);
 }
 
-// Block-engine sizes (compile-time knobs for A/B builds: scripts/ab_build.sh): bytes of products
+// Block-engine sizes (compile-time knobs for A/B builds: probes/ab_build.sh): bytes of products
 // per LDS buffer, nonzeros per batch, B-row loads per lane per batch.
 #ifndef OFX_BE_LDS
 #define OFX_BE_LDS 16384
@@ -1081,7 +1081,7 @@ __global__ void __launch_bounds__(64 * K::WPB)
 
 // ---- main kernel: one work list = hub chunks, then rows in bin order ------------------------
 // Without a plan (`order` == nullptr) the list is simply the rows in index order.
-#ifdef OFX_AB_WPE  // A/B builds only (scripts/ab_build.sh): waves per SIMD the registers must allow
+#ifdef OFX_AB_WPE  // A/B builds only (probes/ab_build.sh): waves per SIMD the registers must allow
 #define OFX_MAIN_WPE __attribute__((amdgpu_waves_per_eu(OFX_AB_WPE)))
 #else
 #define OFX_MAIN_WPE
@@ -1258,7 +1258,7 @@ __global__ void __launch_bounds__(64 * K::WPB) OFX_MAIN_WPE
   // 1.7-1.8%; Reddit-shaped: 53% hubs, where it cost 9%).
   constexpr int64_t kIdxExcluded = 16;
 #if defined(OFX_LIGHT_ORDER)
-  constexpr bool kIdx = false;  // A/B builds only (scripts/ab_build.sh)
+  constexpr bool kIdx = false;  // A/B builds only (probes/ab_build.sh)
 #else
   constexpr bool kIdx = true;
 #endif
@@ -1713,7 +1713,7 @@ int launch_vec(const Launch& L, int lpr, bool nt) {
     return (L.n > 16 && L.n <= 64) ? launch_vec_pf<T, I, VEC, true>(L, lpr)
                                    : launch_vec_pf<T, I, VEC, false>(L, lpr);
   // the bandwidth configuration (forced variants keep it at every size)
-#ifdef OFX_AB_GLOBAL_LOADS  // A/B builds only (scripts/ab_build.sh): global loads, not buffer loads
+#ifdef OFX_AB_GLOBAL_LOADS  // A/B builds only (probes/ab_build.sh): global loads, not buffer loads
   return launch_vec_global<T, I, VEC>(L, lpr, nt);
 #endif
   switch (lpr) {
@@ -1738,7 +1738,7 @@ int launch_vec(const Launch& L, int lpr, bool nt) {
 // columns one pass of single elements is as fast or faster (N = 41 / 47 / 63: 4.6 / 5.0 / 6.1 ms
 // against 4.8 / 5.2 / 6.2; such rows cost whole 128-B lines either way); profiles/r03ad_sweep.jsonl.
 // Round 5: 16-bit rows whose width is not a multiple of 8 above N = 64 the same way (8-element
-// windows at 2-B alignment, scripts/unaligned_probe.hip) instead of one element per lane over 64
+// windows at 2-B alignment, probes/unaligned_probe.hip) instead of one element per lane over 64
 // lanes: 1M power-law bf16 N = 99 / 127 / 255 1,490 / 1,556 / 3,031 -> 917 / 1,040 / 1,799 us
 // (tuning entries 10122 / 10123, gpurun_out/r05h_2_py.txt; N = 128 / 256: 853 / 1,489).
 // And 16-bit rows of 17-63 columns (but 32) in the bandwidth form, where the N / 16-element
@@ -1833,7 +1833,7 @@ bool use_narrow_form(const Launch& L, int elem_bytes) {
 
 // Rows of 17-64 columns of mid-size launches (round 5): the narrow form's
 // shape for every width -- shifted windows (Cfg::SH, any N; 2-B-aligned 8 / 16-B accesses are
-// exact and as fast on gfx950, scripts/unaligned_probe.hip) over 8 lanes, hubs added in the
+// exact and as fast on gfx950, probes/unaligned_probe.hip) over 8 lanes, hubs added in the
 // kernel -- with the wave items (hub chunks, heavy rows) in 32-lane groups, one column pass
 // (the reference gather's word choice, gather_kernel_util.cu:69-104, falls to 2-B words at odd
 // 16-bit widths; the shifted window keeps 8 / 16-B words at any width):
@@ -1920,7 +1920,7 @@ int launch_typed(const Launch& L) {
       return launch_shift<T, I>(L, (L.b_rows * L.ldb * (int64_t)sizeof(T)) > kNtBytes);
   }
   if constexpr (sizeof(T) == 2 || sizeof(T) == 4) {
-#ifndef OFX_AB_NO_SHIFT_PF  // A/B builds only (scripts/ab_build.sh)
+#ifndef OFX_AB_NO_SHIFT_PF  // A/B builds only (probes/ab_build.sh)
     if (use_shift_pf_form(L, (int)sizeof(T)) && buffer_rows_ok<T>(L)) return launch_shift_pf<T, I>(L);
 #endif
   }

@@ -168,7 +168,7 @@ int launch_tuned(const Launch& L, int id) {
     }
   }
   // round 5: 16-bit rows of odd widths with the shifted window (windows at 2-B alignment:
-  // scripts/unaligned_probe.hip) -- 4- and 8-element lanes over 4-16 lanes
+  // probes/unaligned_probe.hip) -- 4- and 8-element lanes over 4-16 lanes
   if constexpr (sizeof(T) == 2 && std::is_same<I, int32_t>::value) {
     constexpr bool P = true, W = true;
     switch (id) {

@@ -7,7 +7,7 @@ from oneflow.framework.docstr.utils import add_docstr
 add_docstr(
     oneflow.spmm,
     r"""
-    spmm(a_csr_row_ptr, a_csr_col_idx, a_csr_values, a_num_rows, a_num_cols, b) -> Tensor
+    spmm(a_csr_row_ptr, a_csr_col_idx, a_csr_values, a_num_rows, a_num_cols, b, static_csr=0) -> Tensor
 
     Multiplies the sparse matrix :math:`A` (:attr:`a_num_rows` :math:`\times` :attr:`a_num_cols`,
     CSR) by the dense matrix :attr:`b` (:attr:`a_num_cols` :math:`\times N`):
@@ -31,6 +31,10 @@ add_docstr(
         a_num_rows (int): M
         a_num_cols (int): K
         b (oneflow.Tensor): dtype of ``a_csr_values``, shape ``[K, N]``
+        static_csr (int, optional): 0 (default) plans the row work list on every call.  A non-zero
+            value promises that the CSR tensors are not modified while calls carry that value;
+            the GPU kernel then keeps the plan in its state and later calls skip the planning
+            kernel.  Give a new CSR built in reused memory a new value.  No numeric effect.
     Returns:
         oneflow.Tensor: shape ``[M, N]``, dtype of ``b``
 

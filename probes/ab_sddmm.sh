@@ -1,6 +1,6 @@
 #!/bin/bash
-# A/B of SDDMM builds (scripts/ab_build.sh tags) through OFX_SPMM_LIB, interleaved, two rounds:
-# bash scripts/ab_sddmm.sh <out.jsonl> "<config:n> ..." "<tag> ..."   (tag "base" = the default build)
+# A/B of SDDMM builds (probes/ab_build.sh tags) through OFX_SPMM_LIB, interleaved, two rounds:
+# bash probes/ab_sddmm.sh <out.jsonl> "<config:n> ..." "<tag> ..."   (tag "base" = the default build)
 set -e
 cd ${GRAFT_REPO_ROOT:-$(dirname "$0")/..}
 mkdir -p gpurun_out

@@ -4,7 +4,7 @@ runs against the job's native graph mode (ofx_spmm_job_set_graph: captured once 
 device C-ABI's hipGraph executable, one graph launch per run), on a BASELINE-shaped graph; plus
 the eager two-layer GCN forward through the op layer for reference.
 
-    python scripts/bench_graph.py [--config cora] [--iters 200]
+    python probes/bench_graph.py [--config cora] [--iters 200]
 """
 import argparse
 import json

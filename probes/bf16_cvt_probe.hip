@@ -2,7 +2,7 @@
 // __bf16) against the software round-to-nearest-even of csrc/spmm_common.h (round_bf16), over
 // every one of the 2^32 f32 bit patterns.  Prints the mismatch count by class (NaN / other) and
 // the first mismatches.  Not product code.
-// build: hipcc --offload-arch=gfx950 -O3 -fno-gpu-flush-denormals-to-zero scripts/bf16_cvt_probe.hip -o bf16_cvt_probe
+// build: hipcc --offload-arch=gfx950 -O3 -fno-gpu-flush-denormals-to-zero probes/bf16_cvt_probe.hip -o bf16_cvt_probe
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstring>

@@ -7,7 +7,7 @@
 // nonzero order) with no load imbalance.  The column index carries a tag in bit 31 (set = cold),
 // made on the host from the in-degree ranking; hot rows load with cache policy A_HOT, cold ones
 // with A_COLD (buffer-load aux bits on gfx950: 1 = sc0, 2 = nt, 16 = sc1).  Each half-wave writes
-// its sum so nothing is dead code.  Built by scripts/cache_policy_probe.py.
+// its sum so nothing is dead code.  Built by probes/cache_policy_probe.py.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>

@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
 """Probe (not product code): products-shaped B-row gather (N=128 fp32) with the B loads steered
-by column hotness through the cache-policy bits (scripts/cache_policy_probe.hip).  The top-T
+by column hotness through the cache-policy bits (probes/cache_policy_probe.hip).  The top-T
 columns by in-degree load with the default policy, the rest with the mode's policy; T sweeps
 from the L2's share (8k rows) to twice the Infinity Cache (1M rows).  Modes are interleaved
 and each timing is the median of 3 rounds of 5 launches (HIP events).
 
-    python scripts/cache_policy_probe.py          # prints one JSON line per (T, mode)
+    python probes/cache_policy_probe.py          # prints one JSON line per (T, mode)
 """
 import ctypes
 import json

@@ -4,7 +4,7 @@ dwordx2 / dword / short loads) issued right behind an `s_waitcnt vmcnt(0)` — a
 start before every older load has returned, i.e. one row in flight per lane.  Prints per kernel:
 loads, loads behind vmcnt(0), VGPRs.
 
-    python scripts/isa_wait_scan.py [of-spmm_amd/build] [--filter spmm_main]"""
+    python probes/isa_wait_scan.py [of-spmm_amd/build] [--filter spmm_main]"""
 import os
 import re
 import subprocess

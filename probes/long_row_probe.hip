@@ -4,7 +4,7 @@
 //   (b) a full wave: quarter q loads the B rows of nonzeros 4u+q, the products are formed in
 //       parallel and added in nonzero order through cross-lane moves (same bits as (a)).
 // Not product code: a standalone timing of the two traversals on one wave.
-// build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off scripts/long_row_probe.hip -o long_row_probe
+// build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off probes/long_row_probe.hip -o long_row_probe
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>

@@ -1,6 +1,6 @@
 """Mid-size op calls for a rocprofv3 kernel trace (the mid form's launches: plan count / scan /
 write, main with block items, reduce): 200 calls per configuration, configurations separated by
-a 50 ms idle gap so scripts/trace_segments.py can split the trace."""
+a 50 ms idle gap so probes/trace_segments.py can split the trace."""
 import sys
 import time
 

@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """Probe (not product code): products-shaped N=16 fp32 gather (64-B B rows) under each
-cache-policy combination of the B-row loads (scripts/narrow_policy_probe.hip).  Interleaved,
+cache-policy combination of the B-row loads (probes/narrow_policy_probe.hip).  Interleaved,
 median of 3 rounds of 5 launches (HIP events); the sums must equal the default policy's.
 
-    python scripts/narrow_policy_probe.py [--aux 17]   # --aux: run only that policy (PMC runs)
+    python probes/narrow_policy_probe.py [--aux 17]   # --aux: run only that policy (PMC runs)
 """
 import argparse
 import ctypes

@@ -4,7 +4,7 @@ any size (30001: block items for hub chunks and heavy rows, big-launch light row
 with small-launch light rows), on BASELINE-shaped graphs over several widths.  Interleaved, median
 of 3 rounds of 5 back-to-back launches (HIP events); outputs must be bit-identical across forms.
 
-    python scripts/probe_forms.py [--configs plaw1m,products] [--widths 16,32,64,128]
+    python probes/probe_forms.py [--configs plaw1m,products] [--widths 16,32,64,128]
 """
 import argparse
 import json

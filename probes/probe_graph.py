@@ -1,9 +1,9 @@
 """Device time against host-submission time per SpMM call: each configuration <graph>:<N>:<variant>
-(graphs of scripts/probe_split.py) is timed eagerly (events around back-to-back calls, as
+(graphs of probes/probe_split.py) is timed eagerly (events around back-to-back calls, as
 probe_split does) and as a captured HIP graph of the same calls replayed (no host launch cost).
 A gap between the two is launch overhead, not kernel time.
 
-    python3 scripts/probe_graph.py arxiv:16:0 arxiv:16:10022 pubmed:16:0
+    python3 probes/probe_graph.py arxiv:16:0 arxiv:16:10022 pubmed:16:0
 """
 import json
 import os

@@ -9,7 +9,7 @@ Per (graph, N): the automatic choice (variant 0), the round-2 split with the aut
 rounds, median over rounds of back-to-back launches (HIP events on the launch stream).  Every
 variant under the same split must give the same bits (checked; the run stops otherwise).
 
-    python scripts/probe_split.py [--graphs pubmed,arxiv,...] [--widths 16,32,64] > out.jsonl
+    python probes/probe_split.py [--graphs pubmed,arxiv,...] [--widths 16,32,64] > out.jsonl
 """
 import argparse
 import json

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Kernel-trace (rocprofv3 --kernel-trace --stats) of bench.py for several configs, one run each.
-# usage: scripts/trace3.sh <tag> <config>...
+# usage: probes/trace3.sh <tag> <config>...
 set -u
 TAG=$1; shift
 export TMPDIR=/tmp

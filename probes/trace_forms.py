@@ -1,10 +1,10 @@
 """Launch sequences for a rocprofv3 kernel trace: 200 back-to-back calls per configuration
-<graph>:<N>:<variant> (graphs of scripts/probe_split.py), configurations separated by a 50 ms
-idle gap so scripts/trace_segments.py can split the trace into one segment each.
+<graph>:<N>:<variant> (graphs of probes/probe_split.py), configurations separated by a 50 ms
+idle gap so probes/trace_segments.py can split the trace into one segment each.
 
     rocprofv3 --kernel-trace --output-format csv -d <dir> -o run -- \
-        python3 scripts/trace_forms.py arxiv:16:0 arxiv:16:30005 pubmed:64:0
-    python3 scripts/trace_segments.py <dir>/..._kernel_trace.csv
+        python3 probes/trace_forms.py arxiv:16:0 arxiv:16:30005 pubmed:64:0
+    python3 probes/trace_segments.py <dir>/..._kernel_trace.csv
 """
 import os
 import sys

@@ -4,7 +4,7 @@
 // values with raw_buffer_load_b64 (b128) and stores them with one 8-B (16-B) store at element e
 // of an output; the host compares.  Also times a window load stream at 2-B offsets against the
 // same stream 8-B aligned.  Not product code.
-// build: hipcc --offload-arch=gfx950 -O3 scripts/unaligned_probe.hip -o unaligned_probe
+// build: hipcc --offload-arch=gfx950 -O3 probes/unaligned_probe.hip -o unaligned_probe
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

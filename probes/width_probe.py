@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Mid-size widths, one configuration per spec <graph>:<dtype>:<N>[:<variant>[:<heavy>]] (graphs of
-scripts/probe_split.py, synthetic power-law, generated once per graph; <graph>@g<gamma> sets the
+probes/probe_split.py, synthetic power-law, generated once per graph; <graph>@g<gamma> sets the
 degree exponent, e.g. arxiv@g50 for nearly even degrees, 2.5 by default):
 
   --mode time   (default) per spec: the form the launch takes (ofx_spmm_csr_describe), the median
@@ -10,7 +10,7 @@ degree exponent, e.g. arxiv@g50 for nearly even degrees, 2.5 by default):
   --mode run    REPS eager calls per spec with an idle gap between specs (rocprofv3 --kernel-trace
                 / --pmc runs of one spec at a time).
 
-    python scripts/width_probe.py arxiv:bf16:47 arxiv:bf16:64 arxiv:f32:17 [--mode run]
+    python probes/width_probe.py arxiv:bf16:47 arxiv:bf16:64 arxiv:f32:17 [--mode run]
 """
 import argparse
 import json

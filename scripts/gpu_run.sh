@@ -36,7 +36,15 @@ for step in "$@"; do
       if [ -n "$arg" ]; then timeout -k 10 900 $PT -x -k "$arg" > $log 2>&1
       else timeout -k 10 1000 $PT -x > $log 2>&1; fi ;;
     dbgtests)
-      OFX_DEBUG_BOUNDS_CHECK=1 OFX_SPMM_LIB=$L/libofx_spmm_dbg.so timeout -k 10 900 $PT -x -k "$arg" > $log 2>&1 ;;
+      # the bounds-checked library exists only for these runs (make -C of-spmm_amd debug; delete
+      # it after, so it is not pushed with every call) and must be newer than every kernel source
+      stale=$(find of-spmm_amd/csrc of-spmm_amd/Makefile -newer $L/libofx_spmm_dbg.so 2>/dev/null | head -3)
+      if [ ! -f $L/libofx_spmm_dbg.so ] || [ -n "$stale" ]; then
+        echo "dbgtests: $L/libofx_spmm_dbg.so is missing or older than: $stale (make -C of-spmm_amd debug)" > $log
+        false
+      else
+        OFX_DEBUG_BOUNDS_CHECK=1 OFX_SPMM_LIB=$L/libofx_spmm_dbg.so timeout -k 10 900 $PT -x -k "$arg" > $log 2>&1
+      fi ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $log 2>&1 ;;
     bench)
