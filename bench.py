@@ -439,6 +439,20 @@ def main():
         cold.append(events[1].ms_to(events[2]))
     del scratch
     cold_ms = float(np.median(cold)) if cold else float("nan")
+    # N=1, reported beside the value (never the value): the same op with attr static_csr, whose
+    # kernel state keeps the work-list plan across calls (a GNN's constant graph)
+    static_ms = None
+    if not rowsplit and on_gpu and opts is None:
+        fs.spmm(d_rp, d_ci, d_v, m, k, d_b, out=out, static_csr=True)  # plans once
+        sync()
+        e0, e1 = Mark(on_gpu), Mark(on_gpu)
+        e0.record()
+        for _ in range(args.steps):
+            fs.spmm(d_rp, d_ci, d_v, m, k, d_b, out=out, static_csr=True)
+        e1.record()
+        sync()
+        static_ms = e0.ms_to(e1) / args.steps
+        fs._C.static_plans(release=True)
     bytes_launch = alg_bytes(rows, nnz_local, n, s_v)
     if rowsplit and rs.exchange in rs.grids:  # the grid's SpMM: its row group x N/C columns
         gp = rs.grids[rs.exchange]
@@ -492,6 +506,9 @@ def main():
     }
     result["extra"] = {"kernel_ms_events_separate_run": round(kern_ms_separate, 4),
                        "kernel_ms_cold_median": round(cold_ms, 4) if cold else None,
+                       "static_csr_ms_per_step": round(static_ms, 4) if static_ms else None,
+                       "static_csr_gflops": round(flops / (static_ms * 1e-3) / 1e9, 2)
+                       if static_ms else None,
                        "gbs_cold": round(bytes_launch / (cold_ms * 1e-3) / 1e9, 1) if cold else None}
     if rowsplit:
         nz = torch.tensor([nnz_local, nnz_local], dtype=torch.float64, device=red_dev)
