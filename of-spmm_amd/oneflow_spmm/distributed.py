@@ -1036,7 +1036,9 @@ class RowSplitSpmm:
         else:
             via += " of the padded Split(0) shards of B"
             depth = self.chunks
-        pipe = f", {depth} column blocks pipelined" if depth > 1 else ""
+        overlap = self.comm_stream is not None and self.comm_kind != "torch"
+        pipe = (f", {depth} column blocks " + ("pipelined on a side stream" if overlap
+                                                else "in sequence")) if depth > 1 else ""
         return f"1-D row split x{w} (BalancedSplitter rows) + {via}{pipe}"
 
     # tests only: "name-prefix:factor[,...]" multiplies the measured time of matching candidates

@@ -12,6 +12,8 @@ for p in (ROOT, os.path.join(ROOT, "of-spmm_amd")):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
     config.addinivalue_line("markers", "slow: full BASELINE-size problems")
+    config.addinivalue_line("markers", "graph_capture: captures launches into a hipGraph (not run "
+                                       "under the bounds-checked library)")
     # GPU calls (scripts/gpu_run.sh): a fatal signal's thread dump also goes to a file that
     # survives pytest's output capture (the r03ai abort's messages were lost)
     path = os.environ.get("OFX_FAULTHANDLER_FILE")
@@ -50,6 +52,11 @@ def _debug_bounds_guard(request):
     if os.environ.get("OFX_DEBUG_BOUNDS_CHECK") != "1" or "gpu" not in request.keywords:
         yield
         return
+    if "graph_capture" in request.keywords:
+        # csrc/dbg_bounds.h publishes each launch's allocation table with a host-to-device copy
+        # of a host stack object; a graph capture records that copy and replays it from memory
+        # that is gone, so captured launches are outside what this instrument can check
+        pytest.skip("graph capture: the bounds-checked library's per-launch table is not capturable")
     import ctypes
     from oneflow_spmm import _lib
     out = (ctypes.c_uint64 * 8)()

@@ -109,6 +109,39 @@ int main(void) {
                             2, &cur) == OFX_OK);
   }
 
+  /* the functional entry with the op's attributes (static_csr is a GPU-kernel state matter: the
+   * kCPU kernel ignores it), through tagged tensor descriptors and a tagged attrs struct */
+  {
+    ofx_tensor_desc d_rp = OFX_TENSOR_DESC_INIT, d_ci = OFX_TENSOR_DESC_INIT,
+                    d_v = OFX_TENSOR_DESC_INIT, d_b = OFX_TENSOR_DESC_INIT,
+                    d_c = OFX_TENSOR_DESC_INIT;
+    d_rp.dtype = OFX_DT_INT32, d_rp.device = -1, d_rp.ndim = 1, d_rp.shape[0] = 3, d_rp.stride[0] = 1;
+    d_rp.data = (void*)rp;
+    d_ci.dtype = OFX_DT_INT32, d_ci.device = -1, d_ci.ndim = 1, d_ci.shape[0] = 3, d_ci.stride[0] = 1;
+    d_ci.data = (void*)col;
+    d_v.dtype = OFX_DT_FLOAT, d_v.device = -1, d_v.ndim = 1, d_v.shape[0] = 3, d_v.stride[0] = 1;
+    d_v.data = (void*)val;
+    d_b.dtype = OFX_DT_FLOAT, d_b.device = -1, d_b.ndim = 2, d_b.shape[0] = 3, d_b.shape[1] = 2;
+    d_b.stride[0] = 2, d_b.stride[1] = 1, d_b.data = (void*)b;
+    d_c.dtype = OFX_DT_FLOAT, d_c.device = -1, d_c.ndim = 2, d_c.shape[0] = 2, d_c.shape[1] = 2;
+    d_c.stride[0] = 2, d_c.stride[1] = 1, d_c.data = c;
+    const int64_t hier[1] = {1};
+    const int32_t axes[1] = {-1};
+    ofx_spmm_attrs at = OFX_SPMM_ATTRS_INIT;
+    at.static_csr = 1;
+    memset(c, 0xff, sizeof(c));
+    EXPECT(ofx_functional_spmm_csr_global_attrs(NULL, &d_rp, &d_ci, &d_v, 2, 3, &d_b, -1, &d_c,
+                                                NULL, 0, 1, hier, axes, 0, 1, NULL, &at) == OFX_OK);
+    EXPECT(c[0] == 3.f && c[1] == 2.f && c[2] == 0.f && c[3] == 3.f);
+    at.magic = 0;
+    EXPECT(ofx_functional_spmm_csr_global_attrs(NULL, &d_rp, &d_ci, &d_v, 2, 3, &d_b, -1, &d_c,
+                                                NULL, 0, 1, hier, axes, 0, 1, NULL, &at) ==
+           OFX_EINVAL);
+    int64_t entries = -1, plans = -1, hits = -1;
+    EXPECT(ofx_spmm_static_plans(&entries, &plans, &hits, 0) == OFX_OK && entries == 0 &&
+           plans == 0 && hits == 0);
+  }
+
   printf("%s %d failures\n", fails ? "FAIL" : "OK", fails);
   return fails ? 1 : 0;
 }

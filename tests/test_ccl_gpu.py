@@ -35,6 +35,7 @@ def test_nccl_logical_all_gather_on_hip(device, hip_placement):
     assert torch.equal(out, x)
 
 
+@pytest.mark.graph_capture
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_spmm_job_on_hip_bitexact_and_graph_replay(device, hip_placement, dt):
     rng = np.random.default_rng(31)
@@ -64,6 +65,7 @@ def test_spmm_job_on_hip_bitexact_and_graph_replay(device, hip_placement, dt):
     assert_bitwise(out, oracle_spmm(rp, ci, v, b2), "graph replay")
 
 
+@pytest.mark.graph_capture
 @pytest.mark.parametrize("stream_kind", ["default", "side"])
 def test_spmm_job_native_graph_mode(device, hip_placement, stream_kind):
     """The job's own graph mode (UserKernel::ForwardUserKernel's CUDA-graph branch,

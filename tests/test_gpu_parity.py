@@ -452,6 +452,7 @@ def test_plan_once_compute_many(device, idx):
             kern(d_rp, d_ci, d_v, b.to(device), out[:10], 0, 10, planned=True)
 
 
+@pytest.mark.graph_capture
 def test_hipgraph_capture_replay(device):
     """The op launches are capture-safe (no allocation / sync inside): capture into a graph,
     replay on new data, same bits as eager."""
@@ -478,6 +479,7 @@ def test_hipgraph_capture_replay(device):
     assert_bitwise(out, ref, "graph replay")
 
 
+@pytest.mark.graph_capture
 def test_row_split_step_hipgraph_capture(device):
     """The whole row-split step (RCCL exchange + local SpMM; the pipelined form on two streams;
     the halo form) is capture-safe: capture once, load a new B shard, replay, same bits."""

@@ -174,6 +174,7 @@ def test_planned_launch_over_an_unplanned_workspace_is_refused(device):
     assert_bitwise(out, oracle_spmm(rp, ci, v, b), "planned after plan()")
 
 
+@pytest.mark.graph_capture
 def test_graph_replay_replans_after_row_ptr_is_rewritten(device):
     """a non-planned launch captured into a hipGraph carried one host epoch for
     every replay, so a replay took the previous replay's status words.  Rewriting row_ptr /

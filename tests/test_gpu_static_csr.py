@@ -86,6 +86,7 @@ def test_rewritten_row_ptr_replans_without_the_attribute(device):
     assert_bitwise(out.cpu(), oracle_spmm(rp_b, ci_b, v_b, b), "graph B, new static value")
 
 
+@pytest.mark.graph_capture
 def test_static_call_captured_in_a_graph(device):
     rng = np.random.default_rng(620)
     m, k, n = 60_000, 60_000, 64
@@ -113,6 +114,7 @@ def test_static_call_captured_in_a_graph(device):
         assert_bitwise(out.cpu(), oracle_spmm(rp, ci, v, b2), f"replay {i}")
 
 
+@pytest.mark.graph_capture
 @pytest.mark.parametrize("graph", [False, True])
 def test_compiled_job_static_plan(device, graph):
     rng = np.random.default_rng(630 + graph)

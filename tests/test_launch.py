@@ -187,7 +187,7 @@ def test_bench_eight_rank_value_is_the_rowsplit_even_when_a_grid_is_faster():
         assert "all-gather" in par and kept_name.startswith("torch/p")
         depth = int(kept_name.split("/p")[1])
         assert ex["pipeline_blocks"] == depth
-        assert (f"{depth} column blocks pipelined" in par) == (depth > 1)
+        assert (f"{depth} column blocks in sequence" in par) == (depth > 1)  # gloo: no side stream
     assert "grid" not in par
     # value = the whole job's FLOPs over the timed steps of that exchange
     c = line["config"]
