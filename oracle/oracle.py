@@ -2,9 +2,16 @@
 
 TEST INFRASTRUCTURE ONLY.  Imported by tests/, __graft_entry__.smoke() and bench.py's
 cpu_baseline leg as the *checker*; the product package (of-spmm_amd/oneflow_spmm) never imports
-it.  Parity status: unpinned against reference-held fixtures (the reference has no SpMM and no
-test pinning one); cross-validated against scipy.sparse and torch.sparse_csr
-(tests/golden/make_golden.py, tests/test_oracle.py).
+it.  Parity status: the reference has no SpMM and no test pinning one.  Its
+two building blocks ARE pinned by the reference's own golden vectors: the embedding test
+python/oneflow/test/modules/test_sparse.py:76-134 holds literal inputs and expected outputs of
+EmbeddingFunctor<kCPU> (the row gather) and EmbeddingGradFunctor<kCPU> (the index-order segment
+sum), oneflow/user/kernels/embedding_kernel_util.cpp:48-88, and tests/test_reference_fixtures.py
+checks this oracle (and the kernels) against them bit for bit
+(tests/golden/ref_embedding_scale_by_freq.npz, extracted by make_reference_fixtures.py).  Those
+sums are exact, so the rounding order of longer sums is pinned by restatement only, and
+cross-validated against scipy.sparse and torch.sparse_csr (tests/golden/make_golden.py,
+tests/test_oracle.py): "parity partially pinned".
 
 Semantics (see spmm_oracle.c header for the reference file:line anchors):
   C[r, :] = sum_{j in row r, ascending} val[j] * B[col[j], :]   from +0, multiply then add.

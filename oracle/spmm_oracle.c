@@ -4,9 +4,12 @@
  * never linked into, or called by, the product (of-spmm_amd/).
  *
  * Parity status: the reference (OneFlow v0.8.1-dev) contains no SpMM and no test pinning one
- *  -> "parity unpinned" against reference-held fixtures.  The restatement is
- * anchored on the reference's own CPU building blocks and cross-checked against scipy.sparse and
- * torch.sparse_csr in tests/golden/make_golden.py:
+ * (SURVEY.md §0, §8c).  Its two building blocks are pinned by the reference's own golden vectors
+ * (the embedding test python/oneflow/test/modules/test_sparse.py:76-134: row gather and
+ * index-order segment sum, embedding_kernel_util.cpp:48-88; tests/test_reference_fixtures.py),
+ * whose sums are exact -> "parity partially pinned": the rounding order of longer sums rests on
+ * the restatement below and the cross-checks against scipy.sparse and torch.sparse_csr in
+ * tests/golden/make_golden.py:
  *
  *   gather     oneflow/user/kernels/gather_kernel_util.cpp:72-92
  *              out[i,:] = in[idx[i],:]   (CHECK_GE(idx, 0) -> error here; an index >= the table
