@@ -34,7 +34,7 @@ namespace {
 constexpr int kPullBlock = 256;
 constexpr int kPullUnroll = 4;       // 16-B loads in flight per lane
 constexpr int kMaxPullBlocks = 2048;  // 8 per CU; blocks stride over the tiles
-constexpr int kPublishBlocks = 64;    // dealt round-robin over the 8 XCDs: 8 per XCD (L2)
+constexpr int kPublishBlocks = 1024;  // one wave each, over all 256 CUs: every XCD's L2 (below)
 
 struct PeerSrc {
   const char* base[OFX_PEER_MAX_RANKS];  // peer p's buffer (the same layout as ours)
@@ -123,8 +123,9 @@ __global__ void __launch_bounds__(kPullBlock)
 
 // A system-scope release on every XCD: each block's first lane writes its XCD's L2 dirty lines
 // back to HBM, where a peer's xGMI reads find them (the L2s are not probed by remote readers).
-// kPublishBlocks blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, "workgroup
-// dispatch"), 8 per XCD.
+// Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, "workgroup dispatch"), so
+// 8 would do; kPublishBlocks = 1024 one-wave blocks (4 per CU) keep every XCD covered whatever
+// the dispatch order (the publish must not rest on that order), for a few µs.
 __global__ void peer_publish_kernel() {
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
