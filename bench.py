@@ -202,7 +202,8 @@ def main():
                          "past its limit names it and exits 75)")
     ap.add_argument("--stall-test", default=os.environ.get("OFX_BENCH_STALL", ""),
                     help="tests only: 'rank:phase' makes that rank sleep in that phase; "
-                         "'rank:exchange' makes it never join its first exchange of B")
+                         "'rank:exchange' makes it never join its first exchange of B; "
+                         "'0:native-tune' fails the first tune as if every native exchange had")
     ap.add_argument("--exchange-deadline", type=float,
                     default=float(os.environ.get("OFX_EXCHANGE_DEADLINE", "120")),
                     help="N>1, set-up / tune / warmup: seconds an exchange of B may take to "
@@ -248,7 +249,8 @@ def main():
         if watch is None:
             return
         watch.phase(name, limit_s)
-        if stall_phase and int(stall_rank) == rank and name.startswith(stall_phase):
+        if (stall_phase and stall_phase != "native-tune" and int(stall_rank) == rank
+                and name.startswith(stall_phase)):
             time.sleep(1e6)  # the watchdog ends this rank
     enter_phase("process group init", 300)
     if rowsplit:
@@ -303,37 +305,41 @@ def main():
             def step():
                 kern(d_rp, d_ci, d_v, d_b, out)
     else:
-        enter_phase("communicator init", 400)
-        try:
-            rs = RowSplitSpmm(m, k, n, nnz_local, dt, torch.int32, device,
-                              comm="torch" if rehearsal else "auto")
-        except fs.OfxError as e:  # own RCCL communicator refused: torch.distributed's (also RCCL)
-            log(f"[bench] native RCCL communicator unavailable ({e}); using torch.distributed")
-            rs = RowSplitSpmm(m, k, n, nnz_local, dt, torch.int32, device, comm="torch")
-        watch.on_abort.append(rs.abort)
-        # set-up, tune and warmup await every exchange (a peer that never joins ends this rank
-        # with the exchange named); the timed steps do not
-        rs.set_exchange_deadline(args.exchange_deadline)
-        if stall_phase == "exchange" and int(stall_rank) == rank:
-            # tests only: this rank never joins its first exchange of B (its peers' deadline fires)
-            rs.gather_block = lambda *a, **kw: time.sleep(1e6)
-        enter_phase("bind (shards, remap, plans, halo and grid layouts)", 900)
-        klo, khi = rs.k_range
-        rs.load_shard(synth.dense(klo, khi, n, dt, device=device))
-        full = None
         pinned_sub = int(args.exchange.split("/s")[1]) if "/s" in args.exchange else 1
         auto = args.exchange in ("auto", "any")
+        full = None
         if auto or args.exchange.startswith(("nsplit", "grid")):
             # the grid / column-split candidates need the whole CSR on every rank
             f_ci = torch.from_numpy(synth.columns(m, k, rp_full, threads=threads)).to(device)
             full = (torch.from_numpy(rp_full.astype(np.int32)).to(device), f_ci,
                     synth.values(0, nnz, dt).to(device))
-        rs.bind(d_rp, d_ci, d_v, halo=auto or args.exchange == "halo", full_csr=full,
-                grid_subs=tuple(sorted({1, 2, pinned_sub})))
+
+        def build_rs(comm):
+            enter_phase("communicator init", 400)
+            try:
+                r = RowSplitSpmm(m, k, n, nnz_local, dt, torch.int32, device, comm=comm)
+            except fs.OfxError as e:  # own RCCL communicator refused: torch.distributed's (also RCCL)
+                log(f"[bench] native RCCL communicator unavailable ({e}); using torch.distributed")
+                r = RowSplitSpmm(m, k, n, nnz_local, dt, torch.int32, device, comm="torch")
+            watch.on_abort.append(r.abort)
+            # set-up, tune and warmup await every exchange (a peer that never joins ends this rank
+            # with the exchange named); the timed steps do not
+            r.set_exchange_deadline(args.exchange_deadline)
+            if stall_phase == "exchange" and int(stall_rank) == rank:
+                # tests only: this rank never joins its first exchange of B (its peers' deadline fires)
+                r.gather_block = lambda *a, **kw: time.sleep(1e6)
+            enter_phase("bind (shards, remap, plans, halo and grid layouts)", 900)
+            klo, khi = r.k_range
+            r.load_shard(synth.dense(klo, khi, n, dt, device=device))
+            r.bind(d_rp, d_ci, d_v, halo=auto or args.exchange == "halo", full_csr=full,
+                   grid_subs=tuple(sorted({1, 2, pinned_sub})))
+            return r
+
+        rs = build_rs("torch" if rehearsal else "auto")
         # exchange: all-gather (ring / point-to-point) x pipeline depth (column blocks gathered
         # while the previous block computes), or halo-only rows; measured here, untimed, the
         # fastest 1-D row-split candidate kept (every candidate gives the same bytes)
-        comm_times, tune_s = {}, None
+        comm_times, tune_s, comm_fallback = {}, None, None
         if args.comm or args.pipeline or not auto:
             rs.exchange = args.exchange if not auto else "allgather"
             if rs.exchange not in ("allgather", "halo") and rs.exchange not in rs.grids:
@@ -345,9 +351,33 @@ def main():
                 rs.set_halo_pipeline(args.pipeline or 1)
         else:
             t_tune = time.time()
-            comm_times = rs.tune(out, force=args.force_rowsplit, budget_s=args.tune_budget, log=log,
-                                 on_candidate=lambda nm: enter_phase(f"tune: {nm}", 180),
-                                 rowsplit_only=args.exchange == "auto")
+
+            def tune():
+                return rs.tune(out, force=args.force_rowsplit, budget_s=args.tune_budget, log=log,
+                               on_candidate=lambda nm: enter_phase(f"tune: {nm}", 180),
+                               rowsplit_only=args.exchange == "auto")
+            # tests only (--stall-test <rank>:native-tune): the first tune fails as if every native
+            # candidate had, so the gloo rehearsal walks the rebuild below
+            fake_fail = stall_phase == "native-tune"
+            try:
+                if fake_fail:
+                    raise RuntimeError("RowSplitSpmm.tune: every exchange failed: (test)")
+                comm_times = tune()
+            except RuntimeError as e:
+                # every candidate on the native communicator failed (on every rank alike: tune's
+                # times are max-reduced): the same exchanges over torch.distributed's RCCL group
+                if ((rs.comm_kind == "torch" and not fake_fail)
+                        or not str(e).startswith("RowSplitSpmm.tune:")):
+                    raise
+                comm_fallback = str(e)[:400]
+                log(f"[bench] {comm_fallback}; rebuilding the exchange on torch.distributed")
+                watch.on_abort.remove(rs.abort)
+                try:
+                    rs.close()
+                except Exception as ce:  # noqa: BLE001 -- an aborted communicator may refuse
+                    log(f"[bench] closing the native communicator: {ce}")
+                rs = build_rs("torch")
+                comm_times = tune()
             tune_s = time.time() - t_tune
             log("[bench] exchange candidates (ms, max over ranks; model-predicted): " +
                 ", ".join(f"{kk} {vv:.3f} ({rs.tune_report[kk]['predicted_ms']:.3f})"
@@ -545,16 +575,18 @@ def main():
             "exchange": rs.exchange, "allgather_schedule": rs.comm_kind,
             "pipeline_blocks": rs.halo_chunks if rs.exchange == "halo" else rs.chunks,
             "halo_rows_received": rs.halo.halo_rows if rs.halo is not None else None,
-            "remote_rows_total": (rs.k - (khi - klo)),
+            "remote_rows_total": (rs.k - (rs.k_range[1] - rs.k_range[0])),
             "allgather_tune_ms": {kk: (round(vv, 4) if np.isfinite(vv) else None)
                                   for kk, vv in comm_times.items()},
             # the north star's configuration (plain row split + one all-gather of B), always
             # measured by tune() whichever exchange wins: ms per step and its aggregate rate
             "rowsplit_allgather_p1": ({"ms": round(comm_times[ag1], 4),
                                        "gflops": round(flops / (comm_times[ag1] * 1e-3) / 1e9, 2)}
-                                      if (ag1 := f"{'torch' if rehearsal else 'rccl'}/p1") in comm_times
+                                      if (ag1 := f"{'torch' if rs.comm_kind == 'torch' else 'rccl'}/p1") in comm_times
                                       and np.isfinite(comm_times[ag1]) else None),
             "tune_errors": getattr(rs, "tune_errors", {}) or None,
+            # every native-RCCL candidate failed and the exchange was rebuilt on torch.distributed
+            "comm_fallback": comm_fallback,
             # every candidate: model time (xGMI assumption), the model refitted to
             # the first measurement, the measured time (max over ranks) and whether it ran
             "tune_candidates": getattr(rs, "tune_report", {}) or None,

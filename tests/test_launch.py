@@ -196,6 +196,23 @@ def test_bench_eight_rank_value_is_the_rowsplit_even_when_a_grid_is_faster():
     assert ex["ranks_seen"] == ex["exchange_comm_ranks"] == line["n_gpus"] == 8
     assert ex["rccl_comm_ranks"] is None  # gloo rehearsal: no RCCL communicator
 
+def test_bench_rebuilds_on_torch_distributed_when_every_native_exchange_fails():
+    """A tune whose every native-RCCL candidate failed (the same on every rank: tune's times are
+    max-reduced) does not end the run: the exchange is rebuilt on torch.distributed's group and
+    tuned again, and the line says so (extra.comm_fallback).  Injected with the tests-only
+    '--stall-test 0:native-tune' on the 2-rank gloo rehearsal."""
+    p = _bench(["--gpus", "2", "--backend", "gloo", "--device", "cpu", "--config", "tiny",
+                "--steps", "2", "--warmup", "1", "--stall-test", "0:native-tune"],
+               {"OMP_NUM_THREADS": "1"}, drop=_SPAWN_ENV_DROP)
+    line = _bench_line(p)
+    ex = line["extra"]
+    assert ex["comm_fallback"] and "every exchange failed" in ex["comm_fallback"]
+    assert "rebuilding the exchange on torch.distributed" in p.stderr + p.stdout
+    assert ex["exchange_is_rowsplit"] and ex["allgather_schedule"] == "torch"
+    assert ex["ranks_seen"] == ex["exchange_comm_ranks"] == 2
+    assert line["value"] > 0
+
+
 def test_bench_stalled_rank_names_its_phase_and_fails():
     """A rank stalled in a phase past its limit (injected: rank 1 sleeps in its first tune
     candidate) prints the phase, exits 75, and the launcher ends the run non-zero instead of
