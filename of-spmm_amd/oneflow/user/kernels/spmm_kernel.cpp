@@ -11,6 +11,7 @@
  */
 #include <list>
 #include <mutex>
+#include <vector>
 
 #include "oneflow/core/framework/framework.h"
 #include "oneflow/core/functional/spmm_functor.h"
@@ -71,6 +72,7 @@ class SpmmCsrPlanState final : public user_op::OpKernelState {
       }
     }
     if (capturing) return OFX_OK;
+    FreeDropped();
     int rc = OFX_OK;
     if (entries_.size() >= kMaxPlans) {
       // an in-flight launch may still read the evicted plan: the device drains first
@@ -90,15 +92,21 @@ class SpmmCsrPlanState final : public user_op::OpKernelState {
     return OFX_OK;
   }
 
-  // Forget key's plan (its launch failed): the next call plans again.
-  void Drop(const Key& key) {
+  // Forget key's plan (its launch failed): the next call plans again.  While the stream is
+  // capturing, the device cannot be drained, so the workspace is freed at the next call outside
+  // a capture (or at Release).
+  void Drop(const Key& key, bool capturing) {
     std::lock_guard<std::mutex> lock(mu_);
     for (auto it = entries_.begin(); it != entries_.end(); ++it) {
       if (it->key == key) {
-        WithDevice(it->key.device, [&]() {
-          ofx_device_synchronize();
-          return ofx_free(it->ws);
-        });
+        if (capturing) {
+          dropped_.push_back(*it);
+        } else {
+          WithDevice(it->key.device, [&]() {
+            ofx_device_synchronize();
+            return ofx_free(it->ws);
+          });
+        }
         entries_.erase(it);
         return;
       }
@@ -114,6 +122,7 @@ class SpmmCsrPlanState final : public user_op::OpKernelState {
 
   void Release() {
     std::lock_guard<std::mutex> lock(mu_);
+    FreeDropped();
     for (Entry& e : entries_) {
       WithDevice(e.key.device, [&]() {
         ofx_device_synchronize();
@@ -129,6 +138,16 @@ class SpmmCsrPlanState final : public user_op::OpKernelState {
     void* ws;
     size_t bytes;
   };
+  // workspaces dropped during a capture (mu_ held)
+  void FreeDropped() {
+    for (Entry& e : dropped_) {
+      WithDevice(e.key.device, [&]() {
+        ofx_device_synchronize();
+        return ofx_free(e.ws);
+      });
+    }
+    dropped_.clear();
+  }
   template <typename F>
   static int WithDevice(int device, F&& f) {
     int prev = -1;
@@ -142,6 +161,7 @@ class SpmmCsrPlanState final : public user_op::OpKernelState {
   const bool key_on_stream_;
   std::mutex mu_;
   std::list<Entry> entries_;
+  std::vector<Entry> dropped_;
   int64_t plans_ = 0, hits_ = 0;
 };
 
@@ -268,7 +288,7 @@ void ComputeSpmmCsr(user_op::KernelComputeContext* ctx, const user_op::OpKernelC
           if (!planned) {
             rc = ofx_spmm_csr_plan(stream, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
                                    row_begin, row_end, sws, need, &opts);
-            if (rc != OFX_OK) plans->Drop(key);
+            if (rc != OFX_OK) plans->Drop(key, hs->IsGraphCapturing());
             OFX_KERNEL_CHECK(rc == OFX_OK, op_name << " kernel failed (" << rc
                                                    << "): " << ofx_last_error());
           }
@@ -283,7 +303,7 @@ void ComputeSpmmCsr(user_op::KernelComputeContext* ctx, const user_op::OpKernelC
                             out->mut_dptr(), out->row_stride(), row_begin, row_end, bias_ptr, act,
                             ws, ws_bytes, &opts);
     // an earlier launch's loud failure (OFX_EPLAN) may have been this key's plan: plan again
-    if (rc != OFX_OK && keyed) plans->Drop(key);
+    if (rc != OFX_OK && keyed) plans->Drop(key, hs->IsGraphCapturing());
   } else {
     const int threads = ctx->stream()->As<ep::CpuStream>()->num_threads();
     rc = ofx_spmm_csr_fused_cpu(threads, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
