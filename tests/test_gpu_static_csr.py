@@ -169,3 +169,56 @@ def test_autograd_cached_transpose_reuses_its_plan(device):
     at_v = torch.from_numpy(at.data.astype(np.float32))
     for g, gb in grads:
         assert_bitwise(gb, oracle_spmm(at_rp, at_ci, at_v, g), "d(b)")
+
+
+def test_plans_past_the_cap_evict_the_least_recently_used(device):
+    """The eager state keeps at most 8 plans (SpmmCsrPlanState::kMaxPlans): a ninth static CSR
+    evicts the least recently used one, after the device drains; an evicted CSR plans again on
+    its next call, and every call stays exact."""
+    rng = np.random.default_rng(650)
+    m, k, n = 40_000, 40_000, 16
+    graphs = []
+    for i in range(10):
+        rp, ci, v = random_csr(m, k, hub_graph(m, k, rng, hubs=((i, 3000),)), rng)
+        graphs.append((rp, ci, v, [rp.to(device), ci.to(device), v.to(device)]))
+    b = random_dense(k, n, rng)
+    db = b.to(device)
+    s0 = _C.static_plans()
+    for i, (rp, ci, v, d) in enumerate(graphs):
+        out = fs.spmm(*d, m, k, db, static_csr=100 + i)
+        assert_bitwise(out.cpu(), oracle_spmm(rp, ci, v, b), f"graph {i}")
+    st = _C.static_plans()
+    assert counters(s0, st) == {"plans": 10, "hits": 0}
+    assert st["entries"] == 8, st
+    rp, ci, v, d = graphs[0]  # evicted: plans again
+    out = fs.spmm(*d, m, k, db, static_csr=100)
+    assert_bitwise(out.cpu(), oracle_spmm(rp, ci, v, b), "graph 0 again")
+    rp, ci, v, d = graphs[9]  # resident: a hit
+    out = fs.spmm(*d, m, k, db, static_csr=109)
+    torch.cuda.synchronize()
+    assert counters(st, _C.static_plans()) == {"plans": 1, "hits": 1}
+    assert_bitwise(out.cpu(), oracle_spmm(rp, ci, v, b), "graph 9 again")
+
+
+def test_each_stream_keeps_its_own_plan(device):
+    """The hub reduce's arrival counters live in the plan workspace, so an eager static CSR used
+    on two streams gets a plan per stream; both streams' results are exact."""
+    rng = np.random.default_rng(660)
+    m, k, n = 40_000, 40_000, 32
+    rp, ci, v = random_csr(m, k, hub_graph(m, k, rng), rng)
+    b = random_dense(k, n, rng)
+    d = [rp.to(device), ci.to(device), v.to(device)]
+    db = b.to(device)
+    ref = oracle_spmm(rp, ci, v, b)
+    streams = [torch.cuda.Stream(device) for _ in range(2)]
+    s0 = _C.static_plans()
+    outs = []
+    for rep in range(2):
+        for s in streams:
+            s.wait_stream(torch.cuda.current_stream(device))
+            with torch.cuda.stream(s):
+                outs.append(fs.spmm(*d, m, k, db, static_csr=11))
+    torch.cuda.synchronize()
+    assert counters(s0, _C.static_plans()) == {"plans": 2, "hits": 2}
+    for i, o in enumerate(outs):
+        assert_bitwise(o.cpu(), ref, f"call {i}")
