@@ -557,8 +557,10 @@ int ofx_functional_spmm_csr_global_attrs(
     size_t tmp_bytes, int hierarchy_ndim, const int64_t* hierarchy, const int32_t* out_split_axes,
     int64_t parallel_id, int num_threads, size_t* tmp_size_out, const ofx_spmm_attrs* attrs);
 /* The static-CSR plans the eager op states hold, summed over devices: live entries, plans built
- * (planner launches) and calls that reused a plan.  release != 0 first frees every entry's
- * workspace (after a device synchronisation) so the next static call plans again.            */
+ * (planner launches) and calls that reused a plan.  A state keeps at most 8 plans, evicting the
+ * least recently used, except plans a graph capture used: a captured graph holds their pointer,
+ * so they stay until released.  release != 0 first frees every entry's workspace (after a device
+ * synchronisation), captured ones included: destroy those graphs first.                        */
 int ofx_spmm_static_plans(int64_t* entries, int64_t* plans, int64_t* hits, int release);
 
 /* 1-D shorthand of ofx_functional_spmm_csr_global: hierarchy {parallel_num}, out split on

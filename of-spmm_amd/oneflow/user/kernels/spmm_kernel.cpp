@@ -11,7 +11,6 @@
  */
 #include <list>
 #include <mutex>
-#include <vector>
 
 #include "oneflow/core/framework/framework.h"
 #include "oneflow/core/functional/spmm_functor.h"
@@ -54,10 +53,12 @@ class SpmmCsrPlanState final : public user_op::OpKernelState {
   bool key_on_stream() const { return key_on_stream_; }
 
   // The workspace for `key`: *planned = true when it already holds key's plan (a hit).  On a miss
-  // a workspace of `bytes` is allocated on the key's device (the least recently used entry is
-  // evicted past kMaxPlans) and the caller plans into it; a miss while the stream is capturing a
-  // graph takes no workspace (*ws = NULL: the ordinary path), as allocation and eviction are not
-  // capturable.
+  // a workspace of `bytes` is allocated on the key's device (past kMaxPlans the least recently
+  // used entry no capture has used is evicted) and the caller plans into it; a miss while the
+  // stream is capturing a graph takes no workspace (*ws = NULL: the ordinary path), as
+  // allocation and eviction are not capturable.  A hit while capturing pins the entry: the graph
+  // holds its pointer and may replay at any later time, so the workspace is never evicted or
+  // freed before Release (the state's end, or ofx_spmm_static_plans(release = 1)).
   int Acquire(const Key& key, size_t bytes, bool capturing, void** ws, bool* planned) {
     std::lock_guard<std::mutex> lock(mu_);
     *ws = nullptr;
@@ -65,6 +66,7 @@ class SpmmCsrPlanState final : public user_op::OpKernelState {
     for (auto it = entries_.begin(); it != entries_.end(); ++it) {
       if (it->key == key && it->bytes >= bytes) {
         entries_.splice(entries_.begin(), entries_, it);  // most recently used first
+        if (capturing) it->pinned = true;
         *ws = it->ws;
         *planned = true;
         ++hits_;
@@ -72,35 +74,40 @@ class SpmmCsrPlanState final : public user_op::OpKernelState {
       }
     }
     if (capturing) return OFX_OK;
-    FreeDropped();
     int rc = OFX_OK;
     if (entries_.size() >= kMaxPlans) {
-      // an in-flight launch may still read the evicted plan: the device drains first
-      rc = WithDevice(entries_.back().key.device, [&]() {
-        const int r = ofx_device_synchronize();
-        return r != OFX_OK ? r : ofx_free(entries_.back().ws);
-      });
-      entries_.pop_back();
-      if (rc != OFX_OK) return rc;
+      // the least recently used unpinned entry (none: the state grows past the cap); an
+      // in-flight launch may still read its plan, so the device drains first
+      auto victim = entries_.end();
+      for (auto it = entries_.begin(); it != entries_.end(); ++it)
+        if (!it->pinned) victim = it;
+      if (victim != entries_.end()) {
+        rc = WithDevice(victim->key.device, [&]() {
+          const int r = ofx_device_synchronize();
+          return r != OFX_OK ? r : ofx_free(victim->ws);
+        });
+        entries_.erase(victim);
+        if (rc != OFX_OK) return rc;
+      }
     }
     void* p = nullptr;
     rc = WithDevice(key.device, [&]() { return ofx_malloc(&p, bytes); });
     if (rc != OFX_OK) return rc;
-    entries_.push_front(Entry{key, p, bytes});
+    entries_.push_front(Entry{key, p, bytes, false});
     *ws = p;
     ++plans_;
     return OFX_OK;
   }
 
-  // Forget key's plan (its launch failed): the next call plans again.  While the stream is
-  // capturing, the device cannot be drained, so the workspace is freed at the next call outside
-  // a capture (or at Release).
+  // Forget key's plan (its launch failed): the next call plans again.  A pinned entry's
+  // workspace (a captured graph holds it) is retired, not freed, until Release; so is one dropped
+  // while the stream captures (the device cannot be drained inside a capture).
   void Drop(const Key& key, bool capturing) {
     std::lock_guard<std::mutex> lock(mu_);
     for (auto it = entries_.begin(); it != entries_.end(); ++it) {
       if (it->key == key) {
-        if (capturing) {
-          dropped_.push_back(*it);
+        if (capturing || it->pinned) {
+          retired_.push_back(*it);
         } else {
           WithDevice(it->key.device, [&]() {
             ofx_device_synchronize();
@@ -120,16 +127,19 @@ class SpmmCsrPlanState final : public user_op::OpKernelState {
     *hits += hits_;
   }
 
+  // Frees every workspace, pinned ones included: the graphs that captured static calls of this
+  // state must be gone (the state's end, or the caller's explicit release).
   void Release() {
     std::lock_guard<std::mutex> lock(mu_);
-    FreeDropped();
-    for (Entry& e : entries_) {
-      WithDevice(e.key.device, [&]() {
-        ofx_device_synchronize();
-        return ofx_free(e.ws);
-      });
+    for (auto* list : {&retired_, &entries_}) {
+      for (Entry& e : *list) {
+        WithDevice(e.key.device, [&]() {
+          ofx_device_synchronize();
+          return ofx_free(e.ws);
+        });
+      }
+      list->clear();
     }
-    entries_.clear();
   }
 
  private:
@@ -137,17 +147,8 @@ class SpmmCsrPlanState final : public user_op::OpKernelState {
     Key key;
     void* ws;
     size_t bytes;
+    bool pinned;  // used by a graph capture: never evicted
   };
-  // workspaces dropped during a capture (mu_ held)
-  void FreeDropped() {
-    for (Entry& e : dropped_) {
-      WithDevice(e.key.device, [&]() {
-        ofx_device_synchronize();
-        return ofx_free(e.ws);
-      });
-    }
-    dropped_.clear();
-  }
   template <typename F>
   static int WithDevice(int device, F&& f) {
     int prev = -1;
@@ -161,7 +162,7 @@ class SpmmCsrPlanState final : public user_op::OpKernelState {
   const bool key_on_stream_;
   std::mutex mu_;
   std::list<Entry> entries_;
-  std::vector<Entry> dropped_;
+  std::list<Entry> retired_;  // dropped but possibly held by a captured graph: freed at Release
   int64_t plans_ = 0, hits_ = 0;
 };
 

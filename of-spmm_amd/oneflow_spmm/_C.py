@@ -176,7 +176,8 @@ _SIG_MEMO: dict = {}
 
 def static_plans(release: bool = False) -> dict:
     """The static-CSR plans the eager op states hold (ofx_spmm_static_plans): live entries,
-    planner launches and calls that reused a plan; release=True frees them first."""
+    planner launches and calls that reused a plan; release=True frees them first -- the plans
+    graph captures used included, so destroy those graphs before releasing."""
     e, p, h = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     check(LIB.ofx_spmm_static_plans(ctypes.byref(e), ctypes.byref(p), ctypes.byref(h),
                                     1 if release else 0), "spmm_static_plans")

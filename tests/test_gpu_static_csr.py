@@ -222,3 +222,40 @@ def test_each_stream_keeps_its_own_plan(device):
     assert counters(s0, _C.static_plans()) == {"plans": 2, "hits": 2}
     for i, o in enumerate(outs):
         assert_bitwise(o.cpu(), ref, f"call {i}")
+
+
+@pytest.mark.graph_capture
+def test_a_captured_plan_outlives_eviction(device):
+    """A graph that captured a static call holds the plan's workspace, so the state pins it: ten
+    other static CSRs afterwards evict only unpinned plans, and the graph still replays exact."""
+    rng = np.random.default_rng(670)
+    m, k, n = 40_000, 40_000, 32
+    rp, ci, v = random_csr(m, k, hub_graph(m, k, rng), rng)
+    b = random_dense(k, n, rng)
+    d = [rp.to(device), ci.to(device), v.to(device)]
+    db = b.to(device)
+    out = torch.empty((m, n), device=device)
+    s = torch.cuda.Stream(device)
+    s.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(s):
+        fs.spmm(*d, m, k, db, out=out, static_csr=21)  # plans, outside the capture
+    torch.cuda.current_stream(device).wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        fs.spmm(*d, m, k, db, out=out, static_csr=21)  # a hit: the entry is pinned
+    others = []
+    for i in range(10):
+        o_rp, o_ci, o_v = random_csr(m, k, hub_graph(m, k, rng, hubs=((i, 2500),)), rng)
+        others.append([o_rp.to(device), o_ci.to(device), o_v.to(device)])
+        fs.spmm(*others[-1], m, k, db, static_csr=300 + i)
+    torch.cuda.synchronize()
+    assert _C.static_plans()["entries"] == 8
+    for i in range(2):
+        b2 = random_dense(k, n, rng)
+        db.copy_(b2.to(device))
+        out.fill_(float("nan"))
+        g.replay()
+        torch.cuda.synchronize()
+        assert_bitwise(out.cpu(), oracle_spmm(rp, ci, v, b2), f"replay {i} after evictions")
+    del g
+    torch.cuda.synchronize()
