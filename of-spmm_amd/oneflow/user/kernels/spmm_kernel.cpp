@@ -51,6 +51,9 @@ class SpmmCsrPlanState final : public user_op::OpKernelState {
   explicit SpmmCsrPlanState(bool key_on_stream) : key_on_stream_(key_on_stream) {}
   ~SpmmCsrPlanState() override { Release(); }
   bool key_on_stream() const { return key_on_stream_; }
+  // Held by a static call from Acquire through its launch's enqueue, so no other thread evicts
+  // (and frees) the workspace in between.
+  std::recursive_mutex& launch_mutex() { return mu_; }
 
   // The workspace for `key`: *planned = true when it already holds key's plan (a hit).  On a miss
   // a workspace of `bytes` is allocated on the key's device (past kMaxPlans the least recently
@@ -60,7 +63,7 @@ class SpmmCsrPlanState final : public user_op::OpKernelState {
   // holds its pointer and may replay at any later time, so the workspace is never evicted or
   // freed before Release (the state's end, or ofx_spmm_static_plans(release = 1)).
   int Acquire(const Key& key, size_t bytes, bool capturing, void** ws, bool* planned) {
-    std::lock_guard<std::mutex> lock(mu_);
+    std::lock_guard<std::recursive_mutex> lock(mu_);
     *ws = nullptr;
     *planned = false;
     for (auto it = entries_.begin(); it != entries_.end(); ++it) {
@@ -103,7 +106,7 @@ class SpmmCsrPlanState final : public user_op::OpKernelState {
   // workspace (a captured graph holds it) is retired, not freed, until Release; so is one dropped
   // while the stream captures (the device cannot be drained inside a capture).
   void Drop(const Key& key, bool capturing) {
-    std::lock_guard<std::mutex> lock(mu_);
+    std::lock_guard<std::recursive_mutex> lock(mu_);
     for (auto it = entries_.begin(); it != entries_.end(); ++it) {
       if (it->key == key) {
         if (capturing || it->pinned) {
@@ -121,7 +124,7 @@ class SpmmCsrPlanState final : public user_op::OpKernelState {
   }
 
   void Stats(int64_t* entries, int64_t* plans, int64_t* hits) {
-    std::lock_guard<std::mutex> lock(mu_);
+    std::lock_guard<std::recursive_mutex> lock(mu_);
     *entries += (int64_t)entries_.size();
     *plans += plans_;
     *hits += hits_;
@@ -130,7 +133,7 @@ class SpmmCsrPlanState final : public user_op::OpKernelState {
   // Frees every workspace, pinned ones included: the graphs that captured static calls of this
   // state must be gone (the state's end, or the caller's explicit release).
   void Release() {
-    std::lock_guard<std::mutex> lock(mu_);
+    std::lock_guard<std::recursive_mutex> lock(mu_);
     for (auto* list : {&retired_, &entries_}) {
       for (Entry& e : *list) {
         WithDevice(e.key.device, [&]() {
@@ -160,7 +163,7 @@ class SpmmCsrPlanState final : public user_op::OpKernelState {
   }
 
   const bool key_on_stream_;
-  std::mutex mu_;
+  std::recursive_mutex mu_;  // held by Acquire / Drop / Release, and by Compute across a launch
   std::list<Entry> entries_;
   std::list<Entry> retired_;  // dropped but possibly held by a captured graph: freed at Release
   int64_t plans_ = 0, hits_ = 0;
@@ -269,7 +272,9 @@ void ComputeSpmmCsr(user_op::KernelComputeContext* ctx, const user_op::OpKernelC
     void* stream = hs->hip_stream();
     SpmmCsrPlanState::Key key{};
     bool keyed = false;
+    std::unique_lock<std::recursive_mutex> hold;
     if (plans != nullptr && static_csr != 0 && row_end > row_begin && n > 0) {
+      hold = std::unique_lock<std::recursive_mutex>(plans->launch_mutex());
       size_t need = 0;
       rc = ofx_spmm_csr_workspace_size(idx_dt, val_dt, m, k, n, nnz, &opts, &need);
       OFX_KERNEL_CHECK(rc == OFX_OK, op_name << " workspace query failed: " << ofx_last_error());
