@@ -41,12 +41,16 @@ def counters(before, after):
     return {k: after[k] - before[k] for k in ("plans", "hits")}
 
 
-@pytest.mark.parametrize("dtype,n", [(torch.float32, 17), (torch.bfloat16, 47),
-                                     (torch.float32, 128), (torch.float64, 16)])
-def test_static_calls_plan_once_and_match_the_oracle(device, dtype, n):
+@pytest.mark.parametrize("dtype,n,idx", [(torch.float32, 17, torch.int32),
+                                         (torch.bfloat16, 47, torch.int32),
+                                         (torch.float32, 128, torch.int32),
+                                         (torch.float64, 16, torch.int32),
+                                         (torch.float16, 64, torch.int32),
+                                         (torch.float32, 32, torch.int64)])
+def test_static_calls_plan_once_and_match_the_oracle(device, dtype, n, idx):
     rng = np.random.default_rng(600 + n)
     m, k = 60_000, 60_000
-    rp, ci, v = random_csr(m, k, hub_graph(m, k, rng), rng)
+    rp, ci, v = random_csr(m, k, hub_graph(m, k, rng), rng, idx_dtype=idx)
     b = random_dense(k, n, rng)
     d = [rp.to(device), ci.to(device), v.to(device, dtype)]
     db = b.to(device, dtype)
