@@ -204,6 +204,7 @@ def test_plans_past_the_cap_evict_the_least_recently_used(device):
     assert_bitwise(out.cpu(), oracle_spmm(rp, ci, v, b), "graph 9 again")
 
 
+@pytest.mark.concurrent_streams
 def test_each_stream_keeps_its_own_plan(device):
     """The hub reduce's arrival counters live in the plan workspace, so an eager static CSR used
     on two streams gets a plan per stream; both streams' results are exact."""
