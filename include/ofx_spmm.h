@@ -581,6 +581,15 @@ int ofx_functional_fused_spmm_csr(void* stream, const ofx_tensor_desc* row_ptr,
                                   int64_t a_num_rows, int64_t a_num_cols, int relu,
                                   ofx_tensor_desc* out, void* tmp, size_t tmp_bytes,
                                   size_t* tmp_size_out);
+/* ofx_functional_fused_spmm_csr with the op's other attributes (attrs == NULL: every default);
+ * static_csr keeps the work-list plan in the eager op's kernel state, as for spmm_csr.          */
+int ofx_functional_fused_spmm_csr_attrs(void* stream, const ofx_tensor_desc* row_ptr,
+                                        const ofx_tensor_desc* col_idx,
+                                        const ofx_tensor_desc* values, const ofx_tensor_desc* b,
+                                        const ofx_tensor_desc* bias, int64_t a_num_rows,
+                                        int64_t a_num_cols, int relu, ofx_tensor_desc* out,
+                                        void* tmp, size_t tmp_bytes, size_t* tmp_size_out,
+                                        const ofx_spmm_attrs* attrs);
 /* Gradient functors (ops "sddmm_csr", "csr_transpose"; oneflow/user/ops/sddmm_op.cpp) through
  * the same op-registry dispatch.  With tmp_size_out != NULL only the tmp-buffer size is
  * computed (nothing runs).  Outputs: sddmm out [nnz] in b's dtype; transpose out_row_ptr [k+1],

@@ -30,6 +30,7 @@ REGISTER_USER_OP("fused_spmm_csr")
     .Attr<int64_t>("a_num_rows", 0)
     .Attr<int64_t>("a_num_cols", 0)
     .Attr<bool>("relu", false)
+    .Attr<int64_t>("static_csr", 0)
     .SetLogicalTensorDescInferFn(FusedSpmmCsrOp::InferLogicalTensorDesc)
     .SetPhysicalTensorDescInferFn(FusedSpmmCsrOp::InferPhysicalTensorDesc)
     .SetGetSbpFn(FusedSpmmCsrOp::GetSbp)

@@ -485,10 +485,14 @@ struct Arg {
 };
 
 Maybe<void> RunUserOp(const std::string& op_name, const std::vector<Arg>& ins,
-                      const std::vector<Arg>& outs, const user_op::AttrMap& attrs, void* stream,
+                      const std::vector<Arg>& outs, const user_op::AttrMap& call_attrs, void* stream,
                       void* tmp, size_t tmp_bytes, size_t* tmp_size_out) {
   const user_op::OpRegistryResult* op = user_op::UserOpRegistryMgr::Get().GetOpRegistryResult(op_name);
   CHECK_OR_RETURN(op != nullptr) << Error::RuntimeError() << "op " << op_name << " is not registered";
+  // the op's attributes: the registered defaults, then this call's values
+  user_op::AttrMap attrs;
+  for (const auto& a : op->attrs) attrs[a.first] = a.second;
+  for (const auto& a : call_attrs) attrs[a.first] = a.second;
   const int device = ins.front().d->device;
   DescMap in;
   for (const Arg& a : ins) {
@@ -543,8 +547,13 @@ Maybe<void> RunUserOp(const std::string& op_name, const std::vector<Arg>& ins,
   ep::Stream* s = device < 0 ? static_cast<ep::Stream*>(&cpu_stream) : static_cast<ep::Stream*>(&hip_stream);
   user_op::KernelComputeContext ctx(s, tensors, attrs, rc.device_type());
   const user_op::OpKernel* kernel = GetKernel(reg);
+  // a static CSR's plan lives in the eager op's kernel state (per registration and device)
+  auto sc = attrs.find("static_csr");
+  user_op::OpKernelState* kstate = nullptr;
+  if (sc != attrs.end() && static_cast<int64_t>(sc->second) != 0)
+    kstate = EagerKernelState(reg, kernel, device, rc.device_type());
   try {
-    kernel->Compute(&ctx, nullptr, nullptr);
+    kernel->Compute(&ctx, kstate, nullptr);
   } catch (const KernelCheckError& e) {
     return Maybe<void>("KernelCheckError", e.msg);
   }
@@ -608,13 +617,35 @@ extern "C" int ofx_functional_fused_spmm_csr(void* stream, const ofx_tensor_desc
                                              int64_t a_num_rows, int64_t a_num_cols, int relu,
                                              ofx_tensor_desc* out, void* tmp, size_t tmp_bytes,
                                              size_t* tmp_size_out) {
+  return ofx_functional_fused_spmm_csr_attrs(stream, row_ptr, col_idx, values, b, bias,
+                                             a_num_rows, a_num_cols, relu, out, tmp, tmp_bytes,
+                                             tmp_size_out, nullptr);
+}
+
+// The same with the op's other attributes (static_csr: the plan kept in the eager op's kernel
+// state, as for spmm_csr).
+extern "C" int ofx_functional_fused_spmm_csr_attrs(
+    void* stream, const ofx_tensor_desc* row_ptr, const ofx_tensor_desc* col_idx,
+    const ofx_tensor_desc* values, const ofx_tensor_desc* b, const ofx_tensor_desc* bias,
+    int64_t a_num_rows, int64_t a_num_cols, int relu, ofx_tensor_desc* out, void* tmp,
+    size_t tmp_bytes, size_t* tmp_size_out, const ofx_spmm_attrs* attrs) {
   return ::ofx::guarded(__func__, [&]() -> int {
+    int64_t static_csr = 0;
+    if (attrs != nullptr) {
+      const char* why = ofx::versioned_struct_problem(attrs, OFX_SPMM_ATTRS_MIN_SIZE);
+      OFX_REQUIRE(why == nullptr, OFX_EINVAL,
+                  "fused_spmm_csr: ofx_spmm_attrs %s (%u bytes): initialise it with "
+                  "OFX_SPMM_ATTRS_INIT", why ? why : "", OFX_SPMM_ATTRS_MIN_SIZE);
+      static_csr = attrs->static_csr;
+    }
+    // an earlier launch's loud failure comes back here as OFX_EPLAN (as for spmm_csr)
+    if (tmp_size_out == nullptr) OFX_TAKE_DEVICE_ERROR("fused_spmm_csr");
     std::vector<Arg> ins = {{"a_csr_row_ptr", row_ptr}, {"a_csr_col_idx", col_idx},
                             {"a_csr_values", values}, {"b", b}};
     if (bias != nullptr) ins.push_back({"bias", bias});
     return ToStatus(RunUserOp("fused_spmm_csr", ins, {{"out", out}},
                               {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols},
-                               {"relu", relu ? 1 : 0}},
+                               {"relu", relu ? 1 : 0}, {"static_csr", static_csr}},
                               stream, tmp, tmp_bytes, tmp_size_out));
   });
 }

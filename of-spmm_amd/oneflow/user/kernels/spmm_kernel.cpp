@@ -361,14 +361,23 @@ class FusedSpmmCsrKernel final : public user_op::OpKernel, public user_op::CudaG
     return CreateSpmmCsrOpKernelCache(ctx);
   }
 
+  // The plans of static CSRs, as spmm_csr's (the fused epilogue does not change the work list).
+  std::shared_ptr<user_op::OpKernelState> CreateOpKernelState(
+      user_op::KernelInitContext* ctx) const override {
+    if (device_type != DeviceType::kHIP) return nullptr;
+    return std::make_shared<SpmmCsrPlanState>(!ctx->has_stream_name_hint());
+  }
+
   bool AlwaysComputeWhenAllOutputsEmpty() const override { return false; }
 
  private:
   using user_op::OpKernel::Compute;
-  void Compute(user_op::KernelComputeContext* ctx, user_op::OpKernelState*,
+  void Compute(user_op::KernelComputeContext* ctx, user_op::OpKernelState* state,
                const user_op::OpKernelCache* cache) const override {
     ComputeSpmmCsr<device_type>(ctx, cache, ctx->Tensor4ArgNameAndIndex("bias", 0),
-                                ctx->Attr<bool>("relu"), "fused_spmm_csr");
+                                ctx->Attr<bool>("relu"), "fused_spmm_csr",
+                                dynamic_cast<SpmmCsrPlanState*>(state),
+                                ctx->Attr<int64_t>("static_csr"));
   }
 };
 

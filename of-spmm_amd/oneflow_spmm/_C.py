@@ -187,9 +187,10 @@ def static_plans(release: bool = False) -> dict:
 def fused_spmm_csr(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor,
                    a_csr_values: torch.Tensor, a_num_rows: int, a_num_cols: int, b: torch.Tensor,
                    bias: torch.Tensor | None = None, *, relu: bool = False,
-                   out: torch.Tensor | None = None) -> torch.Tensor:
+                   out: torch.Tensor | None = None, static_csr: int = 0) -> torch.Tensor:
     """Op "fused_spmm_csr": relu?(A @ b + bias?) in one kernel, the same bits as
-    spmm_csr -> bias_add -> relu run separately."""
+    spmm_csr -> bias_add -> relu run separately.  `static_csr` as for
+    spmm_csr: the plan of an unchanged CSR is kept in the op's kernel state."""
     rp = _prep(a_csr_row_ptr, "a_csr_row_ptr")
     ci = _prep(a_csr_col_idx, "a_csr_col_idx")
     vals = _prep(a_csr_values, "a_csr_values")
@@ -211,9 +212,15 @@ def fused_spmm_csr(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor,
     tmp = None
     if size.value and bb.device.type != "cpu":
         tmp = torch.empty(size.value, dtype=torch.uint8, device=bb.device)
-    check(LIB.ofx_functional_fused_spmm_csr(current_stream_handle(bb), *args,
-                                            tmp.data_ptr() if tmp is not None else None,
-                                            size.value if tmp is not None else 0, None),
+    attrs = None
+    if static_csr:
+        attrs = _lib.SpmmAttrs()
+        attrs.static_csr = int(static_csr)
+        attrs = ctypes.byref(attrs)
+    check(LIB.ofx_functional_fused_spmm_csr_attrs(current_stream_handle(bb), *args,
+                                                  tmp.data_ptr() if tmp is not None else None,
+                                                  size.value if tmp is not None else 0, None,
+                                                  attrs),
           "fused_spmm_csr")
     return out
 

@@ -121,6 +121,8 @@ def _load():
                                     i64, p, i32, popt], i32),
         "ofx_functional_fused_spmm_csr": ([p, pdesc, pdesc, pdesc, pdesc, pdesc, i64, i64, i32, pdesc,
                                            p, sz, ctypes.POINTER(sz)], i32),
+        "ofx_functional_fused_spmm_csr_attrs": ([p, pdesc, pdesc, pdesc, pdesc, pdesc, i64, i64, i32,
+                                                 pdesc, p, sz, ctypes.POINTER(sz), pattrs], i32),
         "ofx_csr_validate": ([p, i32, i64, i64, i64, p, p, p], i32),
         "ofx_spmm_csr_cpu": ([i32, i32, i32, i64, i64, i64, i64, p, p, p, p, i64, p, i64, i64, i64,
                               popt], i32),

@@ -164,8 +164,9 @@ class FusedSpmmCsrFunction(torch.autograd.Function):
     spmm_csr gradients."""
 
     @staticmethod
-    def forward(ctx, row_ptr, col_idx, values, m, k, b, bias, relu):
-        out = _C.fused_spmm_csr(row_ptr, col_idx, values, m, k, b, bias, relu=relu)
+    def forward(ctx, row_ptr, col_idx, values, m, k, b, bias, relu, static_csr=0):
+        out = _C.fused_spmm_csr(row_ptr, col_idx, values, m, k, b, bias, relu=relu,
+                                static_csr=static_csr)
         ctx.save_for_backward(row_ptr, col_idx, values, b, out if relu else None)
         ctx.m, ctx.k, ctx.relu, ctx.has_bias = m, k, relu, bias is not None
         return out
@@ -181,21 +182,23 @@ class FusedSpmmCsrFunction(torch.autograd.Function):
             d_values = sddmm(row_ptr, col_idx, g, b)
         if ctx.needs_input_grad[5]:
             d_b = TRANSPOSE_CACHE.grad_b(row_ptr, col_idx, values.detach(), ctx.m, ctx.k, g)
-        return None, None, d_values, None, None, d_b, d_bias, None
+        return None, None, d_values, None, None, d_b, d_bias, None, None
 
 
 def fused_spmm(a_csr_row_ptr, a_csr_col_idx, a_csr_values, a_num_rows, a_num_cols, b, bias=None,
-               *, relu=False, out=None):
-    """A GCN layer's aggregation + bias + activation: relu?(A @ b + bias?) with autograd."""
+               *, relu=False, out=None, static_csr=0):
+    """A GCN layer's aggregation + bias + activation: relu?(A @ b + bias?) with autograd.
+    `static_csr` as for `spmm`: the forward plans an unchanged CSR once."""
     needs = (a_csr_values.requires_grad or b.requires_grad or
              (bias is not None and bias.requires_grad))
     if torch.is_grad_enabled() and needs:
         if out is not None:
             raise RuntimeError("fused_spmm: out= is not supported when gradients are required")
         return FusedSpmmCsrFunction.apply(a_csr_row_ptr, a_csr_col_idx, a_csr_values,
-                                          int(a_num_rows), int(a_num_cols), b, bias, bool(relu))
+                                          int(a_num_rows), int(a_num_cols), b, bias, bool(relu),
+                                          int(static_csr))
     return _C.fused_spmm_csr(a_csr_row_ptr, a_csr_col_idx, a_csr_values, a_num_rows, a_num_cols, b,
-                             bias, relu=relu, out=out)
+                             bias, relu=relu, out=out, static_csr=int(static_csr))
 
 
 __all__ = ["csr_transpose", "gather_values", "sddmm", "SpmmCsrFunction", "spmm", "TRANSPOSE_CACHE", "ops",

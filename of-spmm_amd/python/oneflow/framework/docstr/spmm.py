@@ -59,9 +59,10 @@ add_docstr(
 add_docstr(
     oneflow._C.fused_spmm_csr,
     r"""
-    fused_spmm_csr(a_csr_row_ptr, a_csr_col_idx, a_csr_values, a_num_rows, a_num_cols, b, bias=None, relu=False) -> Tensor
+    fused_spmm_csr(a_csr_row_ptr, a_csr_col_idx, a_csr_values, a_num_rows, a_num_cols, b, bias=None, relu=False, static_csr=0) -> Tensor
 
     ``relu(spmm(...) + bias)`` in one kernel, with the bits of the three ops run separately
-    (spmm, then bias_add over dim 1, then relu). ``bias`` has shape ``[N]``.
+    (spmm, then bias_add over dim 1, then relu). ``bias`` has shape ``[N]``. ``static_csr`` as
+    for ``oneflow.spmm``: a non-zero value keeps the plan of an unchanged CSR across calls.
     """,
 )

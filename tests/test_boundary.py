@@ -226,3 +226,8 @@ def test_static_csr_is_a_registered_attr_with_default_zero():
     assert re.search(r'DefaultValuedAttr<SI64Attr, "0">:\$static_csr', td)
     yaml = open(os.path.join(root, "oneflow/core/functional/spmm_functional_api.yaml")).read()
     assert "Int64 static_csr=0) => SpmmCsr" in yaml
+    # the fused op carries it too (its kernel keeps plans the same way)
+    fused_block = gen.split('REGISTER_USER_OP("fused_spmm_csr")')[1].split("REGISTER_USER_OP")[0]
+    assert '.Attr<int64_t>("static_csr", 0)' in fused_block
+    assert "Int64 static_csr=0) => FusedSpmmCsr" in yaml
+    assert td.count('DefaultValuedAttr<SI64Attr, "0">:$static_csr') == 2

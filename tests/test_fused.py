@@ -49,6 +49,20 @@ def test_fused_without_epilogue_is_spmm():
                        fs.spmm(rp, ci, v, 50, 40, b).view(torch.int32))
 
 
+def test_cpu_fused_static_csr_is_accepted_and_exact():
+    """The kCPU kernel has no work list: static_csr changes nothing but must be accepted, through
+    the op (_C) and its autograd binding."""
+    rp, ci, v, b, bias = _problem(13, 90, 70, 24, "f32")
+    ref = _ref(rp, ci, v, b, bias, True, "f32")
+    assert_bitwise(_C.fused_spmm_csr(rp, ci, v, 90, 70, b, bias, relu=True, static_csr=3), ref,
+                   "cpu fused static")
+    bb = b.clone().requires_grad_(True)
+    y = fs.fused_spmm(rp, ci, v, 90, 70, bb, bias, relu=True, static_csr=3)
+    assert_bitwise(y.detach(), ref, "cpu fused static (autograd)")
+    y.sum().backward()
+    assert bb.grad is not None and torch.isfinite(bb.grad).all()
+
+
 def test_oracle_bias_act_by_hand():
     c = np.array([[1.5, -0.0, -2.0, 0.25]], dtype=np.float32)
     bias = np.array([-1.5, 0.0, 1.0, -1.0], dtype=np.float32)
@@ -117,6 +131,27 @@ def test_gpu_fused_hub_rows_and_strided_out(device, idx):
     torch.cuda.synchronize()
     assert_bitwise(out, _ref(rp, ci, v, b, bias, True, "f32"), "hub rows fused")
     assert torch.isnan(big[:, :4]).all() and torch.isnan(big[:, 4 + n:]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_gpu_fused_static_csr_plans_once(device, dtype):
+    """static_csr on the fused op: its kernel state plans the CSR once (hub rows: a real work
+    list), later calls reuse the plan, and every call keeps the composition's bits."""
+    m, k, n = 20_000, 20_000, 64
+    rp, ci, v, b, bias = _problem(24, m, k, n, dtype, hubs=True)
+    ref = _ref(rp, ci, v, b, bias, True, dtype)
+    d = [rp.to(device), ci.to(device), v.to(device)]
+    db, dbias = b.to(device), bias.to(device)
+    _C.static_plans(release=True)
+    s0 = _C.static_plans()
+    outs = [_C.fused_spmm_csr(*d, m, k, db, dbias, relu=True, static_csr=5) for _ in range(3)]
+    torch.cuda.synchronize()
+    s1 = _C.static_plans()
+    assert (s1["plans"] - s0["plans"], s1["hits"] - s0["hits"]) == (1, 2), (s0, s1)
+    for i, o in enumerate(outs):
+        assert_bitwise(o, ref, f"fused static call {i}")
+    _C.static_plans(release=True)
 
 
 @pytest.mark.gpu
