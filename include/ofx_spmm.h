@@ -612,6 +612,16 @@ int ofx_functional_spmm_csr_gathered(void* stream, const ofx_tensor_desc* row_pt
                                      const ofx_tensor_desc* values_perm, const ofx_tensor_desc* b,
                                      int64_t a_num_rows, int64_t a_num_cols, ofx_tensor_desc* out,
                                      void* tmp, size_t tmp_bytes, size_t* tmp_size_out);
+/* ofx_functional_spmm_csr_gathered with the op's other attributes (attrs == NULL: defaults):
+ * static_csr keeps the plan of an unchanged A^T in the eager op's kernel state.               */
+int ofx_functional_spmm_csr_gathered_attrs(void* stream, const ofx_tensor_desc* row_ptr,
+                                           const ofx_tensor_desc* col_idx,
+                                           const ofx_tensor_desc* values,
+                                           const ofx_tensor_desc* values_perm,
+                                           const ofx_tensor_desc* b, int64_t a_num_rows,
+                                           int64_t a_num_cols, ofx_tensor_desc* out, void* tmp,
+                                           size_t tmp_bytes, size_t* tmp_size_out,
+                                           const ofx_spmm_attrs* attrs);
 /* The op's registered SBP signatures and no-grad inputs, as text (tests / introspection). */
 int ofx_op_spmm_csr_sbp_signatures(char* buf, size_t len);
 /* Same for any registered op; optional_inputs = comma-separated optional inputs present.   */

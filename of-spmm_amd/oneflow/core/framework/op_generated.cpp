@@ -59,6 +59,7 @@ REGISTER_USER_OP("spmm_csr_gathered")
     .Output("out")
     .Attr<int64_t>("a_num_rows", 0)
     .Attr<int64_t>("a_num_cols", 0)
+    .Attr<int64_t>("static_csr", 0)
     .SetLogicalTensorDescInferFn(SpmmCsrGatheredOp::InferLogicalTensorDesc)
     .SetPhysicalTensorDescInferFn(SpmmCsrGatheredOp::InferPhysicalTensorDesc)
     .SetGetSbpFn(SpmmCsrGatheredOp::GetSbp)

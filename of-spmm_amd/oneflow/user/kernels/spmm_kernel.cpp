@@ -225,6 +225,49 @@ ofx_spmm_options OptionsOf(const SpmmCsrOpKernelCache* cache) {
 
 int DtCode(DataType dt) { return static_cast<int>(dt); }
 
+// A static call on the HIP kernel (attr static_csr != 0): the workspace of `plans` that holds
+// this launch's plan -- built here on a miss -- replaces the tmp buffer, and opts->planned is
+// set.  sp->hold keeps the state's lock until the launch is enqueued (the caller's scope);
+// sp->keyed says a plan is in use (the caller drops it if the launch fails).  A miss while the
+// stream captures keeps the ordinary path (the tmp buffer, planned = 0).
+struct StaticPlan {
+  SpmmCsrPlanState::Key key{};
+  bool keyed = false;
+  std::unique_lock<std::recursive_mutex> hold;
+};
+
+void UseStaticPlan(SpmmCsrPlanState* plans, int64_t static_csr, ep::HipStream* hs,
+                   const void* row_ptr, int idx_dt, int val_dt, int64_t m, int64_t k, int64_t n,
+                   int64_t nnz, int64_t row_begin, int64_t row_end, const char* op_name,
+                   ofx_spmm_options* opts, void** ws, size_t* ws_bytes, StaticPlan* sp) {
+  if (row_end <= row_begin || n <= 0) return;
+  sp->hold = std::unique_lock<std::recursive_mutex>(plans->launch_mutex());
+  size_t need = 0;
+  int rc = ofx_spmm_csr_workspace_size(idx_dt, val_dt, m, k, n, nnz, opts, &need);
+  OFX_KERNEL_CHECK(rc == OFX_OK, op_name << " workspace query failed: " << ofx_last_error());
+  if (need == 0) return;  // no work list to keep (the small form, or the identity order)
+  void* stream = hs->hip_stream();
+  sp->key = SpmmCsrPlanState::Key{static_csr, row_ptr, plans->key_on_stream() ? stream : nullptr,
+                                  hs->device_index(), idx_dt, val_dt, m, k, n, nnz, row_begin,
+                                  row_end, opts->split_threshold, opts->chunk,
+                                  opts->heavy_threshold, opts->range_nnz};
+  void* sws = nullptr;
+  bool planned = false;
+  rc = plans->Acquire(sp->key, need, hs->IsGraphCapturing(), &sws, &planned);
+  OFX_KERNEL_CHECK(rc == OFX_OK, op_name << " static_csr plan workspace: " << ofx_last_error());
+  if (sws == nullptr) return;
+  sp->keyed = true;
+  if (!planned) {
+    rc = ofx_spmm_csr_plan(stream, idx_dt, val_dt, m, k, n, nnz, row_ptr, row_begin, row_end, sws,
+                           need, opts);
+    if (rc != OFX_OK) plans->Drop(sp->key, hs->IsGraphCapturing());
+    OFX_KERNEL_CHECK(rc == OFX_OK, op_name << " kernel failed (" << rc << "): " << ofx_last_error());
+  }
+  opts->planned = 1;
+  *ws = sws;
+  *ws_bytes = need;
+}
+
 // Shared body of "spmm_csr" and "fused_spmm_csr": bias (optional T[N]) and relu are the fused
 // epilogue; the plain op passes none (ofx_spmm_csr_fused with NULL/none == ofx_spmm_csr).
 template <DeviceType device_type>
@@ -270,46 +313,16 @@ void ComputeSpmmCsr(user_op::KernelComputeContext* ctx, const user_op::OpKernelC
     size_t ws_bytes = tmp ? (size_t)tmp->shape_view().elem_cnt() : 0;
     ep::HipStream* hs = ctx->stream()->As<ep::HipStream>();
     void* stream = hs->hip_stream();
-    SpmmCsrPlanState::Key key{};
-    bool keyed = false;
-    std::unique_lock<std::recursive_mutex> hold;
-    if (plans != nullptr && static_csr != 0 && row_end > row_begin && n > 0) {
-      hold = std::unique_lock<std::recursive_mutex>(plans->launch_mutex());
-      size_t need = 0;
-      rc = ofx_spmm_csr_workspace_size(idx_dt, val_dt, m, k, n, nnz, &opts, &need);
-      OFX_KERNEL_CHECK(rc == OFX_OK, op_name << " workspace query failed: " << ofx_last_error());
-      if (need > 0) {  // a launch that plans at all (the small form needs no work list)
-        key = SpmmCsrPlanState::Key{static_csr, row_ptr->dptr(),
-                                    plans->key_on_stream() ? stream : nullptr, hs->device_index(),
-                                    idx_dt, val_dt, m, k, n, nnz, row_begin, row_end,
-                                    opts.split_threshold, opts.chunk, opts.heavy_threshold,
-                                    opts.range_nnz};
-        void* sws = nullptr;
-        bool planned = false;
-        rc = plans->Acquire(key, need, hs->IsGraphCapturing(), &sws, &planned);
-        OFX_KERNEL_CHECK(rc == OFX_OK,
-                         op_name << " static_csr plan workspace: " << ofx_last_error());
-        if (sws != nullptr) {
-          keyed = true;
-          if (!planned) {
-            rc = ofx_spmm_csr_plan(stream, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
-                                   row_begin, row_end, sws, need, &opts);
-            if (rc != OFX_OK) plans->Drop(key, hs->IsGraphCapturing());
-            OFX_KERNEL_CHECK(rc == OFX_OK, op_name << " kernel failed (" << rc
-                                                   << "): " << ofx_last_error());
-          }
-          opts.planned = 1;
-          ws = sws;
-          ws_bytes = need;
-        }
-      }
-    }
+    StaticPlan sp;
+    if (plans != nullptr && static_csr != 0)
+      UseStaticPlan(plans, static_csr, hs, row_ptr->dptr(), idx_dt, val_dt, m, k, n, nnz,
+                    row_begin, row_end, op_name, &opts, &ws, &ws_bytes, &sp);
     rc = ofx_spmm_csr_fused(stream, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
                             col_idx->dptr(), values->dptr(), b->dptr(), b->row_stride(),
                             out->mut_dptr(), out->row_stride(), row_begin, row_end, bias_ptr, act,
                             ws, ws_bytes, &opts);
     // an earlier launch's loud failure (OFX_EPLAN) may have been this key's plan: plan again
-    if (rc != OFX_OK && keyed) plans->Drop(key, hs->IsGraphCapturing());
+    if (rc != OFX_OK && sp.keyed) plans->Drop(sp.key, hs->IsGraphCapturing());
   } else {
     const int threads = ctx->stream()->As<ep::CpuStream>()->num_threads();
     rc = ofx_spmm_csr_fused_cpu(threads, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
@@ -396,11 +409,18 @@ class SpmmCsrGatheredKernel final : public user_op::OpKernel, public user_op::Cu
     return CreateSpmmCsrOpKernelCache(ctx);
   }
 
+  // The plans of static CSRs (the autograd's cached A^T: static while its cache entry lives).
+  std::shared_ptr<user_op::OpKernelState> CreateOpKernelState(
+      user_op::KernelInitContext* ctx) const override {
+    if (device_type != DeviceType::kHIP) return nullptr;
+    return std::make_shared<SpmmCsrPlanState>(!ctx->has_stream_name_hint());
+  }
+
   bool AlwaysComputeWhenAllOutputsEmpty() const override { return false; }
 
  private:
   using user_op::OpKernel::Compute;
-  void Compute(user_op::KernelComputeContext* ctx, user_op::OpKernelState*,
+  void Compute(user_op::KernelComputeContext* ctx, user_op::OpKernelState* state,
                const user_op::OpKernelCache* cache) const override {
     const user_op::Tensor* row_ptr = ctx->Tensor4ArgNameAndIndex("a_csr_row_ptr", 0);
     const user_op::Tensor* col_idx = ctx->Tensor4ArgNameAndIndex("a_csr_col_idx", 0);
@@ -420,21 +440,28 @@ class SpmmCsrGatheredKernel final : public user_op::OpKernel, public user_op::Cu
       row_begin = range->lower();
       row_end = range->upper();
     }
-    const ofx_spmm_options opts = OptionsOf(range);
+    ofx_spmm_options opts = OptionsOf(range);
     OFX_KERNEL_CHECK(out->shape_view().At(0) == row_end - row_begin,
                      "out rows " << out->shape_view().At(0) << " != row range "
                                  << row_end - row_begin);
     const int idx_dt = DtCode(row_ptr->data_type());
     const int val_dt = DtCode(values->data_type());
     void* ws = tmp ? tmp->mut_dptr() : nullptr;
-    const size_t ws_bytes = tmp ? (size_t)tmp->shape_view().elem_cnt() : 0;
+    size_t ws_bytes = tmp ? (size_t)tmp->shape_view().elem_cnt() : 0;
     int rc;
     if (device_type == DeviceType::kHIP) {
-      void* stream = ctx->stream()->As<ep::HipStream>()->hip_stream();
-      rc = ofx_spmm_csr_gathered(stream, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
+      ep::HipStream* hs = ctx->stream()->As<ep::HipStream>();
+      auto* plans = dynamic_cast<SpmmCsrPlanState*>(state);
+      const int64_t static_csr = ctx->Attr<int64_t>("static_csr");
+      StaticPlan sp;
+      if (plans != nullptr && static_csr != 0)
+        UseStaticPlan(plans, static_csr, hs, row_ptr->dptr(), idx_dt, val_dt, m, k, n, nnz,
+                      row_begin, row_end, "spmm_csr_gathered", &opts, &ws, &ws_bytes, &sp);
+      rc = ofx_spmm_csr_gathered(hs->hip_stream(), idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
                                  col_idx->dptr(), values->dptr(), perm->dptr(), b->dptr(),
                                  b->row_stride(), out->mut_dptr(), out->row_stride(), row_begin,
                                  row_end, ws, ws_bytes, &opts);
+      if (rc != OFX_OK && sp.keyed) plans->Drop(sp.key, hs->IsGraphCapturing());
     } else {
       const size_t vbytes = (size_t)nnz * (size_t)GetSizeOfDataType(values->data_type());
       OFX_KERNEL_CHECK(nnz == 0 || ws_bytes >= vbytes, "tmp buffer smaller than the values");

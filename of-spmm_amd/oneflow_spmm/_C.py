@@ -225,18 +225,20 @@ def fused_spmm_csr(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor,
     return out
 
 
-def _run_grad_op(fn, stream_of, ins, outs, extra):
-    """Two-phase call of a functional gradient entry: tmp size, then the run."""
+def _run_grad_op(fn, stream_of, ins, outs, extra, attrs=()):
+    """Two-phase call of a functional gradient entry: tmp size, then the run.  `attrs`: trailing
+    arguments of an `_attrs` entry (an ofx_spmm_attrs pointer)."""
     size = ctypes.c_size_t(0)
     descs_in = [ctypes.byref(desc(t)) for t in ins]
     descs_out = [ctypes.byref(desc(t)) for t in outs]
-    check(fn(None, *descs_in, *extra, *descs_out, None, 0, ctypes.byref(size)), fn.__name__)
+    check(fn(None, *descs_in, *extra, *descs_out, None, 0, ctypes.byref(size), *attrs),
+          fn.__name__)
     tmp = None
     if size.value:  # the op's tmp_buffer, on the op's device (host memory for kCPU kernels)
         tmp = torch.empty(size.value, dtype=torch.uint8, device=stream_of.device)
     check(fn(current_stream_handle(stream_of), *descs_in, *extra, *descs_out,
              tmp.data_ptr() if tmp is not None else None, size.value if tmp is not None else 0,
-             None), fn.__name__)
+             None, *attrs), fn.__name__)
 
 
 def sddmm_csr(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor, a: torch.Tensor,
@@ -257,9 +259,11 @@ def sddmm_csr(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor, a: torch
 
 def spmm_csr_gathered(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor,
                       a_csr_values: torch.Tensor, values_perm: torch.Tensor, a_num_rows: int,
-                      a_num_cols: int, b: torch.Tensor, *, out: torch.Tensor | None = None):
+                      a_num_cols: int, b: torch.Tensor, *, out: torch.Tensor | None = None,
+                      static_csr: int = 0):
     """Op "spmm_csr_gathered": A @ b with nonzero j's value a_csr_values[values_perm[j]] (the
-    d(b) gradient of spmm_csr with learnable values: A^T's structure, A's values, A^T's perm)."""
+    d(b) gradient of spmm_csr with learnable values: A^T's structure, A's values, A^T's perm).
+    `static_csr` as for spmm_csr (the autograd's cached A^T passes its entry's value)."""
     rp, ci = _prep(a_csr_row_ptr, "a_csr_row_ptr"), _prep(a_csr_col_idx, "a_csr_col_idx")
     vals, perm = _prep(a_csr_values, "a_csr_values"), _prep(values_perm, "values_perm")
     bb = _prep(b, "b", matrix=True)
@@ -268,8 +272,14 @@ def spmm_csr_gathered(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor,
                           device=bb.device)
     if out.numel() == 0:
         return out
-    _run_grad_op(LIB.ofx_functional_spmm_csr_gathered, bb, [rp, ci, vals, perm, bb], [out],
-                 [int(a_num_rows), int(a_num_cols)])
+    if static_csr:
+        attrs = _lib.SpmmAttrs()
+        attrs.static_csr = int(static_csr)
+        _run_grad_op(LIB.ofx_functional_spmm_csr_gathered_attrs, bb, [rp, ci, vals, perm, bb],
+                     [out], [int(a_num_rows), int(a_num_cols)], (ctypes.byref(attrs),))
+    else:
+        _run_grad_op(LIB.ofx_functional_spmm_csr_gathered, bb, [rp, ci, vals, perm, bb], [out],
+                     [int(a_num_rows), int(a_num_cols)])
     return out
 
 

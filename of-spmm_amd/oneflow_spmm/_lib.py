@@ -212,6 +212,8 @@ def _load():
                                       ctypes.POINTER(sz)], i32),
         "ofx_functional_spmm_csr_gathered": ([p, pdesc, pdesc, pdesc, pdesc, pdesc, i64, i64, pdesc,
                                               p, sz, ctypes.POINTER(sz)], i32),
+        "ofx_functional_spmm_csr_gathered_attrs": ([p, pdesc, pdesc, pdesc, pdesc, pdesc, i64, i64,
+                                                    pdesc, p, sz, ctypes.POINTER(sz), pattrs], i32),
         "ofx_functional_csr_transpose": ([p, pdesc, pdesc, i64, i64, pdesc, pdesc, pdesc, p, sz,
                                           ctypes.POINTER(sz)], i32),
         "ofx_op_spmm_csr_sbp_signatures": ([ctypes.c_char_p, sz], i32),

@@ -113,7 +113,9 @@ class _TransposeCache:
             self.seen[key] = values  # holds values: its storage cannot be reused under the key
             while len(self.seen) > self.capacity:
                 self.seen.popitem(last=False)
-            return _C.spmm_csr_gathered(rp_t, ci_t, values, perm, k, m, d_out)
+            # the cached A^T's structure is static while its entry lives: its plan is kept too
+            return _C.spmm_csr_gathered(rp_t, ci_t, values, perm, k, m, d_out,
+                                        static_csr=self.static_id(rp_t))
         _, _, vals_t = self.values_t(row_ptr, col_idx, values, k)
         # the cached A^T: its plan is kept across steps (static_csr, a value unique to the entry)
         return spmm_csr(rp_t, ci_t, vals_t, k, m, d_out, static_csr=self.static_id(rp_t))

@@ -226,8 +226,11 @@ def test_static_csr_is_a_registered_attr_with_default_zero():
     assert re.search(r'DefaultValuedAttr<SI64Attr, "0">:\$static_csr', td)
     yaml = open(os.path.join(root, "oneflow/core/functional/spmm_functional_api.yaml")).read()
     assert "Int64 static_csr=0) => SpmmCsr" in yaml
-    # the fused op carries it too (its kernel keeps plans the same way)
+    # the fused op and the gathered d(b) op carry it too (their kernels keep plans the same way)
     fused_block = gen.split('REGISTER_USER_OP("fused_spmm_csr")')[1].split("REGISTER_USER_OP")[0]
     assert '.Attr<int64_t>("static_csr", 0)' in fused_block
     assert "Int64 static_csr=0) => FusedSpmmCsr" in yaml
-    assert td.count('DefaultValuedAttr<SI64Attr, "0">:$static_csr') == 2
+    gathered_block = gen.split('REGISTER_USER_OP("spmm_csr_gathered")')[1].split("REGISTER_USER_OP")[0]
+    assert '.Attr<int64_t>("static_csr", 0)' in gathered_block
+    assert "Int64 static_csr=0) => SpmmCsrGathered" in yaml
+    assert td.count('DefaultValuedAttr<SI64Attr, "0">:$static_csr') == 3

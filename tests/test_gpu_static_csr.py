@@ -264,3 +264,35 @@ def test_a_captured_plan_outlives_eviction(device):
         assert_bitwise(out.cpu(), oracle_spmm(rp, ci, v, b2), f"replay {i} after evictions")
     del g
     torch.cuda.synchronize()
+
+
+def test_autograd_learnable_values_reuse_the_transpose_plan(device):
+    """Learnable edge weights (new values every step) take the gathered d(b) op over the cached
+    A^T; its plan is kept across steps like the constant-values path's, and d(b) stays exact."""
+    rng = np.random.default_rng(680)
+    m, k, n = 30_000, 20_000, 32
+    rp, ci, _ = random_csr(m, k, power_law_degrees(m, 600_000, k, rng), rng)
+    d_rp, d_ci = rp.to(device), ci.to(device)
+    fs.autograd.TRANSPOSE_CACHE.__init__()
+    keep, grads, s0 = [], [], None
+    for step in range(4):
+        v = torch.from_numpy(rng.uniform(-1, 1, ci.numel()).astype(np.float32))
+        dv = v.to(device).requires_grad_(True)  # new values each step: the gathered op
+        keep.append(dv)  # distinct storage per step
+        db = random_dense(k, n, rng).to(device).requires_grad_(True)
+        out = fs.spmm(d_rp, d_ci, dv, m, k, db)
+        g = random_dense(m, n, rng)
+        out.backward(g.to(device))
+        torch.cuda.synchronize()
+        grads.append((v, g, db.grad.cpu()))
+        if step == 0:
+            s0 = _C.static_plans()  # step 0 built A^T and the gathered op's plan
+    st = counters(s0, _C.static_plans())
+    assert st["plans"] == 0 and st["hits"] == 3, st
+    import scipy.sparse as sp
+    for v, g, gb in grads:
+        at = sp.csr_matrix((v.numpy(), ci.numpy(), rp.numpy()), shape=(m, k)).T.tocsr()
+        at.sort_indices()
+        assert_bitwise(gb, oracle_spmm(torch.from_numpy(at.indptr.astype(np.int32)),
+                                       torch.from_numpy(at.indices.astype(np.int32)),
+                                       torch.from_numpy(at.data.astype(np.float32)), g), "d(b)")
