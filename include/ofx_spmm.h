@@ -276,6 +276,17 @@ int ofx_sddmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t
                   int64_t nnz, const void* row_ptr, const void* col_idx, const void* a,
                   int64_t lda, const void* b, int64_t ldb, void* out, int64_t row_begin,
                   int64_t row_end, void* workspace, size_t workspace_bytes);
+/* ofx_sddmm_csr with options (NULL: defaults); only `planned` is read: the workspace already
+ * holds the plan ofx_sddmm_csr_plan built for this row_ptr (contents unchanged), row range and
+ * n, so the launch skips the planner kernel (the static-CSR path of op "sddmm_csr").          */
+int ofx_sddmm_csr_ex(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k, int64_t n,
+                     int64_t nnz, const void* row_ptr, const void* col_idx, const void* a,
+                     int64_t lda, const void* b, int64_t ldb, void* out, int64_t row_begin,
+                     int64_t row_end, void* workspace, size_t workspace_bytes,
+                     const ofx_spmm_options* opts);
+int ofx_sddmm_csr_plan(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t n,
+                       int64_t nnz, const void* row_ptr, int64_t row_begin, int64_t row_end,
+                       void* workspace, size_t workspace_bytes);
 int ofx_sddmm_csr_cpu(int num_threads, int idx_dtype, int val_dtype, int64_t m, int64_t k,
                       int64_t n, int64_t nnz, const void* row_ptr, const void* col_idx,
                       const void* a, int64_t lda, const void* b, int64_t ldb, void* out,
@@ -599,6 +610,14 @@ int ofx_functional_sddmm_csr(void* stream, const ofx_tensor_desc* row_ptr,
                              const ofx_tensor_desc* b, int64_t a_num_rows, int64_t a_num_cols,
                              ofx_tensor_desc* out, void* tmp, size_t tmp_bytes,
                              size_t* tmp_size_out);
+/* ofx_functional_sddmm_csr with the op's other attributes (attrs == NULL: defaults): static_csr
+ * keeps the SDDMM's plan of an unchanged CSR in the eager op's kernel state.                  */
+int ofx_functional_sddmm_csr_attrs(void* stream, const ofx_tensor_desc* row_ptr,
+                                   const ofx_tensor_desc* col_idx, const ofx_tensor_desc* a,
+                                   const ofx_tensor_desc* b, int64_t a_num_rows,
+                                   int64_t a_num_cols, ofx_tensor_desc* out, void* tmp,
+                                   size_t tmp_bytes, size_t* tmp_size_out,
+                                   const ofx_spmm_attrs* attrs);
 int ofx_functional_csr_transpose(void* stream, const ofx_tensor_desc* row_ptr,
                                  const ofx_tensor_desc* col_idx, int64_t a_num_rows,
                                  int64_t a_num_cols, ofx_tensor_desc* out_row_ptr,

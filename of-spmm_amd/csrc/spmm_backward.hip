@@ -415,6 +415,7 @@ struct SddmmArgs {
   int64_t ldc, ldb, row_begin, nrows, n, nnz, k;
   void* ws;
   size_t ws_bytes;
+  bool planned;  // ws already holds this launch's plan (ofx_sddmm_csr_plan): no planner launch
 };
 
 // Work layout only: every dv[j] is its own dot product, so how rows are cut into items never
@@ -451,9 +452,13 @@ int sddmm_cfg(const SddmmArgs& a) {
   if (w.total > 0) {
     OFX_REQUIRE(a.ws && a.ws_bytes >= w.total, OFX_EWORKSPACE,
                 "sddmm_csr: workspace of %zu bytes < %zu required", a.ws_bytes, w.total);
-    const int rc = plan::launch_plan<I>(a.s, static_cast<const I*>(a.rp), a.row_begin, a.nrows,
-                                        a.nnz, sched, w, static_cast<char*>(a.ws), &wl);
-    if (rc) return rc;
+    if (a.planned) {
+      plan::worklist_of(w, static_cast<char*>(a.ws), &wl);
+    } else {
+      const int rc = plan::launch_plan<I>(a.s, static_cast<const I*>(a.rp), a.row_begin, a.nrows,
+                                          a.nnz, sched, w, static_cast<char*>(a.ws), &wl);
+      if (rc) return rc;
+    }
   }
   const int64_t work = a.nrows + (w.total > 0 ? w.max_chunks : 0);
   const int64_t grid = (work + GPB - 1) / GPB;
@@ -493,9 +498,13 @@ int sddmm_aligned(const SddmmArgs& a) {
   if (w.total > 0) {
     OFX_REQUIRE(a.ws && a.ws_bytes >= w.total, OFX_EWORKSPACE,
                 "sddmm_csr: workspace of %zu bytes < %zu required", a.ws_bytes, w.total);
-    const int rc = plan::launch_plan<I>(a.s, static_cast<const I*>(a.rp), a.row_begin, a.nrows,
-                                        a.nnz, sched, w, static_cast<char*>(a.ws), &wl);
-    if (rc) return rc;
+    if (a.planned) {
+      plan::worklist_of(w, static_cast<char*>(a.ws), &wl);
+    } else {
+      const int rc = plan::launch_plan<I>(a.s, static_cast<const I*>(a.rp), a.row_begin, a.nrows,
+                                          a.nnz, sched, w, static_cast<char*>(a.ws), &wl);
+      if (rc) return rc;
+    }
   }
   const int64_t work = a.nrows + (w.total > 0 ? w.max_chunks : 0);
   const int64_t grid = (work + kBlock / 64 - 1) / (kBlock / 64);
@@ -621,8 +630,20 @@ extern "C" int ofx_sddmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t
                              const void* a, int64_t lda, const void* b, int64_t ldb, void* out,
                              int64_t row_begin, int64_t row_end, void* workspace,
                              size_t workspace_bytes) {
+  return ofx_sddmm_csr_ex(stream, idx_dtype, val_dtype, m, k, n, nnz, row_ptr, col_idx, a, lda, b,
+                          ldb, out, row_begin, row_end, workspace, workspace_bytes, nullptr);
+}
+
+// ofx_sddmm_csr with options: only `planned` is read (the workspace holds the plan
+// ofx_sddmm_csr_plan built for this row_ptr, row range and n; the launch skips the planner).
+extern "C" int ofx_sddmm_csr_ex(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t k,
+                                int64_t n, int64_t nnz, const void* row_ptr, const void* col_idx,
+                                const void* a, int64_t lda, const void* b, int64_t ldb, void* out,
+                                int64_t row_begin, int64_t row_end, void* workspace,
+                                size_t workspace_bytes, const ofx_spmm_options* opts) {
   return ::ofx::guarded(__func__, [&]() -> int {
     OFX_TAKE_DEVICE_ERROR("sddmm_csr");  // an earlier launch's loud failure (spmm_plan.h)
+    OFX_READ_OPTIONS(opts, "sddmm_csr");  // NULL: every default (planned = 0)
     OFX_REQUIRE(is_index_dtype(idx_dtype) && is_value_dtype(val_dtype), OFX_EUNSUPPORTED,
                 "sddmm_csr: unsupported dtypes (%d, %d)", idx_dtype, val_dtype);
     OFX_REQUIRE(m >= 0 && k >= 0 && n >= 0 && nnz >= 0 && lda >= n && ldb >= n, OFX_EINVAL,
@@ -635,8 +656,38 @@ extern "C" int ofx_sddmm_csr(void* stream, int idx_dtype, int val_dtype, int64_t
                 "sddmm_csr: NULL pointer");
     if (n == 0) return fail(OFX_EINVAL, "sddmm_csr: n == 0 (use a zero fill)");
     SddmmArgs args{static_cast<hipStream_t>(stream), row_ptr, col_idx, a, b, out, lda, ldb,
-                   row_begin, row_end - row_begin, n, nnz, k, workspace, workspace_bytes};
+                   row_begin, row_end - row_begin, n, nnz, k, workspace, workspace_bytes,
+                   opts->planned != 0};
     if (idx_dtype == OFX_DT_INT32) return sddmm_idx<int32_t>(val_dtype, args);
     return sddmm_idx<int64_t>(val_dtype, args);
+  });
+}
+
+// The SDDMM's work-list plan alone, into `workspace` (ofx_sddmm_csr_workspace_size bytes), for
+// later ofx_sddmm_csr_ex launches with planned = 1 over the same row_ptr, row range and n.
+extern "C" int ofx_sddmm_csr_plan(void* stream, int idx_dtype, int val_dtype, int64_t m, int64_t n,
+                                  int64_t nnz, const void* row_ptr, int64_t row_begin,
+                                  int64_t row_end, void* workspace, size_t workspace_bytes) {
+  return ::ofx::guarded(__func__, [&]() -> int {
+    OFX_TAKE_DEVICE_ERROR("sddmm_csr_plan");
+    OFX_REQUIRE(is_index_dtype(idx_dtype) && is_value_dtype(val_dtype), OFX_EUNSUPPORTED,
+                "sddmm_csr_plan: unsupported dtypes (%d, %d)", idx_dtype, val_dtype);
+    OFX_REQUIRE(m >= 0 && n >= 0 && nnz >= 0 && 0 <= row_begin && row_begin <= row_end &&
+                    row_end <= m, OFX_EINVAL, "sddmm_csr_plan: bad sizes or row range");
+    const int64_t nrows = row_end - row_begin;
+    if (nrows == 0 || nnz == 0 || n == 0) return OFX_OK;  // the launch plans nothing either
+    const Schedule sched = sddmm_schedule(n);
+    const plan::WsLayout w = plan::ws_layout(nrows, nnz, 0, 0, sched);
+    if (w.total == 0) return OFX_OK;
+    OFX_REQUIRE(row_ptr != nullptr, OFX_EINVAL, "sddmm_csr_plan: NULL row_ptr");
+    OFX_REQUIRE(workspace != nullptr && workspace_bytes >= w.total, OFX_EWORKSPACE,
+                "sddmm_csr_plan: workspace of %zu bytes < %zu required", workspace_bytes, w.total);
+    plan::WorkList wl{};
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (idx_dtype == OFX_DT_INT32)
+      return plan::launch_plan<int32_t>(s, static_cast<const int32_t*>(row_ptr), row_begin, nrows,
+                                        nnz, sched, w, static_cast<char*>(workspace), &wl);
+    return plan::launch_plan<int64_t>(s, static_cast<const int64_t*>(row_ptr), row_begin, nrows,
+                                      nnz, sched, w, static_cast<char*>(workspace), &wl);
   });
 }

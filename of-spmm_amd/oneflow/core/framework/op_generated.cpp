@@ -45,6 +45,7 @@ REGISTER_USER_OP("sddmm_csr")
     .Output("out")
     .Attr<int64_t>("a_num_rows", 0)
     .Attr<int64_t>("a_num_cols", 0)
+    .Attr<int64_t>("static_csr", 0)
     .SetLogicalTensorDescInferFn(SddmmCsrOp::InferLogicalTensorDesc)
     .SetPhysicalTensorDescInferFn(SddmmCsrOp::InferPhysicalTensorDesc)
     .SetGetSbpFn(SddmmCsrOp::GetSbp)

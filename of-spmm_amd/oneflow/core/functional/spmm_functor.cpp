@@ -568,10 +568,32 @@ extern "C" int ofx_functional_sddmm_csr(void* stream, const ofx_tensor_desc* row
                                         const ofx_tensor_desc* b, int64_t a_num_rows,
                                         int64_t a_num_cols, ofx_tensor_desc* out, void* tmp,
                                         size_t tmp_bytes, size_t* tmp_size_out) {
+  return ofx_functional_sddmm_csr_attrs(stream, row_ptr, col_idx, a, b, a_num_rows, a_num_cols,
+                                        out, tmp, tmp_bytes, tmp_size_out, nullptr);
+}
+
+// The same with the op's other attributes (static_csr: the SDDMM's plan of an unchanged CSR is
+// kept in the eager op's kernel state -- the values-gradient of a static graph).
+extern "C" int ofx_functional_sddmm_csr_attrs(void* stream, const ofx_tensor_desc* row_ptr,
+                                              const ofx_tensor_desc* col_idx,
+                                              const ofx_tensor_desc* a, const ofx_tensor_desc* b,
+                                              int64_t a_num_rows, int64_t a_num_cols,
+                                              ofx_tensor_desc* out, void* tmp, size_t tmp_bytes,
+                                              size_t* tmp_size_out, const ofx_spmm_attrs* attrs) {
   return ::ofx::guarded(__func__, [&]() -> int {
+    int64_t static_csr = 0;
+    if (attrs != nullptr) {
+      const char* why = ofx::versioned_struct_problem(attrs, OFX_SPMM_ATTRS_MIN_SIZE);
+      OFX_REQUIRE(why == nullptr, OFX_EINVAL,
+                  "sddmm_csr: ofx_spmm_attrs %s (%u bytes): initialise it with "
+                  "OFX_SPMM_ATTRS_INIT", why ? why : "", OFX_SPMM_ATTRS_MIN_SIZE);
+      static_csr = attrs->static_csr;
+    }
     return ToStatus(RunUserOp("sddmm_csr",
                               {{"a_csr_row_ptr", row_ptr}, {"a_csr_col_idx", col_idx}, {"a", a}, {"b", b}},
-                              {{"out", out}}, {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols}},
+                              {{"out", out}},
+                              {{"a_num_rows", a_num_rows}, {"a_num_cols", a_num_cols},
+                               {"static_csr", static_csr}},
                               stream, tmp, tmp_bytes, tmp_size_out));
   });
 }

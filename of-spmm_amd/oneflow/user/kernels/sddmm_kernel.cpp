@@ -4,6 +4,7 @@
  * work through the C-ABI of include/ofx_spmm.h).
  */
 #include "oneflow/core/framework/framework.h"
+#include "oneflow/user/kernels/spmm_plan_state.h"
 #include "ofx_spmm.h"
 
 namespace oneflow {
@@ -15,11 +16,18 @@ int DtCode(DataType dt) { return static_cast<int>(dt); }
 template <DeviceType device_type>
 class SddmmCsrKernel final : public user_op::OpKernel, public user_op::CudaGraphSupport {
  public:
+  // The SDDMM's plans of static CSRs (attr static_csr, as spmm_csr's: spmm_plan_state.h).
+  std::shared_ptr<user_op::OpKernelState> CreateOpKernelState(
+      user_op::KernelInitContext* ctx) const override {
+    if (device_type != DeviceType::kHIP) return nullptr;
+    return std::make_shared<SpmmCsrPlanState>(!ctx->has_stream_name_hint());
+  }
+
   bool AlwaysComputeWhenAllOutputsEmpty() const override { return false; }
 
  private:
   using user_op::OpKernel::Compute;
-  void Compute(user_op::KernelComputeContext* ctx, user_op::OpKernelState*,
+  void Compute(user_op::KernelComputeContext* ctx, user_op::OpKernelState* state,
                const user_op::OpKernelCache*) const override {
     const user_op::Tensor* row_ptr = ctx->Tensor4ArgNameAndIndex("a_csr_row_ptr", 0);
     const user_op::Tensor* col_idx = ctx->Tensor4ArgNameAndIndex("a_csr_col_idx", 0);
@@ -34,11 +42,35 @@ class SddmmCsrKernel final : public user_op::OpKernel, public user_op::CudaGraph
     int rc;
     if (device_type == DeviceType::kHIP) {
       user_op::Tensor* tmp = ctx->Tensor4ArgNameAndIndex("tmp_buffer", 0);
-      rc = ofx_sddmm_csr(ctx->stream()->As<ep::HipStream>()->hip_stream(), idx_dt, val_dt, m, k,
-                         n, nnz, row_ptr->dptr(), col_idx->dptr(), a->dptr(), a->row_stride(),
-                         b->dptr(), b->row_stride(), out->mut_dptr(),
-                         0, m, tmp ? tmp->mut_dptr() : nullptr,
-                         tmp ? (size_t)tmp->shape_view().elem_cnt() : 0);
+      void* ws = tmp ? tmp->mut_dptr() : nullptr;
+      size_t ws_bytes = tmp ? (size_t)tmp->shape_view().elem_cnt() : 0;
+      ep::HipStream* hs = ctx->stream()->As<ep::HipStream>();
+      void* stream = hs->hip_stream();
+      ofx_spmm_options opts = OFX_SPMM_OPTIONS_INIT;
+      auto* plans = dynamic_cast<SpmmCsrPlanState*>(state);
+      const int64_t static_csr = ctx->Attr<int64_t>("static_csr");
+      StaticPlan sp;
+      if (plans != nullptr && static_csr != 0 && m > 0 && n > 0 && nnz > 0) {
+        size_t need = 0;
+        rc = ofx_sddmm_csr_workspace_size(idx_dt, val_dt, m, n, nnz, &need);
+        OFX_KERNEL_CHECK(rc == OFX_OK, "sddmm_csr workspace query failed: " << ofx_last_error());
+        // the SDDMM's schedule is a function of n alone: no options in the key
+        const SpmmCsrPlanState::Key key{static_csr, row_ptr->dptr(),
+                                        plans->key_on_stream() ? stream : nullptr,
+                                        hs->device_index(), idx_dt, val_dt, m, k, n, nnz, 0, m,
+                                        0, 0, 0, 0};
+        auto plan = [&](void* sws, size_t bytes) {
+          return ofx_sddmm_csr_plan(stream, idx_dt, val_dt, m, n, nnz, row_ptr->dptr(), 0, m, sws,
+                                    bytes);
+        };
+        if (UseStaticPlan(plans, key, need, hs->IsGraphCapturing(), "sddmm_csr", plan, &ws,
+                          &ws_bytes, &sp))
+          opts.planned = 1;
+      }
+      rc = ofx_sddmm_csr_ex(stream, idx_dt, val_dt, m, k, n, nnz, row_ptr->dptr(),
+                            col_idx->dptr(), a->dptr(), a->row_stride(), b->dptr(),
+                            b->row_stride(), out->mut_dptr(), 0, m, ws, ws_bytes, &opts);
+      if (rc != OFX_OK && sp.keyed) plans->Drop(sp.key, hs->IsGraphCapturing());
     } else {
       rc = ofx_sddmm_csr_cpu(ctx->stream()->As<ep::CpuStream>()->num_threads(), idx_dt, val_dt, m,
                              k, n, nnz, row_ptr->dptr(), col_idx->dptr(), a->dptr(),

@@ -242,8 +242,10 @@ def _run_grad_op(fn, stream_of, ins, outs, extra, attrs=()):
 
 
 def sddmm_csr(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor, a: torch.Tensor,
-              b: torch.Tensor, a_num_rows: int, a_num_cols: int) -> torch.Tensor:
-    """out[j] = <a[row(j), :], b[col(j), :]> (op "sddmm_csr": the values-gradient of spmm_csr)."""
+              b: torch.Tensor, a_num_rows: int, a_num_cols: int, *,
+              static_csr: int = 0) -> torch.Tensor:
+    """out[j] = <a[row(j), :], b[col(j), :]> (op "sddmm_csr": the values-gradient of spmm_csr).
+    `static_csr` as for spmm_csr: the SDDMM's plan of an unchanged CSR is kept."""
     rp, ci = _prep(a_csr_row_ptr, "a_csr_row_ptr"), _prep(a_csr_col_idx, "a_csr_col_idx")
     a, b = _prep(a, "a", matrix=True), _prep(b, "b", matrix=True)
     if b.dim() == 2 and b.shape[1] == 0:  # empty inner dimension: every dot product is 0
@@ -252,8 +254,14 @@ def sddmm_csr(a_csr_row_ptr: torch.Tensor, a_csr_col_idx: torch.Tensor, a: torch
         out = torch.empty(ci.numel(), dtype=b.dtype, device=b.device)
     if b.dim() == 2 and b.shape[1] == 0 and a.dim() == 2 and a.shape[1] == 0:
         return out
-    _run_grad_op(LIB.ofx_functional_sddmm_csr, b, [rp, ci, a, b], [out],
-                 [int(a_num_rows), int(a_num_cols)])
+    if static_csr:
+        attrs = _lib.SpmmAttrs()
+        attrs.static_csr = int(static_csr)
+        _run_grad_op(LIB.ofx_functional_sddmm_csr_attrs, b, [rp, ci, a, b], [out],
+                     [int(a_num_rows), int(a_num_cols)], (ctypes.byref(attrs),))
+    else:
+        _run_grad_op(LIB.ofx_functional_sddmm_csr, b, [rp, ci, a, b], [out],
+                     [int(a_num_rows), int(a_num_cols)])
     return out
 
 

@@ -134,6 +134,9 @@ def _load():
         "ofx_gather_values_host": ([i32, i32, i64, p, p, p], i32),
         "ofx_sddmm_csr_workspace_size": ([i32, i32, i64, i64, i64, ctypes.POINTER(sz)], i32),
         "ofx_sddmm_csr": ([p, i32, i32, i64, i64, i64, i64, p, p, p, i64, p, i64, p, i64, i64, p, sz], i32),
+        "ofx_sddmm_csr_ex": ([p, i32, i32, i64, i64, i64, i64, p, p, p, i64, p, i64, p, i64, i64, p, sz,
+                              popt], i32),
+        "ofx_sddmm_csr_plan": ([p, i32, i32, i64, i64, i64, p, i64, i64, p, sz], i32),
         "ofx_sddmm_csr_cpu": ([i32, i32, i32, i64, i64, i64, i64, p, p, p, i64, p, i64, p, i64, i64], i32),
         "ofx_coo_to_csr_workspace_size": ([i32, i64, i64, i64, ctypes.POINTER(sz)], i32),
         "ofx_coo_to_csr": ([p, i32, i32, i64, i64, i64, p, p, p, i32, p, p, p, p, p, p, sz], i32),
@@ -210,6 +213,8 @@ def _load():
                                    i32], i32),
         "ofx_functional_sddmm_csr": ([p, pdesc, pdesc, pdesc, pdesc, i64, i64, pdesc, p, sz,
                                       ctypes.POINTER(sz)], i32),
+        "ofx_functional_sddmm_csr_attrs": ([p, pdesc, pdesc, pdesc, pdesc, i64, i64, pdesc, p, sz,
+                                            ctypes.POINTER(sz), pattrs], i32),
         "ofx_functional_spmm_csr_gathered": ([p, pdesc, pdesc, pdesc, pdesc, pdesc, i64, i64, pdesc,
                                               p, sz, ctypes.POINTER(sz)], i32),
         "ofx_functional_spmm_csr_gathered_attrs": ([p, pdesc, pdesc, pdesc, pdesc, pdesc, i64, i64,

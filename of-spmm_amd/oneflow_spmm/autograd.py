@@ -43,9 +43,12 @@ def gather_values(perm: torch.Tensor, values: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def sddmm(row_ptr: torch.Tensor, col_idx: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """out[j] = <a[row(j), :], b[col_idx[j], :]>: op "sddmm_csr" through the op layer."""
-    return _C.sddmm_csr(row_ptr, col_idx, a, b, row_ptr.numel() - 1, b.shape[0])
+def sddmm(row_ptr: torch.Tensor, col_idx: torch.Tensor, a: torch.Tensor, b: torch.Tensor,
+          static_csr: int = 0) -> torch.Tensor:
+    """out[j] = <a[row(j), :], b[col_idx[j], :]>: op "sddmm_csr" through the op layer
+    (`static_csr`: the forward's promise that the CSR is unchanged; its SDDMM plan is kept)."""
+    return _C.sddmm_csr(row_ptr, col_idx, a, b, row_ptr.numel() - 1, b.shape[0],
+                        static_csr=static_csr)
 
 
 # ---- transpose cache (the sparsity pattern of a GNN graph is static across layers/steps) -------
@@ -129,7 +132,7 @@ class SpmmCsrFunction(torch.autograd.Function):
     def forward(ctx, row_ptr, col_idx, values, m, k, b, static_csr=0):
         out = spmm_csr(row_ptr, col_idx, values, m, k, b, static_csr=static_csr)
         ctx.save_for_backward(row_ptr, col_idx, values, b)
-        ctx.m, ctx.k = m, k
+        ctx.m, ctx.k, ctx.static_csr = m, k, static_csr
         return out
 
     @staticmethod
@@ -138,7 +141,7 @@ class SpmmCsrFunction(torch.autograd.Function):
         d_out = d_out.contiguous()
         d_values = d_b = None
         if ctx.needs_input_grad[2]:
-            d_values = sddmm(row_ptr, col_idx, d_out, b)
+            d_values = sddmm(row_ptr, col_idx, d_out, b, ctx.static_csr)
         if ctx.needs_input_grad[5]:
             d_b = TRANSPOSE_CACHE.grad_b(row_ptr, col_idx, values.detach(), ctx.m, ctx.k, d_out)
         return None, None, d_values, None, None, d_b, None
@@ -171,6 +174,7 @@ class FusedSpmmCsrFunction(torch.autograd.Function):
                                 static_csr=static_csr)
         ctx.save_for_backward(row_ptr, col_idx, values, b, out if relu else None)
         ctx.m, ctx.k, ctx.relu, ctx.has_bias = m, k, relu, bias is not None
+        ctx.static_csr = static_csr
         return out
 
     @staticmethod
@@ -181,7 +185,7 @@ class FusedSpmmCsrFunction(torch.autograd.Function):
                                        bias_grad=ctx.has_bias and ctx.needs_input_grad[6])
         d_values = d_b = None
         if ctx.needs_input_grad[2]:
-            d_values = sddmm(row_ptr, col_idx, g, b)
+            d_values = sddmm(row_ptr, col_idx, g, b, ctx.static_csr)
         if ctx.needs_input_grad[5]:
             d_b = TRANSPOSE_CACHE.grad_b(row_ptr, col_idx, values.detach(), ctx.m, ctx.k, g)
         return None, None, d_values, None, None, d_b, d_bias, None, None

@@ -234,3 +234,5 @@ def test_static_csr_is_a_registered_attr_with_default_zero():
     assert '.Attr<int64_t>("static_csr", 0)' in gathered_block
     assert "Int64 static_csr=0) => SpmmCsrGathered" in yaml
     assert td.count('DefaultValuedAttr<SI64Attr, "0">:$static_csr') == 3
+    sddmm_block = gen.split('REGISTER_USER_OP("sddmm_csr")')[1].split("REGISTER_USER_OP")[0]
+    assert '.Attr<int64_t>("static_csr", 0)' in sddmm_block

@@ -296,3 +296,52 @@ def test_autograd_learnable_values_reuse_the_transpose_plan(device):
         assert_bitwise(gb, oracle_spmm(torch.from_numpy(at.indptr.astype(np.int32)),
                                        torch.from_numpy(at.indices.astype(np.int32)),
                                        torch.from_numpy(at.data.astype(np.float32)), g), "d(b)")
+
+
+def test_sddmm_static_plans_once(device):
+    """Op sddmm_csr with static_csr: its own kernel state plans the CSR once (hub rows: a real
+    work list); every call keeps the oracle's bits."""
+    from oracle import oracle
+    rng = np.random.default_rng(690)
+    m, k, n = 30_000, 20_000, 64
+    rp, ci, _ = random_csr(m, k, power_law_degrees(m, 600_000, k, rng), rng)
+    a = random_dense(m, n, rng)
+    b = random_dense(k, n, rng)
+    ref = oracle.sddmm(rp.numpy(), ci.numpy(), a.numpy(), b.numpy())
+    d_rp, d_ci, da, db = rp.to(device), ci.to(device), a.to(device), b.to(device)
+    s0 = _C.static_plans()
+    outs = [_C.sddmm_csr(d_rp, d_ci, da, db, m, k, static_csr=31) for _ in range(3)]
+    torch.cuda.synchronize()
+    assert counters(s0, _C.static_plans()) == {"plans": 1, "hits": 2}
+    for i, o in enumerate(outs):
+        assert np.array_equal(o.cpu().numpy().view(np.uint32), ref.view(np.uint32)), f"call {i}"
+
+
+def test_static_training_step_plans_each_op_once(device):
+    """A training step of a static graph with learnable edge weights: the forward SpMM, the
+    backward SDDMM (d values) and the gathered A^T SpMM (d b) each plan once, then reuse."""
+    from oracle import oracle
+    rng = np.random.default_rng(700)
+    m, k, n = 30_000, 20_000, 32
+    rp, ci, _ = random_csr(m, k, power_law_degrees(m, 600_000, k, rng), rng)
+    d_rp, d_ci = rp.to(device), ci.to(device)
+    fs.autograd.TRANSPOSE_CACHE.__init__()
+    keep, s0 = [], None
+    for step in range(4):
+        v = torch.from_numpy(rng.uniform(-1, 1, ci.numel()).astype(np.float32))
+        dv = v.to(device).requires_grad_(True)
+        keep.append(dv)
+        b = random_dense(k, n, rng)
+        db = b.to(device).requires_grad_(True)
+        out = fs.spmm(d_rp, d_ci, dv, m, k, db, static_csr=41)
+        g = random_dense(m, n, rng)
+        out.backward(g.to(device))
+        torch.cuda.synchronize()
+        if step == 0:
+            s0 = _C.static_plans()
+        ref_dv = oracle.sddmm(rp.numpy(), ci.numpy(), g.numpy(), b.numpy())
+        assert np.array_equal(dv.grad.cpu().numpy().view(np.uint32), ref_dv.view(np.uint32)), \
+            f"d(values) step {step}"
+        assert_bitwise(out.detach().cpu(), oracle_spmm(rp, ci, v, b), f"forward step {step}")
+    st = counters(s0, _C.static_plans())
+    assert st == {"plans": 0, "hits": 9}, st  # 3 ops x 3 later steps
